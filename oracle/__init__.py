@@ -1,0 +1,140 @@
+"""oracle — TEST INFRASTRUCTURE ONLY.
+
+ctypes view of ``oracle/lib/libzc_oracle.so`` (the C restatement in ``c4_oracle.c``).
+Allowed importers: ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s cpu_baseline
+leg — always as the checker or the baseline, never as the product path.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libzc_oracle.so")
+
+
+def build(quiet: bool = True) -> str:
+    subprocess.run(["make", "-C", HERE, "lib"], check=True,
+                   stdout=subprocess.DEVNULL if quiet else None)
+    return LIB_PATH
+
+
+class _MT(ctypes.Structure):
+    _fields_ = [("mt", ctypes.c_uint32 * 624), ("index", ctypes.c_int), ("drawn", ctypes.c_uint64)]
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = ctypes.CDLL(LIB_PATH)
+        P = ctypes.POINTER
+        L.zco_mt_seed.argtypes = [P(_MT), ctypes.c_uint64]
+        L.zco_mt_u32.argtypes = [P(_MT)]
+        L.zco_mt_u32.restype = ctypes.c_uint32
+        L.zco_randbelow.argtypes = [P(_MT), ctypes.c_uint32]
+        L.zco_randbelow.restype = ctypes.c_uint32
+        L.zco_set_order.argtypes = [ctypes.c_int, P(ctypes.c_int)]
+        L.zco_check_win.argtypes = [ctypes.c_char_p, ctypes.c_int]
+        L.zco_check_draw.argtypes = [ctypes.c_char_p]
+        L.zco_rollout.argtypes = [ctypes.c_char_p, ctypes.c_int, P(_MT)]
+        L.zco_get_move.argtypes = [ctypes.c_char_p, ctypes.c_int, P(_MT), ctypes.c_int, ctypes.c_double,
+                                   ctypes.c_int, P(ctypes.c_int), P(ctypes.c_int), P(ctypes.c_int)]
+        L.zco_get_move_batch.argtypes = [ctypes.c_int, ctypes.c_char_p, P(ctypes.c_int), P(ctypes.c_uint64),
+                                         ctypes.c_int, ctypes.c_double, ctypes.c_int, ctypes.c_int,
+                                         P(ctypes.c_int), P(ctypes.c_int), P(ctypes.c_uint64)]
+        _lib = L
+    return _lib
+
+
+class MT:
+    """CPython-compatible MT19937 stream (oracle restatement)."""
+
+    def __init__(self, seed: int):
+        self.s = _MT()
+        lib().zco_mt_seed(ctypes.byref(self.s), seed)
+
+    def u32(self) -> int:
+        return lib().zco_mt_u32(ctypes.byref(self.s))
+
+    def randbelow(self, n: int) -> int:
+        return lib().zco_randbelow(ctypes.byref(self.s), n)
+
+    @property
+    def drawn(self) -> int:
+        return self.s.drawn
+
+    def state(self):
+        return list(self.s.mt), self.s.index
+
+
+def set_order(mask: int) -> list[int]:
+    out = (ctypes.c_int * 7)()
+    n = lib().zco_set_order(mask, out)
+    return list(out[:n])
+
+
+def check_win(board: str, turn: int) -> bool:
+    return bool(lib().zco_check_win(board.encode(), turn))
+
+
+def check_draw(board: str) -> bool:
+    return bool(lib().zco_check_draw(board.encode()))
+
+
+def rollout(board: str, turn: int, seed: int):
+    mt = MT(seed)
+    v = lib().zco_rollout(board.encode(), turn, ctypes.byref(mt.s))
+    return v, mt.drawn
+
+
+def get_move(board: str, turn: int, seed: int, sims: int, c: float = 1.4, bs: int = 32):
+    """Returns (column, root_na in move-list order, move-list order, words consumed)."""
+    mt = MT(seed)
+    na = (ctypes.c_int * 7)()
+    order = (ctypes.c_int * 7)()
+    n = ctypes.c_int(0)
+    col = lib().zco_get_move(board.encode(), turn, ctypes.byref(mt.s), sims, c, bs, na, order, ctypes.byref(n))
+    return col, list(na[:n.value]), list(order[:n.value]), mt.drawn
+
+
+def get_move_mt(board: str, turn: int, mt: MT, sims: int, c: float = 1.4, bs: int = 32):
+    """get_move continuing an existing stream (self-play: one random.seed per game)."""
+    na = (ctypes.c_int * 7)()
+    order = (ctypes.c_int * 7)()
+    n = ctypes.c_int(0)
+    col = lib().zco_get_move(board.encode(), turn, ctypes.byref(mt.s), sims, c, bs, na, order, ctypes.byref(n))
+    return col, list(na[:n.value]), list(order[:n.value])
+
+
+def play(board: str, turn: int, col: int):
+    """c4_backend.play_move on the 42-char encoding (row 0 = top)."""
+    b = list(board)
+    for r in range(5, -1, -1):
+        if b[r * 7 + col] == ".":
+            b[r * 7 + col] = "XO"[turn]
+            break
+    return "".join(b), 1 - turn
+
+
+def get_move_batch(boards: list[str], turns, seeds, sims: int, c: float = 1.4, bs: int = 32, threads: int = 1):
+    """Baseline entry: returns (moves[n], root_na_by_column[n,7], consumed[n])."""
+    n = len(boards)
+    b = "".join(boards).encode()
+    t = np.ascontiguousarray(turns, dtype=np.int32)
+    s = np.ascontiguousarray(seeds, dtype=np.uint64)
+    mv = np.zeros(n, np.int32)
+    na = np.zeros((n, 7), np.int32)
+    cons = np.zeros(n, np.uint64)
+    P = ctypes.POINTER
+    lib().zco_get_move_batch(n, b, t.ctypes.data_as(P(ctypes.c_int)), s.ctypes.data_as(P(ctypes.c_uint64)),
+                             sims, c, bs, threads, mv.ctypes.data_as(P(ctypes.c_int)),
+                             na.ctypes.data_as(P(ctypes.c_int)), cons.ctypes.data_as(P(ctypes.c_uint64)))
+    return mv, na, cons
