@@ -1,0 +1,182 @@
+#!/usr/bin/env python3
+"""bench.py — MCTS node-expansions/sec, Connect4 self-play at 800 sims/move (BASELINE.json).
+
+Workload (BASELINE.json configs[1] = SURVEY.md §8(d) C2; with --gpus N it is C3's sharding):
+4096 concurrent Connect4 self-play games per GPU, 800 simulations per move, leaf batch 32,
+c = 1.4, the reference's random_rollout value and random expansion policy, exact-RNG mode
+(every game's CPython MT19937 stream consumed in the reference's order).  One STEP = one
+move for every game: the whole search (select/expand/rollout/backup x 800) on the GPU,
+then Engine.play_move + _evaluate on the device, finished games restarting from the
+opening (scripts/train.py:151-170 refill).  Games are sharded across ranks by global game
+id (seed = base + id) — no collective on the data path, so "scaling" is "weak".
+
+value = expansions created on all ranks in the K timed steps / max over ranks of the
+wall time of those K steps (barrier + device sync on both sides).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch  # noqa: E402  (first: our library then shares torch's HIP runtime)
+import torch.distributed as dist
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+
+from zeroclone_amd import _native  # noqa: E402
+
+METRIC = "MCTS node-expansions/sec (whole node), Connect4 800 sims/move at 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+
+
+def bytes_per_expansion_model(expansions: int, depth_sum: int) -> int:
+    """bytes(d) = 152*d + 96 algorithmic tree-walk bytes per expansion."""
+    return 152 * depth_sum + 96 * expansions
+
+
+def cpu_baseline(sims: int, bs: int, c: float, budget_s: float = 15.0):
+    """The oracle port (oracle/c4_oracle.c, bit-exact to the reference), timed on host cores."""
+    import oracle
+    threads = max(1, min(16, os.cpu_count() or 1))
+    # calibrate on a small sample, then size the timed sample to ~budget_s
+    n0 = threads
+    t = time.perf_counter()
+    oracle.get_move_batch(["." * 42] * n0, [0] * n0, list(range(n0)), sims, c, bs, threads=threads)
+    rate0 = n0 * sims / max(time.perf_counter() - t, 1e-6)
+    n = int(max(threads, min(65536, rate0 * budget_s / sims)))
+    n = max(threads, (n // threads) * threads)
+    t = time.perf_counter()
+    _, _, _ = oracle.get_move_batch(["." * 42] * n, [0] * n, list(range(1000, 1000 + n)), sims, c, bs, threads=threads)
+    dt = time.perf_counter() - t
+    return {"value": round(n * sims / dt, 1), "unit": "expansions/s", "cores": threads, "kind": "port",
+            "sample": f"{n} games x 1 move x {sims} sims from the opening (expansions = sims there), "
+                      f"batch {bs}, {threads} pthreads, oracle/c4_oracle.c, {dt:.1f}s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--games", type=int, default=4096, help="games per GPU")
+    ap.add_argument("--sims", type=int, default=800)
+    ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--c", type=float, default=1.4)
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic-bytes", type=float, default=None,
+                    help="per-launch HBM bytes of the search kernel from a separate rocprofv3 --pmc pass")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    G, S, B = args.games, args.sims, args.batch
+    eng = _native.NativeEngine(max_games=G, max_sims=S, max_batch=B, device=local)
+    first_id = rank * G
+    eng.seed(0, [args.seed + first_id + g for g in range(G)])
+
+    roots = torch.zeros((G, 3), dtype=torch.int64, device=dev)   # zc_c4_state: stones[2], turn|reserved
+    moves = torch.zeros(G, dtype=torch.int32, device=dev)
+    na = torch.zeros((G, 7), dtype=torch.int32, device=dev)
+    stats = torch.zeros((G, 6), dtype=torch.int64, device=dev)   # zc_game_stats
+    results = torch.zeros(G, dtype=torch.int32, device=dev)
+    acc = torch.zeros(4, dtype=torch.int64, device=dev)          # expansions, depth_sum, finished, leaves
+
+    def step(ev=None):
+        stream = torch.cuda.current_stream(dev).cuda_stream
+        if ev is not None:
+            ev[0].record()
+        eng.c4_search_async(roots.data_ptr(), G, S, args.c, B, moves.data_ptr(), na.data_ptr(),
+                            stats.data_ptr(), stream=stream)
+        if ev is not None:
+            ev[1].record()
+        eng.c4_play_async(roots.data_ptr(), G, moves.data_ptr(), results.data_ptr(), reset=True, stream=stream)
+        acc[0] += stats[:, 0].sum()
+        acc[1] += stats[:, 1].sum()
+        acc[2] += (results != _native.ZC_C4_ONGOING).sum()
+        acc[3] += stats[:, 2].sum()
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    acc.zero_()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step(evs[k])
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+
+    bad = int((stats[:, 5] != 0).sum().item())
+    if bad:
+        raise RuntimeError(f"{bad} games reported a nonzero search status")
+    kernel_ms = [a.elapsed_time(b) for a, b in evs]
+    tot = acc.clone()
+    dtt = torch.tensor([dt], dtype=torch.float64, device=dev)
+    kms = torch.tensor([sum(kernel_ms)], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+        dist.all_reduce(dtt, op=dist.ReduceOp.MAX)
+        dist.all_reduce(kms, op=dist.ReduceOp.MAX)
+    expansions, depth_sum, finished, leaves = (int(x) for x in tot.tolist())
+    dt_max = float(dtt.item())
+
+    if rank == 0:
+        launches = args.steps * world
+        bytes_launch = bytes_per_expansion_model(expansions, depth_sum) / launches
+        avg_kernel_s = float(kms.item()) / 1e3 / args.steps
+        achieved = bytes_launch / avg_kernel_s / 1e9
+        out = {
+            "metric": METRIC,
+            "value": round(expansions / dt_max, 1),
+            "unit": "expansions/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(dt_max / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic: self-play from the empty board, per-game CPython MT19937 seeds base+game_id",
+            "config": {"workload": f"C2/C3 Connect4 self-play, {G} games/GPU, {S} sims/move, batch {B}, "
+                                   f"c {args.c}, random_rollout exact-RNG mode",
+                       "games_per_gpu": G, "global_games": G * world, "sims": S, "batch_size": B,
+                       "parallelism": f"games sharded over {world} GPU(s), 1 process/GPU"},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 5),
+                         "traffic": args.traffic_bytes,
+                         "kernel": "c4_search_kernel", "avg_launch_ms": round(avg_kernel_s * 1e3, 3),
+                         "bytes_per_launch_model": round(bytes_launch),
+                         "model": "SURVEY §8(d): 152*d+96 B per expansion, d counted in-kernel"},
+            "extra": {"expansions": expansions, "leaves": leaves, "mean_depth": round(depth_sum / max(expansions, 1), 3),
+                      "games_finished": finished, "search_ms_per_step": [round(x, 3) for x in kernel_ms]},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(S, B, args.c)
+        else:
+            out["cpu_baseline"] = None
+        print(json.dumps(out), flush=True)
+    eng.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

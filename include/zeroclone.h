@@ -1,0 +1,135 @@
+/* zeroclone.h — C-ABI of libzeroclone_amd.so, the MI355X-native batched-MCTS engine.
+ *
+ * Drop-in boundary for the reference's search core.  The reference binds ONE function,
+ *     mcts.get_move(state, value, policy, backend, simulations=1000, c=1.4, batch_size=32)
+ *     (engine/mcts/src/bindings_mcts.cpp:9-11, implemented at engine/mcts/src/mcts.cpp:102-160)
+ * and calls it once per game per move from Python threads (engine/engine.py:119-138).  Here
+ * one call searches MANY games at once on the GPU; the Python layer in zeroclone_amd/
+ * keeps the reference's get_move / Engine API on top of these entry points.
+ *
+ * Conventions: plain C types only; every function returns 0 (ZC_OK) or a negative
+ * ZC_E* code and records a message retrievable with zc_last_error() (thread-local).
+ * An engine is bound to one HIP device; calls on one engine are serialised internally.
+ */
+#ifndef ZEROCLONE_H
+#define ZEROCLONE_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ZC_OK 0
+#define ZC_EINVAL -1     /* bad argument (reference: ValueError / UB)               */
+#define ZC_EHIP -2       /* HIP runtime error                                       */
+#define ZC_ENOMEM -3     /* device allocation failed                                */
+#define ZC_ECAPACITY -4  /* request exceeds the engine's configured capacity        */
+#define ZC_EDEVICE -5    /* a kernel reported an internal error (status word)       */
+
+/* Connect4 position.  Bit (7*col + r) of stones[p] is set when the cell in column `col`,
+ * r-th row counted from the BOTTOM (r = 0..5), holds player p's token ('X' = player 0,
+ * 'O' = player 1).  Bit 7*col+6 is a sentinel and must be 0.  In the reference's
+ * c4_backend.State (engine/games/connect4/c4_backend.py:4-12) board[row][col] has row 0 at
+ * the TOP, i.e. r = 5 - row.  `turn` is the side to move (State.turn). */
+typedef struct zc_c4_state {
+    uint64_t stones[2];
+    int32_t turn;
+    int32_t reserved;
+} zc_c4_state;
+
+/* Per-game counters of one search (all int64 so a device array of them is plain data). */
+typedef struct zc_game_stats {
+    int64_t expansions;      /* nodes created (= simulations that expanded)              */
+    int64_t depth_sum;       /* sum over expansions of the new node's depth d (root = 0) */
+    int64_t leaves;          /* leaves evaluated (= simulations)                          */
+    int64_t rollout_plies;   /* plies played inside random rollouts                      */
+    int64_t rng_words;       /* MT19937 words consumed                                   */
+    int64_t status;          /* 0 = ok; nonzero = internal error code                    */
+} zc_game_stats;
+
+typedef struct zc_engine_config {
+    int32_t device;          /* HIP device ordinal                                        */
+    int32_t max_games;       /* games resident on this engine                             */
+    int32_t max_sims;        /* simulations per move (tree capacity = max_sims + 1 nodes) */
+    int32_t max_batch;       /* leaf batch size (reference batch_size)                    */
+} zc_engine_config;
+
+typedef struct zc_engine zc_engine;
+
+const char *zc_version(void);
+const char *zc_last_error(void);
+int zc_device_count(int32_t *count);
+
+int zc_engine_create(const zc_engine_config *cfg, zc_engine **out);
+int zc_engine_destroy(zc_engine *eng);
+/* Device bytes held by the engine. */
+int zc_engine_footprint(const zc_engine *eng, int64_t *bytes);
+
+/* ---- per-game random streams: CPython 3.10 `random.Random` (MT19937) -----------------
+ * The reference draws every random number from Python's global `random` module
+ * (engine/policy_functions.py:12, engine/value_functions.py:40).  Each engine game owns one
+ * such stream; the search consumes it in exactly the reference's order. */
+/* random.seed(seeds[i]) for games first..first+n-1 (seeds are non-negative ints < 2**64). */
+int zc_rng_seed(zc_engine *eng, int32_t first_game, int32_t n_games, const uint64_t *seeds);
+/* random.setstate((3, tuple(mt) + (index,), None)) / random.getstate() for one game. */
+int zc_rng_set_state(zc_engine *eng, int32_t game, const uint32_t *mt624, int32_t index);
+int zc_rng_get_state(zc_engine *eng, int32_t game, uint32_t *mt624, int32_t *index);
+
+/* ---- Connect4 search: replaces mcts.get_move (mcts.cpp:102-160) for
+ *      backend = c4_backend, policy = Policy('random'), value = Value('random_rollout').
+ * Games first_game .. first_game+n_games-1 are searched from roots[i] with `sims`
+ * simulations, exploration constant `c` and leaf batch `batch_size`.  Outputs:
+ *   out_move[i]          chosen column (first max of child visit count, move-list order)
+ *   out_root_na[7*i+col] visits of the root child that drops in column `col` (0 if illegal)
+ *   out_stats[i]         counters (may be NULL)
+ * A root with no legal move, sims < 1 or batch_size < 1 is ZC_EINVAL (the reference
+ * indexes moves[-1] there: mcts.cpp:150-157).  Host pointers; blocks until done. */
+int zc_c4_search(zc_engine *eng, int32_t first_game, int32_t n_games, const zc_c4_state *roots,
+                 int32_t sims, double c, int32_t batch_size,
+                 int32_t *out_move, int32_t *out_root_na, zc_game_stats *out_stats);
+
+/* Same, with DEVICE pointers, enqueued on `hip_stream` (a hipStream_t; NULL = the engine's
+ * stream) without synchronising.  Argument validation that needs the roots happens on the
+ * device: a bad root sets out_stats[i].status (ZC_STATUS_*). */
+int zc_c4_search_async(zc_engine *eng, int32_t first_game, int32_t n_games, const zc_c4_state *d_roots,
+                       int32_t sims, double c, int32_t batch_size,
+                       int32_t *d_out_move, int32_t *d_out_root_na, zc_game_stats *d_out_stats,
+                       void *hip_stream);
+
+/* Engine.play_move + Engine._evaluate on the device for n games (engine/engine.py:98-108,
+ * 148-153): states[i] = c4_backend.play_move(states[i], (moves[i], 0)) and
+ *   results[i] = turn*2-1 if check_win (i.e. +1 when 'X' just won), 0 if check_draw, else
+ *   ZC_C4_ONGOING.
+ * A negative move leaves the game untouched (result ZC_C4_ONGOING).  With reset != 0 a
+ * finished game restarts from create_init_state() — the self-play refill of
+ * scripts/train.py:151-170.  Device pointers, enqueued on hip_stream (NULL = engine's). */
+int zc_c4_play_async(zc_engine *eng, int32_t n_games, zc_c4_state *d_states, const int32_t *d_moves,
+                     int32_t *d_results, int32_t reset, void *hip_stream);
+#define ZC_C4_ONGOING 2
+
+#define ZC_STATUS_NO_MOVES 1     /* root has no legal move                                */
+#define ZC_STATUS_BAD_STATE 2    /* sentinel bits set / overlapping stones / bad turn    */
+#define ZC_STATUS_INTERNAL 3     /* search invariant violated (never expected)            */
+
+/* ---- Connect4 rules on the host (engine/games/connect4/c4_backend.py) --------------- */
+/* rows: 42 chars, row 0 = top, 'X', 'O', anything else = empty. */
+int zc_c4_from_rows(const char *rows42, int32_t turn, zc_c4_state *out);
+int zc_c4_to_rows(const zc_c4_state *s, char *rows42);
+/* CPython iteration order of c4_backend.get_legal_moves' set for a legal-column mask
+ * (bit c = column c playable); writes the columns to cols[0..n) and returns n (0..7). */
+int zc_c4_legal_order(int32_t mask, int32_t *cols);
+
+/* ---- self-test hooks (used by the parity tests) -------------------------------------
+ * UCT score exactly as the search kernel computes it (mcts.cpp:41-45), evaluated ON THE
+ * DEVICE for n inputs: out[i] = na[i]==0 ? +inf : fma(c, sqrt(logn[i]/na[i]), q[i]). */
+int zc_debug_uct(zc_engine *eng, int32_t n, const double *logn, const int32_t *na, const double *q,
+                 double c, double *out);
+/* Value('random_rollout') on the device for n positions, game i using engine game
+ * first_game+i's stream: out_value[i] in {-1,0,1}, out_words[i] = words consumed. */
+int zc_debug_c4_rollout(zc_engine *eng, int32_t first_game, int32_t n, const zc_c4_state *states,
+                        int32_t *out_value, int64_t *out_words);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,224 @@
+"""ctypes binding of libzeroclone_amd.so (the C-ABI in include/zeroclone.h).
+
+There is no CPU fallback: if the library or a GPU is missing, constructing an engine raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import numpy as np
+
+from .build import LIB
+
+P = ctypes.POINTER
+
+ZC_OK = 0
+ZC_EINVAL = -1
+ZC_EHIP = -2
+ZC_ENOMEM = -3
+ZC_ECAPACITY = -4
+ZC_EDEVICE = -5
+ZC_C4_ONGOING = 2
+ZC_STATUS_NO_MOVES = 1
+ZC_STATUS_BAD_STATE = 2
+
+
+class C4State(ctypes.Structure):
+    _fields_ = [("stones", ctypes.c_uint64 * 2), ("turn", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+
+
+class GameStats(ctypes.Structure):
+    _fields_ = [("expansions", ctypes.c_int64), ("depth_sum", ctypes.c_int64), ("leaves", ctypes.c_int64),
+                ("rollout_plies", ctypes.c_int64), ("rng_words", ctypes.c_int64), ("status", ctypes.c_int64)]
+
+
+class EngineConfig(ctypes.Structure):
+    _fields_ = [("device", ctypes.c_int32), ("max_games", ctypes.c_int32), ("max_sims", ctypes.c_int32),
+                ("max_batch", ctypes.c_int32)]
+
+
+C4_STATE_DTYPE = np.dtype([("stones", "<u8", (2,)), ("turn", "<i4"), ("reserved", "<i4")])
+STATS_DTYPE = np.dtype([("expansions", "<i8"), ("depth_sum", "<i8"), ("leaves", "<i8"),
+                        ("rollout_plies", "<i8"), ("rng_words", "<i8"), ("status", "<i8")])
+assert C4_STATE_DTYPE.itemsize == ctypes.sizeof(C4State) == 24
+assert STATS_DTYPE.itemsize == ctypes.sizeof(GameStats) == 48
+
+# Every symbol include/zeroclone.h declares: (name, restype, argtypes)
+SIGNATURES = [
+    ("zc_version", ctypes.c_char_p, []),
+    ("zc_last_error", ctypes.c_char_p, []),
+    ("zc_device_count", ctypes.c_int, [P(ctypes.c_int32)]),
+    ("zc_engine_create", ctypes.c_int, [P(EngineConfig), P(ctypes.c_void_p)]),
+    ("zc_engine_destroy", ctypes.c_int, [ctypes.c_void_p]),
+    ("zc_engine_footprint", ctypes.c_int, [ctypes.c_void_p, P(ctypes.c_int64)]),
+    ("zc_rng_seed", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, P(ctypes.c_uint64)]),
+    ("zc_rng_set_state", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, P(ctypes.c_uint32), ctypes.c_int32]),
+    ("zc_rng_get_state", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, P(ctypes.c_uint32), P(ctypes.c_int32)]),
+    ("zc_c4_search", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p,
+                                    ctypes.c_int32, ctypes.c_double, ctypes.c_int32, ctypes.c_void_p,
+                                    ctypes.c_void_p, ctypes.c_void_p]),
+    ("zc_c4_search_async", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p,
+                                          ctypes.c_int32, ctypes.c_double, ctypes.c_int32, ctypes.c_void_p,
+                                          ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    ("zc_c4_play_async", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p,
+                                        ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p]),
+    ("zc_c4_from_rows", ctypes.c_int, [ctypes.c_char_p, ctypes.c_int32, P(C4State)]),
+    ("zc_c4_to_rows", ctypes.c_int, [P(C4State), ctypes.c_char_p]),
+    ("zc_c4_legal_order", ctypes.c_int, [ctypes.c_int32, P(ctypes.c_int32)]),
+    ("zc_debug_uct", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p,
+                                    ctypes.c_void_p, ctypes.c_double, ctypes.c_void_p]),
+    ("zc_debug_c4_rollout", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p,
+                                           ctypes.c_void_p, ctypes.c_void_p]),
+]
+
+_lib = None
+_lock = threading.Lock()
+
+
+class ZeroCloneError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"[zc {code}] {msg}")
+        self.code = code
+
+
+def lib(build_if_missing: bool = True):
+    """Load libzeroclone_amd.so (building it with hipcc if absent and allowed)."""
+    global _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB):
+                if not build_if_missing:
+                    raise ImportError(f"{LIB} not built (run python -m zeroclone_amd.build)")
+                from .build import build
+                build()
+            L = ctypes.CDLL(LIB)
+            for name, res, args in SIGNATURES:
+                fn = getattr(L, name)
+                fn.restype = res
+                fn.argtypes = args
+            _lib = L
+    return _lib
+
+
+def check(rc: int):
+    if rc < 0:
+        msg = lib().zc_last_error().decode(errors="replace")
+        if rc == ZC_EINVAL:
+            raise ValueError(msg)
+        raise ZeroCloneError(rc, msg)
+    return rc
+
+
+def _ptr(a: np.ndarray):
+    return ctypes.c_void_p(a.ctypes.data)
+
+
+def device_count() -> int:
+    n = ctypes.c_int32(0)
+    check(lib().zc_device_count(ctypes.byref(n)))
+    return n.value
+
+
+def c4_from_rows(rows42: str, turn: int) -> np.void:
+    s = C4State()
+    check(lib().zc_c4_from_rows(rows42.encode(), int(turn), ctypes.byref(s)))
+    out = np.zeros((), C4_STATE_DTYPE)
+    out["stones"] = (s.stones[0], s.stones[1])
+    out["turn"] = s.turn
+    return out
+
+
+def c4_legal_order(mask: int) -> list[int]:
+    cols = (ctypes.c_int32 * 7)()
+    n = check(lib().zc_c4_legal_order(int(mask), cols))
+    return list(cols[:n])
+
+
+class NativeEngine:
+    """One HIP device's arena: `max_games` resident games, trees of max_sims+1 nodes."""
+
+    def __init__(self, max_games: int, max_sims: int, max_batch: int = 32, device: int = 0):
+        L = lib()
+        cfg = EngineConfig(device, max_games, max_sims, max_batch)
+        h = ctypes.c_void_p()
+        check(L.zc_engine_create(ctypes.byref(cfg), ctypes.byref(h)))
+        self._h = h
+        self.max_games, self.max_sims, self.max_batch, self.device = max_games, max_sims, max_batch, device
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().zc_engine_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def handle(self):
+        return self._h
+
+    def footprint(self) -> int:
+        b = ctypes.c_int64(0)
+        check(lib().zc_engine_footprint(self._h, ctypes.byref(b)))
+        return b.value
+
+    # ---- random streams
+    def seed(self, first_game: int, seeds) -> None:
+        s = np.ascontiguousarray(seeds, dtype=np.uint64)
+        check(lib().zc_rng_seed(self._h, first_game, len(s), s.ctypes.data_as(P(ctypes.c_uint64))))
+
+    def set_rng_state(self, game: int, mt624, index: int) -> None:
+        mt = np.ascontiguousarray(mt624, dtype=np.uint32)
+        assert mt.shape == (624,)
+        check(lib().zc_rng_set_state(self._h, game, mt.ctypes.data_as(P(ctypes.c_uint32)), int(index)))
+
+    def get_rng_state(self, game: int):
+        mt = np.zeros(624, np.uint32)
+        idx = ctypes.c_int32(0)
+        check(lib().zc_rng_get_state(self._h, game, mt.ctypes.data_as(P(ctypes.c_uint32)), ctypes.byref(idx)))
+        return mt, idx.value
+
+    # ---- search
+    def c4_search(self, roots: np.ndarray, sims: int, c: float = 1.4, batch_size: int = 32, first_game: int = 0):
+        roots = np.ascontiguousarray(roots, dtype=C4_STATE_DTYPE)
+        n = roots.shape[0]
+        mv = np.zeros(n, np.int32)
+        na = np.zeros((n, 7), np.int32)
+        st = np.zeros(n, STATS_DTYPE)
+        check(lib().zc_c4_search(self._h, first_game, n, _ptr(roots), int(sims), float(c), int(batch_size),
+                                 _ptr(mv), _ptr(na), _ptr(st)))
+        return mv, na, st
+
+    def c4_search_async(self, d_roots: int, n: int, sims: int, c: float, batch_size: int, d_move: int, d_na: int,
+                        d_stats: int, stream: int = 0, first_game: int = 0) -> None:
+        """Device-pointer entry (ints from torch .data_ptr()); enqueued on `stream`."""
+        check(lib().zc_c4_search_async(self._h, first_game, n, ctypes.c_void_p(d_roots), int(sims), float(c),
+                                       int(batch_size), ctypes.c_void_p(d_move), ctypes.c_void_p(d_na),
+                                       ctypes.c_void_p(d_stats), ctypes.c_void_p(stream or None)))
+
+    def c4_play_async(self, d_states: int, n: int, d_moves: int, d_results: int, reset: bool = True,
+                      stream: int = 0) -> None:
+        check(lib().zc_c4_play_async(self._h, n, ctypes.c_void_p(d_states), ctypes.c_void_p(d_moves),
+                                     ctypes.c_void_p(d_results), int(bool(reset)), ctypes.c_void_p(stream or None)))
+
+    # ---- self-test hooks
+    def debug_uct(self, logn, na, q, c: float):
+        logn = np.ascontiguousarray(logn, np.float64)
+        na = np.ascontiguousarray(na, np.int32)
+        q = np.ascontiguousarray(q, np.float64)
+        out = np.zeros(len(logn), np.float64)
+        check(lib().zc_debug_uct(self._h, len(logn), _ptr(logn), _ptr(na), _ptr(q), float(c), _ptr(out)))
+        return out
+
+    def debug_c4_rollout(self, states: np.ndarray, first_game: int = 0):
+        states = np.ascontiguousarray(states, dtype=C4_STATE_DTYPE)
+        n = states.shape[0]
+        v = np.zeros(n, np.int32)
+        w = np.zeros(n, np.int64)
+        check(lib().zc_debug_c4_rollout(self._h, first_game, n, _ptr(states), _ptr(v), _ptr(w)))
+        return v, w

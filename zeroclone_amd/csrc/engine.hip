@@ -1,0 +1,398 @@
+// engine.hip — host side of the C-ABI (include/zeroclone.h): engine arena in HBM, per-game
+// CPython-compatible random streams, argument checking, and the synchronous / stream-
+// ordered search entry points.
+#include <math.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <vector>
+
+#include "c4_order_table.h"
+#include "zc_internal.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char *fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+#define ZC_HIP(call)                                                                                   \
+    do {                                                                                               \
+        hipError_t e_ = (call);                                                                        \
+        if (e_ != hipSuccess) return fail(ZC_EHIP, "%s failed: %s", #call, hipGetErrorString(e_));     \
+    } while (0)
+
+// CPython 3.10 Modules/_randommodule.c: random.seed(int) -> init_by_array(abs(n) as LE words).
+void mt_init_by_array(uint32_t *mt, const uint32_t *key, int len) {
+    mt[0] = 19650218u;
+    for (int i = 1; i < 624; i++) mt[i] = 1812433253u * (mt[i - 1] ^ (mt[i - 1] >> 30)) + (uint32_t)i;
+    int i = 1, j = 0;
+    for (int k = (624 > len ? 624 : len); k; k--) {
+        mt[i] = (mt[i] ^ ((mt[i - 1] ^ (mt[i - 1] >> 30)) * 1664525u)) + key[j] + (uint32_t)j;
+        i++;
+        j++;
+        if (i >= 624) { mt[0] = mt[623]; i = 1; }
+        if (j >= len) j = 0;
+    }
+    for (int k = 623; k; k--) {
+        mt[i] = (mt[i] ^ ((mt[i - 1] ^ (mt[i - 1] >> 30)) * 1566083941u)) - (uint32_t)i;
+        i++;
+        if (i >= 624) { mt[0] = mt[623]; i = 1; }
+    }
+    mt[0] = 0x80000000u;
+}
+
+template <class T>
+int dalloc(zc_engine *e, T **p, size_t count) {
+    const size_t bytes = count * sizeof(T);
+    if (hipMalloc((void **)p, bytes ? bytes : 16) != hipSuccess)
+        return fail(ZC_ENOMEM, "hipMalloc(%zu bytes) failed", bytes);
+    e->bytes += (int64_t)bytes;
+    return ZC_OK;
+}
+
+void free_arena(zc::Arena &a) {
+    void *ptrs[] = {a.nodes, a.W, a.path, a.pstate, a.pmeta, a.pval, a.ring, a.rngpos,
+                    a.logtab, a.roots, a.move, a.na, a.stats};
+    for (void *p : ptrs)
+        if (p) (void)hipFree(p);
+    a = zc::Arena{};
+}
+
+int check_games(const zc_engine *e, int32_t first, int32_t n) {
+    if (first < 0 || n < 0 || (int64_t)first + n > e->cfg.max_games)
+        return fail(ZC_ECAPACITY, "games [%d, %d) outside engine capacity %d", first, first + n, e->cfg.max_games);
+    return ZC_OK;
+}
+
+int check_search(const zc_engine *e, int32_t first, int32_t n, int32_t sims, double c, int32_t bs) {
+    if (int r = check_games(e, first, n)) return r;
+    if (sims < 1) return fail(ZC_EINVAL, "simulations must be >= 1 (got %d)", sims);
+    if (bs < 1) return fail(ZC_EINVAL, "batch_size must be >= 1 (got %d)", bs);
+    if (sims > e->cfg.max_sims) return fail(ZC_ECAPACITY, "simulations %d > engine max_sims %d", sims, e->cfg.max_sims);
+    if (bs > e->cfg.max_batch) return fail(ZC_ECAPACITY, "batch_size %d > engine max_batch %d", bs, e->cfg.max_batch);
+    if (!isfinite(c)) return fail(ZC_EINVAL, "c must be finite");
+    return ZC_OK;
+}
+
+bool valid_c4(const zc_c4_state &s) {
+    const uint64_t full = 0x0000040810204081ull * 0x3Full;
+    if ((s.stones[0] & s.stones[1]) || ((s.stones[0] | s.stones[1]) & ~full) || (s.turn & ~1)) return false;
+    const uint64_t occ = s.stones[0] | s.stones[1];
+    for (int c = 0; c < 7; ++c) {
+        const uint64_t col = (occ >> (7 * c)) & 0x3Full;
+        if (col & (col + 1)) return false;
+    }
+    return true;
+}
+
+zc::SearchParams make_params(zc_engine *e, int32_t first, int32_t n, const zc_c4_state *roots, int32_t sims,
+                             double c, int32_t bs, int32_t *mv, int32_t *na, zc_game_stats *st) {
+    zc::SearchParams p{};
+    p.first_game = first;
+    p.n_games = n;
+    p.sims = sims;
+    p.bs = bs;
+    p.M = e->M;
+    p.c = c;
+    p.roots = roots;
+    p.out_move = mv;
+    p.out_na = na;
+    p.out_stats = st;
+    p.a = e->a;
+    p.max_batch = e->cfg.max_batch;
+    return p;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char *zc_version(void) { return "zeroclone_amd 0.1.0 (gfx950)"; }
+
+const char *zc_last_error(void) { return g_err.c_str(); }
+
+int zc_device_count(int32_t *count) {
+    int n = 0;
+    ZC_HIP(hipGetDeviceCount(&n));
+    *count = n;
+    return ZC_OK;
+}
+
+int zc_engine_create(const zc_engine_config *cfg, zc_engine **out) {
+    if (!cfg || !out) return fail(ZC_EINVAL, "null argument");
+    *out = nullptr;
+    if (cfg->max_games < 1) return fail(ZC_EINVAL, "max_games must be >= 1");
+    if (cfg->max_sims < 1 || cfg->max_sims > 65533) return fail(ZC_EINVAL, "max_sims must be in [1, 65533]");
+    if (cfg->max_batch < 1) return fail(ZC_EINVAL, "max_batch must be >= 1");
+    int ndev = 0;
+    ZC_HIP(hipGetDeviceCount(&ndev));
+    if (cfg->device < 0 || cfg->device >= ndev) return fail(ZC_EINVAL, "device %d not present (%d devices)", cfg->device, ndev);
+    ZC_HIP(hipSetDevice(cfg->device));
+
+    zc_engine *e = new zc_engine();
+    e->cfg = *cfg;
+    e->M = cfg->max_sims + 1;
+    const size_t G = (size_t)cfg->max_games, M = (size_t)e->M, B = (size_t)cfg->max_batch;
+    zc::Arena &a = e->a;
+    int rc = ZC_OK;
+    if (!rc) rc = dalloc(e, &a.nodes, G * M * zc::kRecBytes);
+    if (!rc) rc = dalloc(e, &a.W, G * M * zc::kSlots);
+    if (!rc) rc = dalloc(e, &a.path, G * B * zc::kMaxDepth);
+    if (!rc) rc = dalloc(e, &a.pstate, G * B * 2);
+    if (!rc) rc = dalloc(e, &a.pmeta, G * B);
+    if (!rc) rc = dalloc(e, &a.pval, G * B);
+    if (!rc) rc = dalloc(e, &a.ring, G * zc::kRingWords);
+    if (!rc) rc = dalloc(e, &a.rngpos, G * 2);
+    if (!rc) rc = dalloc(e, &a.logtab, M + 2);
+    if (!rc) rc = dalloc(e, &a.roots, G);
+    if (!rc) rc = dalloc(e, &a.move, G);
+    if (!rc) rc = dalloc(e, &a.na, G * 7);
+    if (!rc) rc = dalloc(e, &a.stats, G);
+    if (!rc && hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess)
+        rc = fail(ZC_EHIP, "hipStreamCreate failed");
+    if (!rc) {
+        // log(N) exactly as the reference gets it: glibc log on the host (mcts.cpp:44).
+        std::vector<double> lg(M + 2);
+        for (size_t n = 0; n < M + 2; ++n) lg[n] = log((double)n);
+        if (hipMemcpy(a.logtab, lg.data(), lg.size() * sizeof(double), hipMemcpyHostToDevice) != hipSuccess)
+            rc = fail(ZC_EHIP, "logtab upload failed");
+    }
+    if (rc) {
+        free_arena(a);
+        if (e->stream) (void)hipStreamDestroy(e->stream);
+        delete e;
+        return rc;
+    }
+    *out = e;
+    // every game starts as random.seed(game index)
+    std::vector<uint64_t> seeds(G);
+    for (size_t g = 0; g < G; ++g) seeds[g] = g;
+    return zc_rng_seed(e, 0, (int32_t)G, seeds.data());
+}
+
+int zc_engine_destroy(zc_engine *eng) {
+    if (!eng) return ZC_OK;
+    {
+        std::lock_guard<std::mutex> lk(eng->mu);
+        (void)hipSetDevice(eng->cfg.device);
+        (void)hipStreamSynchronize(eng->stream);
+        free_arena(eng->a);
+        (void)hipStreamDestroy(eng->stream);
+    }
+    delete eng;
+    return ZC_OK;
+}
+
+int zc_engine_footprint(const zc_engine *eng, int64_t *bytes) {
+    if (!eng || !bytes) return fail(ZC_EINVAL, "null argument");
+    *bytes = eng->bytes;
+    return ZC_OK;
+}
+
+int zc_rng_seed(zc_engine *eng, int32_t first, int32_t n, const uint64_t *seeds) {
+    if (!eng || (!seeds && n)) return fail(ZC_EINVAL, "null argument");
+    if (int r = check_games(eng, first, n)) return r;
+    std::lock_guard<std::mutex> lk(eng->mu);
+    ZC_HIP(hipSetDevice(eng->cfg.device));
+    std::vector<uint32_t> words((size_t)n * 624);
+    std::vector<uint64_t> pos((size_t)n * 2);
+    for (int32_t i = 0; i < n; ++i) {
+        const uint32_t key[2] = {(uint32_t)seeds[i], (uint32_t)(seeds[i] >> 32)};
+        mt_init_by_array(&words[(size_t)i * 624], key, key[1] ? 2 : 1);
+        pos[2 * (size_t)i] = 624;   // index 624: the next draw twists (random.seed leaves this)
+        pos[2 * (size_t)i + 1] = 624;
+    }
+    if (n) {
+        ZC_HIP(hipMemcpy2DAsync(eng->a.ring + (size_t)first * zc::kRingWords, zc::kRingWords * sizeof(uint32_t),
+                                words.data(), 624 * sizeof(uint32_t), 624 * sizeof(uint32_t), (size_t)n,
+                                hipMemcpyHostToDevice, eng->stream));
+        ZC_HIP(hipMemcpyAsync(eng->a.rngpos + 2 * (size_t)first, pos.data(), pos.size() * sizeof(uint64_t),
+                              hipMemcpyHostToDevice, eng->stream));
+        ZC_HIP(hipStreamSynchronize(eng->stream));
+    }
+    return ZC_OK;
+}
+
+int zc_rng_set_state(zc_engine *eng, int32_t game, const uint32_t *mt624, int32_t index) {
+    if (!eng || !mt624) return fail(ZC_EINVAL, "null argument");
+    if (int r = check_games(eng, game, 1)) return r;
+    if (index < 0 || index > 624) return fail(ZC_EINVAL, "MT index must be in [0, 624] (got %d)", index);
+    std::lock_guard<std::mutex> lk(eng->mu);
+    ZC_HIP(hipSetDevice(eng->cfg.device));
+    const uint64_t pos[2] = {(uint64_t)index, 624};
+    ZC_HIP(hipMemcpyAsync(eng->a.ring + (size_t)game * zc::kRingWords, mt624, 624 * sizeof(uint32_t),
+                          hipMemcpyHostToDevice, eng->stream));
+    ZC_HIP(hipMemcpyAsync(eng->a.rngpos + 2 * (size_t)game, pos, sizeof pos, hipMemcpyHostToDevice, eng->stream));
+    ZC_HIP(hipStreamSynchronize(eng->stream));
+    return ZC_OK;
+}
+
+int zc_rng_get_state(zc_engine *eng, int32_t game, uint32_t *mt624, int32_t *index) {
+    if (!eng || !mt624 || !index) return fail(ZC_EINVAL, "null argument");
+    if (int r = check_games(eng, game, 1)) return r;
+    std::lock_guard<std::mutex> lk(eng->mu);
+    ZC_HIP(hipSetDevice(eng->cfg.device));
+    uint64_t pos[2];
+    std::vector<uint32_t> ring(zc::kRingWords);
+    ZC_HIP(hipMemcpyAsync(pos, eng->a.rngpos + 2 * (size_t)game, sizeof pos, hipMemcpyDeviceToHost, eng->stream));
+    ZC_HIP(hipMemcpyAsync(ring.data(), eng->a.ring + (size_t)game * zc::kRingWords, zc::kRingWords * sizeof(uint32_t),
+                          hipMemcpyDeviceToHost, eng->stream));
+    ZC_HIP(hipStreamSynchronize(eng->stream));
+    // Python's state after consuming word `use-1`: the 624-word block holding it, and the
+    // offset of the next word inside that block (624 = block exhausted).
+    const uint64_t use = pos[0];
+    const uint64_t blk = use == 0 ? 0 : (use - 1) / 624;
+    for (int i = 0; i < 624; ++i) mt624[i] = ring[(blk * 624 + (uint64_t)i) & (zc::kRingWords - 1)];
+    *index = (int32_t)(use - blk * 624);
+    return ZC_OK;
+}
+
+int zc_c4_search_async(zc_engine *eng, int32_t first, int32_t n, const zc_c4_state *d_roots, int32_t sims, double c,
+                       int32_t bs, int32_t *d_move, int32_t *d_na, zc_game_stats *d_stats, void *hip_stream) {
+    if (!eng || (n && (!d_roots || !d_move || !d_na || !d_stats))) return fail(ZC_EINVAL, "null argument");
+    if (int r = check_search(eng, first, n, sims, c, bs)) return r;
+    if (!n) return ZC_OK;
+    std::lock_guard<std::mutex> lk(eng->mu);
+    ZC_HIP(hipSetDevice(eng->cfg.device));
+    hipStream_t s = hip_stream ? (hipStream_t)hip_stream : eng->stream;
+    zc::launch_c4_search(make_params(eng, first, n, d_roots, sims, c, bs, d_move, d_na, d_stats), s);
+    ZC_HIP(hipGetLastError());
+    return ZC_OK;
+}
+
+int zc_c4_search(zc_engine *eng, int32_t first, int32_t n, const zc_c4_state *roots, int32_t sims, double c,
+                 int32_t bs, int32_t *out_move, int32_t *out_na, zc_game_stats *out_stats) {
+    if (!eng || (n && (!roots || !out_move || !out_na))) return fail(ZC_EINVAL, "null argument");
+    if (int r = check_search(eng, first, n, sims, c, bs)) return r;
+    if (!n) return ZC_OK;
+    std::lock_guard<std::mutex> lk(eng->mu);
+    ZC_HIP(hipSetDevice(eng->cfg.device));
+    zc::Arena &a = eng->a;
+    hipStream_t s = eng->stream;
+    ZC_HIP(hipMemcpyAsync(a.roots, roots, (size_t)n * sizeof(zc_c4_state), hipMemcpyHostToDevice, s));
+    zc::launch_c4_search(make_params(eng, first, n, a.roots, sims, c, bs, a.move, a.na, a.stats), s);
+    ZC_HIP(hipGetLastError());
+    std::vector<zc_game_stats> st((size_t)n);
+    ZC_HIP(hipMemcpyAsync(out_move, a.move, (size_t)n * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    ZC_HIP(hipMemcpyAsync(out_na, a.na, (size_t)n * 7 * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    ZC_HIP(hipMemcpyAsync(st.data(), a.stats, (size_t)n * sizeof(zc_game_stats), hipMemcpyDeviceToHost, s));
+    ZC_HIP(hipStreamSynchronize(s));
+    if (out_stats) memcpy(out_stats, st.data(), st.size() * sizeof(zc_game_stats));
+    for (int32_t i = 0; i < n; ++i) {
+        if (st[i].status == ZC_STATUS_NO_MOVES)
+            return fail(ZC_EINVAL, "game %d: root has no legal move (reference: undefined behaviour)", first + i);
+        if (st[i].status == ZC_STATUS_INTERNAL)
+            return fail(ZC_EDEVICE, "game %d: search invariant violated on the device", first + i);
+        if (st[i].status)
+            return fail(ZC_EINVAL, "game %d: invalid Connect4 state (status %lld)", first + i, (long long)st[i].status);
+    }
+    return ZC_OK;
+}
+
+int zc_c4_play_async(zc_engine *eng, int32_t n, zc_c4_state *d_states, const int32_t *d_moves, int32_t *d_results,
+                     int32_t reset, void *hip_stream) {
+    if (!eng || n < 0 || (n && (!d_states || !d_moves || !d_results))) return fail(ZC_EINVAL, "bad argument");
+    if (!n) return ZC_OK;
+    std::lock_guard<std::mutex> lk(eng->mu);
+    ZC_HIP(hipSetDevice(eng->cfg.device));
+    hipStream_t s = hip_stream ? (hipStream_t)hip_stream : eng->stream;
+    zc::launch_c4_play(n, d_states, d_moves, d_results, reset, s);
+    ZC_HIP(hipGetLastError());
+    return ZC_OK;
+}
+
+int zc_c4_from_rows(const char *rows, int32_t turn, zc_c4_state *out) {
+    if (!rows || !out) return fail(ZC_EINVAL, "null argument");
+    if (turn != 0 && turn != 1) return fail(ZC_EINVAL, "turn must be 0 or 1");
+    zc_c4_state s{};
+    for (int r = 0; r < 6; ++r)
+        for (int c = 0; c < 7; ++c) {
+            const char ch = rows[r * 7 + c];
+            const uint64_t bit = 1ull << (7 * c + (5 - r));
+            if (ch == 'X') s.stones[0] |= bit;
+            else if (ch == 'O') s.stones[1] |= bit;
+        }
+    s.turn = turn;
+    *out = s;
+    return ZC_OK;
+}
+
+int zc_c4_to_rows(const zc_c4_state *s, char *rows) {
+    if (!s || !rows) return fail(ZC_EINVAL, "null argument");
+    for (int r = 0; r < 6; ++r)
+        for (int c = 0; c < 7; ++c) {
+            const uint64_t bit = 1ull << (7 * c + (5 - r));
+            rows[r * 7 + c] = (s->stones[0] & bit) ? 'X' : (s->stones[1] & bit) ? 'O' : ' ';
+        }
+    return ZC_OK;
+}
+
+int zc_c4_legal_order(int32_t mask, int32_t *cols) {
+    if (mask < 0 || mask > 127 || !cols) return fail(ZC_EINVAL, "mask must be in [0, 127]");
+    const uint32_t w = ZC_C4_ORDER_INIT[mask];
+    const int n = (int)((w >> 24) & 15u);
+    for (int k = 0; k < n; ++k) cols[k] = (int32_t)((w >> (3 * k)) & 7u);
+    return n;
+}
+
+int zc_debug_uct(zc_engine *eng, int32_t n, const double *logn, const int32_t *na, const double *q, double c,
+                 double *out) {
+    if (!eng || n < 0) return fail(ZC_EINVAL, "bad argument");
+    if (!n) return ZC_OK;
+    std::lock_guard<std::mutex> lk(eng->mu);
+    ZC_HIP(hipSetDevice(eng->cfg.device));
+    double *dl, *dq, *dout;
+    int32_t *dn;
+    ZC_HIP(hipMalloc(&dl, n * sizeof(double)));
+    ZC_HIP(hipMalloc(&dq, n * sizeof(double)));
+    ZC_HIP(hipMalloc(&dout, n * sizeof(double)));
+    ZC_HIP(hipMalloc(&dn, n * sizeof(int32_t)));
+    hipStream_t s = eng->stream;
+    ZC_HIP(hipMemcpyAsync(dl, logn, n * sizeof(double), hipMemcpyHostToDevice, s));
+    ZC_HIP(hipMemcpyAsync(dq, q, n * sizeof(double), hipMemcpyHostToDevice, s));
+    ZC_HIP(hipMemcpyAsync(dn, na, n * sizeof(int32_t), hipMemcpyHostToDevice, s));
+    zc::launch_uct_debug(n, dl, dn, dq, c, dout, s);
+    ZC_HIP(hipGetLastError());
+    ZC_HIP(hipMemcpyAsync(out, dout, n * sizeof(double), hipMemcpyDeviceToHost, s));
+    ZC_HIP(hipStreamSynchronize(s));
+    (void)hipFree(dl);
+    (void)hipFree(dq);
+    (void)hipFree(dout);
+    (void)hipFree(dn);
+    return ZC_OK;
+}
+
+int zc_debug_c4_rollout(zc_engine *eng, int32_t first, int32_t n, const zc_c4_state *states, int32_t *out_value,
+                        int64_t *out_words) {
+    if (!eng || (n && (!states || !out_value || !out_words))) return fail(ZC_EINVAL, "null argument");
+    if (int r = check_games(eng, first, n)) return r;
+    for (int32_t i = 0; i < n; ++i)
+        if (!valid_c4(states[i])) return fail(ZC_EINVAL, "state %d is not a valid Connect4 position", i);
+    if (!n) return ZC_OK;
+    std::lock_guard<std::mutex> lk(eng->mu);
+    ZC_HIP(hipSetDevice(eng->cfg.device));
+    zc::Arena &a = eng->a;
+    hipStream_t s = eng->stream;
+    int64_t *dw;
+    ZC_HIP(hipMalloc(&dw, n * sizeof(int64_t)));
+    ZC_HIP(hipMemcpyAsync(a.roots, states, (size_t)n * sizeof(zc_c4_state), hipMemcpyHostToDevice, s));
+    zc::launch_c4_rollout_debug(a, eng->M, first, n, a.roots, a.move, dw, s);
+    ZC_HIP(hipGetLastError());
+    ZC_HIP(hipMemcpyAsync(out_value, a.move, (size_t)n * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    ZC_HIP(hipMemcpyAsync(out_words, dw, (size_t)n * sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    ZC_HIP(hipStreamSynchronize(s));
+    (void)hipFree(dw);
+    return ZC_OK;
+}
+
+}  // extern "C"

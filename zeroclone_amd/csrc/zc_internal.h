@@ -1,0 +1,88 @@
+// zc_internal.h — engine state, HBM layout and launch declarations shared by the host
+// API (engine.hip) and the kernels (c4_search.hip).  gfx950 only.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdint>
+#include <mutex>
+#include <string>
+
+#include "../../include/zeroclone.h"
+
+namespace zc {
+
+// ---------------------------------------------------------------- HBM layout (Connect4)
+// One game owns a contiguous arena of M = max_sims + 1 node records.  A record is one
+// 128-byte line — everything selection reads for a node (mcts.cpp:10-39 Node, minus the
+// Python objects) — so the per-level load of the tree walk is one L2 line per game:
+//
+//   +0   u32  N            visit count of this node                   (Node::N)
+//   +4   u32  untried      bits 0..20: 3-bit move indices in order   (Node::untried)
+//                          bits 24..27: #untried, bits 28..31: #moves (Node::moves.size())
+//   +8   u16  parent       0xFFFF at the root                         (Node::parent)
+//   +10  u8   pact         index of this node in parent's moves       (parent_action_idx)
+//   +11  u8   depth        root = 0
+//   +12  u32  order        packed columns of the move list (CPython set order)
+//   +16  u16  child[8]     0xFFFF = null                              (Node::children)
+//   +32  i32  Na[8]                                                    (Node::Na)
+//   +64  f64  Q[8]         Q[a] = W[a]/Na[a]; slot 7 holds log(N) of THIS node
+//                                                                      (Node::Qa)
+// Wa (integer in rollout mode) lives in a separate [game][M][8] i32 array: only backup
+// touches it.  Boards are not stored: the walk re-applies moves from the root.
+constexpr int kRecBytes = 128;
+constexpr int kSlots = 8;
+constexpr int kMaxDepth = 44;          // levels 0..42 (a C4 game has at most 42 plies)
+constexpr int kRingLog2 = 12;          // per-game MT19937 ring: 4096 raw words
+constexpr int kRingWords = 1 << kRingLog2;
+constexpr int kLookahead = 2048;       // words generated ahead at each flush start
+constexpr int kChunk = 224;            // words per generation step (<= 227, multiple of 8)
+constexpr int kGroup = 8;              // lanes cooperating on one game
+constexpr int kBlock = 64;             // threads per workgroup (one wave, 8 games)
+
+static_assert(kLookahead + kChunk + 624 + 16 < kRingWords, "ring must retain the current MT block");
+
+struct Arena {
+    uint8_t *nodes = nullptr;     // [G][M][128 B]
+    int32_t *W = nullptr;         // [G][M][8]
+    uint32_t *path = nullptr;     // [G][B][kMaxDepth]  node | pact<<16
+    uint64_t *pstate = nullptr;   // [G][B][2]          leaf stones
+    uint32_t *pmeta = nullptr;    // [G][B]             leaf node | depth<<16 | turn<<24
+    int32_t *pval = nullptr;      // [G][B]             leaf values
+    uint32_t *ring = nullptr;     // [G][kRingWords]    raw (untempered) MT words
+    uint64_t *rngpos = nullptr;   // [G][2]             {next word to use, words generated}
+    double *logtab = nullptr;     // [M+2]              glibc log(n), n = 0..M+1
+    // staging for the synchronous host entry points
+    zc_c4_state *roots = nullptr;
+    int32_t *move = nullptr;
+    int32_t *na = nullptr;
+    zc_game_stats *stats = nullptr;
+};
+
+struct SearchParams {
+    int first_game, n_games, sims, bs, M;
+    double c;
+    const zc_c4_state *roots;
+    int32_t *out_move, *out_na;
+    zc_game_stats *out_stats;
+    Arena a;
+    int max_batch;
+};
+
+void launch_c4_search(const SearchParams &p, hipStream_t s);
+void launch_c4_rollout_debug(const Arena &a, int M, int first_game, int n, const zc_c4_state *states,
+                             int32_t *out_value, int64_t *out_words, hipStream_t s);
+void launch_c4_play(int n, zc_c4_state *states, const int32_t *moves, int32_t *results, int reset, hipStream_t s);
+void launch_uct_debug(int n, const double *logn, const int32_t *na, const double *q, double c, double *out,
+                      hipStream_t s);
+
+}  // namespace zc
+
+struct zc_engine {
+    zc_engine_config cfg{};
+    int M = 0;
+    hipStream_t stream = nullptr;
+    zc::Arena a;
+    int64_t bytes = 0;
+    std::mutex mu;
+};
