@@ -92,8 +92,11 @@ def main():
     results = torch.zeros(G, dtype=torch.int32, device=dev)
     acc = torch.zeros(4, dtype=torch.int64, device=dev)          # expansions, depth_sum, finished, leaves
 
+    torch_stream = torch.cuda.Stream(dev)   # every launch of the step, and the timing events, on it
+    torch.cuda.set_stream(torch_stream)
+
     def step(ev=None):
-        stream = torch.cuda.current_stream(dev).cuda_stream
+        stream = torch_stream.cuda_stream
         if ev is not None:
             ev[0].record()
         eng.c4_search_async(roots.data_ptr(), G, S, args.c, B, moves.data_ptr(), na.data_ptr(),

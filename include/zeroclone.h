@@ -88,7 +88,7 @@ int zc_c4_search(zc_engine *eng, int32_t first_game, int32_t n_games, const zc_c
                  int32_t sims, double c, int32_t batch_size,
                  int32_t *out_move, int32_t *out_root_na, zc_game_stats *out_stats);
 
-/* Same, with DEVICE pointers, enqueued on `hip_stream` (a hipStream_t; NULL = the engine's
+/* Same, with DEVICE pointers, enqueued on `hip_stream` (a hipStream_t; NULL = the null
  * stream) without synchronising.  Argument validation that needs the roots happens on the
  * device: a bad root sets out_stats[i].status (ZC_STATUS_*). */
 int zc_c4_search_async(zc_engine *eng, int32_t first_game, int32_t n_games, const zc_c4_state *d_roots,
@@ -102,7 +102,7 @@ int zc_c4_search_async(zc_engine *eng, int32_t first_game, int32_t n_games, cons
  *   ZC_C4_ONGOING.
  * A negative move leaves the game untouched (result ZC_C4_ONGOING).  With reset != 0 a
  * finished game restarts from create_init_state() — the self-play refill of
- * scripts/train.py:151-170.  Device pointers, enqueued on hip_stream (NULL = engine's). */
+ * scripts/train.py:151-170.  Device pointers, enqueued on hip_stream (NULL = null stream). */
 int zc_c4_play_async(zc_engine *eng, int32_t n_games, zc_c4_state *d_states, const int32_t *d_moves,
                      int32_t *d_results, int32_t reset, void *hip_stream);
 #define ZC_C4_ONGOING 2
@@ -128,6 +128,12 @@ int zc_debug_uct(zc_engine *eng, int32_t n, const double *logn, const int32_t *n
  * first_game+i's stream: out_value[i] in {-1,0,1}, out_words[i] = words consumed. */
 int zc_debug_c4_rollout(zc_engine *eng, int32_t first_game, int32_t n, const zc_c4_state *states,
                         int32_t *out_value, int64_t *out_words);
+
+/* Diagnostic phase stamps: returns (into out4, may be NULL) the shader-cycle sums since the
+ * previous call of {RNG generation, select+expand, rollouts, backup} over all games, resets
+ * them, and switches the stamped kernel build on (enable != 0) or off for later searches.
+ * Synchronises the device.  Stamped runs are for phase SHARES only, never for timing. */
+int zc_debug_phase_cycles(zc_engine *eng, int32_t enable, int64_t *out4);
 
 #ifdef __cplusplus
 }

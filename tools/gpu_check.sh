@@ -1,0 +1,38 @@
+#!/bin/bash
+# Runs ON THE GPU BOX (via gpurun): stages given as arguments, in order, each under its own
+# time limit; stops at the first stage that faults / aborts / times out (pytest failures,
+# rc=1, still let later stages run so a bench line is recorded).
+#   stages: pytest smoke bench bench8 prof pmc
+set -u
+cd "$(dirname "$0")/.."
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+run() {
+  local name=$1 to=$2; shift 2
+  echo "== $name: $*" >> gpurun_out/steps.log
+  timeout -k 10 "$to" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "== $name rc=$rc" >> gpurun_out/steps.log
+  tail -5 "gpurun_out/$name.log"
+  return $rc
+}
+for st in "$@"; do
+  case $st in
+    pytest) run pytest_gpu 1200 python -m pytest tests -m gpu -x -q -p no:cacheprovider; rc=$?
+            if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi ;;
+    smoke)  run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit $? ;;
+    bench)  run bench 900 python bench.py || exit $? ;;
+    benchq) run benchq 600 python bench.py --steps 3 --warmup 1 --no-cpu-baseline || exit $? ;;
+    prof)   run prof 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv \
+                -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline || exit $? ;;
+    diag)   run diag 600 python tools/diag_c4.py || exit $? ;;
+    pmc)    run pmc 600 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/pmc -o pmc \
+                --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY \
+                -- python3 tools/one_search.py --reps 2 || exit $? ;;
+    hbm)    run hbm_fetch 600 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/hbm -o fetch \
+                --pmc FETCH_SIZE -- python3 tools/one_search.py --reps 2 || exit $?
+            run hbm_write 600 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/hbm -o write \
+                --pmc WRITE_SIZE -- python3 tools/one_search.py --reps 2 || exit $? ;;
+    *) echo "unknown stage $st"; exit 2 ;;
+  esac
+done

@@ -69,6 +69,7 @@ SIGNATURES = [
     ("zc_c4_legal_order", ctypes.c_int, [ctypes.c_int32, P(ctypes.c_int32)]),
     ("zc_debug_uct", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p,
                                     ctypes.c_void_p, ctypes.c_double, ctypes.c_void_p]),
+    ("zc_debug_phase_cycles", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, P(ctypes.c_int64)]),
     ("zc_debug_c4_rollout", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p,
                                            ctypes.c_void_p, ctypes.c_void_p]),
 ]
@@ -214,6 +215,11 @@ class NativeEngine:
         out = np.zeros(len(logn), np.float64)
         check(lib().zc_debug_uct(self._h, len(logn), _ptr(logn), _ptr(na), _ptr(q), float(c), _ptr(out)))
         return out
+
+    def phase_cycles(self, enable: bool):
+        out = (ctypes.c_int64 * 4)()
+        check(lib().zc_debug_phase_cycles(self._h, int(bool(enable)), out))
+        return dict(zip(["rng", "select_expand", "rollout", "backup"], list(out)))
 
     def debug_c4_rollout(self, states: np.ndarray, first_game: int = 0):
         states = np.ascontiguousarray(states, dtype=C4_STATE_DTYPE)

@@ -5,13 +5,21 @@
 // (engine/policy_functions.py:10-12) and Value('random_rollout')
 // (engine/value_functions.py:35-45), for thousands of games per launch.
 //
-// Execution model.  A game is owned by a group of 8 lanes (8 games per wave64, one wave per
-// workgroup); the whole search of a move — every flush of `batch_size` leaves — runs inside
-// one launch, so games never synchronise with each other.  Inside a group all lanes follow
-// the same control flow; the lanes split the per-node work (lane k owns child slot k, tree
-// level l is backed up by lane l % 8, the RNG window holds word wbase+k in lane k) and agree
-// through ballots / shuffles.  Every random number is drawn from the game's own CPython
-// MT19937 stream in the reference's order, so results are bit-identical to the reference.
+// Execution model: ONE GAME PER WAVE.  A game's search is a strictly serial chain (every
+// random number comes from one CPython MT19937 stream, consumed in the reference's order),
+// so the chip is filled with games, not with work from inside one game: 4096 games are
+// 4096 waves, 16 per CU.  Inside a wave all control flow is wave-uniform, the game state
+// (board, stream position, node counter) lives in SGPRs and runs on the scalar unit, and
+// the 64 lanes take the parts that are parallel:
+//   - selection: lane k scores child slot k (UCT in fp64, exactly mcts.cpp:41-45) and a
+//     DPP reduction picks the first maximum;
+//   - RNG: lane k holds word wbase+k of a 64-word window of the stream, so a
+//     random.choice draw (with its rejection loop) is one ballot;
+//   - rollouts: a block of plies is simulated at once, one ply per lane (c4_rollouts);
+//   - backup: lane l updates tree level l of the leaf's path (all levels at once);
+//   - stream refill: the MT recurrence is regenerated 192 words at a time.
+// The whole move (every flush of `batch_size` leaves) runs in one launch; games never
+// synchronise with each other.
 #include <math.h>
 
 #include "c4_order_table.h"
@@ -27,6 +35,50 @@ constexpr uint64_t kBottom = 0x0000040810204081ull;  // bit 7c: bottom cell of c
 constexpr uint64_t kFull = kBottom * 0x3Full;        // the 42 playable cells
 constexpr uint64_t kTop = kBottom << 5;              // top playable cell of each column
 constexpr uint32_t kIdentDigits = 0 | (1u << 3) | (2u << 6) | (3u << 9) | (4u << 12) | (5u << 15) | (6u << 18);
+constexpr int kWin = 64;                             // RNG window: one word per lane
+
+// ------------------------------------------------------------------ wave helpers
+__device__ __forceinline__ uint32_t uni(uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); }
+__device__ __forceinline__ int uni(int x) { return __builtin_amdgcn_readfirstlane(x); }
+__device__ __forceinline__ uint64_t uni64(uint64_t x) {
+    return ((uint64_t)uni((uint32_t)(x >> 32)) << 32) | (uint64_t)uni((uint32_t)x);
+}
+__device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
+
+__device__ __forceinline__ void wave_mem_order() {
+    // Same-wave hand-offs through memory (one lane stores, another loads) are ordered by
+    // program order on gfx950 (wavefront scope needs no cache action); this only stops the
+    // compiler from moving memory operations across the point.
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+}
+
+template <int CTRL>
+__device__ __forceinline__ int dpp(int x) {
+    return __builtin_amdgcn_mov_dpp(x, CTRL, 0xF, 0xF, false);
+}
+template <int CTRL>
+__device__ __forceinline__ double dpp(double x) {
+    const int lo = dpp<CTRL>(__double2loint(x));
+    const int hi = dpp<CTRL>(__double2hiint(x));
+    return __hiloint2double(hi, lo);
+}
+
+// First maximum over lanes 0..7 (ties -> lower slot), as mcts.cpp:55-58 (`v > best_val`,
+// scanning slots in order).  Three DPP steps inside each 8-lane half row: xor 1, xor 2,
+// mirror; afterwards every lane of the half row holds the winner.
+template <class T>
+__device__ __forceinline__ void argmax_step(T &v, int &i, T ov, int oi) {
+    if (ov > v || (ov == v && oi < i)) {
+        v = ov;
+        i = oi;
+    }
+}
+template <class T>
+__device__ __forceinline__ void argmax8(T &v, int &i) {
+    argmax_step(v, i, dpp<0xB1>(v), dpp<0xB1>(i));    // quad_perm [1,0,3,2]
+    argmax_step(v, i, dpp<0x4E>(v), dpp<0x4E>(i));    // quad_perm [2,3,0,1]
+    argmax_step(v, i, dpp<0x141>(v), dpp<0x141>(i));  // row_half_mirror
+}
 
 // ------------------------------------------------------------------ Connect4 bitboards
 __device__ __forceinline__ uint64_t drop_bit(uint64_t occ, int col) {
@@ -57,43 +109,6 @@ __device__ __forceinline__ bool has_four(uint64_t b) {
     return r != 0;
 }
 
-// ------------------------------------------------------------------ group primitives
-__device__ __forceinline__ unsigned group_ballot(bool p, int gbase) {
-    return (unsigned)((__ballot(p) >> gbase) & 0xFFull);
-}
-
-// First maximum over the group (ties -> lower slot), as mcts.cpp:55-58 (`v > best_val`).
-__device__ __forceinline__ void group_argmax(double &v, int &i) {
-#pragma unroll
-    for (int off = 1; off < kGroup; off <<= 1) {
-        const double ov = __shfl_xor(v, off);
-        const int oi = __shfl_xor(i, off);
-        if (ov > v || (ov == v && oi < i)) {
-            v = ov;
-            i = oi;
-        }
-    }
-}
-
-__device__ __forceinline__ void group_argmax_int(int &v, int &i) {
-#pragma unroll
-    for (int off = 1; off < kGroup; off <<= 1) {
-        const int ov = __shfl_xor(v, off);
-        const int oi = __shfl_xor(i, off);
-        if (ov > v || (ov == v && oi < i)) {
-            v = ov;
-            i = oi;
-        }
-    }
-}
-
-__device__ __forceinline__ void wave_mem_order() {
-    // Same-wave hand-offs through memory (one lane stores, another loads) are ordered by
-    // program order on gfx950 (wavefront scope needs no cache action); this only stops the
-    // compiler from moving memory operations across the point.
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-}
-
 // ------------------------------------------------------------------ CPython MT19937
 __device__ __forceinline__ uint32_t temper(uint32_t y) {
     y ^= y >> 11;
@@ -105,21 +120,23 @@ __device__ __forceinline__ uint32_t temper(uint32_t y) {
 
 // The game's stream lives in a ring of RAW MT words x[p] (absolute position p, slot
 // p % kRingWords).  The recurrence x[p] = x[p-227] ^ twist(x[p-624], x[p-623]) regenerates
-// it 224 words at a time, all lanes in parallel (every input is >= 227 words older).
+// it kChunk words at a time, all lanes in parallel (every input is >= 227 words older).
 struct Rng {
     uint32_t *ring;
-    uint64_t use;    // next word to consume
-    uint64_t gen;    // words generated so far
-    uint64_t wbase;  // window start (multiple of 8); use in [wbase, wbase + 8]
-    uint32_t wt;     // tempered x[wbase + sub]
-    uint32_t wn;     // tempered x[wbase + 8 + sub]
+    uint64_t gen;    // words generated so far                              (uniform)
+    uint64_t wbase;  // window start, a multiple of 64                      (uniform)
+    uint32_t off;    // next word to consume = wbase + off, off in [0, 64]   (uniform)
+    uint32_t wt;     // tempered x[wbase + lane]
+    uint32_t wn;     // raw x[wbase + 64 + lane], in flight until the window advances
+    __device__ __forceinline__ uint64_t use() const { return wbase + off; }
 };
 
-__device__ __noinline__ uint64_t rng_generate(uint32_t *ring, uint64_t gen, uint64_t target, int sub) {
+__device__ __forceinline__ uint64_t rng_generate(uint32_t *ring, uint64_t gen, uint64_t target) {
+    const uint32_t lane = lane_id();
     while (gen < target) {
-#pragma unroll 4
-        for (int i = sub; i < kChunk; i += kGroup) {
-            const uint64_t p = gen + (uint64_t)i;
+#pragma unroll
+        for (int k = 0; k < kChunk / 64; ++k) {
+            const uint64_t p = gen + lane + 64u * k;
             const uint32_t a = ring[(p - 624) & kRingMask];
             const uint32_t b = ring[(p - 623) & kRingMask];
             const uint32_t m = ring[(p - 227) & kRingMask];
@@ -132,74 +149,168 @@ __device__ __noinline__ uint64_t rng_generate(uint32_t *ring, uint64_t gen, uint
     return gen;
 }
 
-__device__ __forceinline__ void rng_fill(Rng &r, uint64_t target, int sub) {
-    if (r.gen < target) r.gen = rng_generate(r.ring, r.gen, target, sub);
+__device__ __forceinline__ void rng_fill(Rng &r, uint64_t target) {
+    if (r.gen < target) r.gen = rng_generate(r.ring, r.gen, target);
 }
 
-__device__ __forceinline__ void rng_open(Rng &r, uint32_t *ring, uint64_t use, uint64_t gen, int sub) {
+__device__ __forceinline__ void rng_open(Rng &r, uint32_t *ring, uint64_t use, uint64_t gen) {
     r.ring = ring;
-    r.use = use;
     r.gen = gen;
-    r.wbase = use & ~7ull;
-    rng_fill(r, r.wbase + 16, sub);
-    r.wt = temper(r.ring[(r.wbase + sub) & kRingMask]);
-    r.wn = temper(r.ring[(r.wbase + 8 + sub) & kRingMask]);
+    r.wbase = use & ~(uint64_t)(kWin - 1);
+    r.off = (uint32_t)(use - r.wbase);
+    rng_fill(r, r.wbase + 2 * kWin);
+    r.wt = temper(r.ring[(r.wbase + lane_id()) & kRingMask]);
+    r.wn = r.ring[(r.wbase + kWin + lane_id()) & kRingMask];
+}
+
+__device__ __forceinline__ void rng_advance(Rng &r) {
+    r.wbase += kWin;
+    r.off = 0;
+    r.wt = temper(r.wn);
+    if (r.gen < r.wbase + 2 * kWin) rng_fill(r, r.wbase + 2 * kWin);
+    r.wn = r.ring[(r.wbase + kWin + lane_id()) & kRingMask];
 }
 
 // random._randbelow_with_getrandbits(n), 1 <= n <= 7: k = n.bit_length(); draw
-// getrandbits(k) = word >> (32-k) until < n.  The 8 window words are tested at once; the
+// getrandbits(k) = word >> (32-k) until < n.  All window words are tested at once; the
 // first accepted one (in stream order) is the draw, and everything before it is consumed.
-__device__ __forceinline__ uint32_t rng_below(Rng &r, uint32_t n, int sub, int gbase) {
-    const int sh = __clz(n);
+__device__ __forceinline__ uint32_t rng_below(Rng &r, uint32_t n) {
+    const uint32_t sh = (uint32_t)__clz(n);
+    const uint32_t lane = lane_id();
     for (;;) {
-        if (r.use >= r.wbase + 8) {
-            r.wbase += 8;
-            r.wt = r.wn;
-            if (r.gen < r.wbase + 16) rng_fill(r, r.wbase + 16, sub);
-            r.wn = temper(r.ring[(r.wbase + 8 + sub) & kRingMask]);
-        }
+        if (r.off >= (uint32_t)kWin) rng_advance(r);
         const uint32_t v = r.wt >> sh;
-        const unsigned off = (unsigned)(r.use - r.wbase);
-        const unsigned bal = group_ballot(((unsigned)sub >= off) && (v < n), gbase);
+        const uint64_t bal = __ballot(lane >= r.off && v < n);
         if (bal) {
-            const int f = __ffs(bal) - 1;
-            r.use = r.wbase + (uint64_t)f + 1;
-            return (uint32_t)__shfl((int)v, gbase + f);
+            const int f = __builtin_ctzll(bal);
+            r.off = (uint32_t)f + 1;
+            return (uint32_t)__builtin_amdgcn_readlane((int)v, f);
         }
-        r.use = r.wbase + 8;
+        r.off = kWin;
     }
 }
 
-// ------------------------------------------------------------------ random rollout
-// Value.random_rollout (value_functions.py:35-45) from the side to move `turn`:
+// ------------------------------------------------------------------ random rollouts
+// A pending leaf, kept in LDS between the phases of a flush.
+struct Leaf {
+    uint64_t p0, p1;  // stones of 'X' / 'O'
+    uint32_t meta;    // node | depth << 16 | turn << 24
+    int32_t val;      // rollout value from the leaf's side to move
+};
+
+__device__ __forceinline__ uint64_t readlane64(uint64_t x, int l) {
+    return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(x >> 32), l) << 32) |
+           (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)x, l);
+}
+
+__device__ __forceinline__ uint32_t mbcnt(uint64_t m) {  // set bits of m in lanes below this one
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+// Inclusive prefix OR over the 64 lanes (DPP: row_shr 1,2,4,8, then row_bcast 15 / 31).
+__device__ __forceinline__ uint32_t scan_or32(uint32_t x) {
+    x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, false);
+    x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, false);
+    x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, false);
+    x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, false);
+    x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false);
+    x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false);
+    return x;
+}
+__device__ __forceinline__ uint64_t scan_or(uint64_t x) {
+    return ((uint64_t)scan_or32((uint32_t)(x >> 32)) << 32) | (uint64_t)scan_or32((uint32_t)x);
+}
+
+// Value.random_rollout (value_functions.py:35-45) for the nb pending leaves of one flush, in
+// pending order (value.batch: mcts.cpp:118).  Per leaf, from the side to move `turn`:
 //   while not check_win(s) and not check_draw(s): s = play(s, choice(list(legal(s))))
 //   win -> -1 if the side to move at the end (the loser) is the leaf's side to move, else +1
 // check_win looks at the LAST mover only (c4_backend.py:27, tokens[1 - turn]).
-__device__ int c4_rollout(uint64_t p0, uint64_t p1, int turn, Rng &rng, const uint32_t *s_order, int sub,
-                          int gbase, int64_t &plies) {
-    uint64_t me = turn ? p1 : p0;   // side to move
-    uint64_t op = turn ? p0 : p1;   // last mover
-    uint64_t occ = me | op;
-    int mask = legal_mask(occ);
-    uint32_t ow = s_order[mask];
-    int parity = 0;
-    for (;;) {
-        if (has_four(op)) return parity ? 1 : -1;
-        if (occ == kFull) return 0;
-        const uint32_t r = rng_below(rng, (ow >> 24) & 15u, sub, gbase);
-        const int col = (int)((ow >> (3 * r)) & 7u);
-        const uint64_t bit = drop_bit(occ, col);
-        if (!bit) return 0;  // unreachable for valid states; guarantees termination
-        const uint64_t moved = me | bit;
-        me = op;
-        op = moved;
-        occ |= bit;
-        parity ^= 1;
-        ++plies;
-        if (bit & kTop) {  // column just filled: the legal set (and its order) changes
-            mask &= ~(1 << col);
-            ow = s_order[mask];
+//
+// Plies are simulated a BLOCK at a time.  While the legal set is unchanged (no column has
+// filled), the draws are exactly the window words w with (w >> (32-k)) < n, in stream
+// order — so one ballot yields the moves of every ply the window covers.  Lane k (an
+// accepted word) is ply q_k = #accepted lanes below it; its stone's row is the column
+// height plus #earlier accepted lanes in the same column; prefix-OR scans over the lanes
+// build each player's stones after every ply, and every lane tests check_win / full board
+// / column filled for ITS ply.  The first lane with an event ends the block (a fill changes
+// the legal set, so the next block restarts from the following word).
+__device__ void c4_rollouts(Leaf *L, int nb, Rng &rng, int64_t &plies_total) {
+    const uint32_t lane = lane_id();
+    for (int j = 0; j < nb; ++j) {
+        const uint64_t x0 = uni64(L[j].p0);
+        const uint64_t x1 = uni64(L[j].p1);
+        const int tn = (int)(uni(L[j].meta) >> 24);
+        uint64_t me = tn ? x1 : x0;  // side to move
+        uint64_t op = tn ? x0 : x1;  // last mover
+        int val = 0;
+        int q = 0;  // plies played in this rollout
+        if (has_four(op)) {
+            val = -1;
+        } else if ((me | op) != kFull) {
+            int mask = legal_mask(me | op);
+            uint32_t ow = d_order[mask];
+            uint32_t n = (ow >> 24) & 15u;
+            int stones = __popcll(me | op);
+            for (;;) {
+                if (rng.off >= (uint32_t)kWin) rng_advance(rng);
+                const uint32_t v = rng.wt >> __clz(n);
+                const bool acc = lane >= rng.off && v < n;
+                const uint64_t A = __ballot(acc);
+                if (!A) {
+                    rng.off = kWin;
+                    continue;
+                }
+                const uint32_t qk = mbcnt(A);                    // this lane's ply in the block
+                const uint32_t col = (ow >> (3 * (v & 7u))) & 7u;  // its column (if accepted)
+                uint32_t same = 0;                               // earlier plies in that column
+#pragma unroll
+                for (uint32_t c = 0; c < 7; ++c) {
+                    const uint64_t Mc = __ballot(acc && col == c);
+                    same = (col == c) ? mbcnt(Mc) : same;
+                }
+                const uint64_t occ = me | op;
+                const uint32_t h0 = (uint32_t)__popcll((occ >> (7 * col)) & 0x3Full);
+                const uint32_t row = min(h0 + same, 6u);
+                const uint64_t bit = acc ? (1ull << (7 * col + row)) : 0ull;
+                const bool even = (qk & 1u) == 0;
+                const uint64_t E = scan_or(even ? bit : 0ull);  // stones of the block's first mover
+                const uint64_t O = scan_or(even ? 0ull : bit);  // stones of the other side
+                const bool win = has_four(even ? (me | E) : (op | O));
+                const bool full = stones + (int)qk + 1 == 42;
+                const uint64_t W = __ballot(acc && win);
+                const uint64_t EV = W | __ballot(acc && (full || row == 5));
+                const int kend = EV ? __builtin_ctzll(EV) : 63 - __builtin_clzll(A);
+                const int np = __builtin_amdgcn_readlane((int)qk, kend) + 1;  // plies in this block
+                const uint64_t a2 = me | readlane64(E, kend);
+                const uint64_t b2 = op | readlane64(O, kend);
+                if (np & 1) {
+                    me = b2;
+                    op = a2;
+                } else {
+                    me = a2;
+                    op = b2;
+                }
+                q += np;
+                stones += np;
+                rng.off = EV ? (uint32_t)kend + 1 : (uint32_t)kWin;
+                if (!EV) continue;
+                if ((W >> kend) & 1ull) {  // the ply's mover completed four
+                    val = (q & 1) ? 1 : -1;
+                    break;
+                }
+                if (stones >= 42) {  // check_draw: board full
+                    val = 0;
+                    break;
+                }
+                // a column filled: the legal set (and its CPython order) changes
+                mask &= ~(1 << __builtin_amdgcn_readlane((int)col, kend));
+                ow = d_order[mask];
+                n = (ow >> 24) & 15u;
+            }
         }
+        if (lane == 0) L[j].val = val;
+        plies_total += q;
     }
 }
 
@@ -216,21 +327,24 @@ struct Tree {
 };
 
 // Node(state, legal_moves, parent, idx) (mcts.cpp:23-34): all moves untried, in list order.
-__device__ __forceinline__ void node_init(const Tree &t, int nd, int parent, int pact, int depth, uint32_t ow,
-                                          int sub) {
+// Lanes 0..7 write slot `lane`; lane 0 writes the header.
+__device__ __forceinline__ void node_init(const Tree &t, int nd, int parent, int pact, int depth, uint32_t ow) {
+    const uint32_t lane = lane_id();
     const uint32_t n = (ow >> 24) & 15u;
-    if (sub == 0) {
+    if (lane == 0) {
         uint4 h;
-        h.x = 0;                                                         // N
+        h.x = 0;                                                                 // N
         h.y = (kIdentDigits & ((1u << (3 * n)) - 1u)) | (n << 24) | (n << 28);  // untried, #moves
         h.z = (uint32_t)(parent & 0xFFFF) | ((uint32_t)(pact & 0xFF) << 16) | ((uint32_t)depth << 24);
         h.w = ow;
         *(uint4 *)t.rec(nd) = h;
     }
-    t.child(nd)[sub] = 0xFFFF;
-    t.na(nd)[sub] = 0;
-    t.q(nd)[sub] = (sub == 7) ? -INFINITY : 0.0;  // slot 7 = log(N) = log(0)
-    t.w(nd)[sub] = 0;
+    if (lane < kSlots) {
+        t.child(nd)[lane] = 0xFFFF;
+        t.na(nd)[lane] = 0;
+        t.q(nd)[lane] = (lane == 7) ? -INFINITY : 0.0;  // slot 7 = log(N) = log(0)
+        t.w(nd)[lane] = 0;
+    }
 }
 
 __device__ __forceinline__ bool valid_state(uint64_t p0, uint64_t p1, int turn) {
@@ -245,98 +359,100 @@ __device__ __forceinline__ bool valid_state(uint64_t p0, uint64_t p1, int turn) 
 }
 
 // ------------------------------------------------------------------ the search kernel
+// STAMP = diagnostic build: lane 0 adds s_memtime deltas per phase into p.a.phase[g][0..3] =
+// {rng generation at flush start, select+expand, rollouts, backup}.
+template <bool STAMP>
 __global__ __launch_bounds__(kBlock) void c4_search_kernel(SearchParams p) {
-    __shared__ uint32_t s_order[128];
-    for (int i = threadIdx.x; i < 128; i += kBlock) s_order[i] = d_order[i];
-    __syncthreads();
+    extern __shared__ __attribute__((aligned(16))) uint8_t s_dyn[];
+    Leaf *const leaves = (Leaf *)s_dyn;                                   // [bs]
+    uint32_t *const paths = (uint32_t *)(s_dyn + sizeof(Leaf) * (size_t)p.bs);  // [bs][kMaxDepth]
 
-    const int lane = threadIdx.x & 63;
-    const int sub = lane & (kGroup - 1);
-    const int gbase = lane & ~(kGroup - 1);
-    const int gl = blockIdx.x * (kBlock / kGroup) + (threadIdx.x / kGroup);  // game within call
-    if (gl >= p.n_games) return;                                            // whole group leaves
-    const int g = p.first_game + gl;                                          // engine game
+    const uint32_t lane = lane_id();
+    const int gl = blockIdx.x;  // game within this call (one wave per game)
+    if (gl >= p.n_games) return;
+    const int g = p.first_game + gl;
 
     const zc_c4_state root = p.roots[gl];
-    const uint64_t rp0 = root.stones[0], rp1 = root.stones[1];
-    const int rturn = root.turn;
+    const uint64_t rp0 = uni64(root.stones[0]), rp1 = uni64(root.stones[1]);
+    const int rturn = uni(root.turn);
     zc_game_stats st{};
     if (!valid_state(rp0, rp1, rturn) || legal_mask(rp0 | rp1) == 0) {
-        if (sub == 0) {
+        if (lane == 0) {
             st.status = valid_state(rp0, rp1, rturn) ? ZC_STATUS_NO_MOVES : ZC_STATUS_BAD_STATE;
             p.out_stats[gl] = st;
             p.out_move[gl] = -1;
         }
-        if (sub < 7) p.out_na[(size_t)gl * 7 + sub] = 0;
+        if (lane < 7) p.out_na[(size_t)gl * 7 + lane] = 0;
         return;
     }
 
     const Arena &a = p.a;
-    Tree t{a.nodes + (size_t)g * p.M * kRecBytes, a.W + (size_t)g * p.M * kSlots};
-    uint32_t *const path0 = a.path + (size_t)g * p.max_batch * kMaxDepth;
-    uint64_t *const pstate = a.pstate + (size_t)g * p.max_batch * 2;
-    uint32_t *const pmeta = a.pmeta + (size_t)g * p.max_batch;
-    int32_t *const pval = a.pval + (size_t)g * p.max_batch;
+    const Tree t{a.nodes + (size_t)g * p.M * kRecBytes, a.W + (size_t)g * p.M * kSlots};
 
     Rng rng;
-    const uint64_t use0 = a.rngpos[2 * (size_t)g];
-    rng_open(rng, a.ring + (size_t)g * kRingWords, use0, a.rngpos[2 * (size_t)g + 1], sub);
+    const uint64_t use0 = uni64(a.rngpos[2 * (size_t)g]);
+    rng_open(rng, a.ring + (size_t)g * kRingWords, use0, uni64(a.rngpos[2 * (size_t)g + 1]));
 
-    node_init(t, 0, 0xFFFF, 0xFF, 0, s_order[legal_mask(rp0 | rp1)], sub);
+    node_init(t, 0, 0xFFFF, 0xFF, 0, d_order[legal_mask(rp0 | rp1)]);
     int nnodes = 1;
     int64_t plies = 0;
     wave_mem_order();
 
+    uint64_t ph[4] = {0, 0, 0, 0};
+    uint64_t tstamp = STAMP ? __builtin_amdgcn_s_memtime() : 0;
+#define ZC_STAMP(k)                                          \
+    if (STAMP) {                                             \
+        const uint64_t now_ = __builtin_amdgcn_s_memtime();  \
+        ph[k] += now_ - tstamp;                              \
+        tstamp = now_;                                       \
+    }
     for (int done = 0; done < p.sims;) {
         const int nb = min(p.bs, p.sims - done);
-        rng_fill(rng, rng.use + kLookahead, sub);
+        rng_fill(rng, rng.use() + kLookahead);
+        ZC_STAMP(0)
 
         // ---- selection + expansion of nb leaves (mcts.cpp:129-147) -------------------------
         // Within a flush no backup happens, so UCT scores on the path above the node that
         // was just expanded cannot change: leaf j+1's walk resumes there (exactly the walk
-        // the reference repeats from the root).
+        // the reference repeats from the root).  Lane l holds level l of the current path.
         int xnode = 0, xdepth = 0, xturn = rturn;
         uint64_t x0 = rp0, x1 = rp1;
+        uint32_t pathv = (lane == 0) ? 0x00FF0000u : 0u;
         for (int j = 0; j < nb; ++j) {
-            uint32_t *const pj = path0 + (size_t)j * kMaxDepth;
             int node = xnode, depth = xdepth, turn = xturn;
             uint64_t b0 = x0, b1 = x1;
-            if (j == 0) {
-                if (sub == 0) pj[0] = 0x00FF0000u;
-            } else {
-                const uint32_t *pp = pj - kMaxDepth;
-                for (int l = sub; l <= depth; l += kGroup) pj[l] = pp[l];
-            }
             uint32_t u, ow;
             for (;;) {  // select (mcts.cpp:47-63)
-                const uint32_t *h = t.hdr(node);
-                u = h[1];
-                ow = h[3];
+                const uint8_t *R = t.rec(node);
+                const uint32_t k = lane & 7u;
+                const uint4 h = *(const uint4 *)R;
+                const uint16_t ch = ((const uint16_t *)(R + 16))[k];
+                const int32_t na = ((const int32_t *)(R + 32))[k];
+                const double q = ((const double *)(R + 64))[k];
+                const double lg = ((const double *)(R + 64))[7];
+                u = uni(h.y);
+                ow = uni(h.w);
                 if ((u >> 24) & 15u) break;  // untried moves left: expand here
                 if (depth >= kMaxDepth - 2) {  // unreachable (a C4 tree is <= 42 deep); never spin
                     st.status = ZC_STATUS_INTERNAL;
                     u = 0;
                     break;
                 }
-                const int nm = (int)(u >> 28);
-                const uint16_t ch = t.child(node)[sub];
-                const int32_t na = t.na(node)[sub];
-                const double q = t.q(node)[sub];
-                const double lg = t.q(node)[7];
+                const uint32_t nm = u >> 28;
                 // UCT (mcts.cpp:41-45) = fma(c, sqrt(log(N)/Na), Qa); unvisited -> +inf
-                double v = (sub < nm && ch != 0xFFFF)
-                               ? (na == 0 ? INFINITY : fma(p.c, sqrt(lg / (double)na), q))
-                               : -INFINITY;
-                int bi = sub;
-                group_argmax(v, bi);
-                if (v == -INFINITY) break;  // no child at all: terminal node is its own leaf
-                const int nxt = __shfl((int)ch, gbase + bi);
-                const uint64_t bit = drop_bit(b0 | b1, (int)((ow >> (3 * bi)) & 7u));
+                double v = (k < nm && ch != 0xFFFF) ? (na == 0 ? INFINITY : fma(p.c, sqrt(lg / (double)na), q))
+                                                    : -INFINITY;
+                int bi = (int)k;
+                argmax8(v, bi);
+                const int best = uni(bi);
+                if ((__ballot(v == -INFINITY) & 1ull) != 0) break;  // no child: terminal node is its own leaf
+                const int nxt = __builtin_amdgcn_readlane((int)ch, best);
+                const uint64_t bit = drop_bit(b0 | b1, (int)((ow >> (3 * best)) & 7u));
                 if (turn) b1 |= bit; else b0 |= bit;
                 turn ^= 1;
                 node = nxt;
                 ++depth;
-                if (sub == (depth & (kGroup - 1))) pj[depth] = (uint32_t)node | ((uint32_t)bi << 16);
+                if (lane == (uint32_t)depth) pathv = (uint32_t)node | ((uint32_t)best << 16);
             }
             // the walk ends here; leaf j+1 resumes from this node
             xnode = node;
@@ -347,57 +463,55 @@ __global__ __launch_bounds__(kBlock) void c4_search_kernel(SearchParams p) {
             int leaf = node;
             const uint32_t cnt = (u >> 24) & 15u;
             if (cnt) {  // expand (mcts.cpp:65-78): policy = random.choice(untried)
-                const uint32_t r = rng_below(rng, cnt, sub, gbase);
+                const uint32_t r = rng_below(rng, cnt);
                 const uint32_t digits = u & 0x1FFFFFu;
                 const int mi = (int)((digits >> (3 * r)) & 7u);
                 const uint32_t low = (1u << (3 * r)) - 1u;
                 const uint32_t rest = (digits & low) | ((digits >> 3) & ~low & 0x1FFFFFu);
-                if (sub == 0) t.hdr(node)[1] = rest | ((cnt - 1u) << 24) | (u & 0xF0000000u);
+                if (lane == 0) t.hdr(node)[1] = rest | ((cnt - 1u) << 24) | (u & 0xF0000000u);
                 const uint64_t bit = drop_bit(b0 | b1, (int)((ow >> (3 * mi)) & 7u));
                 if (turn) b1 |= bit; else b0 |= bit;
                 turn ^= 1;
                 leaf = nnodes++;
                 ++depth;
-                node_init(t, leaf, node, mi, depth, s_order[legal_mask(b0 | b1)], sub);
-                if (sub == mi) t.child(node)[mi] = (uint16_t)leaf;
-                if (sub == (depth & (kGroup - 1))) pj[depth] = (uint32_t)leaf | ((uint32_t)mi << 16);
+                node_init(t, leaf, node, mi, depth, d_order[legal_mask(b0 | b1)]);
+                if (lane == (uint32_t)mi) t.child(node)[mi] = (uint16_t)leaf;
+                if (lane == (uint32_t)depth) pathv = (uint32_t)leaf | ((uint32_t)mi << 16);
                 st.expansions += 1;
                 st.depth_sum += depth;
             }
-            if (sub == 0) {
-                pstate[2 * j] = b0;
-                pstate[2 * j + 1] = b1;
-                pmeta[j] = (uint32_t)leaf | ((uint32_t)depth << 16) | ((uint32_t)turn << 24);
+            if (lane == 0) {
+                leaves[j].p0 = b0;
+                leaves[j].p1 = b1;
+                leaves[j].meta = (uint32_t)leaf | ((uint32_t)depth << 16) | ((uint32_t)turn << 24);
             }
+            if (lane < (uint32_t)kMaxDepth) paths[j * kMaxDepth + lane] = pathv;
             wave_mem_order();
         }
+        ZC_STAMP(1)
 
         // ---- value.batch: random rollouts in pending order (mcts.cpp:112-124) ---------------
-        for (int j = 0; j < nb; ++j) {
-            const uint32_t meta = pmeta[j];
-            const int v = c4_rollout(pstate[2 * j], pstate[2 * j + 1], (int)(meta >> 24), rng, s_order, sub, gbase,
-                                     plies);
-            if (sub == 0) pval[j] = v;
-        }
+        c4_rollouts(leaves, nb, rng, plies);
         wave_mem_order();
+        ZC_STAMP(2)
 
         // ---- backprop in pending order (mcts.cpp:80-100, :124-125) --------------------------
-        // Level l of every path is handled by lane l % 8; a node's level never changes, so
-        // every read-modify-write of a given word stays in one lane, in leaf order.
+        // Lane l updates level l of the leaf's path.  A node's level never changes, so every
+        // read-modify-write of a given word stays in one lane, in leaf order.
         for (int j = 0; j < nb; ++j) {
-            const uint32_t *pj = path0 + (size_t)j * kMaxDepth;
-            const int d = (int)((pmeta[j] >> 16) & 0xFFu);
-            const int v = pval[j];
-            for (int l = sub; l <= d; l += kGroup) {
-                const uint32_t e = pj[l];
+            const uint32_t meta = uni(leaves[j].meta);
+            const int d = (int)((meta >> 16) & 0xFFu);
+            const int v = uni(leaves[j].val);
+            if (lane <= (uint32_t)d) {
+                const uint32_t e = paths[j * kMaxDepth + lane];
                 const int nd = (int)(e & 0xFFFFu);
-                const int vl = ((d - l) & 1) ? -v : v;
+                const int vl = ((d - (int)lane) & 1) ? -v : v;
                 uint32_t *h = t.hdr(nd);
                 const uint32_t n1 = h[0] + 1u;
                 h[0] = n1;
                 t.q(nd)[7] = a.logtab[n1];
-                if (l > 0) {
-                    const int par = (int)(pj[l - 1] & 0xFFFFu);
+                if (lane > 0) {
+                    const int par = (int)(paths[j * kMaxDepth + lane - 1] & 0xFFFFu);
                     const int act = (int)(e >> 16);
                     const int32_t na1 = t.na(par)[act] + 1;
                     const int32_t w1 = t.w(par)[act] - vl;  // Wa -= result
@@ -408,56 +522,65 @@ __global__ __launch_bounds__(kBlock) void c4_search_kernel(SearchParams p) {
             }
             wave_mem_order();
         }
+        ZC_STAMP(3)
         st.leaves += nb;
         done += nb;
     }
+#undef ZC_STAMP
+    if (STAMP && lane == 0)
+        for (int k = 0; k < 4; ++k) a.phase[4 * (size_t)g + k] += (int64_t)ph[k];
 
     // ---- best move: first max of child N over the root's move list (mcts.cpp:150-157) ----
-    const uint32_t u = t.hdr(0)[1];
-    const uint32_t ow = t.hdr(0)[3];
-    const int nm = (int)(u >> 28);
-    const int na = (sub < nm) ? t.na(0)[sub] : -1;
-    int bv = na, bi = sub;
-    group_argmax_int(bv, bi);
-    int pos = 0;
-    bool found = false;
-    for (int k = 0; k < nm; ++k)
-        if ((int)((ow >> (3 * k)) & 7u) == sub) { pos = k; found = true; }
-    const int na_col = __shfl(na, gbase + pos);
-    if (sub < 7) p.out_na[(size_t)gl * 7 + sub] = found ? na_col : 0;
-    if (sub == 0) {
-        p.out_move[gl] = (int)((ow >> (3 * bi)) & 7u);
+    const uint32_t u = uni(t.hdr(0)[1]);
+    const uint32_t ow = uni(t.hdr(0)[3]);
+    const uint32_t nm = u >> 28;
+    const uint32_t k = lane & 7u;
+    int bv = (k < nm) ? t.na(0)[k] : -1;
+    int bi = (int)k;
+    argmax8(bv, bi);
+    const int best = uni(bi);
+    if (lane < 7) {  // visits per column
+        int pos = -1;
+        for (uint32_t s = 0; s < nm; ++s)
+            if (((ow >> (3 * s)) & 7u) == lane) pos = (int)s;
+        p.out_na[(size_t)gl * 7 + lane] = pos >= 0 ? t.na(0)[pos] : 0;
+    }
+    if (lane == 0) {
+        p.out_move[gl] = (int)((ow >> (3 * best)) & 7u);
         st.rollout_plies = plies;
-        st.rng_words = (int64_t)(rng.use - use0);
+        st.rng_words = (int64_t)(rng.use() - use0);
         p.out_stats[gl] = st;
-        a.rngpos[2 * (size_t)g] = rng.use;
+        a.rngpos[2 * (size_t)g] = rng.use();
         a.rngpos[2 * (size_t)g + 1] = rng.gen;
     }
 }
 
-// ------------------------------------------------------------------ self-test kernels
+// ------------------------------------------------------------------ small kernels
 __global__ __launch_bounds__(kBlock) void c4_rollout_debug_kernel(Arena a, int first_game, int n,
                                                                   const zc_c4_state *states, int32_t *out_value,
                                                                   int64_t *out_words) {
-    __shared__ uint32_t s_order[128];
-    for (int i = threadIdx.x; i < 128; i += kBlock) s_order[i] = d_order[i];
-    __syncthreads();
-    const int lane = threadIdx.x & 63;
-    const int sub = lane & (kGroup - 1);
-    const int gbase = lane & ~(kGroup - 1);
-    const int gl = blockIdx.x * (kBlock / kGroup) + (threadIdx.x / kGroup);
+    __shared__ Leaf s_leaf[1];
+    const uint32_t lane = lane_id();
+    const int gl = blockIdx.x;
     if (gl >= n) return;
     const int g = first_game + gl;
     Rng rng;
-    const uint64_t use0 = a.rngpos[2 * (size_t)g];
-    rng_open(rng, a.ring + (size_t)g * kRingWords, use0, a.rngpos[2 * (size_t)g + 1], sub);
+    const uint64_t use0 = uni64(a.rngpos[2 * (size_t)g]);
+    rng_open(rng, a.ring + (size_t)g * kRingWords, use0, uni64(a.rngpos[2 * (size_t)g + 1]));
     const zc_c4_state s = states[gl];
+    if (lane == 0) {
+        s_leaf[0].p0 = s.stones[0];
+        s_leaf[0].p1 = s.stones[1];
+        s_leaf[0].meta = (uint32_t)s.turn << 24;
+    }
+    wave_mem_order();
     int64_t plies = 0;
-    const int v = c4_rollout(s.stones[0], s.stones[1], s.turn, rng, s_order, sub, gbase, plies);
-    if (sub == 0) {
-        out_value[gl] = v;
-        out_words[gl] = (int64_t)(rng.use - use0);
-        a.rngpos[2 * (size_t)g] = rng.use;
+    c4_rollouts(s_leaf, 1, rng, plies);
+    wave_mem_order();
+    if (lane == 0) {
+        out_value[gl] = s_leaf[0].val;
+        out_words[gl] = (int64_t)(rng.use() - use0);
+        a.rngpos[2 * (size_t)g] = rng.use();
         a.rngpos[2 * (size_t)g + 1] = rng.gen;
     }
 }
@@ -475,7 +598,7 @@ __global__ void c4_play_kernel(int n, zc_c4_state *states, const int32_t *moves,
     s.stones[turn] |= drop_bit(s.stones[0] | s.stones[1], col);
     s.turn = turn ^ 1;
     int r = ZC_C4_ONGOING;
-    if (has_four(s.stones[turn])) r = s.turn * 2 - 1;   // check_win: the side that just moved
+    if (has_four(s.stones[turn])) r = s.turn * 2 - 1;  // Engine._evaluate: check_win -> turn*2-1
     else if ((s.stones[0] | s.stones[1]) == kFull) r = 0;
     if (reset && r != ZC_C4_ONGOING) s = zc_c4_state{{0, 0}, 0, 0};
     states[i] = s;
@@ -491,18 +614,21 @@ __global__ void uct_debug_kernel(int n, const double *logn, const int32_t *na, c
 
 }  // namespace
 
+size_t c4_search_lds_bytes(int bs) { return (sizeof(Leaf) + sizeof(uint32_t) * kMaxDepth) * (size_t)bs; }
+
 void launch_c4_search(const SearchParams &p, hipStream_t s) {
-    const int per_block = kBlock / kGroup;
-    const int blocks = (p.n_games + per_block - 1) / per_block;
-    hipLaunchKernelGGL(c4_search_kernel, dim3(blocks), dim3(kBlock), 0, s, p);
+    const size_t lds = c4_search_lds_bytes(p.bs);
+    if (p.stamp)
+        hipLaunchKernelGGL(c4_search_kernel<true>, dim3(p.n_games), dim3(kBlock), lds, s, p);
+    else
+        hipLaunchKernelGGL(c4_search_kernel<false>, dim3(p.n_games), dim3(kBlock), lds, s, p);
 }
 
 void launch_c4_rollout_debug(const Arena &a, int M, int first_game, int n, const zc_c4_state *states,
                              int32_t *out_value, int64_t *out_words, hipStream_t s) {
     (void)M;
-    const int per_block = kBlock / kGroup;
-    hipLaunchKernelGGL(c4_rollout_debug_kernel, dim3((n + per_block - 1) / per_block), dim3(kBlock), 0, s, a,
-                       first_game, n, states, out_value, out_words);
+    hipLaunchKernelGGL(c4_rollout_debug_kernel, dim3(n), dim3(kBlock), 0, s, a, first_game, n, states, out_value,
+                       out_words);
 }
 
 void launch_c4_play(int n, zc_c4_state *states, const int32_t *moves, int32_t *results, int reset, hipStream_t s) {

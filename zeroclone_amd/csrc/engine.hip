@@ -61,8 +61,8 @@ int dalloc(zc_engine *e, T **p, size_t count) {
 }
 
 void free_arena(zc::Arena &a) {
-    void *ptrs[] = {a.nodes, a.W, a.path, a.pstate, a.pmeta, a.pval, a.ring, a.rngpos,
-                    a.logtab, a.roots, a.move, a.na, a.stats};
+    void *ptrs[] = {a.nodes, a.W, a.path, a.ring, a.rngpos,
+                    a.logtab, a.phase, a.roots, a.move, a.na, a.stats};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
     a = zc::Arena{};
@@ -110,6 +110,7 @@ zc::SearchParams make_params(zc_engine *e, int32_t first, int32_t n, const zc_c4
     p.out_stats = st;
     p.a = e->a;
     p.max_batch = e->cfg.max_batch;
+    p.stamp = e->stamp;
     return p;
 }
 
@@ -133,7 +134,7 @@ int zc_engine_create(const zc_engine_config *cfg, zc_engine **out) {
     *out = nullptr;
     if (cfg->max_games < 1) return fail(ZC_EINVAL, "max_games must be >= 1");
     if (cfg->max_sims < 1 || cfg->max_sims > 65533) return fail(ZC_EINVAL, "max_sims must be in [1, 65533]");
-    if (cfg->max_batch < 1) return fail(ZC_EINVAL, "max_batch must be >= 1");
+    if (cfg->max_batch < 1 || cfg->max_batch > 512) return fail(ZC_EINVAL, "max_batch must be in [1, 512]");
     int ndev = 0;
     ZC_HIP(hipGetDeviceCount(&ndev));
     if (cfg->device < 0 || cfg->device >= ndev) return fail(ZC_EINVAL, "device %d not present (%d devices)", cfg->device, ndev);
@@ -148,12 +149,11 @@ int zc_engine_create(const zc_engine_config *cfg, zc_engine **out) {
     if (!rc) rc = dalloc(e, &a.nodes, G * M * zc::kRecBytes);
     if (!rc) rc = dalloc(e, &a.W, G * M * zc::kSlots);
     if (!rc) rc = dalloc(e, &a.path, G * B * zc::kMaxDepth);
-    if (!rc) rc = dalloc(e, &a.pstate, G * B * 2);
-    if (!rc) rc = dalloc(e, &a.pmeta, G * B);
-    if (!rc) rc = dalloc(e, &a.pval, G * B);
     if (!rc) rc = dalloc(e, &a.ring, G * zc::kRingWords);
     if (!rc) rc = dalloc(e, &a.rngpos, G * 2);
     if (!rc) rc = dalloc(e, &a.logtab, M + 2);
+    if (!rc) rc = dalloc(e, &a.phase, G * 4);
+    if (!rc && hipMemset(a.phase, 0, G * 4 * sizeof(int64_t)) != hipSuccess) rc = fail(ZC_EHIP, "memset failed");
     if (!rc) rc = dalloc(e, &a.roots, G);
     if (!rc) rc = dalloc(e, &a.move, G);
     if (!rc) rc = dalloc(e, &a.na, G * 7);
@@ -264,7 +264,7 @@ int zc_c4_search_async(zc_engine *eng, int32_t first, int32_t n, const zc_c4_sta
     if (!n) return ZC_OK;
     std::lock_guard<std::mutex> lk(eng->mu);
     ZC_HIP(hipSetDevice(eng->cfg.device));
-    hipStream_t s = hip_stream ? (hipStream_t)hip_stream : eng->stream;
+    hipStream_t s = (hipStream_t)hip_stream;
     zc::launch_c4_search(make_params(eng, first, n, d_roots, sims, c, bs, d_move, d_na, d_stats), s);
     ZC_HIP(hipGetLastError());
     return ZC_OK;
@@ -305,7 +305,7 @@ int zc_c4_play_async(zc_engine *eng, int32_t n, zc_c4_state *d_states, const int
     if (!n) return ZC_OK;
     std::lock_guard<std::mutex> lk(eng->mu);
     ZC_HIP(hipSetDevice(eng->cfg.device));
-    hipStream_t s = hip_stream ? (hipStream_t)hip_stream : eng->stream;
+    hipStream_t s = (hipStream_t)hip_stream;
     zc::launch_c4_play(n, d_states, d_moves, d_results, reset, s);
     ZC_HIP(hipGetLastError());
     return ZC_OK;
@@ -392,6 +392,24 @@ int zc_debug_c4_rollout(zc_engine *eng, int32_t first, int32_t n, const zc_c4_st
     ZC_HIP(hipMemcpyAsync(out_words, dw, (size_t)n * sizeof(int64_t), hipMemcpyDeviceToHost, s));
     ZC_HIP(hipStreamSynchronize(s));
     (void)hipFree(dw);
+    return ZC_OK;
+}
+
+int zc_debug_phase_cycles(zc_engine *eng, int32_t enable, int64_t *out4) {
+    if (!eng) return fail(ZC_EINVAL, "null argument");
+    std::lock_guard<std::mutex> lk(eng->mu);
+    ZC_HIP(hipSetDevice(eng->cfg.device));
+    ZC_HIP(hipDeviceSynchronize());
+    const size_t G = (size_t)eng->cfg.max_games;
+    if (out4) {
+        std::vector<int64_t> ph(G * 4);
+        ZC_HIP(hipMemcpy(ph.data(), eng->a.phase, ph.size() * sizeof(int64_t), hipMemcpyDeviceToHost));
+        for (int k = 0; k < 4; ++k) out4[k] = 0;
+        for (size_t g = 0; g < G; ++g)
+            for (int k = 0; k < 4; ++k) out4[k] += ph[4 * g + k];
+    }
+    ZC_HIP(hipMemset(eng->a.phase, 0, G * 4 * sizeof(int64_t)));
+    eng->stamp = enable ? 1 : 0;
     return ZC_OK;
 }
 

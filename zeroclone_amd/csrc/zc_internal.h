@@ -36,22 +36,19 @@ constexpr int kMaxDepth = 44;          // levels 0..42 (a C4 game has at most 42
 constexpr int kRingLog2 = 12;          // per-game MT19937 ring: 4096 raw words
 constexpr int kRingWords = 1 << kRingLog2;
 constexpr int kLookahead = 2048;       // words generated ahead at each flush start
-constexpr int kChunk = 224;            // words per generation step (<= 227, multiple of 8)
-constexpr int kGroup = 8;              // lanes cooperating on one game
-constexpr int kBlock = 64;             // threads per workgroup (one wave, 8 games)
+constexpr int kChunk = 192;            // words per generation step (<= 227, multiple of 64)
+constexpr int kBlock = 64;             // threads per workgroup: one wave = one game
 
-static_assert(kLookahead + kChunk + 624 + 16 < kRingWords, "ring must retain the current MT block");
+static_assert(kLookahead + kChunk + 624 + 128 < kRingWords, "ring must retain the current MT block");
 
 struct Arena {
     uint8_t *nodes = nullptr;     // [G][M][128 B]
     int32_t *W = nullptr;         // [G][M][8]
     uint32_t *path = nullptr;     // [G][B][kMaxDepth]  node | pact<<16
-    uint64_t *pstate = nullptr;   // [G][B][2]          leaf stones
-    uint32_t *pmeta = nullptr;    // [G][B]             leaf node | depth<<16 | turn<<24
-    int32_t *pval = nullptr;      // [G][B]             leaf values
     uint32_t *ring = nullptr;     // [G][kRingWords]    raw (untempered) MT words
     uint64_t *rngpos = nullptr;   // [G][2]             {next word to use, words generated}
     double *logtab = nullptr;     // [M+2]              glibc log(n), n = 0..M+1
+    int64_t *phase = nullptr;     // [G][4]             diagnostic phase cycles (stamp build)
     // staging for the synchronous host entry points
     zc_c4_state *roots = nullptr;
     int32_t *move = nullptr;
@@ -67,8 +64,10 @@ struct SearchParams {
     zc_game_stats *out_stats;
     Arena a;
     int max_batch;
+    int stamp;
 };
 
+size_t c4_search_lds_bytes(int bs);
 void launch_c4_search(const SearchParams &p, hipStream_t s);
 void launch_c4_rollout_debug(const Arena &a, int M, int first_game, int n, const zc_c4_state *states,
                              int32_t *out_value, int64_t *out_words, hipStream_t s);
@@ -84,5 +83,6 @@ struct zc_engine {
     hipStream_t stream = nullptr;
     zc::Arena a;
     int64_t bytes = 0;
+    int stamp = 0;
     std::mutex mu;
 };
