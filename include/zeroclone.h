@@ -129,11 +129,12 @@ int zc_debug_uct(zc_engine *eng, int32_t n, const double *logn, const int32_t *n
 int zc_debug_c4_rollout(zc_engine *eng, int32_t first_game, int32_t n, const zc_c4_state *states,
                         int32_t *out_value, int64_t *out_words);
 
-/* Diagnostic phase stamps: returns (into out4, may be NULL) the shader-cycle sums since the
- * previous call of {RNG generation, select+expand, rollouts, backup} over all games, resets
- * them, and switches the stamped kernel build on (enable != 0) or off for later searches.
- * Synchronises the device.  Stamped runs are for phase SHARES only, never for timing. */
-int zc_debug_phase_cycles(zc_engine *eng, int32_t enable, int64_t *out4);
+/* Diagnostic phase stamps: returns (into out8, may be NULL) the shader-cycle sums since the
+ * previous call, over all games, of {RNG generation, first walk of each flush, resumed
+ * walks, expansion + leaf bookkeeping, rollouts, backup, 0, 0}, resets them, and switches
+ * the stamped kernel build on (enable != 0) or off for later searches.  Synchronises the
+ * device.  Stamped runs are for phase SHARES only, never for timing. */
+int zc_debug_phase_cycles(zc_engine *eng, int32_t enable, int64_t *out8);
 
 #ifdef __cplusplus
 }

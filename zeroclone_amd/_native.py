@@ -217,9 +217,9 @@ class NativeEngine:
         return out
 
     def phase_cycles(self, enable: bool):
-        out = (ctypes.c_int64 * 4)()
+        out = (ctypes.c_int64 * 8)()
         check(lib().zc_debug_phase_cycles(self._h, int(bool(enable)), out))
-        return dict(zip(["rng", "select_expand", "rollout", "backup"], list(out)))
+        return dict(zip(["rng", "walk_first", "walk_resumed", "expand", "rollout", "backup"], list(out)[:6]))
 
     def debug_c4_rollout(self, states: np.ndarray, first_game: int = 0):
         states = np.ascontiguousarray(states, dtype=C4_STATE_DTYPE)

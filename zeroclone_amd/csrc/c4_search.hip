@@ -89,11 +89,11 @@ __device__ __forceinline__ uint64_t drop_bit(uint64_t occ, int col) {
 
 __device__ __forceinline__ int legal_mask(uint64_t occ) {
     // c4_backend.get_legal_moves (:49-50): column c is legal while its top cell is empty.
+    // Gather bit 7c -> bit c with one multiply: the 49 partial products t_c * 2^(56-6i) land
+    // on distinct bit positions (7c - 6i is injective on 0..6 x 0..6), so nothing carries
+    // and bits 56..62 of the product are exactly t_0..t_6.
     const uint64_t t = (~occ & kTop) >> 5;  // bit 7c
-    int m = 0;
-#pragma unroll
-    for (int c = 0; c < 7; ++c) m |= (int)((t >> (6 * c)) & (1ull << c));
-    return m;
+    return (int)((t * 0x0104104104100000ull) >> 56) & 0x7F;
 }
 
 __device__ __forceinline__ bool has_four(uint64_t b) {
@@ -133,15 +133,22 @@ struct Rng {
 
 __device__ __forceinline__ uint64_t rng_generate(uint32_t *ring, uint64_t gen, uint64_t target) {
     const uint32_t lane = lane_id();
+    constexpr int K = kChunk / 64;
     while (gen < target) {
+        // every input of the chunk is >= 227 words older than any output: load all, then store
+        uint32_t a[K], b[K], m[K];
 #pragma unroll
-        for (int k = 0; k < kChunk / 64; ++k) {
-            const uint64_t p = gen + lane + 64u * k;
-            const uint32_t a = ring[(p - 624) & kRingMask];
-            const uint32_t b = ring[(p - 623) & kRingMask];
-            const uint32_t m = ring[(p - 227) & kRingMask];
-            const uint32_t y = (a & 0x80000000u) | (b & 0x7fffffffu);
-            ring[p & kRingMask] = m ^ (y >> 1) ^ ((b & 1u) ? 0x9908b0dfu : 0u);
+        for (int k = 0; k < K; ++k) {
+            const uint32_t p = (uint32_t)gen + lane + 64u * k;
+            a[k] = ring[(p - 624) & kRingMask];
+            b[k] = ring[(p - 623) & kRingMask];
+            m[k] = ring[(p - 227) & kRingMask];
+        }
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const uint32_t p = (uint32_t)gen + lane + 64u * k;
+            const uint32_t y = (a[k] & 0x80000000u) | (b[k] & 0x7fffffffu);
+            ring[p & kRingMask] = m[k] ^ (y >> 1) ^ ((b[k] & 1u) ? 0x9908b0dfu : 0u);
         }
         gen += kChunk;
         wave_mem_order();
@@ -194,9 +201,20 @@ __device__ __forceinline__ uint32_t rng_below(Rng &r, uint32_t n) {
 // A pending leaf, kept in LDS between the phases of a flush.
 struct Leaf {
     uint64_t p0, p1;  // stones of 'X' / 'O'
-    uint32_t meta;    // node | depth << 16 | turn << 24
+    uint32_t meta;    // node | depth << 16 | turn << 24 | legal mask << 25
     int32_t val;      // rollout value from the leaf's side to move
 };
+
+// LDS copy of a node created in the current flush.  During selection the node lives only
+// here; its HBM record is written in one coalesced batch when the flush's leaves are chosen.
+struct Fresh {
+    uint32_t u;       // untried word (record +4)
+    uint32_t ow;      // packed move-list columns (record +12)
+    uint32_t link;    // parent | pact << 16 | depth << 24 (record +8)
+    uint32_t pad;
+    uint16_t ch[8];   // children (record +16)
+};
+static_assert(sizeof(Fresh) == 32, "Fresh is two 16-byte LDS slots");
 
 __device__ __forceinline__ uint64_t readlane64(uint64_t x, int l) {
     return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(x >> 32), l) << 32) |
@@ -205,6 +223,17 @@ __device__ __forceinline__ uint64_t readlane64(uint64_t x, int l) {
 
 __device__ __forceinline__ uint32_t mbcnt(uint64_t m) {  // set bits of m in lanes below this one
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+// Inclusive prefix SUM over the 64 lanes (same DPP pattern as scan_or32).
+__device__ __forceinline__ uint32_t scan_add32(uint32_t x) {
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, false);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, false);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, false);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, false);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false);
+    return x;
 }
 
 // Inclusive prefix OR over the 64 lanes (DPP: row_shr 1,2,4,8, then row_bcast 15 / 31).
@@ -240,7 +269,8 @@ __device__ void c4_rollouts(Leaf *L, int nb, Rng &rng, int64_t &plies_total) {
     for (int j = 0; j < nb; ++j) {
         const uint64_t x0 = uni64(L[j].p0);
         const uint64_t x1 = uni64(L[j].p1);
-        const int tn = (int)(uni(L[j].meta) >> 24);
+        const uint32_t lm = uni(L[j].meta);
+        const int tn = (int)((lm >> 24) & 1u);
         uint64_t me = tn ? x1 : x0;  // side to move
         uint64_t op = tn ? x0 : x1;  // last mover
         int val = 0;
@@ -248,7 +278,7 @@ __device__ void c4_rollouts(Leaf *L, int nb, Rng &rng, int64_t &plies_total) {
         if (has_four(op)) {
             val = -1;
         } else if ((me | op) != kFull) {
-            int mask = legal_mask(me | op);
+            int mask = (int)(lm >> 25);
             uint32_t ow = d_order[mask];
             uint32_t n = (ow >> 24) & 15u;
             int stones = __popcll(me | op);
@@ -263,12 +293,11 @@ __device__ void c4_rollouts(Leaf *L, int nb, Rng &rng, int64_t &plies_total) {
                 }
                 const uint32_t qk = mbcnt(A);                    // this lane's ply in the block
                 const uint32_t col = (ow >> (3 * (v & 7u))) & 7u;  // its column (if accepted)
-                uint32_t same = 0;                               // earlier plies in that column
-#pragma unroll
-                for (uint32_t c = 0; c < 7; ++c) {
-                    const uint64_t Mc = __ballot(acc && col == c);
-                    same = (col == c) ? mbcnt(Mc) : same;
-                }
+                // earlier plies in the same column: 4-bit per-column counters, prefix-summed
+                // (a nibble can only overflow past 15 plies in one column, i.e. after that
+                // column filled — beyond the block's first event, so never read)
+                const uint32_t one = acc ? (1u << (4 * col)) : 0u;
+                const uint32_t same = ((scan_add32(one) - one) >> (4 * col)) & 15u;
                 const uint64_t occ = me | op;
                 const uint32_t h0 = (uint32_t)__popcll((occ >> (7 * col)) & 0x3Full);
                 const uint32_t row = min(h0 + same, 6u);
@@ -342,7 +371,7 @@ __device__ __forceinline__ void node_init(const Tree &t, int nd, int parent, int
     if (lane < kSlots) {
         t.child(nd)[lane] = 0xFFFF;
         t.na(nd)[lane] = 0;
-        t.q(nd)[lane] = (lane == 7) ? -INFINITY : 0.0;  // slot 7 = log(N) = log(0)
+        t.q(nd)[lane] = 0.0;
         t.w(nd)[lane] = 0;
     }
 }
@@ -359,13 +388,20 @@ __device__ __forceinline__ bool valid_state(uint64_t p0, uint64_t p1, int turn) 
 }
 
 // ------------------------------------------------------------------ the search kernel
-// STAMP = diagnostic build: lane 0 adds s_memtime deltas per phase into p.a.phase[g][0..3] =
-// {rng generation at flush start, select+expand, rollouts, backup}.
+// STAMP = diagnostic build: lane 0 adds s_memtime deltas per phase into p.a.phase[g][0..7] =
+// {rng generation at flush start, first walk of a flush, resumed walks, expansion + leaf
+//  bookkeeping, rollouts, backup, -, -}.
 template <bool STAMP>
 __global__ __launch_bounds__(kBlock) void c4_search_kernel(SearchParams p) {
     extern __shared__ __attribute__((aligned(16))) uint8_t s_dyn[];
-    Leaf *const leaves = (Leaf *)s_dyn;                                   // [bs]
-    uint32_t *const paths = (uint32_t *)(s_dyn + sizeof(Leaf) * (size_t)p.bs);  // [bs][kMaxDepth]
+    // LDS (16-byte aligned pieces first): fresh[bs] (32 B), leaves[bs] (24 B), paths[bs][kMaxDepth]
+    Fresh *const fresh = (Fresh *)s_dyn;
+    Leaf *const leaves = (Leaf *)(s_dyn + sizeof(Fresh) * (size_t)p.bs);
+    uint32_t *const paths = (uint32_t *)(s_dyn + (sizeof(Fresh) + sizeof(Leaf)) * (size_t)p.bs);
+    // log(N) table read through the constant address space: uniform index -> scalar loads,
+    // which do not sit in the vector-memory counter the walk and the RNG window wait on.
+    const __attribute__((address_space(4))) double *logtab =
+        (const __attribute__((address_space(4))) double *)p.a.logtab;
 
     const uint32_t lane = lane_id();
     const int gl = blockIdx.x;  // game within this call (one wave per game)
@@ -398,7 +434,7 @@ __global__ __launch_bounds__(kBlock) void c4_search_kernel(SearchParams p) {
     int64_t plies = 0;
     wave_mem_order();
 
-    uint64_t ph[4] = {0, 0, 0, 0};
+    uint64_t ph[kPhases] = {};
     uint64_t tstamp = STAMP ? __builtin_amdgcn_s_memtime() : 0;
 #define ZC_STAMP(k)                                          \
     if (STAMP) {                                             \
@@ -414,24 +450,67 @@ __global__ __launch_bounds__(kBlock) void c4_search_kernel(SearchParams p) {
         // ---- selection + expansion of nb leaves (mcts.cpp:129-147) -------------------------
         // Within a flush no backup happens, so UCT scores on the path above the node that
         // was just expanded cannot change: leaf j+1's walk resumes there (exactly the walk
-        // the reference repeats from the root).  Lane l holds level l of the current path.
-        int xnode = 0, xdepth = 0, xturn = rturn;
+        // the reference repeats from the root), from a register copy of that node.  Nodes
+        // created in this flush ("fresh": id >= f0) have Na = Q = 0 on every edge; their
+        // untried list and children are mirrored in LDS, so walking them needs no HBM read.
+        // N of a node is its parent's Na on the edge in (root: leaves flushed so far).
+        // Lane l holds level l of the current path.
+        const int f0 = nnodes;
+        int xnode = 0, xdepth = 0, xturn = rturn, xN = done;
         uint64_t x0 = rp0, x1 = rp1;
         uint32_t pathv = (lane == 0) ? 0x00FF0000u : 0u;
+        int c_node = -1;  // register copy of one record: the node the last walk ended at
+        bool c_dirty = false;  // copy of an older (HBM) node modified by expansions
+        uint32_t c_u = 0, c_ow = 0;
+        uint32_t c_ch = 0xFFFF;
+        int32_t c_na = 0;
+        double c_q = 0.0;
+        const uint32_t k = lane & 7u;
         for (int j = 0; j < nb; ++j) {
-            int node = xnode, depth = xdepth, turn = xturn;
+            int node = xnode, depth = xdepth, turn = xturn, nN = xN;
             uint64_t b0 = x0, b1 = x1;
             uint32_t u, ow;
+            ZC_STAMP(3)
             for (;;) {  // select (mcts.cpp:47-63)
-                const uint8_t *R = t.rec(node);
-                const uint32_t k = lane & 7u;
-                const uint4 h = *(const uint4 *)R;
-                const uint16_t ch = ((const uint16_t *)(R + 16))[k];
-                const int32_t na = ((const int32_t *)(R + 32))[k];
-                const double q = ((const double *)(R + 64))[k];
-                const double lg = ((const double *)(R + 64))[7];
-                u = uni(h.y);
-                ow = uni(h.w);
+                uint32_t ch;
+                int32_t na;
+                double q;
+                if (node == c_node) {
+                    u = c_u;
+                    ow = c_ow;
+                    ch = c_ch;
+                    na = c_na;
+                    q = c_q;
+                } else {
+                    if (c_dirty) {  // write the modified older node back before dropping the copy
+                        if (lane == 0) t.hdr(c_node)[1] = c_u;
+                        if (lane < kSlots) t.child(c_node)[lane] = (uint16_t)c_ch;
+                        c_dirty = false;
+                    }
+                    if (node >= f0) {
+                        const Fresh &F = fresh[node - f0];
+                        u = uni(F.u);
+                        ow = uni(F.ow);
+                        ch = F.ch[k];
+                        na = 0;
+                        q = 0.0;
+                    } else {
+                        const uint8_t *R = t.rec(node);
+                        const uint4 h = *(const uint4 *)R;
+                        ch = ((const uint16_t *)(R + 16))[k];
+                        na = ((const int32_t *)(R + 32))[k];
+                        q = ((const double *)(R + 64))[k];
+                        u = uni(h.y);
+                        ow = uni(h.w);
+                    }
+                }
+                const double lg = logtab[nN];  // log(N), glibc values tabulated on the host
+                c_node = node;
+                c_u = u;
+                c_ow = ow;
+                c_ch = ch;
+                c_na = na;
+                c_q = q;
                 if ((u >> 24) & 15u) break;  // untried moves left: expand here
                 if (depth >= kMaxDepth - 2) {  // unreachable (a C4 tree is <= 42 deep); never spin
                     st.status = ZC_STATUS_INTERNAL;
@@ -447,6 +526,7 @@ __global__ __launch_bounds__(kBlock) void c4_search_kernel(SearchParams p) {
                 const int best = uni(bi);
                 if ((__ballot(v == -INFINITY) & 1ull) != 0) break;  // no child: terminal node is its own leaf
                 const int nxt = __builtin_amdgcn_readlane((int)ch, best);
+                nN = __builtin_amdgcn_readlane(na, best);
                 const uint64_t bit = drop_bit(b0 | b1, (int)((ow >> (3 * best)) & 7u));
                 if (turn) b1 |= bit; else b0 |= bit;
                 turn ^= 1;
@@ -454,13 +534,20 @@ __global__ __launch_bounds__(kBlock) void c4_search_kernel(SearchParams p) {
                 ++depth;
                 if (lane == (uint32_t)depth) pathv = (uint32_t)node | ((uint32_t)best << 16);
             }
-            // the walk ends here; leaf j+1 resumes from this node
+            if (j == 0) {
+                ZC_STAMP(1)
+            } else {
+                ZC_STAMP(2)
+            }
+            // the walk ends here; leaf j+1 resumes from this node (c_node == node)
             xnode = node;
             xdepth = depth;
             xturn = turn;
+            xN = nN;
             x0 = b0;
             x1 = b1;
             int leaf = node;
+            int lmask;
             const uint32_t cnt = (u >> 24) & 15u;
             if (cnt) {  // expand (mcts.cpp:65-78): policy = random.choice(untried)
                 const uint32_t r = rng_below(rng, cnt);
@@ -468,67 +555,110 @@ __global__ __launch_bounds__(kBlock) void c4_search_kernel(SearchParams p) {
                 const int mi = (int)((digits >> (3 * r)) & 7u);
                 const uint32_t low = (1u << (3 * r)) - 1u;
                 const uint32_t rest = (digits & low) | ((digits >> 3) & ~low & 0x1FFFFFu);
-                if (lane == 0) t.hdr(node)[1] = rest | ((cnt - 1u) << 24) | (u & 0xF0000000u);
+                const uint32_t nu = rest | ((cnt - 1u) << 24) | (u & 0xF0000000u);
                 const uint64_t bit = drop_bit(b0 | b1, (int)((ow >> (3 * mi)) & 7u));
                 if (turn) b1 |= bit; else b0 |= bit;
                 turn ^= 1;
                 leaf = nnodes++;
                 ++depth;
-                node_init(t, leaf, node, mi, depth, d_order[legal_mask(b0 | b1)]);
-                if (lane == (uint32_t)mi) t.child(node)[mi] = (uint16_t)leaf;
+                lmask = legal_mask(b0 | b1);
+                const uint32_t low_ = d_order[lmask];
+                // parent: untried list and child link (copy; and LDS if the parent is fresh)
+                c_u = nu;
+                if (k == (uint32_t)mi) c_ch = (uint32_t)leaf;
+                if (node >= f0) {
+                    if (lane == 0) fresh[node - f0].u = nu;
+                    if (lane == (uint32_t)mi) fresh[node - f0].ch[mi] = (uint16_t)leaf;
+                } else {
+                    c_dirty = true;
+                }
+                // the new node (Node ctor, mcts.cpp:23-34): all moves untried, no children
+                {
+                    Fresh &F = fresh[leaf - f0];
+                    const uint32_t n = (low_ >> 24) & 15u;
+                    if (lane == 0) {
+                        F.u = (kIdentDigits & ((1u << (3 * n)) - 1u)) | (n << 24) | (n << 28);
+                        F.ow = low_;
+                        F.link = (uint32_t)node | ((uint32_t)mi << 16) | ((uint32_t)depth << 24);
+                    }
+                    if (lane < kSlots) F.ch[lane] = 0xFFFF;
+                }
                 if (lane == (uint32_t)depth) pathv = (uint32_t)leaf | ((uint32_t)mi << 16);
                 st.expansions += 1;
                 st.depth_sum += depth;
+            } else {
+                lmask = legal_mask(b0 | b1);  // terminal leaf
             }
             if (lane == 0) {
                 leaves[j].p0 = b0;
                 leaves[j].p1 = b1;
-                leaves[j].meta = (uint32_t)leaf | ((uint32_t)depth << 16) | ((uint32_t)turn << 24);
+                leaves[j].meta = (uint32_t)leaf | ((uint32_t)depth << 16) | ((uint32_t)turn << 24) |
+                                 ((uint32_t)lmask << 25);
             }
             if (lane < (uint32_t)kMaxDepth) paths[j * kMaxDepth + lane] = pathv;
             wave_mem_order();
         }
-        ZC_STAMP(1)
+        // ---- publish this flush's tree changes to HBM --------------------------------------
+        if (c_dirty) {
+            if (lane == 0) t.hdr(c_node)[1] = c_u;
+            if (lane < kSlots) t.child(c_node)[lane] = (uint16_t)c_ch;
+        }
+        {
+            // each fresh record = 8 x 16 B: {N=0, u, link, ow}, children, Na = 0 (2), Q = 0 (4)
+            const int nf = nnodes - f0;
+            for (int base = 0; base < nf * 8; base += 64) {
+                const int idx = base + (int)lane;
+                if (idx < nf * 8) {
+                    const int r = idx >> 3, part = idx & 7;
+                    const Fresh &F = fresh[r];
+                    uint4 v = make_uint4(0u, 0u, 0u, 0u);
+                    if (part == 0) v = make_uint4(0u, F.u, F.link, F.ow);
+                    else if (part == 1) v = *(const uint4 *)F.ch;
+                    *(uint4 *)(t.rec(f0 + r) + 16 * part) = v;
+                }
+            }
+            for (int base = 0; base < nf * 2; base += 64) {  // W rows: 2 x 16 B of zeros
+                const int idx = base + (int)lane;
+                if (idx < nf * 2) *(uint4 *)(t.w(f0 + (idx >> 1)) + 4 * (idx & 1)) = make_uint4(0u, 0u, 0u, 0u);
+            }
+        }
+        ZC_STAMP(3)
 
         // ---- value.batch: random rollouts in pending order (mcts.cpp:112-124) ---------------
         c4_rollouts(leaves, nb, rng, plies);
         wave_mem_order();
-        ZC_STAMP(2)
+        ZC_STAMP(4)
 
         // ---- backprop in pending order (mcts.cpp:80-100, :124-125) --------------------------
-        // Lane l updates level l of the leaf's path.  A node's level never changes, so every
-        // read-modify-write of a given word stays in one lane, in leaf order.
+        // Lane l >= 1 updates the edge into level l of the leaf's path (Na += 1, Wa -= r,
+        // Qa = Wa/Na; r alternates sign per level).  Node::N is not stored: it always equals
+        // the parent's Na on the edge in (root: the leaves flushed so far).  A node's level
+        // never changes, so every read-modify-write of a given word stays in one lane, in
+        // leaf order.
         for (int j = 0; j < nb; ++j) {
             const uint32_t meta = uni(leaves[j].meta);
             const int d = (int)((meta >> 16) & 0xFFu);
             const int v = uni(leaves[j].val);
-            if (lane <= (uint32_t)d) {
+            if (lane >= 1 && lane <= (uint32_t)d) {
                 const uint32_t e = paths[j * kMaxDepth + lane];
-                const int nd = (int)(e & 0xFFFFu);
+                const int par = (int)(paths[j * kMaxDepth + lane - 1] & 0xFFFFu);
+                const int act = (int)(e >> 16);
                 const int vl = ((d - (int)lane) & 1) ? -v : v;
-                uint32_t *h = t.hdr(nd);
-                const uint32_t n1 = h[0] + 1u;
-                h[0] = n1;
-                t.q(nd)[7] = a.logtab[n1];
-                if (lane > 0) {
-                    const int par = (int)(paths[j * kMaxDepth + lane - 1] & 0xFFFFu);
-                    const int act = (int)(e >> 16);
-                    const int32_t na1 = t.na(par)[act] + 1;
-                    const int32_t w1 = t.w(par)[act] - vl;  // Wa -= result
-                    t.na(par)[act] = na1;
-                    t.w(par)[act] = w1;
-                    t.q(par)[act] = (double)w1 / (double)na1;  // Qa = Wa / Na
-                }
+                const int32_t na1 = t.na(par)[act] + 1;
+                const int32_t w1 = t.w(par)[act] - vl;  // Wa -= result
+                t.na(par)[act] = na1;
+                t.w(par)[act] = w1;
+                t.q(par)[act] = (double)w1 / (double)na1;  // Qa = Wa / Na
             }
             wave_mem_order();
         }
-        ZC_STAMP(3)
+        ZC_STAMP(5)
         st.leaves += nb;
         done += nb;
     }
 #undef ZC_STAMP
     if (STAMP && lane == 0)
-        for (int k = 0; k < 4; ++k) a.phase[4 * (size_t)g + k] += (int64_t)ph[k];
+        for (int k = 0; k < kPhases; ++k) a.phase[kPhases * (size_t)g + k] += (int64_t)ph[k];
 
     // ---- best move: first max of child N over the root's move list (mcts.cpp:150-157) ----
     const uint32_t u = uni(t.hdr(0)[1]);
@@ -571,7 +701,7 @@ __global__ __launch_bounds__(kBlock) void c4_rollout_debug_kernel(Arena a, int f
     if (lane == 0) {
         s_leaf[0].p0 = s.stones[0];
         s_leaf[0].p1 = s.stones[1];
-        s_leaf[0].meta = (uint32_t)s.turn << 24;
+        s_leaf[0].meta = ((uint32_t)s.turn << 24) | ((uint32_t)legal_mask(s.stones[0] | s.stones[1]) << 25);
     }
     wave_mem_order();
     int64_t plies = 0;
@@ -614,7 +744,9 @@ __global__ void uct_debug_kernel(int n, const double *logn, const int32_t *na, c
 
 }  // namespace
 
-size_t c4_search_lds_bytes(int bs) { return (sizeof(Leaf) + sizeof(uint32_t) * kMaxDepth) * (size_t)bs; }
+size_t c4_search_lds_bytes(int bs) {
+    return (sizeof(Leaf) + sizeof(Fresh) + sizeof(uint32_t) * kMaxDepth) * (size_t)bs;
+}
 
 void launch_c4_search(const SearchParams &p, hipStream_t s) {
     const size_t lds = c4_search_lds_bytes(p.bs);

@@ -152,8 +152,8 @@ int zc_engine_create(const zc_engine_config *cfg, zc_engine **out) {
     if (!rc) rc = dalloc(e, &a.ring, G * zc::kRingWords);
     if (!rc) rc = dalloc(e, &a.rngpos, G * 2);
     if (!rc) rc = dalloc(e, &a.logtab, M + 2);
-    if (!rc) rc = dalloc(e, &a.phase, G * 4);
-    if (!rc && hipMemset(a.phase, 0, G * 4 * sizeof(int64_t)) != hipSuccess) rc = fail(ZC_EHIP, "memset failed");
+    if (!rc) rc = dalloc(e, &a.phase, G * zc::kPhases);
+    if (!rc && hipMemset(a.phase, 0, G * zc::kPhases * sizeof(int64_t)) != hipSuccess) rc = fail(ZC_EHIP, "memset failed");
     if (!rc) rc = dalloc(e, &a.roots, G);
     if (!rc) rc = dalloc(e, &a.move, G);
     if (!rc) rc = dalloc(e, &a.na, G * 7);
@@ -395,20 +395,21 @@ int zc_debug_c4_rollout(zc_engine *eng, int32_t first, int32_t n, const zc_c4_st
     return ZC_OK;
 }
 
-int zc_debug_phase_cycles(zc_engine *eng, int32_t enable, int64_t *out4) {
+int zc_debug_phase_cycles(zc_engine *eng, int32_t enable, int64_t *out8) {
     if (!eng) return fail(ZC_EINVAL, "null argument");
     std::lock_guard<std::mutex> lk(eng->mu);
     ZC_HIP(hipSetDevice(eng->cfg.device));
     ZC_HIP(hipDeviceSynchronize());
     const size_t G = (size_t)eng->cfg.max_games;
-    if (out4) {
-        std::vector<int64_t> ph(G * 4);
+    constexpr int K = zc::kPhases;
+    if (out8) {
+        std::vector<int64_t> ph(G * K);
         ZC_HIP(hipMemcpy(ph.data(), eng->a.phase, ph.size() * sizeof(int64_t), hipMemcpyDeviceToHost));
-        for (int k = 0; k < 4; ++k) out4[k] = 0;
+        for (int k = 0; k < K; ++k) out8[k] = 0;
         for (size_t g = 0; g < G; ++g)
-            for (int k = 0; k < 4; ++k) out4[k] += ph[4 * g + k];
+            for (int k = 0; k < K; ++k) out8[k] += ph[K * g + k];
     }
-    ZC_HIP(hipMemset(eng->a.phase, 0, G * 4 * sizeof(int64_t)));
+    ZC_HIP(hipMemset(eng->a.phase, 0, G * K * sizeof(int64_t)));
     eng->stamp = enable ? 1 : 0;
     return ZC_OK;
 }

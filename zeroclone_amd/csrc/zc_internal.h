@@ -38,6 +38,7 @@ constexpr int kRingWords = 1 << kRingLog2;
 constexpr int kLookahead = 2048;       // words generated ahead at each flush start
 constexpr int kChunk = 192;            // words per generation step (<= 227, multiple of 64)
 constexpr int kBlock = 64;             // threads per workgroup: one wave = one game
+constexpr int kPhases = 8;             // diagnostic phase-stamp slots per game
 
 static_assert(kLookahead + kChunk + 624 + 128 < kRingWords, "ring must retain the current MT block");
 
@@ -48,7 +49,7 @@ struct Arena {
     uint32_t *ring = nullptr;     // [G][kRingWords]    raw (untempered) MT words
     uint64_t *rngpos = nullptr;   // [G][2]             {next word to use, words generated}
     double *logtab = nullptr;     // [M+2]              glibc log(n), n = 0..M+1
-    int64_t *phase = nullptr;     // [G][4]             diagnostic phase cycles (stamp build)
+    int64_t *phase = nullptr;     // [G][kPhases]       diagnostic phase cycles (stamp build)
     // staging for the synchronous host entry points
     zc_c4_state *roots = nullptr;
     int32_t *move = nullptr;
