@@ -140,6 +140,17 @@ def main():
     expansions, depth_sum, finished, leaves = (int(x) for x in tot.tolist())
     dt_max = float(dtt.item())
 
+    traffic, traffic_src = args.traffic_bytes, "--traffic-bytes" if args.traffic_bytes else None
+    if traffic is None:  # the committed PMC summary of this kernel (tools/summarize_profile.py)
+        import glob
+        prof = sorted(glob.glob(os.path.join(HERE, "profiles", "r*_c4_search_summary.json")))
+        if prof:
+            with open(prof[-1]) as fh:
+                hbm = json.load(fh).get("hbm")
+            if hbm:
+                traffic = hbm["bytes_per_launch"]
+                traffic_src = os.path.relpath(prof[-1], HERE)
+
     if rank == 0:
         launches = args.steps * world
         bytes_launch = bytes_per_expansion_model(expansions, depth_sum) / launches
@@ -164,7 +175,7 @@ def main():
                        "parallelism": f"games sharded over {world} GPU(s), 1 process/GPU"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 5),
-                         "traffic": args.traffic_bytes,
+                         "traffic": traffic, "traffic_source": traffic_src,
                          "kernel": "c4_search_kernel", "avg_launch_ms": round(avg_kernel_s * 1e3, 3),
                          "bytes_per_launch_model": round(bytes_launch),
                          "model": "SURVEY §8(d): 152*d+96 B per expansion, d counted in-kernel"},
