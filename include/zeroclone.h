@@ -88,6 +88,11 @@ int zc_c4_search(zc_engine *eng, int32_t first_game, int32_t n_games, const zc_c
                  int32_t sims, double c, int32_t batch_size,
                  int32_t *out_move, int32_t *out_root_na, zc_game_stats *out_stats);
 
+/* Same for an arbitrary set of engine games: entry i searches game games[i] (distinct). */
+int zc_c4_search_games(zc_engine *eng, int32_t n_games, const int32_t *games, const zc_c4_state *roots,
+                       int32_t sims, double c, int32_t batch_size,
+                       int32_t *out_move, int32_t *out_root_na, zc_game_stats *out_stats);
+
 /* Same, with DEVICE pointers, enqueued on `hip_stream` (a hipStream_t; NULL = the null
  * stream) without synchronising.  Argument validation that needs the roots happens on the
  * device: a bad root sets out_stats[i].status (ZC_STATUS_*). */
@@ -110,6 +115,14 @@ int zc_c4_play_async(zc_engine *eng, int32_t n_games, zc_c4_state *d_states, con
 #define ZC_STATUS_NO_MOVES 1     /* root has no legal move                                */
 #define ZC_STATUS_BAD_STATE 2    /* sentinel bits set / overlapping stones / bad turn    */
 #define ZC_STATUS_INTERNAL 3     /* search invariant violated (never expected)            */
+
+/* Value('random_rollout').batch(states, backend=c4_backend) (engine/value_functions.py:20-45)
+ * on the device: the n states are rolled out IN ORDER on engine game `game`'s stream, as the
+ * reference does with its one global `random` stream.  out_values[i] in {-1, 0, 1} is the
+ * value for states[i]'s side to move; *out_words (may be NULL) = words consumed.  Host
+ * pointers; blocks. */
+int zc_c4_rollouts(zc_engine *eng, int32_t game, int32_t n_states, const zc_c4_state *states,
+                   int32_t *out_values, int64_t *out_words);
 
 /* ---- Connect4 rules on the host (engine/games/connect4/c4_backend.py) --------------- */
 /* rows: 42 chars, row 0 = top, 'X', 'O', anything else = empty. */

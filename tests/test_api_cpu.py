@@ -1,0 +1,73 @@
+"""Host-side checks of the reference-API layer (no GPU compute)."""
+import numpy as np
+import pytest
+
+from zeroclone_amd.engine.games.connect4 import c4_backend as c4
+
+
+def dec(s):
+    return [[(" " if ch == "." else ch) for ch in s[r * 7:(r + 1) * 7]] for r in range(6)]
+
+
+def test_c4_backend_matches_reference_fixtures(golden):
+    for c in golden("c4_backend.json")["cases"]:
+        st = c4.State(dec(c["board"]), c["turn"])
+        assert [m[0] for m in list(c4.get_legal_moves(st))] == c["legal"]
+        assert c4.check_win(st) == c["win"]
+        assert c4.check_draw(st) == c["draw"]
+        t = c4.state_to_tensor(st)
+        assert t.shape == (2, 6, 7) and t.dtype == np.float32
+        assert "".join("1" if v else "0" for v in t[0].ravel()) == c["cur"]
+        assert "".join("1" if v else "0" for v in t[1].ravel()) == c["opp"]
+
+
+def test_bitboard_conversion_matches_c_abi(golden):
+    from zeroclone_amd import _native
+    for c in golden("c4_backend.json")["cases"][:80]:
+        st = c4.State(dec(c["board"]), c["turn"])
+        s0, s1, t = c4.to_zc(st)
+        ref = _native.c4_from_rows(c["board"], c["turn"])
+        assert (s0, s1, t) == (int(ref["stones"][0]), int(ref["stones"][1]), int(ref["turn"]))
+        assert c4.from_zc(s0, s1, t) == st
+
+
+def test_play_move_semantics():
+    s = c4.create_init_state()
+    for _ in range(6):
+        s = c4.play_move(s, (2, 0))
+    assert (2, 0) not in c4.get_legal_moves(s)
+    s2 = c4.play_move(s, (2, 0))      # full column: board unchanged, turn flips (reference :14-23)
+    assert s2.board == s.board and s2.turn == 1 - s.turn
+
+
+def test_engine_surface_without_gpu():
+    from zeroclone_amd.engine import Engine
+    e = Engine({"game": "connect4", "backend": "c4_backend", "value_function": "random_rollout", "threads": 3})
+    assert len(e.states) == 3 and e.add_game() == 3
+    assert e.play_move((3, 0), 0) is None           # Connect4 (col, 0) moves are legal here
+    with pytest.raises(ValueError):
+        e.play_move((9, 0), 0)
+    assert e.get_hist(0)[-1] == e.get_state(0)
+    # dataset labels: finished game -> alternating labels, reversed (engine.py:60-89)
+    for col in [0, 1, 0, 1, 0, 1]:
+        e.play_move((col, 0), 1)
+    assert e.play_move((0, 0), 1) == 1    # X completes four; O to move -> turn*2-1 = +1 (engine.py:150)
+    X, y = e.get_dataset()
+    assert X.shape == (8, 2, 6, 7) and y.shape == (8,)
+    assert set(np.unique(y)) <= {-1.0, 1.0}
+    e.reset_all_games()
+    assert len(e.states) == 3
+
+
+def test_unsupported_plugins_fail_loudly():
+    from zeroclone_amd.engine import Policy, Value, mcts
+    with pytest.raises(NotImplementedError):
+        Value("network_latest", model_type="chess_value")
+    v = Value("random_rollout")
+    with pytest.raises(NotImplementedError):
+        mcts.get_move(c4.create_init_state(), v, Policy("immediate_value"), c4, 10)
+
+    class Other:
+        __name__ = "chess_backend"
+    with pytest.raises(NotImplementedError):
+        mcts.get_move(c4.create_init_state(), v, Policy("random"), Other(), 10)

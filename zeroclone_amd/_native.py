@@ -59,11 +59,16 @@ SIGNATURES = [
     ("zc_c4_search", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p,
                                     ctypes.c_int32, ctypes.c_double, ctypes.c_int32, ctypes.c_void_p,
                                     ctypes.c_void_p, ctypes.c_void_p]),
+    ("zc_c4_search_games", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p,
+                                          ctypes.c_int32, ctypes.c_double, ctypes.c_int32, ctypes.c_void_p,
+                                          ctypes.c_void_p, ctypes.c_void_p]),
     ("zc_c4_search_async", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p,
                                           ctypes.c_int32, ctypes.c_double, ctypes.c_int32, ctypes.c_void_p,
                                           ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     ("zc_c4_play_async", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p,
                                         ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p]),
+    ("zc_c4_rollouts", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p,
+                                      ctypes.c_void_p, P(ctypes.c_int64)]),
     ("zc_c4_from_rows", ctypes.c_int, [ctypes.c_char_p, ctypes.c_int32, P(C4State)]),
     ("zc_c4_to_rows", ctypes.c_int, [P(C4State), ctypes.c_char_p]),
     ("zc_c4_legal_order", ctypes.c_int, [ctypes.c_int32, P(ctypes.c_int32)]),
@@ -195,6 +200,18 @@ class NativeEngine:
                                  _ptr(mv), _ptr(na), _ptr(st)))
         return mv, na, st
 
+    def c4_search_games(self, games, roots: np.ndarray, sims: int, c: float = 1.4, batch_size: int = 32):
+        ids = np.ascontiguousarray(games, dtype=np.int32)
+        roots = np.ascontiguousarray(roots, dtype=C4_STATE_DTYPE)
+        n = roots.shape[0]
+        assert ids.shape == (n,)
+        mv = np.zeros(n, np.int32)
+        na = np.zeros((n, 7), np.int32)
+        st = np.zeros(n, STATS_DTYPE)
+        check(lib().zc_c4_search_games(self._h, n, _ptr(ids), _ptr(roots), int(sims), float(c), int(batch_size),
+                                       _ptr(mv), _ptr(na), _ptr(st)))
+        return mv, na, st
+
     def c4_search_async(self, d_roots: int, n: int, sims: int, c: float, batch_size: int, d_move: int, d_na: int,
                         d_stats: int, stream: int = 0, first_game: int = 0) -> None:
         """Device-pointer entry (ints from torch .data_ptr()); enqueued on `stream`."""
@@ -206,6 +223,14 @@ class NativeEngine:
                       stream: int = 0) -> None:
         check(lib().zc_c4_play_async(self._h, n, ctypes.c_void_p(d_states), ctypes.c_void_p(d_moves),
                                      ctypes.c_void_p(d_results), int(bool(reset)), ctypes.c_void_p(stream or None)))
+
+    def c4_rollouts(self, states: np.ndarray, game: int = 0):
+        """Sequential rollouts of `states` on one game's stream: (values[n], words consumed)."""
+        states = np.ascontiguousarray(states, dtype=C4_STATE_DTYPE)
+        v = np.zeros(states.shape[0], np.int32)
+        w = ctypes.c_int64(0)
+        check(lib().zc_c4_rollouts(self._h, game, states.shape[0], _ptr(states), _ptr(v), ctypes.byref(w)))
+        return v, w.value
 
     # ---- self-test hooks
     def debug_uct(self, logn, na, q, c: float):

@@ -406,7 +406,7 @@ __global__ __launch_bounds__(kBlock) void c4_search_kernel(SearchParams p) {
     const uint32_t lane = lane_id();
     const int gl = blockIdx.x;  // game within this call (one wave per game)
     if (gl >= p.n_games) return;
-    const int g = p.first_game + gl;
+    const int g = p.game_ids ? uni(p.game_ids[gl]) : p.first_game + gl;
 
     const zc_c4_state root = p.roots[gl];
     const uint64_t rp0 = uni64(root.stones[0]), rp1 = uni64(root.stones[1]);
@@ -715,6 +715,37 @@ __global__ __launch_bounds__(kBlock) void c4_rollout_debug_kernel(Arena a, int f
     }
 }
 
+// Value('random_rollout').batch: n states rolled out IN ORDER on one game's stream.
+__global__ __launch_bounds__(kBlock) void c4_rollout_seq_kernel(Arena a, int g, int n, const zc_c4_state *states,
+                                                                int32_t *out_value, int64_t *out_words) {
+    __shared__ Leaf s_leaf[kBlock];
+    const uint32_t lane = lane_id();
+    Rng rng;
+    const uint64_t use0 = uni64(a.rngpos[2 * (size_t)g]);
+    rng_open(rng, a.ring + (size_t)g * kRingWords, use0, uni64(a.rngpos[2 * (size_t)g + 1]));
+    int64_t plies = 0;
+    for (int base = 0; base < n; base += kBlock) {
+        const int cnt = min(kBlock, n - base);
+        if ((int)lane < cnt) {
+            const zc_c4_state s = states[base + lane];
+            s_leaf[lane].p0 = s.stones[0];
+            s_leaf[lane].p1 = s.stones[1];
+            s_leaf[lane].meta = ((uint32_t)s.turn << 24) | ((uint32_t)legal_mask(s.stones[0] | s.stones[1]) << 25);
+        }
+        wave_mem_order();
+        rng_fill(rng, rng.use() + kLookahead);
+        c4_rollouts(s_leaf, cnt, rng, plies);
+        wave_mem_order();
+        if ((int)lane < cnt) out_value[base + lane] = s_leaf[lane].val;
+        wave_mem_order();
+    }
+    if (lane == 0) {
+        out_words[0] = (int64_t)(rng.use() - use0);
+        a.rngpos[2 * (size_t)g] = rng.use();
+        a.rngpos[2 * (size_t)g + 1] = rng.gen;
+    }
+}
+
 __global__ void c4_play_kernel(int n, zc_c4_state *states, const int32_t *moves, int32_t *results, int reset) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
@@ -761,6 +792,11 @@ void launch_c4_rollout_debug(const Arena &a, int M, int first_game, int n, const
     (void)M;
     hipLaunchKernelGGL(c4_rollout_debug_kernel, dim3(n), dim3(kBlock), 0, s, a, first_game, n, states, out_value,
                        out_words);
+}
+
+void launch_c4_rollout_seq(const Arena &a, int game, int n, const zc_c4_state *states, int32_t *out_value,
+                           int64_t *out_words, hipStream_t s) {
+    hipLaunchKernelGGL(c4_rollout_seq_kernel, dim3(1), dim3(kBlock), 0, s, a, game, n, states, out_value, out_words);
 }
 
 void launch_c4_play(int n, zc_c4_state *states, const int32_t *moves, int32_t *results, int reset, hipStream_t s) {

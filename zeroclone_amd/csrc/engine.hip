@@ -62,7 +62,7 @@ int dalloc(zc_engine *e, T **p, size_t count) {
 
 void free_arena(zc::Arena &a) {
     void *ptrs[] = {a.nodes, a.W, a.path, a.ring, a.rngpos,
-                    a.logtab, a.phase, a.roots, a.move, a.na, a.stats};
+                    a.logtab, a.phase, a.roots, a.move, a.na, a.ids, a.stats};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
     a = zc::Arena{};
@@ -157,6 +157,7 @@ int zc_engine_create(const zc_engine_config *cfg, zc_engine **out) {
     if (!rc) rc = dalloc(e, &a.roots, G);
     if (!rc) rc = dalloc(e, &a.move, G);
     if (!rc) rc = dalloc(e, &a.na, G * 7);
+    if (!rc) rc = dalloc(e, &a.ids, G);
     if (!rc) rc = dalloc(e, &a.stats, G);
     if (!rc && hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess)
         rc = fail(ZC_EHIP, "hipStreamCreate failed");
@@ -270,17 +271,18 @@ int zc_c4_search_async(zc_engine *eng, int32_t first, int32_t n, const zc_c4_sta
     return ZC_OK;
 }
 
-int zc_c4_search(zc_engine *eng, int32_t first, int32_t n, const zc_c4_state *roots, int32_t sims, double c,
-                 int32_t bs, int32_t *out_move, int32_t *out_na, zc_game_stats *out_stats) {
-    if (!eng || (n && (!roots || !out_move || !out_na))) return fail(ZC_EINVAL, "null argument");
-    if (int r = check_search(eng, first, n, sims, c, bs)) return r;
-    if (!n) return ZC_OK;
+namespace {
+int search_sync(zc_engine *eng, int32_t first, int32_t n, const int32_t *ids, const zc_c4_state *roots, int32_t sims,
+                double c, int32_t bs, int32_t *out_move, int32_t *out_na, zc_game_stats *out_stats) {
     std::lock_guard<std::mutex> lk(eng->mu);
     ZC_HIP(hipSetDevice(eng->cfg.device));
     zc::Arena &a = eng->a;
     hipStream_t s = eng->stream;
     ZC_HIP(hipMemcpyAsync(a.roots, roots, (size_t)n * sizeof(zc_c4_state), hipMemcpyHostToDevice, s));
-    zc::launch_c4_search(make_params(eng, first, n, a.roots, sims, c, bs, a.move, a.na, a.stats), s);
+    if (ids) ZC_HIP(hipMemcpyAsync(a.ids, ids, (size_t)n * sizeof(int32_t), hipMemcpyHostToDevice, s));
+    zc::SearchParams p = make_params(eng, first, n, a.roots, sims, c, bs, a.move, a.na, a.stats);
+    p.game_ids = ids ? a.ids : nullptr;
+    zc::launch_c4_search(p, s);
     ZC_HIP(hipGetLastError());
     std::vector<zc_game_stats> st((size_t)n);
     ZC_HIP(hipMemcpyAsync(out_move, a.move, (size_t)n * sizeof(int32_t), hipMemcpyDeviceToHost, s));
@@ -289,14 +291,39 @@ int zc_c4_search(zc_engine *eng, int32_t first, int32_t n, const zc_c4_state *ro
     ZC_HIP(hipStreamSynchronize(s));
     if (out_stats) memcpy(out_stats, st.data(), st.size() * sizeof(zc_game_stats));
     for (int32_t i = 0; i < n; ++i) {
+        const int g = ids ? ids[i] : first + i;
         if (st[i].status == ZC_STATUS_NO_MOVES)
-            return fail(ZC_EINVAL, "game %d: root has no legal move (reference: undefined behaviour)", first + i);
+            return fail(ZC_EINVAL, "game %d: root has no legal move (reference: undefined behaviour)", g);
         if (st[i].status == ZC_STATUS_INTERNAL)
-            return fail(ZC_EDEVICE, "game %d: search invariant violated on the device", first + i);
+            return fail(ZC_EDEVICE, "game %d: search invariant violated on the device", g);
         if (st[i].status)
-            return fail(ZC_EINVAL, "game %d: invalid Connect4 state (status %lld)", first + i, (long long)st[i].status);
+            return fail(ZC_EINVAL, "game %d: invalid Connect4 state (status %lld)", g, (long long)st[i].status);
     }
     return ZC_OK;
+}
+}  // namespace
+
+int zc_c4_search(zc_engine *eng, int32_t first, int32_t n, const zc_c4_state *roots, int32_t sims, double c,
+                 int32_t bs, int32_t *out_move, int32_t *out_na, zc_game_stats *out_stats) {
+    if (!eng || (n && (!roots || !out_move || !out_na))) return fail(ZC_EINVAL, "null argument");
+    if (int r = check_search(eng, first, n, sims, c, bs)) return r;
+    if (!n) return ZC_OK;
+    return search_sync(eng, first, n, nullptr, roots, sims, c, bs, out_move, out_na, out_stats);
+}
+
+int zc_c4_search_games(zc_engine *eng, int32_t n, const int32_t *games, const zc_c4_state *roots, int32_t sims,
+                       double c, int32_t bs, int32_t *out_move, int32_t *out_na, zc_game_stats *out_stats) {
+    if (!eng || (n && (!games || !roots || !out_move || !out_na))) return fail(ZC_EINVAL, "null argument");
+    if (int r = check_search(eng, 0, 0, sims, c, bs)) return r;
+    if (n > eng->cfg.max_games) return fail(ZC_ECAPACITY, "%d games > engine capacity %d", n, eng->cfg.max_games);
+    std::vector<char> seen((size_t)eng->cfg.max_games, 0);
+    for (int32_t i = 0; i < n; ++i) {
+        if (games[i] < 0 || games[i] >= eng->cfg.max_games)
+            return fail(ZC_ECAPACITY, "game %d outside engine capacity %d", games[i], eng->cfg.max_games);
+        if (seen[(size_t)games[i]]++) return fail(ZC_EINVAL, "game %d listed twice", games[i]);
+    }
+    if (!n) return ZC_OK;
+    return search_sync(eng, 0, n, games, roots, sims, c, bs, out_move, out_na, out_stats);
 }
 
 int zc_c4_play_async(zc_engine *eng, int32_t n, zc_c4_state *d_states, const int32_t *d_moves, int32_t *d_results,
@@ -308,6 +335,35 @@ int zc_c4_play_async(zc_engine *eng, int32_t n, zc_c4_state *d_states, const int
     hipStream_t s = (hipStream_t)hip_stream;
     zc::launch_c4_play(n, d_states, d_moves, d_results, reset, s);
     ZC_HIP(hipGetLastError());
+    return ZC_OK;
+}
+
+int zc_c4_rollouts(zc_engine *eng, int32_t game, int32_t n, const zc_c4_state *states, int32_t *out_values,
+                   int64_t *out_words) {
+    if (!eng || n < 0 || (n && (!states || !out_values))) return fail(ZC_EINVAL, "bad argument");
+    if (int r = check_games(eng, game, 1)) return r;
+    for (int32_t i = 0; i < n; ++i)
+        if (!valid_c4(states[i])) return fail(ZC_EINVAL, "state %d is not a valid Connect4 position", i);
+    std::lock_guard<std::mutex> lk(eng->mu);
+    ZC_HIP(hipSetDevice(eng->cfg.device));
+    hipStream_t s = eng->stream;
+    zc_c4_state *ds = nullptr;
+    int32_t *dv = nullptr;
+    int64_t *dw = nullptr;
+    ZC_HIP(hipMalloc(&ds, (n ? n : 1) * sizeof(zc_c4_state)));
+    ZC_HIP(hipMalloc(&dv, (n ? n : 1) * sizeof(int32_t)));
+    ZC_HIP(hipMalloc(&dw, sizeof(int64_t)));
+    if (n) ZC_HIP(hipMemcpyAsync(ds, states, (size_t)n * sizeof(zc_c4_state), hipMemcpyHostToDevice, s));
+    zc::launch_c4_rollout_seq(eng->a, game, n, ds, dv, dw, s);
+    ZC_HIP(hipGetLastError());
+    int64_t words = 0;
+    if (n) ZC_HIP(hipMemcpyAsync(out_values, dv, (size_t)n * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    ZC_HIP(hipMemcpyAsync(&words, dw, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    ZC_HIP(hipStreamSynchronize(s));
+    (void)hipFree(ds);
+    (void)hipFree(dv);
+    (void)hipFree(dw);
+    if (out_words) *out_words = words;
     return ZC_OK;
 }
 

@@ -54,12 +54,14 @@ struct Arena {
     zc_c4_state *roots = nullptr;
     int32_t *move = nullptr;
     int32_t *na = nullptr;
+    int32_t *ids = nullptr;
     zc_game_stats *stats = nullptr;
 };
 
 struct SearchParams {
     int first_game, n_games, sims, bs, M;
     double c;
+    const int32_t *game_ids;  // optional: engine game of call entry i (else first_game + i)
     const zc_c4_state *roots;
     int32_t *out_move, *out_na;
     zc_game_stats *out_stats;
@@ -72,6 +74,8 @@ size_t c4_search_lds_bytes(int bs);
 void launch_c4_search(const SearchParams &p, hipStream_t s);
 void launch_c4_rollout_debug(const Arena &a, int M, int first_game, int n, const zc_c4_state *states,
                              int32_t *out_value, int64_t *out_words, hipStream_t s);
+void launch_c4_rollout_seq(const Arena &a, int game, int n, const zc_c4_state *states, int32_t *out_value,
+                           int64_t *out_words, hipStream_t s);
 void launch_c4_play(int n, zc_c4_state *states, const int32_t *moves, int32_t *results, int reset, hipStream_t s);
 void launch_uct_debug(int n, const double *logn, const int32_t *na, const double *q, double c, double *out,
                       hipStream_t s);
