@@ -1,0 +1,165 @@
+"""Device-resident Connect4 self-play and the multi-GPU trajectory exchange.
+
+`C4SelfPlay` is the batched form of scripts/train.py:simulate_games (:151-170) +
+Engine.play_mcts_parallel (engine/engine.py:131-138): G games live on one GPU as bitboards;
+one `step()` searches every game (zc_c4_search_async), plays the chosen moves and
+evaluates them (zc_c4_play_async, Engine.play_move/_evaluate), and restarts finished games
+from the opening — the refill the reference does with add_game.  Game slot g of rank r is
+global game r*G + g and draws from its own CPython MT19937 stream seeded seed + global id,
+so per-game results do not depend on the number of GPUs.
+
+Finished games are labelled exactly as Engine.get_dataset (engine.py:60-89) labels them and
+kept as compact positions (zc_c4_state rows: stones X, stones O, turn | label << 32).
+`gather_positions` all-gathers every rank's finished positions (counts first, then a padded
+payload) over torch.distributed — RCCL over xGMI on the GPUs, gloo on CPU — the one
+collective of the scale-out path.  `ReplayBuffer` is
+scripts/train.py:_update_replay (:27-50).
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from . import _native
+
+ONGOING = _native.ZC_C4_ONGOING
+
+
+def dataset_labels(n_states: int, result: int) -> np.ndarray:
+    """Engine.get_dataset's labels for one finished history of n_states positions
+    (initial ... terminal): factor starts at 0 (draw) or -1, alternates sign, and the
+    per-game list is appended REVERSED (engine.py:72-81)."""
+    factor = 0 if result == 0 else -1
+    entry = []
+    for _ in range(n_states):
+        entry.append(factor)
+        factor = -factor
+    return np.asarray(list(reversed(entry)), dtype=np.float32)
+
+
+def planes(positions: np.ndarray) -> np.ndarray:
+    """Compact rows -> c4_backend.state_to_tensor planes [n, 2, 6, 7] (side to move first)."""
+    n = positions.shape[0]
+    out = np.zeros((n, 2, 6, 7), np.float32)
+    s0 = positions[:, 0].astype(np.uint64)
+    s1 = positions[:, 1].astype(np.uint64)
+    turn = (positions[:, 2] & 1).astype(np.int64)
+    for r in range(6):
+        for c in range(7):
+            bit = np.uint64(1) << np.uint64(7 * c + (5 - r))
+            x = (s0 & bit) != 0
+            o = (s1 & bit) != 0
+            out[:, 0, r, c] = np.where(turn == 0, x, o)
+            out[:, 1, r, c] = np.where(turn == 0, o, x)
+    return out
+
+
+class C4SelfPlay:
+    def __init__(self, games: int, sims: int, c: float = 1.4, batch_size: int = 32, seed: int = 0,
+                 rank: int = 0, device: int = 0, record: bool = True):
+        self.G, self.sims, self.c, self.bs = games, sims, c, batch_size
+        self.dev = torch.device("cuda", device)
+        self.eng = _native.NativeEngine(max_games=games, max_sims=sims, max_batch=batch_size, device=device)
+        self.first_id = rank * games
+        self.eng.seed(0, [seed + self.first_id + g for g in range(games)])
+        self.roots = torch.zeros((games, 3), dtype=torch.int64, device=self.dev)
+        self.moves = torch.zeros(games, dtype=torch.int32, device=self.dev)
+        self.na = torch.zeros((games, 7), dtype=torch.int32, device=self.dev)
+        self.stats = torch.zeros((games, 6), dtype=torch.int64, device=self.dev)
+        self.results = torch.zeros(games, dtype=torch.int32, device=self.dev)
+        self.record = record
+        # current game of every slot: positions so far (host copies, appended per step)
+        self._hist = [[] for _ in range(games)]
+        self.finished = []   # (global game id, move list, result, positions[n,3])
+        self._moves = [[] for _ in range(games)]
+
+    def step(self) -> torch.Tensor:
+        """One move for every game (on torch's current stream); returns the per-game results
+        tensor (ONGOING = 2).  Finished games restart from the opening."""
+        s = torch.cuda.current_stream(self.dev).cuda_stream
+        before = self.roots.clone() if self.record else None
+        self.eng.c4_search_async(self.roots.data_ptr(), self.G, self.sims, self.c, self.bs, self.moves.data_ptr(),
+                                 self.na.data_ptr(), self.stats.data_ptr(), stream=s)
+        self.eng.c4_play_async(self.roots.data_ptr(), self.G, self.moves.data_ptr(), self.results.data_ptr(),
+                               reset=False, stream=s)
+        if self.record:
+            self._collect(before)
+        else:
+            self._refill()
+        return self.results
+
+    def _refill(self):
+        done = self.results != ONGOING
+        self.roots[done] = 0
+
+    def _collect(self, before: torch.Tensor):
+        pre = before.cpu().numpy()
+        post = self.roots.cpu().numpy()
+        res = self.results.cpu().numpy()
+        mv = self.moves.cpu().numpy()
+        for g in range(self.G):
+            if not self._hist[g]:
+                self._hist[g].append(pre[g].copy())
+            self._moves[g].append(int(mv[g]))
+            self._hist[g].append(post[g].copy())
+            if res[g] != ONGOING:
+                pos = np.stack(self._hist[g]).astype(np.int64)
+                lab = dataset_labels(len(pos), int(res[g]))
+                pos[:, 2] = (pos[:, 2] & 1) | (lab.astype(np.int64) << 32)
+                self.finished.append((self.first_id + g, self._moves[g], int(res[g]), pos))
+                self._hist[g], self._moves[g] = [], []
+        self._refill()
+
+    def take_positions(self):
+        """Positions of the games finished since the last call: [n, 3] int64 rows with the
+        Engine.get_dataset label in the high half of column 2."""
+        rows = [f[3] for f in self.finished]
+        self.finished = []
+        return np.concatenate(rows) if rows else np.zeros((0, 3), np.int64)
+
+    def close(self):
+        self.eng.close()
+
+
+def gather_positions(local: torch.Tensor, group=None) -> torch.Tensor:
+    """All-gather variable-length [n_r, 3] int64 position rows from every rank (rank order):
+    an all_gather of the counts, then of payloads padded to the largest count."""
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    n = torch.tensor([local.shape[0]], dtype=torch.int64, device=local.device)
+    counts = [torch.zeros_like(n) for _ in range(world)]
+    dist.all_gather(counts, n, group=group)
+    counts = [int(c.item()) for c in counts]
+    m = max(counts) if counts else 0
+    pad = torch.zeros((m, 3), dtype=torch.int64, device=local.device)
+    pad[: local.shape[0]] = local
+    bufs = [torch.zeros_like(pad) for _ in range(world)]
+    dist.all_gather(bufs, pad, group=group)
+    return torch.cat([b[:c] for b, c in zip(bufs, counts)], dim=0)
+
+
+class ReplayBuffer:
+    """scripts/train.py:_update_replay (:27-50): the training set of a cycle = all new data +
+    a uniform sample (without replacement) of 30 % of everything seen before."""
+
+    def __init__(self, frac_old: float = 0.30, seed: int | None = None):
+        self.frac_old = frac_old
+        self.states, self.values = [], []
+        self.rng = np.random.default_rng(seed)
+
+    def update(self, states_new: np.ndarray, values_new: np.ndarray):
+        if not self.states:
+            self.states.append(states_new)
+            self.values.append(values_new)
+            return states_new, values_new
+        old_s = np.concatenate(self.states, axis=0)
+        old_v = np.concatenate(self.values, axis=0)
+        k = int(self.frac_old * len(old_s))
+        if k > 0:
+            idx = self.rng.choice(len(old_s), k, replace=False)
+            ss, sv = old_s[idx], old_v[idx]
+        else:
+            ss, sv = old_s[:0], old_v[:0]
+        self.states.append(states_new)
+        self.values.append(values_new)
+        return np.concatenate([ss, states_new], axis=0), np.concatenate([sv, values_new], axis=0)
