@@ -85,3 +85,21 @@ def test_engine_parallel_per_game_streams():
     e2.play_mcts_parallel(list(range(n)), sims, 1.4)
     for i in (3, 5, 7):
         assert e.get_state(i) == e2.get_state(i)
+
+
+def test_integration_md_ctypes_stub_works(golden):
+    """The ctypes stub shown in INTEGRATION.md §2 runs as written and is a drop-in."""
+    import os
+    import re
+    from conftest import REPO
+    text = open(os.path.join(REPO, "INTEGRATION.md")).read()
+    block = [b for b in re.findall(r"```python\n(.*?)```", text, re.S) if "zc_ctypes" in b][0]
+    block = block.replace("/path/to/zeroclone_amd/libzeroclone_amd.so",
+                          os.path.join(REPO, "zeroclone_amd", "libzeroclone_amd.so"))
+    ns = {}
+    exec(compile(block, "INTEGRATION.md", "exec"), ns)
+    for c in golden("c4_get_move.json")["cases"][:40]:
+        st = c4.State(dec(c["board"]), c["turn"])
+        random.seed(c["seed"])
+        assert ns["get_move"](st, None, None, None, c["sims"], c["c"], c["bs"]) == (c["move"], 0)
+        assert random.getrandbits(32) == c["next_word"]

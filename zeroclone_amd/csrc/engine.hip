@@ -61,7 +61,7 @@ int dalloc(zc_engine *e, T **p, size_t count) {
 }
 
 void free_arena(zc::Arena &a) {
-    void *ptrs[] = {a.nodes, a.W, a.path, a.ring, a.rngpos,
+    void *ptrs[] = {a.nodes, a.W, a.ring, a.rngpos,
                     a.logtab, a.phase, a.roots, a.move, a.na, a.ids, a.stats};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
@@ -143,12 +143,11 @@ int zc_engine_create(const zc_engine_config *cfg, zc_engine **out) {
     zc_engine *e = new zc_engine();
     e->cfg = *cfg;
     e->M = cfg->max_sims + 1;
-    const size_t G = (size_t)cfg->max_games, M = (size_t)e->M, B = (size_t)cfg->max_batch;
+    const size_t G = (size_t)cfg->max_games, M = (size_t)e->M;
     zc::Arena &a = e->a;
     int rc = ZC_OK;
     if (!rc) rc = dalloc(e, &a.nodes, G * M * zc::kRecBytes);
     if (!rc) rc = dalloc(e, &a.W, G * M * zc::kSlots);
-    if (!rc) rc = dalloc(e, &a.path, G * B * zc::kMaxDepth);
     if (!rc) rc = dalloc(e, &a.ring, G * zc::kRingWords);
     if (!rc) rc = dalloc(e, &a.rngpos, G * 2);
     if (!rc) rc = dalloc(e, &a.logtab, M + 2);

@@ -45,7 +45,6 @@ static_assert(kLookahead + kChunk + 624 + 128 < kRingWords, "ring must retain th
 struct Arena {
     uint8_t *nodes = nullptr;     // [G][M][128 B]
     int32_t *W = nullptr;         // [G][M][8]
-    uint32_t *path = nullptr;     // [G][B][kMaxDepth]  node | pact<<16
     uint32_t *ring = nullptr;     // [G][kRingWords]    raw (untempered) MT words
     uint64_t *rngpos = nullptr;   // [G][2]             {next word to use, words generated}
     double *logtab = nullptr;     // [M+2]              glibc log(n), n = 0..M+1
