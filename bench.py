@@ -88,7 +88,7 @@ def main():
     roots = torch.zeros((G, 3), dtype=torch.int64, device=dev)   # zc_c4_state: stones[2], turn|reserved
     moves = torch.zeros(G, dtype=torch.int32, device=dev)
     na = torch.zeros((G, 7), dtype=torch.int32, device=dev)
-    stats = torch.zeros((G, 6), dtype=torch.int64, device=dev)   # zc_game_stats
+    stats = torch.zeros((G, _native.STATS_FIELDS), dtype=torch.int64, device=dev)   # zc_game_stats
     results = torch.zeros(G, dtype=torch.int32, device=dev)
     acc = torch.zeros(4, dtype=torch.int64, device=dev)          # expansions, depth_sum, finished, leaves
 

@@ -45,6 +45,8 @@ typedef struct zc_game_stats {
     int64_t rollout_plies;   /* plies played inside random rollouts                      */
     int64_t rng_words;       /* MT19937 words consumed                                   */
     int64_t status;          /* 0 = ok; nonzero = internal error code                    */
+    int64_t rollout_blocks;  /* lane-parallel ply blocks the rollouts took                */
+    int64_t reserved;
 } zc_game_stats;
 
 typedef struct zc_engine_config {
@@ -144,7 +146,7 @@ int zc_debug_c4_rollout(zc_engine *eng, int32_t first_game, int32_t n, const zc_
 
 /* Diagnostic phase stamps: returns (into out8, may be NULL) the shader-cycle sums since the
  * previous call, over all games, of {RNG generation, first walk of each flush, resumed
- * walks, expansion + leaf bookkeeping, rollouts, backup, 0, 0}, resets them, and switches
+ * walks, expansion + leaf bookkeeping, rollouts, backup, publish, 0}, resets them, and switches
  * the stamped kernel build on (enable != 0) or off for later searches.  Synchronises the
  * device.  Stamped runs are for phase SHARES only, never for timing. */
 int zc_debug_phase_cycles(zc_engine *eng, int32_t enable, int64_t *out8);

@@ -33,7 +33,8 @@ def main():
         t, st = timed(eng, G, S, B)
         res[G] = {"ms": round(t * 1e3, 3), "Mexp_s": round(st["expansions"].sum() / t / 1e6, 2),
                   "plies_per_leaf": round(st["rollout_plies"].sum() / st["leaves"].sum(), 2),
-                  "words_per_leaf": round(st["rng_words"].sum() / st["leaves"].sum(), 2)}
+                  "words_per_leaf": round(st["rng_words"].sum() / st["leaves"].sum(), 2),
+                  "blocks_per_leaf": round(st["rollout_blocks"].sum() / st["leaves"].sum(), 3)}
         print(G, res[G], flush=True)
     eng.phase_cycles(True)
     roots = np.zeros(4096, _native.C4_STATE_DTYPE)

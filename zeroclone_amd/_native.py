@@ -31,7 +31,8 @@ class C4State(ctypes.Structure):
 
 class GameStats(ctypes.Structure):
     _fields_ = [("expansions", ctypes.c_int64), ("depth_sum", ctypes.c_int64), ("leaves", ctypes.c_int64),
-                ("rollout_plies", ctypes.c_int64), ("rng_words", ctypes.c_int64), ("status", ctypes.c_int64)]
+                ("rollout_plies", ctypes.c_int64), ("rng_words", ctypes.c_int64), ("status", ctypes.c_int64),
+                ("rollout_blocks", ctypes.c_int64), ("reserved", ctypes.c_int64)]
 
 
 class EngineConfig(ctypes.Structure):
@@ -41,9 +42,11 @@ class EngineConfig(ctypes.Structure):
 
 C4_STATE_DTYPE = np.dtype([("stones", "<u8", (2,)), ("turn", "<i4"), ("reserved", "<i4")])
 STATS_DTYPE = np.dtype([("expansions", "<i8"), ("depth_sum", "<i8"), ("leaves", "<i8"),
-                        ("rollout_plies", "<i8"), ("rng_words", "<i8"), ("status", "<i8")])
+                        ("rollout_plies", "<i8"), ("rng_words", "<i8"), ("status", "<i8"),
+                        ("rollout_blocks", "<i8"), ("reserved", "<i8")])
 assert C4_STATE_DTYPE.itemsize == ctypes.sizeof(C4State) == 24
-assert STATS_DTYPE.itemsize == ctypes.sizeof(GameStats) == 48
+assert STATS_DTYPE.itemsize == ctypes.sizeof(GameStats) == 64
+STATS_FIELDS = 8
 
 # Every symbol include/zeroclone.h declares: (name, restype, argtypes)
 SIGNATURES = [
@@ -244,7 +247,8 @@ class NativeEngine:
     def phase_cycles(self, enable: bool):
         out = (ctypes.c_int64 * 8)()
         check(lib().zc_debug_phase_cycles(self._h, int(bool(enable)), out))
-        return dict(zip(["rng", "walk_first", "walk_resumed", "expand", "rollout", "backup"], list(out)[:6]))
+        return dict(zip(["rng", "walk_first", "walk_resumed", "expand", "rollout", "backup", "publish"],
+                        list(out)[:7]))
 
     def debug_c4_rollout(self, states: np.ndarray, first_game: int = 0):
         states = np.ascontiguousarray(states, dtype=C4_STATE_DTYPE)

@@ -211,10 +211,13 @@ struct Fresh {
     uint32_t u;       // untried word (record +4)
     uint32_t ow;      // packed move-list columns (record +12)
     uint32_t link;    // parent | pact << 16 | depth << 24 (record +8)
-    uint32_t pad;
+    uint32_t pad0;
+    int32_t na;       // the edge INTO this node: Na (backup accumulates here, LDS atomics)
+    int32_t w;        //                          Wa
+    uint32_t pad1, pad2;
     uint16_t ch[8];   // children (record +16)
 };
-static_assert(sizeof(Fresh) == 32, "Fresh is two 16-byte LDS slots");
+static_assert(sizeof(Fresh) == 48, "Fresh is three 16-byte LDS slots");
 
 __device__ __forceinline__ uint64_t readlane64(uint64_t x, int l) {
     return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(x >> 32), l) << 32) |
@@ -264,7 +267,7 @@ __device__ __forceinline__ uint64_t scan_or(uint64_t x) {
 // build each player's stones after every ply, and every lane tests check_win / full board
 // / column filled for ITS ply.  The first lane with an event ends the block (a fill changes
 // the legal set, so the next block restarts from the following word).
-__device__ void c4_rollouts(Leaf *L, int nb, Rng &rng, int64_t &plies_total) {
+__device__ void c4_rollouts(Leaf *L, int nb, Rng &rng, int64_t &plies_total, int64_t &blocks) {
     const uint32_t lane = lane_id();
     for (int j = 0; j < nb; ++j) {
         const uint64_t x0 = uni64(L[j].p0);
@@ -291,6 +294,7 @@ __device__ void c4_rollouts(Leaf *L, int nb, Rng &rng, int64_t &plies_total) {
                     rng.off = kWin;
                     continue;
                 }
+                ++blocks;
                 const uint32_t qk = mbcnt(A);                    // this lane's ply in the block
                 const uint32_t col = (ow >> (3 * (v & 7u))) & 7u;  // its column (if accepted)
                 // earlier plies in the same column: 4-bit per-column counters, prefix-summed
@@ -394,7 +398,7 @@ __device__ __forceinline__ bool valid_state(uint64_t p0, uint64_t p1, int turn) 
 template <bool STAMP>
 __global__ __launch_bounds__(kBlock) void c4_search_kernel(SearchParams p) {
     extern __shared__ __attribute__((aligned(16))) uint8_t s_dyn[];
-    // LDS (16-byte aligned pieces first): fresh[bs] (32 B), leaves[bs] (24 B), paths[bs][kMaxDepth]
+    // LDS (16-byte aligned pieces first): fresh[bs] (48 B), leaves[bs] (24 B), paths[bs][kMaxDepth]
     Fresh *const fresh = (Fresh *)s_dyn;
     Leaf *const leaves = (Leaf *)(s_dyn + sizeof(Fresh) * (size_t)p.bs);
     uint32_t *const paths = (uint32_t *)(s_dyn + (sizeof(Fresh) + sizeof(Leaf)) * (size_t)p.bs);
@@ -404,7 +408,8 @@ __global__ __launch_bounds__(kBlock) void c4_search_kernel(SearchParams p) {
         (const __attribute__((address_space(4))) double *)p.a.logtab;
 
     const uint32_t lane = lane_id();
-    const int gl = blockIdx.x;  // game within this call (one wave per game)
+    const uint32_t k = lane & 7u;  // child slot handled by this lane (lanes 8.. mirror 0..7)
+    const int gl = blockIdx.x;     // game within this call (one wave per game)
     if (gl >= p.n_games) return;
     const int g = p.game_ids ? uni(p.game_ids[gl]) : p.first_game + gl;
 
@@ -436,10 +441,10 @@ __global__ __launch_bounds__(kBlock) void c4_search_kernel(SearchParams p) {
 
     uint64_t ph[kPhases] = {};
     uint64_t tstamp = STAMP ? __builtin_amdgcn_s_memtime() : 0;
-#define ZC_STAMP(k)                                          \
+#define ZC_STAMP(k_)                                         \
     if (STAMP) {                                             \
         const uint64_t now_ = __builtin_amdgcn_s_memtime();  \
-        ph[k] += now_ - tstamp;                              \
+        ph[k_] += now_ - tstamp;                             \
         tstamp = now_;                                       \
     }
     for (int done = 0; done < p.sims;) {
@@ -448,105 +453,89 @@ __global__ __launch_bounds__(kBlock) void c4_search_kernel(SearchParams p) {
         ZC_STAMP(0)
 
         // ---- selection + expansion of nb leaves (mcts.cpp:129-147) -------------------------
-        // Within a flush no backup happens, so UCT scores on the path above the node that
-        // was just expanded cannot change: leaf j+1's walk resumes there (exactly the walk
-        // the reference repeats from the root), from a register copy of that node.  Nodes
-        // created in this flush ("fresh": id >= f0) have Na = Q = 0 on every edge; their
-        // untried list and children are mirrored in LDS, so walking them needs no HBM read.
-        // N of a node is its parent's Na on the edge in (root: leaves flushed so far).
-        // Lane l holds level l of the current path.
+        // No backup happens inside a flush, so (1) the UCT path from the root to the node X0
+        // where the flush's first walk stops is shared by every leaf of the flush (each walk
+        // resumes where the previous one expanded, always at or below X0), and (2) every node
+        // below X0 is created in this flush ("fresh": id >= f0, Na = Q = 0 on every edge).
+        // The reference's walk from a node without untried moves takes the first child with
+        // the largest UCT; an unvisited child scores +inf, so below X0 that is simply the
+        // lowest slot holding a fresh child — no arithmetic, no HBM.  Fresh nodes live in
+        // LDS until the flush is published.  Lane l holds level l of the current path.
         const int f0 = nnodes;
-        int xnode = 0, xdepth = 0, xturn = rturn, xN = done;
-        uint64_t x0 = rp0, x1 = rp1;
+        int node = 0, depth = 0, turn = rturn, nN = done;  // nN = N(node) = Na of its in-edge
+        uint64_t b0 = rp0, b1 = rp1;
         uint32_t pathv = (lane == 0) ? 0x00FF0000u : 0u;
-        int c_node = -1;  // register copy of one record: the node the last walk ended at
-        bool c_dirty = false;  // copy of an older (HBM) node modified by expansions
-        uint32_t c_u = 0, c_ow = 0;
-        uint32_t c_ch = 0xFFFF;
-        int32_t c_na = 0;
-        double c_q = 0.0;
-        const uint32_t k = lane & 7u;
-        for (int j = 0; j < nb; ++j) {
-            int node = xnode, depth = xdepth, turn = xturn, nN = xN;
-            uint64_t b0 = x0, b1 = x1;
-            uint32_t u, ow;
-            ZC_STAMP(3)
-            for (;;) {  // select (mcts.cpp:47-63)
-                uint32_t ch;
-                int32_t na;
-                double q;
-                if (node == c_node) {
-                    u = c_u;
-                    ow = c_ow;
-                    ch = c_ch;
-                    na = c_na;
-                    q = c_q;
-                } else {
-                    if (c_dirty) {  // write the modified older node back before dropping the copy
-                        if (lane == 0) t.hdr(c_node)[1] = c_u;
-                        if (lane < kSlots) t.child(c_node)[lane] = (uint16_t)c_ch;
-                        c_dirty = false;
-                    }
-                    if (node >= f0) {
-                        const Fresh &F = fresh[node - f0];
-                        u = uni(F.u);
-                        ow = uni(F.ow);
-                        ch = F.ch[k];
-                        na = 0;
-                        q = 0.0;
-                    } else {
-                        const uint8_t *R = t.rec(node);
-                        const uint4 h = *(const uint4 *)R;
-                        ch = ((const uint16_t *)(R + 16))[k];
-                        na = ((const int32_t *)(R + 32))[k];
-                        q = ((const double *)(R + 64))[k];
-                        u = uni(h.y);
-                        ow = uni(h.w);
-                    }
-                }
-                const double lg = logtab[nN];  // log(N), glibc values tabulated on the host
-                c_node = node;
-                c_u = u;
-                c_ow = ow;
-                c_ch = ch;
-                c_na = na;
-                c_q = q;
-                if ((u >> 24) & 15u) break;  // untried moves left: expand here
-                if (depth >= kMaxDepth - 2) {  // unreachable (a C4 tree is <= 42 deep); never spin
-                    st.status = ZC_STATUS_INTERNAL;
-                    u = 0;
-                    break;
-                }
-                const uint32_t nm = u >> 28;
-                // UCT (mcts.cpp:41-45) = fma(c, sqrt(log(N)/Na), Qa); unvisited -> +inf
-                double v = (k < nm && ch != 0xFFFF) ? (na == 0 ? INFINITY : fma(p.c, sqrt(lg / (double)na), q))
-                                                    : -INFINITY;
+        uint32_t u, ow, ch;  // the current node's record (ch: slot k)
+        for (;;) {  // the first walk: select (mcts.cpp:47-63) over HBM records
+            const uint8_t *R = t.rec(node);
+            const uint4 h = *(const uint4 *)R;
+            ch = ((const uint16_t *)(R + 16))[k];
+            const int32_t na = ((const int32_t *)(R + 32))[k];
+            const double q = ((const double *)(R + 64))[k];
+            const double lg = logtab[nN];  // log(N), glibc values tabulated on the host
+            u = uni(h.y);
+            ow = uni(h.w);
+            if ((u >> 24) & 15u) break;    // untried moves left: expand here
+            if (depth >= kMaxDepth - 2) {  // unreachable (a C4 tree is <= 42 deep); never spin
+                st.status = ZC_STATUS_INTERNAL;
+                u = 0;
+                break;
+            }
+            const uint32_t nm = u >> 28;
+            const bool valid = k < nm && ch != 0xFFFF;
+            int best;
+            const uint64_t unvisited = __ballot(valid && na == 0) & 0xFFull;
+            if (unvisited) {  // +inf beats everything; first such slot
+                best = __builtin_ctzll(unvisited);
+            } else {
+                // UCT (mcts.cpp:41-45) = fma(c, sqrt(log(N)/Na), Qa), first max in slot order
+                double v = valid ? fma(p.c, sqrt(lg / (double)na), q) : -INFINITY;
                 int bi = (int)k;
                 argmax8(v, bi);
-                const int best = uni(bi);
-                if ((__ballot(v == -INFINITY) & 1ull) != 0) break;  // no child: terminal node is its own leaf
-                const int nxt = __builtin_amdgcn_readlane((int)ch, best);
-                nN = __builtin_amdgcn_readlane(na, best);
-                const uint64_t bit = drop_bit(b0 | b1, (int)((ow >> (3 * best)) & 7u));
+                if ((__ballot(v == -INFINITY) & 1ull) != 0) break;  // no child: terminal leaf
+                best = uni(bi);
+            }
+            const int nxt = __builtin_amdgcn_readlane((int)ch, best);
+            nN = __builtin_amdgcn_readlane(na, best);
+            const uint64_t bit = drop_bit(b0 | b1, (int)((ow >> (3 * best)) & 7u));
+            if (turn) b1 |= bit; else b0 |= bit;
+            turn ^= 1;
+            node = nxt;
+            ++depth;
+            if (lane == (uint32_t)depth) pathv = (uint32_t)node | ((uint32_t)best << 16);
+        }
+        const int x0node = node, d0 = depth;  // X0: shared by every leaf of this flush
+        const uint32_t ppath = pathv;         // root .. X0 (lanes 0..d0)
+        bool x0_dirty = false;
+        uint32_t x_u = u, x_ch = ch;          // X0's record as last seen (written back if dirty)
+        ZC_STAMP(1)
+
+        for (int j = 0; j < nb; ++j) {
+            // resume at `node` (fully described by u, ow, ch in registers)
+            for (;;) {
+                if ((u >> 24) & 15u) break;  // untried moves: expand here
+                const uint64_t fm = __ballot(k < (u >> 28) && ch != 0xFFFF && (int)ch >= f0) & 0xFFull;
+                if (!fm) break;              // no child at all: terminal, re-queued as its own leaf
+                const int s = __builtin_ctzll(fm);
+                const int child = __builtin_amdgcn_readlane((int)ch, s);
+                if (node == x0node) {  // leaving X0 for good (walks never go back up)
+                    x_u = u;
+                    x_ch = ch;
+                }
+                const uint64_t bit = drop_bit(b0 | b1, (int)((ow >> (3 * s)) & 7u));
                 if (turn) b1 |= bit; else b0 |= bit;
                 turn ^= 1;
-                node = nxt;
                 ++depth;
-                if (lane == (uint32_t)depth) pathv = (uint32_t)node | ((uint32_t)best << 16);
+                if (lane == (uint32_t)depth) pathv = (uint32_t)child | ((uint32_t)s << 16);
+                node = child;
+                const Fresh &F = fresh[child - f0];
+                u = uni(F.u);
+                ow = uni(F.ow);
+                ch = F.ch[k];
             }
-            if (j == 0) {
-                ZC_STAMP(1)
-            } else {
-                ZC_STAMP(2)
-            }
-            // the walk ends here; leaf j+1 resumes from this node (c_node == node)
-            xnode = node;
-            xdepth = depth;
-            xturn = turn;
-            xN = nN;
-            x0 = b0;
-            x1 = b1;
-            int leaf = node;
+            ZC_STAMP(2)
+            int leaf = node, ldepth = depth, lturn = turn;
+            uint64_t l0 = b0, l1 = b1;
             int lmask;
             const uint32_t cnt = (u >> 24) & 15u;
             if (cnt) {  // expand (mcts.cpp:65-78): policy = random.choice(untried)
@@ -555,116 +544,150 @@ __global__ __launch_bounds__(kBlock) void c4_search_kernel(SearchParams p) {
                 const int mi = (int)((digits >> (3 * r)) & 7u);
                 const uint32_t low = (1u << (3 * r)) - 1u;
                 const uint32_t rest = (digits & low) | ((digits >> 3) & ~low & 0x1FFFFFu);
-                const uint32_t nu = rest | ((cnt - 1u) << 24) | (u & 0xF0000000u);
+                u = rest | ((cnt - 1u) << 24) | (u & 0xF0000000u);
                 const uint64_t bit = drop_bit(b0 | b1, (int)((ow >> (3 * mi)) & 7u));
-                if (turn) b1 |= bit; else b0 |= bit;
-                turn ^= 1;
+                if (turn) l1 |= bit; else l0 |= bit;
+                lturn = turn ^ 1;
                 leaf = nnodes++;
-                ++depth;
-                lmask = legal_mask(b0 | b1);
+                ldepth = depth + 1;
+                lmask = legal_mask(l0 | l1);
                 const uint32_t low_ = d_order[lmask];
-                // parent: untried list and child link (copy; and LDS if the parent is fresh)
-                c_u = nu;
-                if (k == (uint32_t)mi) c_ch = (uint32_t)leaf;
-                if (node >= f0) {
-                    if (lane == 0) fresh[node - f0].u = nu;
+                if (k == (uint32_t)mi) ch = (uint32_t)leaf;
+                if (node >= f0) {  // the parent's copy in LDS
+                    if (lane == 0) fresh[node - f0].u = u;
                     if (lane == (uint32_t)mi) fresh[node - f0].ch[mi] = (uint16_t)leaf;
                 } else {
-                    c_dirty = true;
+                    x0_dirty = true;  // X0 itself: written back when the flush is published
                 }
-                // the new node (Node ctor, mcts.cpp:23-34): all moves untried, no children
-                {
+                {  // Node(state, legal_moves) (mcts.cpp:23-34): all moves untried, no children
                     Fresh &F = fresh[leaf - f0];
                     const uint32_t n = (low_ >> 24) & 15u;
                     if (lane == 0) {
                         F.u = (kIdentDigits & ((1u << (3 * n)) - 1u)) | (n << 24) | (n << 28);
                         F.ow = low_;
-                        F.link = (uint32_t)node | ((uint32_t)mi << 16) | ((uint32_t)depth << 24);
+                        F.link = (uint32_t)node | ((uint32_t)mi << 16) | ((uint32_t)ldepth << 24);
+                        F.na = 0;
+                        F.w = 0;
                     }
                     if (lane < kSlots) F.ch[lane] = 0xFFFF;
                 }
-                if (lane == (uint32_t)depth) pathv = (uint32_t)leaf | ((uint32_t)mi << 16);
                 st.expansions += 1;
-                st.depth_sum += depth;
+                st.depth_sum += ldepth;
             } else {
-                lmask = legal_mask(b0 | b1);  // terminal leaf
+                lmask = legal_mask(b0 | b1);
             }
+            // the leaf's path: the walk's path plus the new node (the next walk resumes at `node`)
+            const uint32_t lpath = (cnt && lane == (uint32_t)ldepth) ? (uint32_t)leaf : pathv;
             if (lane == 0) {
-                leaves[j].p0 = b0;
-                leaves[j].p1 = b1;
-                leaves[j].meta = (uint32_t)leaf | ((uint32_t)depth << 16) | ((uint32_t)turn << 24) |
+                leaves[j].p0 = l0;
+                leaves[j].p1 = l1;
+                leaves[j].meta = (uint32_t)leaf | ((uint32_t)ldepth << 16) | ((uint32_t)lturn << 24) |
                                  ((uint32_t)lmask << 25);
             }
-            if (lane < (uint32_t)kMaxDepth) paths[j * kMaxDepth + lane] = pathv;
+            if (lane < (uint32_t)kMaxDepth) paths[j * kMaxDepth + lane] = lpath;
             wave_mem_order();
+            ZC_STAMP(3)
         }
-        // ---- publish this flush's tree changes to HBM --------------------------------------
-        if (c_dirty) {
-            if (lane == 0) t.hdr(c_node)[1] = c_u;
-            if (lane < kSlots) t.child(c_node)[lane] = (uint16_t)c_ch;
+        if (node == x0node) {
+            x_u = u;
+            x_ch = ch;
         }
-        {
-            // each fresh record = 8 x 16 B: {N=0, u, link, ow}, children, Na = 0 (2), Q = 0 (4)
-            const int nf = nnodes - f0;
-            for (int base = 0; base < nf * 8; base += 64) {
-                const int idx = base + (int)lane;
-                if (idx < nf * 8) {
-                    const int r = idx >> 3, part = idx & 7;
-                    const Fresh &F = fresh[r];
-                    uint4 v = make_uint4(0u, 0u, 0u, 0u);
-                    if (part == 0) v = make_uint4(0u, F.u, F.link, F.ow);
-                    else if (part == 1) v = *(const uint4 *)F.ch;
-                    *(uint4 *)(t.rec(f0 + r) + 16 * part) = v;
-                }
-            }
-            for (int base = 0; base < nf * 2; base += 64) {  // W rows: 2 x 16 B of zeros
-                const int idx = base + (int)lane;
-                if (idx < nf * 2) *(uint4 *)(t.w(f0 + (idx >> 1)) + 4 * (idx & 1)) = make_uint4(0u, 0u, 0u, 0u);
-            }
-        }
-        ZC_STAMP(3)
 
         // ---- value.batch: random rollouts in pending order (mcts.cpp:112-124) ---------------
-        c4_rollouts(leaves, nb, rng, plies);
+        c4_rollouts(leaves, nb, rng, plies, st.rollout_blocks);
         wave_mem_order();
         ZC_STAMP(4)
 
-        // ---- backprop in pending order (mcts.cpp:80-100, :124-125) --------------------------
-        // Lane l >= 1 updates the edge into level l of the leaf's path (Na += 1, Wa -= r,
-        // Qa = Wa/Na; r alternates sign per level).  Node::N is not stored: it always equals
-        // the parent's Na on the edge in (root: the leaves flushed so far).  A node's level
-        // never changes, so every read-modify-write of a given word stays in one lane, in
-        // leaf order.
+        // ---- backprop of the whole flush (mcts.cpp:80-100, :124-125) ------------------------
+        // Leaf j adds Na += 1 and Wa -= v_j * (-1)^(d_j - l) on the edge into level l of its
+        // path, l = 1..d_j.  Integer adds commute, so the flush is applied as a sum:
+        //   levels 1..d0 (root -> X0, on every path): Na += nb, Wa -= (-1)^l * S with
+        //     S = sum_j v_j (-1)^d_j — one read-modify-write per level, all levels at once;
+        //   levels > d0 (fresh nodes): LDS atomics into the fresh node's in-edge counters,
+        //     written to HBM with the fresh records below.
+        // Node::N is not stored: it equals Na of the in-edge (root: leaves flushed so far).
+        int S = 0;
+        for (int base = 0; base < nb; base += 64) {
+            const int jj = base + (int)lane;
+            int sv = 0;
+            if (jj < nb) {
+                const int v = leaves[jj].val;
+                sv = ((leaves[jj].meta >> 16) & 1u) ? -v : v;
+            }
+            S += __popcll(__ballot(sv > 0)) - __popcll(__ballot(sv < 0));
+        }
         for (int j = 0; j < nb; ++j) {
             const uint32_t meta = uni(leaves[j].meta);
             const int d = (int)((meta >> 16) & 0xFFu);
             const int v = uni(leaves[j].val);
-            if (lane >= 1 && lane <= (uint32_t)d) {
-                const uint32_t e = paths[j * kMaxDepth + lane];
-                const int par = (int)(paths[j * kMaxDepth + lane - 1] & 0xFFFFu);
-                const int act = (int)(e >> 16);
+            if (lane > (uint32_t)d0 && lane <= (uint32_t)d) {
+                const int fi = (int)(paths[j * kMaxDepth + lane] & 0xFFFFu) - f0;
                 const int vl = ((d - (int)lane) & 1) ? -v : v;
-                const int32_t na1 = t.na(par)[act] + 1;
-                const int32_t w1 = t.w(par)[act] - vl;  // Wa -= result
-                t.na(par)[act] = na1;
-                t.w(par)[act] = w1;
-                t.q(par)[act] = (double)w1 / (double)na1;  // Qa = Wa / Na
+                atomicAdd(&fresh[fi].na, 1);
+                atomicAdd(&fresh[fi].w, -vl);
             }
-            wave_mem_order();
         }
+        if (lane >= 1 && lane <= (uint32_t)d0) {
+            const int par = __shfl((int)(ppath & 0xFFFFu), (int)lane - 1);
+            const int act = (int)(ppath >> 16);
+            const int dw = (lane & 1u) ? S : -S;  // Wa -= (-1)^l * S
+            const int32_t na1 = t.na(par)[act] + nb;
+            const int32_t w1 = t.w(par)[act] + dw;
+            t.na(par)[act] = na1;
+            t.w(par)[act] = w1;
+            t.q(par)[act] = (double)w1 / (double)na1;  // Qa = Wa / Na
+        }
+        wave_mem_order();
         ZC_STAMP(5)
+
+        // ---- publish: X0's changes and every fresh node, in coalesced stores ------------------
+        if (x0_dirty) {
+            if (lane == 0) t.hdr(x0node)[1] = x_u;
+            if (lane < kSlots) {
+                t.child(x0node)[lane] = (uint16_t)x_ch;
+                if (x_ch != 0xFFFF && (int)x_ch >= f0) {  // edge into a fresh child
+                    const int32_t na = fresh[x_ch - f0].na, w = fresh[x_ch - f0].w;
+                    t.na(x0node)[lane] = na;
+                    t.w(x0node)[lane] = w;
+                    t.q(x0node)[lane] = (double)w / (double)na;
+                }
+            }
+        }
+        {
+            const int nf = nnodes - f0;
+            for (int base = 0; base < nf * 8; base += 64) {
+                const int idx = base + (int)lane;
+                if (idx < nf * 8) {
+                    const int r = idx >> 3, slot = idx & 7;
+                    const Fresh &F = fresh[r];
+                    const uint16_t c = F.ch[slot];
+                    int32_t na = 0, w = 0;
+                    if (c != 0xFFFF) {
+                        na = fresh[c - f0].na;
+                        w = fresh[c - f0].w;
+                    }
+                    uint8_t *R = t.rec(f0 + r);
+                    if (slot == 0) *(uint4 *)R = make_uint4(0u, F.u, F.link, F.ow);
+                    ((uint16_t *)(R + 16))[slot] = c;
+                    ((int32_t *)(R + 32))[slot] = na;
+                    ((double *)(R + 64))[slot] = na ? (double)w / (double)na : 0.0;
+                    t.w(f0 + r)[slot] = w;
+                }
+            }
+        }
+        wave_mem_order();
+        ZC_STAMP(6)
         st.leaves += nb;
         done += nb;
     }
 #undef ZC_STAMP
     if (STAMP && lane == 0)
-        for (int k = 0; k < kPhases; ++k) a.phase[kPhases * (size_t)g + k] += (int64_t)ph[k];
+        for (int k_ = 0; k_ < kPhases; ++k_) a.phase[kPhases * (size_t)g + k_] += (int64_t)ph[k_];
 
     // ---- best move: first max of child N over the root's move list (mcts.cpp:150-157) ----
     const uint32_t u = uni(t.hdr(0)[1]);
     const uint32_t ow = uni(t.hdr(0)[3]);
     const uint32_t nm = u >> 28;
-    const uint32_t k = lane & 7u;
     int bv = (k < nm) ? t.na(0)[k] : -1;
     int bi = (int)k;
     argmax8(bv, bi);
@@ -705,7 +728,8 @@ __global__ __launch_bounds__(kBlock) void c4_rollout_debug_kernel(Arena a, int f
     }
     wave_mem_order();
     int64_t plies = 0;
-    c4_rollouts(s_leaf, 1, rng, plies);
+    int64_t blocks = 0;
+    c4_rollouts(s_leaf, 1, rng, plies, blocks);
     wave_mem_order();
     if (lane == 0) {
         out_value[gl] = s_leaf[0].val;
@@ -723,7 +747,7 @@ __global__ __launch_bounds__(kBlock) void c4_rollout_seq_kernel(Arena a, int g, 
     Rng rng;
     const uint64_t use0 = uni64(a.rngpos[2 * (size_t)g]);
     rng_open(rng, a.ring + (size_t)g * kRingWords, use0, uni64(a.rngpos[2 * (size_t)g + 1]));
-    int64_t plies = 0;
+    int64_t plies = 0, blocks = 0;
     for (int base = 0; base < n; base += kBlock) {
         const int cnt = min(kBlock, n - base);
         if ((int)lane < cnt) {
@@ -734,7 +758,7 @@ __global__ __launch_bounds__(kBlock) void c4_rollout_seq_kernel(Arena a, int g, 
         }
         wave_mem_order();
         rng_fill(rng, rng.use() + kLookahead);
-        c4_rollouts(s_leaf, cnt, rng, plies);
+        c4_rollouts(s_leaf, cnt, rng, plies, blocks);
         wave_mem_order();
         if ((int)lane < cnt) out_value[base + lane] = s_leaf[lane].val;
         wave_mem_order();

@@ -65,7 +65,7 @@ class C4SelfPlay:
         self.roots = torch.zeros((games, 3), dtype=torch.int64, device=self.dev)
         self.moves = torch.zeros(games, dtype=torch.int32, device=self.dev)
         self.na = torch.zeros((games, 7), dtype=torch.int32, device=self.dev)
-        self.stats = torch.zeros((games, 6), dtype=torch.int64, device=self.dev)
+        self.stats = torch.zeros((games, _native.STATS_FIELDS), dtype=torch.int64, device=self.dev)
         self.results = torch.zeros(games, dtype=torch.int32, device=self.dev)
         self.record = record
         # current game of every slot: positions so far (host copies, appended per step)
