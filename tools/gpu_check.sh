@@ -26,12 +26,6 @@ for st in "$@"; do
     prof)   run prof 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv \
                 -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline || exit $? ;;
     diag)   run diag 600 python tools/diag_c4.py || exit $? ;;
-    pcs)    run pcs 600 rocprofv3 --pc-sampling-beta-enabled --pc-sampling-method stochastic \
-                --pc-sampling-unit cycles --pc-sampling-interval 65536 --output-format csv -d gpurun_out/pcs -o pcs \
-                -- python3 tools/one_search.py --reps 2 || exit $? ;;
-    pcsh)   run pcsh 600 rocprofv3 --pc-sampling-beta-enabled --pc-sampling-method host_trap \
-                --pc-sampling-unit time --pc-sampling-interval 1 --output-format csv -d gpurun_out/pcsh -o pcsh \
-                -- python3 tools/one_search.py --reps 2 || exit $? ;;
     pmc)    run pmc 600 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/pmc -o pmc \
                 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY \
                 -- python3 tools/one_search.py --reps 2 || exit $? ;;

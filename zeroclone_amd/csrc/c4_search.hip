@@ -34,7 +34,29 @@ constexpr uint32_t kRingMask = kRingWords - 1;
 constexpr uint64_t kBottom = 0x0000040810204081ull;  // bit 7c: bottom cell of column c
 constexpr uint64_t kFull = kBottom * 0x3Full;        // the 42 playable cells
 constexpr uint64_t kTop = kBottom << 5;              // top playable cell of each column
-constexpr uint32_t kIdentDigits = 0 | (1u << 3) | (2u << 6) | (3u << 9) | (4u << 12) | (5u << 15) | (6u << 18);
+constexpr int kTabBytes = 128 * 4 + 128 * 8;  // LDS tables: move-list order[128], select[128][8]
+
+// Untried moves of a node (record +4 / Fresh.u): bit i (i < 7) set while move i of the
+// node's move list is untried; bits 28..31 = number of moves.  The reference keeps the
+// untried INDICES in list order and lets random.choice pick the r-th (mcts.cpp:67-72); the
+// r-th remaining index is the r-th set bit of the mask (table sel[mask][r]).
+__device__ __forceinline__ uint32_t untried_init(uint32_t n) { return ((1u << n) - 1u) | (n << 28); }
+__device__ __forceinline__ uint32_t untried_count(uint32_t u) { return (uint32_t)__popc(u & 0x7Fu); }
+
+// Fill the LDS tables (whole wave): s_order = d_order, s_sel[m*8 + r] = r-th set bit of m.
+__device__ __forceinline__ void load_tables(uint32_t *s_order, uint8_t *s_sel) {
+    for (int i = (int)threadIdx.x; i < 128; i += blockDim.x) s_order[i] = d_order[i];
+    for (int i = (int)threadIdx.x; i < 1024; i += blockDim.x) {
+        const uint32_t m = (uint32_t)i >> 3, r = (uint32_t)i & 7u;
+        uint32_t x = m, c = 0, bitpos = 7;
+        for (uint32_t b = 0; b < 7; ++b)
+            if ((x >> b) & 1u) {
+                if (c == r) { bitpos = b; break; }
+                ++c;
+            }
+        s_sel[i] = (uint8_t)bitpos;
+    }
+}
 constexpr int kWin = 64;                             // RNG window: one word per lane
 
 // ------------------------------------------------------------------ wave helpers
@@ -123,59 +145,70 @@ __device__ __forceinline__ uint32_t temper(uint32_t y) {
 // it kChunk words at a time, all lanes in parallel (every input is >= 227 words older).
 struct Rng {
     uint32_t *ring;
-    uint64_t gen;    // words generated so far                              (uniform)
-    uint64_t wbase;  // window start, a multiple of 64                      (uniform)
-    uint32_t off;    // next word to consume = wbase + off, off in [0, 64]   (uniform)
-    uint32_t wt;     // tempered x[wbase + lane]
-    uint32_t wn;     // raw x[wbase + 64 + lane], in flight until the window advances
-    __device__ __forceinline__ uint64_t use() const { return wbase + off; }
+    uint32_t base;   // low 32 bits of the absolute position at the search's start (use0)
+    int32_t wrel;    // window start - use0 (a multiple of 64 in absolute terms; may be < 0)
+    uint32_t off;    // next word to consume = window start + off, off in [0, 64]
+    int32_t grel;    // words generated so far - use0
+    uint32_t wt;     // tempered x[window start + lane]
+    uint32_t wn;     // raw x[window start + 64 + lane], in flight until the window advances
+    __device__ __forceinline__ int32_t use() const { return wrel + (int32_t)off; }  // relative to use0
+    __device__ __forceinline__ uint32_t slot(int32_t rel) const { return (base + (uint32_t)rel) & kRingMask; }
 };
 
-__device__ __forceinline__ uint64_t rng_generate(uint32_t *ring, uint64_t gen, uint64_t target) {
+__device__ __forceinline__ int32_t rng_generate(uint32_t *ring, uint32_t base, int32_t grel, int32_t target) {
     const uint32_t lane = lane_id();
     constexpr int K = kChunk / 64;
-    while (gen < target) {
+    while (grel < target) {
         // every input of the chunk is >= 227 words older than any output: load all, then store
         uint32_t a[K], b[K], m[K];
+        const uint32_t p0 = base + (uint32_t)grel + lane;
 #pragma unroll
         for (int k = 0; k < K; ++k) {
-            const uint32_t p = (uint32_t)gen + lane + 64u * k;
+            const uint32_t p = p0 + 64u * k;
             a[k] = ring[(p - 624) & kRingMask];
             b[k] = ring[(p - 623) & kRingMask];
             m[k] = ring[(p - 227) & kRingMask];
         }
 #pragma unroll
         for (int k = 0; k < K; ++k) {
-            const uint32_t p = (uint32_t)gen + lane + 64u * k;
+            const uint32_t p = p0 + 64u * k;
             const uint32_t y = (a[k] & 0x80000000u) | (b[k] & 0x7fffffffu);
             ring[p & kRingMask] = m[k] ^ (y >> 1) ^ ((b[k] & 1u) ? 0x9908b0dfu : 0u);
         }
-        gen += kChunk;
+        grel += kChunk;
         wave_mem_order();
     }
-    return gen;
+    return grel;
 }
 
-__device__ __forceinline__ void rng_fill(Rng &r, uint64_t target) {
-    if (r.gen < target) r.gen = rng_generate(r.ring, r.gen, target);
+__device__ __forceinline__ void rng_fill(Rng &r, int32_t target) {
+    if (r.grel < target) r.grel = rng_generate(r.ring, r.base, r.grel, target);
 }
 
-__device__ __forceinline__ void rng_open(Rng &r, uint32_t *ring, uint64_t use, uint64_t gen) {
+// use0 / gen0: absolute positions (words consumed / generated) from the game's rngpos.
+__device__ __forceinline__ void rng_open(Rng &r, uint32_t *ring, uint64_t use0, uint64_t gen0) {
     r.ring = ring;
-    r.gen = gen;
-    r.wbase = use & ~(uint64_t)(kWin - 1);
-    r.off = (uint32_t)(use - r.wbase);
-    rng_fill(r, r.wbase + 2 * kWin);
-    r.wt = temper(r.ring[(r.wbase + lane_id()) & kRingMask]);
-    r.wn = r.ring[(r.wbase + kWin + lane_id()) & kRingMask];
+    r.base = (uint32_t)use0;
+    r.grel = (int32_t)(gen0 - use0);
+    r.off = (uint32_t)use0 & (uint32_t)(kWin - 1);
+    r.wrel = -(int32_t)r.off;
+    rng_fill(r, r.wrel + 2 * kWin);
+    r.wt = temper(r.ring[r.slot(r.wrel + (int32_t)lane_id())]);
+    r.wn = r.ring[r.slot(r.wrel + kWin + (int32_t)lane_id())];
 }
 
 __device__ __forceinline__ void rng_advance(Rng &r) {
-    r.wbase += kWin;
+    r.wrel += kWin;
     r.off = 0;
     r.wt = temper(r.wn);
-    if (r.gen < r.wbase + 2 * kWin) rng_fill(r, r.wbase + 2 * kWin);
-    r.wn = r.ring[(r.wbase + kWin + lane_id()) & kRingMask];
+    if (r.grel < r.wrel + 2 * kWin) rng_fill(r, r.wrel + 2 * kWin);
+    r.wn = r.ring[r.slot(r.wrel + kWin + (int32_t)lane_id())];
+}
+
+// rngpos after the search: {use0 + use(), use0 + grel}
+__device__ __forceinline__ void rng_close(const Rng &r, uint64_t use0, uint64_t *rngpos) {
+    rngpos[0] = use0 + (uint64_t)(int64_t)r.use();
+    rngpos[1] = use0 + (uint64_t)(int64_t)r.grel;
 }
 
 // random._randbelow_with_getrandbits(n), 1 <= n <= 7: k = n.bit_length(); draw
@@ -197,6 +230,12 @@ __device__ __forceinline__ uint32_t rng_below(Rng &r, uint32_t n) {
     }
 }
 
+// Per-search counters, accumulated in lane 0 of VGPRs (off the scalar unit, no SGPRs).
+struct Counters {
+    int32_t expansions = 0, depth_sum = 0, plies = 0, blocks = 0;
+    __device__ __forceinline__ void add(int32_t &c, int32_t v) { c += (lane_id() == 0) ? v : 0; }
+};
+
 // ------------------------------------------------------------------ random rollouts
 // A pending leaf, kept in LDS between the phases of a flush.
 struct Leaf {
@@ -211,7 +250,7 @@ struct Fresh {
     uint32_t u;       // untried word (record +4)
     uint32_t ow;      // packed move-list columns (record +12)
     uint32_t link;    // parent | pact << 16 | depth << 24 (record +8)
-    uint32_t pad0;
+    uint32_t lmask;   // legal-column mask of the node's position
     int32_t na;       // the edge INTO this node: Na (backup accumulates here, LDS atomics)
     int32_t w;        //                          Wa
     uint32_t pad1, pad2;
@@ -267,7 +306,7 @@ __device__ __forceinline__ uint64_t scan_or(uint64_t x) {
 // build each player's stones after every ply, and every lane tests check_win / full board
 // / column filled for ITS ply.  The first lane with an event ends the block (a fill changes
 // the legal set, so the next block restarts from the following word).
-__device__ void c4_rollouts(Leaf *L, int nb, Rng &rng, int64_t &plies_total, int64_t &blocks) {
+__device__ void c4_rollouts(Leaf *L, int nb, Rng &rng, const uint32_t *s_order, Counters &cn) {
     const uint32_t lane = lane_id();
     for (int j = 0; j < nb; ++j) {
         const uint64_t x0 = uni64(L[j].p0);
@@ -282,7 +321,7 @@ __device__ void c4_rollouts(Leaf *L, int nb, Rng &rng, int64_t &plies_total, int
             val = -1;
         } else if ((me | op) != kFull) {
             int mask = (int)(lm >> 25);
-            uint32_t ow = d_order[mask];
+            uint32_t ow = uni(s_order[mask]);
             uint32_t n = (ow >> 24) & 15u;
             int stones = __popcll(me | op);
             for (;;) {
@@ -294,7 +333,7 @@ __device__ void c4_rollouts(Leaf *L, int nb, Rng &rng, int64_t &plies_total, int
                     rng.off = kWin;
                     continue;
                 }
-                ++blocks;
+                cn.add(cn.blocks, 1);
                 const uint32_t qk = mbcnt(A);                    // this lane's ply in the block
                 const uint32_t col = (ow >> (3 * (v & 7u))) & 7u;  // its column (if accepted)
                 // earlier plies in the same column: 4-bit per-column counters, prefix-summed
@@ -338,12 +377,12 @@ __device__ void c4_rollouts(Leaf *L, int nb, Rng &rng, int64_t &plies_total, int
                 }
                 // a column filled: the legal set (and its CPython order) changes
                 mask &= ~(1 << __builtin_amdgcn_readlane((int)col, kend));
-                ow = d_order[mask];
+                ow = uni(s_order[mask]);
                 n = (ow >> 24) & 15u;
             }
         }
         if (lane == 0) L[j].val = val;
-        plies_total += q;
+        cn.add(cn.plies, q);
     }
 }
 
@@ -367,7 +406,7 @@ __device__ __forceinline__ void node_init(const Tree &t, int nd, int parent, int
     if (lane == 0) {
         uint4 h;
         h.x = 0;                                                                 // N
-        h.y = (kIdentDigits & ((1u << (3 * n)) - 1u)) | (n << 24) | (n << 28);  // untried, #moves
+        h.y = untried_init(n);                                                   // untried, #moves
         h.z = (uint32_t)(parent & 0xFFFF) | ((uint32_t)(pact & 0xFF) << 16) | ((uint32_t)depth << 24);
         h.w = ow;
         *(uint4 *)t.rec(nd) = h;
@@ -398,10 +437,15 @@ __device__ __forceinline__ bool valid_state(uint64_t p0, uint64_t p1, int turn) 
 template <bool STAMP>
 __global__ __launch_bounds__(kBlock) void c4_search_kernel(SearchParams p) {
     extern __shared__ __attribute__((aligned(16))) uint8_t s_dyn[];
-    // LDS (16-byte aligned pieces first): fresh[bs] (48 B), leaves[bs] (24 B), paths[bs][kMaxDepth]
-    Fresh *const fresh = (Fresh *)s_dyn;
-    Leaf *const leaves = (Leaf *)(s_dyn + sizeof(Fresh) * (size_t)p.bs);
-    uint32_t *const paths = (uint32_t *)(s_dyn + (sizeof(Fresh) + sizeof(Leaf)) * (size_t)p.bs);
+    // LDS: tables (order[128] u32, sel[128][8] u8), fresh[bs] (48 B), leaves[bs] (24 B),
+    //      paths[bs][kMaxDepth] (u16 node ids)
+    uint32_t *const s_order = (uint32_t *)s_dyn;
+    uint8_t *const s_sel = s_dyn + 512;
+    Fresh *const fresh = (Fresh *)(s_dyn + kTabBytes);
+    Leaf *const leaves = (Leaf *)(s_dyn + kTabBytes + sizeof(Fresh) * (size_t)p.bs);
+    uint16_t *const paths = (uint16_t *)(s_dyn + kTabBytes + (sizeof(Fresh) + sizeof(Leaf)) * (size_t)p.bs);
+    load_tables(s_order, s_sel);
+    __syncthreads();
     // log(N) table read through the constant address space: uniform index -> scalar loads,
     // which do not sit in the vector-memory counter the walk and the RNG window wait on.
     const __attribute__((address_space(4))) double *logtab =
@@ -413,30 +457,35 @@ __global__ __launch_bounds__(kBlock) void c4_search_kernel(SearchParams p) {
     if (gl >= p.n_games) return;
     const int g = p.game_ids ? uni(p.game_ids[gl]) : p.first_game + gl;
 
-    const zc_c4_state root = p.roots[gl];
-    const uint64_t rp0 = uni64(root.stones[0]), rp1 = uni64(root.stones[1]);
-    const int rturn = uni(root.turn);
-    zc_game_stats st{};
-    if (!valid_state(rp0, rp1, rturn) || legal_mask(rp0 | rp1) == 0) {
-        if (lane == 0) {
-            st.status = valid_state(rp0, rp1, rturn) ? ZC_STATUS_NO_MOVES : ZC_STATUS_BAD_STATE;
-            p.out_stats[gl] = st;
-            p.out_move[gl] = -1;
+    {
+        const zc_c4_state root = p.roots[gl];
+        const uint64_t rp0 = uni64(root.stones[0]), rp1 = uni64(root.stones[1]);
+        const int rturn = uni(root.turn);
+        if (!valid_state(rp0, rp1, rturn) || legal_mask(rp0 | rp1) == 0) {
+            if (lane == 0) {
+                zc_game_stats st{};
+                st.status = valid_state(rp0, rp1, rturn) ? ZC_STATUS_NO_MOVES : ZC_STATUS_BAD_STATE;
+                p.out_stats[gl] = st;
+                p.out_move[gl] = -1;
+            }
+            if (lane < 7) p.out_na[(size_t)gl * 7 + lane] = 0;
+            return;
         }
-        if (lane < 7) p.out_na[(size_t)gl * 7 + lane] = 0;
-        return;
     }
 
     const Arena &a = p.a;
     const Tree t{a.nodes + (size_t)g * p.M * kRecBytes, a.W + (size_t)g * p.M * kSlots};
 
     Rng rng;
-    const uint64_t use0 = uni64(a.rngpos[2 * (size_t)g]);
-    rng_open(rng, a.ring + (size_t)g * kRingWords, use0, uni64(a.rngpos[2 * (size_t)g + 1]));
+    rng_open(rng, a.ring + (size_t)g * kRingWords, uni64(a.rngpos[2 * (size_t)g]), uni64(a.rngpos[2 * (size_t)g + 1]));
+    Counters cn;
+    int status = 0;
 
-    node_init(t, 0, 0xFFFF, 0xFF, 0, d_order[legal_mask(rp0 | rp1)]);
+    {
+        const zc_c4_state root = p.roots[gl];
+        node_init(t, 0, 0xFFFF, 0xFF, 0, uni(s_order[legal_mask(uni64(root.stones[0]) | uni64(root.stones[1]))]));
+    }
     int nnodes = 1;
-    int64_t plies = 0;
     wave_mem_order();
 
     uint64_t ph[kPhases] = {};
@@ -462,8 +511,15 @@ __global__ __launch_bounds__(kBlock) void c4_search_kernel(SearchParams p) {
         // lowest slot holding a fresh child — no arithmetic, no HBM.  Fresh nodes live in
         // LDS until the flush is published.  Lane l holds level l of the current path.
         const int f0 = nnodes;
-        int node = 0, depth = 0, turn = rturn, nN = done;  // nN = N(node) = Na of its in-edge
-        uint64_t b0 = rp0, b1 = rp1;
+        for (int i = (int)lane; i < nb; i += 64) {  // fresh slots: no children, zero in-edge counters
+            fresh[i].na = 0;
+            fresh[i].w = 0;
+            *(uint4 *)fresh[i].ch = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
+        }
+        // the root position, re-read every flush rather than held in registers
+        const zc_c4_state root = p.roots[gl];
+        int node = 0, depth = 0, turn = uni(root.turn), nN = done;  // nN = N(node) = Na of its in-edge
+        uint64_t b0 = uni64(root.stones[0]), b1 = uni64(root.stones[1]);
         uint32_t pathv = (lane == 0) ? 0x00FF0000u : 0u;
         uint32_t u, ow, ch;  // the current node's record (ch: slot k)
         for (;;) {  // the first walk: select (mcts.cpp:47-63) over HBM records
@@ -475,9 +531,9 @@ __global__ __launch_bounds__(kBlock) void c4_search_kernel(SearchParams p) {
             const double lg = logtab[nN];  // log(N), glibc values tabulated on the host
             u = uni(h.y);
             ow = uni(h.w);
-            if ((u >> 24) & 15u) break;    // untried moves left: expand here
+            if (untried_count(u)) break;  // untried moves left: expand here
             if (depth >= kMaxDepth - 2) {  // unreachable (a C4 tree is <= 42 deep); never spin
-                st.status = ZC_STATUS_INTERNAL;
+                status = ZC_STATUS_INTERNAL;
                 u = 0;
                 break;
             }
@@ -504,6 +560,7 @@ __global__ __launch_bounds__(kBlock) void c4_search_kernel(SearchParams p) {
             ++depth;
             if (lane == (uint32_t)depth) pathv = (uint32_t)node | ((uint32_t)best << 16);
         }
+        int cmask = legal_mask(b0 | b1);      // legal columns of the current node
         const int x0node = node, d0 = depth;  // X0: shared by every leaf of this flush
         const uint32_t ppath = pathv;         // root .. X0 (lanes 0..d0)
         bool x0_dirty = false;
@@ -511,11 +568,11 @@ __global__ __launch_bounds__(kBlock) void c4_search_kernel(SearchParams p) {
         ZC_STAMP(1)
 
         for (int j = 0; j < nb; ++j) {
-            // resume at `node` (fully described by u, ow, ch in registers)
+            // resume at `node` (fully described by u, ow, ch, cmask in registers)
             for (;;) {
-                if ((u >> 24) & 15u) break;  // untried moves: expand here
+                if (untried_count(u)) break;  // untried moves: expand here
                 const uint64_t fm = __ballot(k < (u >> 28) && ch != 0xFFFF && (int)ch >= f0) & 0xFFull;
-                if (!fm) break;              // no child at all: terminal, re-queued as its own leaf
+                if (!fm) break;               // no child at all: terminal, re-queued as its own leaf
                 const int s = __builtin_ctzll(fm);
                 const int child = __builtin_amdgcn_readlane((int)ch, s);
                 if (node == x0node) {  // leaving X0 for good (walks never go back up)
@@ -528,53 +585,40 @@ __global__ __launch_bounds__(kBlock) void c4_search_kernel(SearchParams p) {
                 ++depth;
                 if (lane == (uint32_t)depth) pathv = (uint32_t)child | ((uint32_t)s << 16);
                 node = child;
-                const Fresh &F = fresh[child - f0];
-                u = uni(F.u);
-                ow = uni(F.ow);
-                ch = F.ch[k];
+                const uint4 fh = *(const uint4 *)&fresh[child - f0];  // u, ow, link, lmask
+                u = uni(fh.x);
+                ow = uni(fh.y);
+                cmask = uni((int)fh.w);
+                ch = fresh[child - f0].ch[k];
             }
             ZC_STAMP(2)
-            int leaf = node, ldepth = depth, lturn = turn;
+            int leaf = node, ldepth = depth, lturn = turn, lmask = cmask;
             uint64_t l0 = b0, l1 = b1;
-            int lmask;
-            const uint32_t cnt = (u >> 24) & 15u;
+            const uint32_t cnt = untried_count(u);
             if (cnt) {  // expand (mcts.cpp:65-78): policy = random.choice(untried)
                 const uint32_t r = rng_below(rng, cnt);
-                const uint32_t digits = u & 0x1FFFFFu;
-                const int mi = (int)((digits >> (3 * r)) & 7u);
-                const uint32_t low = (1u << (3 * r)) - 1u;
-                const uint32_t rest = (digits & low) | ((digits >> 3) & ~low & 0x1FFFFFu);
-                u = rest | ((cnt - 1u) << 24) | (u & 0xF0000000u);
-                const uint64_t bit = drop_bit(b0 | b1, (int)((ow >> (3 * mi)) & 7u));
+                const int mi = (int)uni((uint32_t)s_sel[(u & 0x7Fu) * 8u + r]);
+                u &= ~(1u << mi);
+                const int col = (int)((ow >> (3 * mi)) & 7u);
+                const uint64_t bit = drop_bit(b0 | b1, col);
                 if (turn) l1 |= bit; else l0 |= bit;
                 lturn = turn ^ 1;
                 leaf = nnodes++;
                 ldepth = depth + 1;
-                lmask = legal_mask(l0 | l1);
-                const uint32_t low_ = d_order[lmask];
+                if (bit & kTop) lmask &= ~(1 << col);  // the column just filled
+                const uint32_t low_ = uni(s_order[lmask]);
                 if (k == (uint32_t)mi) ch = (uint32_t)leaf;
-                if (node >= f0) {  // the parent's copy in LDS
-                    if (lane == 0) fresh[node - f0].u = u;
-                    if (lane == (uint32_t)mi) fresh[node - f0].ch[mi] = (uint16_t)leaf;
-                } else {
-                    x0_dirty = true;  // X0 itself: written back when the flush is published
+                if (node < f0) x0_dirty = true;  // X0 itself: written back when the flush is published
+                if (lane == 0) {
+                    // Node(state, legal_moves) (mcts.cpp:23-34): all moves untried, no children
+                    *(uint4 *)&fresh[leaf - f0] =
+                        make_uint4(untried_init((low_ >> 24) & 15u), low_,
+                                   (uint32_t)node | ((uint32_t)mi << 16) | ((uint32_t)ldepth << 24), (uint32_t)lmask);
+                    if (node >= f0) fresh[node - f0].u = u;  // the parent's copy in LDS
                 }
-                {  // Node(state, legal_moves) (mcts.cpp:23-34): all moves untried, no children
-                    Fresh &F = fresh[leaf - f0];
-                    const uint32_t n = (low_ >> 24) & 15u;
-                    if (lane == 0) {
-                        F.u = (kIdentDigits & ((1u << (3 * n)) - 1u)) | (n << 24) | (n << 28);
-                        F.ow = low_;
-                        F.link = (uint32_t)node | ((uint32_t)mi << 16) | ((uint32_t)ldepth << 24);
-                        F.na = 0;
-                        F.w = 0;
-                    }
-                    if (lane < kSlots) F.ch[lane] = 0xFFFF;
-                }
-                st.expansions += 1;
-                st.depth_sum += ldepth;
-            } else {
-                lmask = legal_mask(b0 | b1);
+                if (node >= f0 && lane == (uint32_t)mi) fresh[node - f0].ch[mi] = (uint16_t)leaf;
+                cn.add(cn.expansions, 1);
+                cn.add(cn.depth_sum, ldepth);
             }
             // the leaf's path: the walk's path plus the new node (the next walk resumes at `node`)
             const uint32_t lpath = (cnt && lane == (uint32_t)ldepth) ? (uint32_t)leaf : pathv;
@@ -584,7 +628,7 @@ __global__ __launch_bounds__(kBlock) void c4_search_kernel(SearchParams p) {
                 leaves[j].meta = (uint32_t)leaf | ((uint32_t)ldepth << 16) | ((uint32_t)lturn << 24) |
                                  ((uint32_t)lmask << 25);
             }
-            if (lane < (uint32_t)kMaxDepth) paths[j * kMaxDepth + lane] = lpath;
+            if (lane < (uint32_t)kMaxDepth) paths[j * kMaxDepth + lane] = (uint16_t)lpath;
             wave_mem_order();
             ZC_STAMP(3)
         }
@@ -594,7 +638,7 @@ __global__ __launch_bounds__(kBlock) void c4_search_kernel(SearchParams p) {
         }
 
         // ---- value.batch: random rollouts in pending order (mcts.cpp:112-124) ---------------
-        c4_rollouts(leaves, nb, rng, plies, st.rollout_blocks);
+        c4_rollouts(leaves, nb, rng, s_order, cn);
         wave_mem_order();
         ZC_STAMP(4)
 
@@ -621,7 +665,7 @@ __global__ __launch_bounds__(kBlock) void c4_search_kernel(SearchParams p) {
             const int d = (int)((meta >> 16) & 0xFFu);
             const int v = uni(leaves[j].val);
             if (lane > (uint32_t)d0 && lane <= (uint32_t)d) {
-                const int fi = (int)(paths[j * kMaxDepth + lane] & 0xFFFFu) - f0;
+                const int fi = (int)paths[j * kMaxDepth + lane] - f0;
                 const int vl = ((d - (int)lane) & 1) ? -v : v;
                 atomicAdd(&fresh[fi].na, 1);
                 atomicAdd(&fresh[fi].w, -vl);
@@ -677,7 +721,6 @@ __global__ __launch_bounds__(kBlock) void c4_search_kernel(SearchParams p) {
         }
         wave_mem_order();
         ZC_STAMP(6)
-        st.leaves += nb;
         done += nb;
     }
 #undef ZC_STAMP
@@ -700,11 +743,16 @@ __global__ __launch_bounds__(kBlock) void c4_search_kernel(SearchParams p) {
     }
     if (lane == 0) {
         p.out_move[gl] = (int)((ow >> (3 * best)) & 7u);
-        st.rollout_plies = plies;
-        st.rng_words = (int64_t)(rng.use() - use0);
+        zc_game_stats st{};
+        st.status = status;
+        st.expansions = cn.expansions;
+        st.depth_sum = cn.depth_sum;
+        st.leaves = p.sims;
+        st.rollout_plies = cn.plies;
+        st.rollout_blocks = cn.blocks;
+        st.rng_words = rng.use();
         p.out_stats[gl] = st;
-        a.rngpos[2 * (size_t)g] = rng.use();
-        a.rngpos[2 * (size_t)g + 1] = rng.gen;
+        rng_close(rng, a.rngpos[2 * (size_t)g], a.rngpos + 2 * (size_t)g);
     }
 }
 
@@ -713,6 +761,10 @@ __global__ __launch_bounds__(kBlock) void c4_rollout_debug_kernel(Arena a, int f
                                                                   const zc_c4_state *states, int32_t *out_value,
                                                                   int64_t *out_words) {
     __shared__ Leaf s_leaf[1];
+    __shared__ uint32_t s_order[128];
+    __shared__ uint8_t s_sel[1024];
+    load_tables(s_order, s_sel);
+    __syncthreads();
     const uint32_t lane = lane_id();
     const int gl = blockIdx.x;
     if (gl >= n) return;
@@ -727,15 +779,13 @@ __global__ __launch_bounds__(kBlock) void c4_rollout_debug_kernel(Arena a, int f
         s_leaf[0].meta = ((uint32_t)s.turn << 24) | ((uint32_t)legal_mask(s.stones[0] | s.stones[1]) << 25);
     }
     wave_mem_order();
-    int64_t plies = 0;
-    int64_t blocks = 0;
-    c4_rollouts(s_leaf, 1, rng, plies, blocks);
+    Counters cn;
+    c4_rollouts(s_leaf, 1, rng, s_order, cn);
     wave_mem_order();
     if (lane == 0) {
         out_value[gl] = s_leaf[0].val;
-        out_words[gl] = (int64_t)(rng.use() - use0);
-        a.rngpos[2 * (size_t)g] = rng.use();
-        a.rngpos[2 * (size_t)g + 1] = rng.gen;
+        out_words[gl] = rng.use();
+        rng_close(rng, use0, a.rngpos + 2 * (size_t)g);
     }
 }
 
@@ -743,11 +793,15 @@ __global__ __launch_bounds__(kBlock) void c4_rollout_debug_kernel(Arena a, int f
 __global__ __launch_bounds__(kBlock) void c4_rollout_seq_kernel(Arena a, int g, int n, const zc_c4_state *states,
                                                                 int32_t *out_value, int64_t *out_words) {
     __shared__ Leaf s_leaf[kBlock];
+    __shared__ uint32_t s_order[128];
+    __shared__ uint8_t s_sel[1024];
+    load_tables(s_order, s_sel);
+    __syncthreads();
     const uint32_t lane = lane_id();
     Rng rng;
     const uint64_t use0 = uni64(a.rngpos[2 * (size_t)g]);
     rng_open(rng, a.ring + (size_t)g * kRingWords, use0, uni64(a.rngpos[2 * (size_t)g + 1]));
-    int64_t plies = 0, blocks = 0;
+    Counters cn;
     for (int base = 0; base < n; base += kBlock) {
         const int cnt = min(kBlock, n - base);
         if ((int)lane < cnt) {
@@ -758,15 +812,14 @@ __global__ __launch_bounds__(kBlock) void c4_rollout_seq_kernel(Arena a, int g, 
         }
         wave_mem_order();
         rng_fill(rng, rng.use() + kLookahead);
-        c4_rollouts(s_leaf, cnt, rng, plies, blocks);
+        c4_rollouts(s_leaf, cnt, rng, s_order, cn);
         wave_mem_order();
         if ((int)lane < cnt) out_value[base + lane] = s_leaf[lane].val;
         wave_mem_order();
     }
     if (lane == 0) {
-        out_words[0] = (int64_t)(rng.use() - use0);
-        a.rngpos[2 * (size_t)g] = rng.use();
-        a.rngpos[2 * (size_t)g + 1] = rng.gen;
+        out_words[0] = rng.use();
+        rng_close(rng, use0, a.rngpos + 2 * (size_t)g);
     }
 }
 
@@ -800,7 +853,7 @@ __global__ void uct_debug_kernel(int n, const double *logn, const int32_t *na, c
 }  // namespace
 
 size_t c4_search_lds_bytes(int bs) {
-    return (sizeof(Leaf) + sizeof(Fresh) + sizeof(uint32_t) * kMaxDepth) * (size_t)bs;
+    return kTabBytes + (sizeof(Leaf) + sizeof(Fresh) + sizeof(uint16_t) * kMaxDepth) * (size_t)bs;
 }
 
 void launch_c4_search(const SearchParams &p, hipStream_t s) {
