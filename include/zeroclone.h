@@ -126,6 +126,46 @@ int zc_c4_play_async(zc_engine *eng, int32_t n_games, zc_c4_state *d_states, con
 int zc_c4_rollouts(zc_engine *eng, int32_t game, int32_t n_states, const zc_c4_state *states,
                    int32_t *out_values, int64_t *out_words);
 
+/* ---- Connect4 stepwise search: the flush handed to the caller ------------------------
+ * mcts.get_move (mcts.cpp:102-160) with ANY value function: the search pauses at every
+ * flush (mcts.cpp:112-127) and the caller evaluates the pending leaves — with a neural
+ * network on the same device (Value('network_*'), value_functions.py:61-99) or with any
+ * Python Value.batch — then resumes the search with their values.  Policy stays
+ * Policy('random') (random.choice on the game's stream).  Wa is fp64 here, summed in pending
+ * order exactly as mcts.cpp:90-95 does.  Device pointers, enqueued on hip_stream (NULL =
+ * null stream), never synchronising, so a whole move can be captured in a HIP graph:
+ *
+ *   zc_c4_ext_begin(...)
+ *   for f in 0 .. ceil(sims / batch_size) - 1:
+ *       zc_c4_ext_select(..., f, ...)   -> leaves / planes of flush f
+ *       values = value.batch(leaves)    (caller: NN forward, host callback, ...)
+ *       zc_c4_ext_backup(..., f, values)
+ *   zc_c4_ext_end(...)                  -> move, root visit counts, stats
+ *
+ * The sims / c / batch_size given to begin hold until end; one stepwise search per engine
+ * game range at a time.  Leaf j of game i (j < the flush's leaf count) is slot
+ * i*batch_size + j of every per-leaf buffer. */
+int zc_c4_ext_begin(zc_engine *eng, int32_t first_game, int32_t n_games, const zc_c4_state *d_roots,
+                    int32_t sims, double c, int32_t batch_size, void *hip_stream);
+/* Selection + expansion of flush `flush`.  Outputs (each may be NULL):
+ *   d_leaves[i*bs + j]  leaf state (zc_c4_state)
+ *   d_planes            c4_backend.state_to_tensor (c4_backend.py:52-61) of every leaf:
+ *                       [n_games*bs][2][6][7], plane 0 = side to move, row 0 = top;
+ *                       planes_dtype ZC_F32 or ZC_F16
+ *   d_counts[i]         leaves in this flush (0 for a game whose root is bad/terminal) */
+int zc_c4_ext_select(zc_engine *eng, int32_t first_game, int32_t n_games, int32_t flush,
+                     zc_c4_state *d_leaves, void *d_planes, int32_t planes_dtype, int32_t *d_counts,
+                     void *hip_stream);
+#define ZC_F32 0
+#define ZC_F16 1
+/* Backprop of flush `flush` (mcts.cpp:80-100 in pending order): d_values[i*bs + j] is the
+ * value of leaf j for ITS side to move, as Value.batch returns it. */
+int zc_c4_ext_backup(zc_engine *eng, int32_t first_game, int32_t n_games, int32_t flush, const double *d_values,
+                     void *hip_stream);
+/* Final move selection (mcts.cpp:150-157) and counters; outputs as zc_c4_search_async. */
+int zc_c4_ext_end(zc_engine *eng, int32_t first_game, int32_t n_games, int32_t *d_out_move, int32_t *d_out_root_na,
+                  zc_game_stats *d_out_stats, void *hip_stream);
+
 /* ---- Connect4 rules on the host (engine/games/connect4/c4_backend.py) --------------- */
 /* rows: 42 chars, row 0 = top, 'X', 'O', anything else = empty. */
 int zc_c4_from_rows(const char *rows42, int32_t turn, zc_c4_state *out);

@@ -50,8 +50,16 @@ def lib():
         L.zco_get_move_batch.argtypes = [ctypes.c_int, ctypes.c_char_p, P(ctypes.c_int), P(ctypes.c_uint64),
                                          ctypes.c_int, ctypes.c_double, ctypes.c_int, ctypes.c_int,
                                          P(ctypes.c_int), P(ctypes.c_int), P(ctypes.c_uint64)]
+        L.zco_get_move_valued.argtypes = [ctypes.c_char_p, ctypes.c_int, P(_MT), ctypes.c_int, ctypes.c_double,
+                                          ctypes.c_int, P(ctypes.c_int), P(ctypes.c_int), P(ctypes.c_int),
+                                          VALUE_FN, ctypes.c_void_p]
         _lib = L
     return _lib
+
+
+# void vfn(void *ctx, int n, const char *boards, const int *turns, double *out)
+VALUE_FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_char),
+                            ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_double))
 
 
 class MT:
@@ -112,6 +120,23 @@ def get_move_mt(board: str, turn: int, mt: MT, sims: int, c: float = 1.4, bs: in
     n = ctypes.c_int(0)
     col = lib().zco_get_move(board.encode(), turn, ctypes.byref(mt.s), sims, c, bs, na, order, ctypes.byref(n))
     return col, list(na[:n.value]), list(order[:n.value])
+
+
+def get_move_valued(board: str, turn: int, mt: "MT", sims: int, c: float, bs: int, value_batch):
+    """get_move with Value.batch = value_batch(boards: list[str], turns: list[int]) -> values
+    (one call per flush, pending order).  Returns (column, root_na, order)."""
+    def cb(_ctx, n, boards, turns, out):
+        raw = ctypes.string_at(boards, 42 * n).decode()
+        vals = value_batch([raw[42 * j: 42 * j + 42] for j in range(n)], [turns[j] for j in range(n)])
+        for j in range(n):
+            out[j] = float(vals[j])
+    fn = VALUE_FN(cb)
+    na = (ctypes.c_int * 7)()
+    order = (ctypes.c_int * 7)()
+    k = ctypes.c_int(0)
+    col = lib().zco_get_move_valued(board.encode(), turn, ctypes.byref(mt.s), sims, c, bs, na, order,
+                                    ctypes.byref(k), fn, None)
+    return col, list(na[:k.value]), list(order[:k.value])
 
 
 def play(board: str, turn: int, col: int):

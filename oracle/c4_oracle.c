@@ -301,8 +301,10 @@ static void backprop(onode *P, int node, double v) {   /* mcts.cpp:80-100 */
     }
 }
 
-int zco_get_move(const char *board, int turn, zco_mt *r, int sims, double c, int bs,
-                 int *root_na, int *order, int *n_moves) {   /* mcts.cpp:102-160 */
+/* mcts.cpp:102-160.  vfn == NULL: Value('random_rollout') on the same stream; otherwise
+ * vfn(ctx, n, boards, turns, out) is Value.batch over the flush's pending leaves. */
+static int get_move_impl(const char *board, int turn, zco_mt *r, int sims, double c, int bs,
+                         int *root_na, int *order, int *n_moves, zco_value_fn vfn, void *ctx) {
     pthread_once(&g_order_once, order_init);
     if (bs < 1) bs = 1;
     onode *P = (onode *)malloc(sizeof(onode) * (size_t)(sims > 0 ? sims + 1 : 1));
@@ -311,13 +313,23 @@ int zco_get_move(const char *board, int turn, zco_mt *r, int sims, double c, int
     if (n_moves) *n_moves = P[0].n;
     int *pend = (int *)malloc(sizeof(int) * (size_t)bs);
     double *vals = (double *)malloc(sizeof(double) * (size_t)bs);
+    char *lb = vfn ? (char *)malloc(42 * (size_t)bs) : NULL;
+    int *lt = vfn ? (int *)malloc(sizeof(int) * (size_t)bs) : NULL;
     int npend = 0;
     for (int i = 0; i < sims; i++) {
         int node = select_leaf(P, c);
         int leaf = P[node].nu > 0 ? expand(P, &np, node, r) : node;
         pend[npend++] = leaf;
         if (npend >= bs || i == sims - 1) {            /* flush :112-127, final flush :149 */
-            for (int j = 0; j < npend; j++) vals[j] = zco_rollout(P[pend[j]].b, P[pend[j]].turn, r);
+            if (vfn) {
+                for (int j = 0; j < npend; j++) {
+                    memcpy(lb + 42 * (size_t)j, P[pend[j]].b, 42);
+                    lt[j] = P[pend[j]].turn;
+                }
+                vfn(ctx, npend, lb, lt, vals);
+            } else {
+                for (int j = 0; j < npend; j++) vals[j] = zco_rollout(P[pend[j]].b, P[pend[j]].turn, r);
+            }
             for (int j = 0; j < npend; j++) backprop(P, pend[j], vals[j]);
             npend = 0;
         }
@@ -332,10 +344,22 @@ int zco_get_move(const char *board, int turn, zco_mt *r, int sims, double c, int
         if (order) order[i] = P[0].mv[i];
     }
     const int col = best >= 0 ? P[0].mv[best] : -1;
+    free(lt);
+    free(lb);
     free(vals);
     free(pend);
     free(P);
     return col;
+}
+
+int zco_get_move(const char *board, int turn, zco_mt *r, int sims, double c, int bs,
+                 int *root_na, int *order, int *n_moves) {
+    return get_move_impl(board, turn, r, sims, c, bs, root_na, order, n_moves, NULL, NULL);
+}
+
+int zco_get_move_valued(const char *board, int turn, zco_mt *r, int sims, double c, int bs,
+                        int *root_na, int *order, int *n_moves, zco_value_fn vfn, void *ctx) {
+    return get_move_impl(board, turn, r, sims, c, bs, root_na, order, n_moves, vfn, ctx);
 }
 
 /* ------------------------------------------------------------- threaded CPU baseline */

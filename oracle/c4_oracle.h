@@ -43,6 +43,13 @@ int  zco_rollout(const char *board, int turn, zco_mt *r);
 int  zco_get_move(const char *board, int turn, zco_mt *r, int sims, double c, int bs,
                   int *root_na, int *order, int *n_moves);
 
+/* The same search with Value.batch supplied by the caller: at every flush (mcts.cpp:112-127)
+ * vfn(ctx, n, boards n*42 chars, turns, out_values) evaluates the n pending leaves in
+ * pending order (value_functions.py:16-32).  Policy stays random.choice on r. */
+typedef void (*zco_value_fn)(void *ctx, int n, const char *boards, const int *turns, double *out);
+int  zco_get_move_valued(const char *board, int turn, zco_mt *r, int sims, double c, int bs,
+                         int *root_na, int *order, int *n_moves, zco_value_fn vfn, void *ctx);
+
 /* Convenience for the CPU baseline: n games, game g seeded with seeds[g], spread over
  * n_threads pthreads.  Boards are n*42 chars.  Returns 0. */
 int  zco_get_move_batch(int n, const char *boards, const int *turns, const uint64_t *seeds,

@@ -1,0 +1,181 @@
+"""GPU parity of the stepwise search (zc_c4_ext_*): the tree search pauses at every flush
+and the caller supplies the leaf values.  Checked bit-exactly against the reference's own
+outputs (tests/golden/c4_get_move_valued.json, value = c4_values.hash_value) and against
+the oracle replaying the values a network produced on the GPU."""
+import random
+from collections import defaultdict
+
+import numpy as np
+import pytest
+import torch
+
+import oracle
+from c4_values import bits_from_rows, hash_value
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def eng():
+    from zeroclone_amd._native import NativeEngine
+    e = NativeEngine(max_games=256, max_sims=1024, max_batch=128)
+    yield e
+    e.close()
+
+
+def roots_tensor(cases):
+    from zeroclone_amd._native import c4_from_rows
+    rows = np.zeros((len(cases), 3), np.int64)
+    for i, c in enumerate(cases):
+        s = c4_from_rows(c["board"].replace(".", " "), c["turn"])
+        rows[i, 0] = np.int64(np.uint64(s["stones"][0]))
+        rows[i, 1] = np.int64(np.uint64(s["stones"][1]))
+        rows[i, 2] = int(s["turn"])
+    return torch.from_numpy(rows).cuda()
+
+
+def hash_values(leaves, planes, counts):
+    rows = leaves.cpu().numpy().view(np.uint64)
+    out = np.array([hash_value(int(r[0]), int(r[1]), int(r[2]) & 1) for r in rows])
+    return torch.from_numpy(out).cuda()
+
+
+def test_stepwise_matches_reference_goldens(eng, golden):
+    from zeroclone_amd.valued import C4ValuedSearch
+    cases = golden("c4_get_move_valued.json")["cases"]
+    groups = defaultdict(list)
+    for c in cases:
+        groups[(c["sims"], c["bs"], c["c"])].append(c)
+    for (sims, bs, cc), grp in groups.items():
+        eng.seed(0, [c["seed"] for c in grp])
+        vs = C4ValuedSearch(eng, len(grp), bs)
+        mv, na, st = vs.run(roots_tensor(grp), sims, cc, hash_values)
+        mv, na, st = mv.cpu().numpy(), na.cpu().numpy(), st.cpu().numpy()
+        for i, c in enumerate(grp):
+            assert [int(na[i, col]) for col in c["order"]] == c["root_na"], (i, c)
+            assert int(mv[i]) == c["move"]
+            assert st[i, 5] == 0
+            assert st[i, 4] == c["consumed"]
+            assert st[i, 2] == c["leaves"]
+            mt, idx = eng.get_rng_state(i)
+            r = random.Random()
+            r.setstate((3, tuple(int(x) for x in mt) + (idx,), None))
+            assert r.getrandbits(32) == c["next_word"]
+
+
+def test_planes_are_state_to_tensor_of_the_leaves(eng):
+    from zeroclone_amd.engine.games.connect4 import c4_backend as zb
+    from zeroclone_amd.valued import C4ValuedSearch
+    n, bs = 32, 32
+    eng.seed(0, list(range(n)))
+    seen = []
+
+    def fn(leaves, planes, counts):
+        seen.append((leaves.cpu().numpy().view(np.uint64).copy(), planes.float().cpu().numpy().copy(),
+                     counts.cpu().numpy().copy()))
+        return hash_values(leaves, planes, counts)
+
+    roots = torch.zeros((n, 3), dtype=torch.int64, device="cuda")
+    C4ValuedSearch(eng, n, bs).run(roots, 96, 1.4, fn)
+    assert len(seen) == 3
+    for rows, pl, cnt in seen:
+        assert (cnt == bs).all()
+        for k in range(0, rows.shape[0], 7):
+            st = zb.from_zc(int(rows[k, 0]), int(rows[k, 1]), int(rows[k, 2]) & 1)
+            np.testing.assert_array_equal(pl[k], zb.state_to_tensor(st))
+
+
+def small_net(in_planes=2, seed=0):
+    from zeroclone_amd.nets import ValueNetwork, for_inference
+    torch.manual_seed(seed)
+    net = ValueNetwork(channels=32, blocks=2, in_planes=in_planes).eval()
+    return for_inference(net, "cuda", torch.float16)
+
+
+def test_network_values_replay_into_the_oracle(eng):
+    """Values from the fp16 network on the GPU, replayed flush by flush into the oracle's
+    valued get_move: the searches must agree exactly (the search is exact given values)."""
+    from zeroclone_amd.valued import C4ValuedSearch, NetValue
+    n, bs, sims = 16, 32, 200
+    seeds = [100 + i for i in range(n)]
+    eng.seed(0, seeds)
+    net = NetValue(small_net())
+    log = []
+
+    def fn(leaves, planes, counts):
+        v = net(leaves, planes, counts)
+        log.append((v.cpu().numpy().copy(), counts.cpu().numpy().copy()))
+        return v
+
+    roots = torch.zeros((n, 3), dtype=torch.int64, device="cuda")
+    mv, na, st = C4ValuedSearch(eng, n, bs).run(roots, sims, 1.4, fn)
+    mv, na = mv.cpu().numpy(), na.cpu().numpy()
+    assert len({round(float(x), 6) for x in log[0][0]}) > 10  # a real spread of values
+    for i in range(n):
+        it = iter(range(len(log)))
+
+        def replay(boards, turns, i=i, it=it):
+            f = next(it)
+            vals, cnt = log[f]
+            assert cnt[i] == len(boards)
+            return [float(x) for x in vals[i * bs: i * bs + len(boards)]]
+
+        mt = oracle.MT(seeds[i])
+        col, rna, order = oracle.get_move_valued("." * 42, 0, mt, sims, 1.4, bs, replay)
+        assert [int(na[i, c]) for c in order] == rna
+        assert int(mv[i]) == col
+
+
+def test_graph_capture_replays_the_eager_move(eng):
+    from zeroclone_amd.valued import C4ValuedSearch, NetValue
+    n, bs, sims = 64, 32, 160
+    net = NetValue(small_net(seed=3))
+    roots = torch.zeros((n, 3), dtype=torch.int64, device="cuda")
+    vs = C4ValuedSearch(eng, n, bs)
+    eng.seed(0, list(range(n)))
+    mv, na, _ = vs.run(roots, sims, 1.4, net)
+    mv, na = mv.clone(), na.clone()
+    g = vs.capture(roots, sims, 1.4, net)
+    eng.seed(0, list(range(n)))
+    vs.move.zero_()
+    vs.na.zero_()
+    g.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(vs.move, mv)
+    assert torch.equal(vs.na, na)
+
+
+def test_get_move_runs_any_value_object(golden):
+    """mcts.get_move with a non-rollout Value object: stepwise search, value.batch on the
+    host per flush, Python `random` handed back exactly as the reference leaves it."""
+    from zeroclone_amd.engine import mcts
+    from zeroclone_amd.engine.games.connect4 import c4_backend as zb
+    from zeroclone_amd.engine.policy_functions import Policy
+
+    class HashValue:
+        name = "hash"
+
+        def batch(self, states, backend=None):
+            return [hash_value(*bits_from_rows(s.board), s.turn) for s in states]
+
+    for c in golden("c4_get_move_valued.json")["cases"][:6]:
+        st = zb.State([list(c["board"][r * 7:(r + 1) * 7].replace(".", " ")) for r in range(6)], c["turn"])
+        random.seed(c["seed"])
+        mv = mcts.get_move(st, HashValue(), Policy("random"), zb, c["sims"], c["c"], c["bs"])
+        assert mv == (c["move"], 0)
+        assert random.getrandbits(32) == c["next_word"]
+
+
+def test_fp16_network_on_gpu_tracks_the_reference_fp32(golden):
+    """ValueNetwork() with the reference's seeded init, folded to fp16 channels-last on the
+    GPU, against the reference's fp32 CPU outputs (tolerance: fp16 arithmetic)."""
+    from zeroclone_amd.nets import ValueNetwork, for_inference
+    g = golden("value_network.json")
+    torch.manual_seed(g["seed"])
+    net = ValueNetwork().eval()
+    bits = np.unpackbits(np.frombuffer(bytes.fromhex(g["inputs_packed_hex"]), np.uint8))
+    x = torch.from_numpy(bits[:int(np.prod(g["shape"]))].astype(np.float32).reshape(g["shape"]))
+    m = for_inference(net, "cuda", torch.float16)
+    with torch.no_grad():
+        y = m(x.cuda().half()).float().reshape(-1).cpu().numpy()
+    np.testing.assert_allclose(y, np.array(g["outputs"]), rtol=0, atol=2e-2)

@@ -23,6 +23,8 @@ ZC_EDEVICE = -5
 ZC_C4_ONGOING = 2
 ZC_STATUS_NO_MOVES = 1
 ZC_STATUS_BAD_STATE = 2
+ZC_F32 = 0
+ZC_F16 = 1
 
 
 class C4State(ctypes.Structure):
@@ -70,6 +72,15 @@ SIGNATURES = [
                                           ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     ("zc_c4_play_async", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p,
                                         ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p]),
+    ("zc_c4_ext_begin", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p,
+                                       ctypes.c_int32, ctypes.c_double, ctypes.c_int32, ctypes.c_void_p]),
+    ("zc_c4_ext_select", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                        ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p,
+                                        ctypes.c_void_p]),
+    ("zc_c4_ext_backup", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                        ctypes.c_void_p, ctypes.c_void_p]),
+    ("zc_c4_ext_end", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p,
+                                     ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     ("zc_c4_rollouts", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p,
                                       ctypes.c_void_p, P(ctypes.c_int64)]),
     ("zc_c4_from_rows", ctypes.c_int, [ctypes.c_char_p, ctypes.c_int32, P(C4State)]),
@@ -226,6 +237,26 @@ class NativeEngine:
                       stream: int = 0) -> None:
         check(lib().zc_c4_play_async(self._h, n, ctypes.c_void_p(d_states), ctypes.c_void_p(d_moves),
                                      ctypes.c_void_p(d_results), int(bool(reset)), ctypes.c_void_p(stream or None)))
+
+    # ---- stepwise search (caller-supplied values); device pointers as ints, 0 = NULL
+    def c4_ext_begin(self, first_game: int, n: int, d_roots: int, sims: int, c: float, batch_size: int,
+                     stream: int = 0) -> None:
+        check(lib().zc_c4_ext_begin(self._h, first_game, n, ctypes.c_void_p(d_roots), int(sims), float(c),
+                                    int(batch_size), ctypes.c_void_p(stream or None)))
+
+    def c4_ext_select(self, first_game: int, n: int, flush: int, d_leaves: int = 0, d_planes: int = 0,
+                      planes_f16: bool = True, d_counts: int = 0, stream: int = 0) -> None:
+        check(lib().zc_c4_ext_select(self._h, first_game, n, int(flush), ctypes.c_void_p(d_leaves or None),
+                                     ctypes.c_void_p(d_planes or None), ZC_F16 if planes_f16 else ZC_F32,
+                                     ctypes.c_void_p(d_counts or None), ctypes.c_void_p(stream or None)))
+
+    def c4_ext_backup(self, first_game: int, n: int, flush: int, d_values: int, stream: int = 0) -> None:
+        check(lib().zc_c4_ext_backup(self._h, first_game, n, int(flush), ctypes.c_void_p(d_values),
+                                     ctypes.c_void_p(stream or None)))
+
+    def c4_ext_end(self, first_game: int, n: int, d_move: int, d_na: int, d_stats: int, stream: int = 0) -> None:
+        check(lib().zc_c4_ext_end(self._h, first_game, n, ctypes.c_void_p(d_move), ctypes.c_void_p(d_na),
+                                  ctypes.c_void_p(d_stats), ctypes.c_void_p(stream or None)))
 
     def c4_rollouts(self, states: np.ndarray, game: int = 0):
         """Sequential rollouts of `states` on one game's stream: (values[n], words consumed)."""

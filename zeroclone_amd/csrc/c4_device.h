@@ -1,0 +1,473 @@
+// c4_device.h — device-side building blocks shared by the Connect4 search kernels
+// (c4_search.hip: fused rollout search; c4_ext.hip: stepwise search with caller values).
+// Included by exactly those translation units; everything is internal to each of them.
+#pragma once
+#include <math.h>
+
+#include "c4_order_table.h"
+#include "zc_internal.h"
+
+namespace zc {
+namespace {
+
+__constant__ uint32_t d_order[128] = {ZC_C4_ORDER_LIST};
+
+constexpr uint32_t kRingMask = kRingWords - 1;
+constexpr uint64_t kBottom = 0x0000040810204081ull;  // bit 7c: bottom cell of column c
+constexpr uint64_t kFull = kBottom * 0x3Full;        // the 42 playable cells
+constexpr uint64_t kTop = kBottom << 5;              // top playable cell of each column
+constexpr int kTabBytes = 128 * 4 + 128 * 8;  // LDS tables: move-list order[128], select[128][8]
+
+// Untried moves of a node (record +4 / Fresh.u): bit i (i < 7) set while move i of the
+// node's move list is untried; bits 28..31 = number of moves.  The reference keeps the
+// untried INDICES in list order and lets random.choice pick the r-th (mcts.cpp:67-72); the
+// r-th remaining index is the r-th set bit of the mask (table sel[mask][r]).
+__device__ __forceinline__ uint32_t untried_init(uint32_t n) { return ((1u << n) - 1u) | (n << 28); }
+__device__ __forceinline__ uint32_t untried_count(uint32_t u) { return (uint32_t)__popc(u & 0x7Fu); }
+
+// Fill the LDS tables (whole wave): s_order = d_order, s_sel[m*8 + r] = r-th set bit of m.
+__device__ __forceinline__ void load_tables(uint32_t *s_order, uint8_t *s_sel) {
+    for (int i = (int)threadIdx.x; i < 128; i += blockDim.x) s_order[i] = d_order[i];
+    for (int i = (int)threadIdx.x; i < 1024; i += blockDim.x) {
+        const uint32_t m = (uint32_t)i >> 3, r = (uint32_t)i & 7u;
+        uint32_t x = m, c = 0, bitpos = 7;
+        for (uint32_t b = 0; b < 7; ++b)
+            if ((x >> b) & 1u) {
+                if (c == r) { bitpos = b; break; }
+                ++c;
+            }
+        s_sel[i] = (uint8_t)bitpos;
+    }
+}
+constexpr int kWin = 64;                             // RNG window: one word per lane
+
+// ------------------------------------------------------------------ wave helpers
+__device__ __forceinline__ uint32_t uni(uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); }
+__device__ __forceinline__ int uni(int x) { return __builtin_amdgcn_readfirstlane(x); }
+__device__ __forceinline__ uint64_t uni64(uint64_t x) {
+    return ((uint64_t)uni((uint32_t)(x >> 32)) << 32) | (uint64_t)uni((uint32_t)x);
+}
+__device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
+
+__device__ __forceinline__ void wave_mem_order() {
+    // Same-wave hand-offs through memory (one lane stores, another loads) are ordered by
+    // program order on gfx950 (wavefront scope needs no cache action); this only stops the
+    // compiler from moving memory operations across the point.
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+}
+
+template <int CTRL>
+__device__ __forceinline__ int dpp(int x) {
+    return __builtin_amdgcn_mov_dpp(x, CTRL, 0xF, 0xF, false);
+}
+template <int CTRL>
+__device__ __forceinline__ double dpp(double x) {
+    const int lo = dpp<CTRL>(__double2loint(x));
+    const int hi = dpp<CTRL>(__double2hiint(x));
+    return __hiloint2double(hi, lo);
+}
+
+// First maximum over lanes 0..7 (ties -> lower slot), as mcts.cpp:55-58 (`v > best_val`,
+// scanning slots in order).  Three DPP steps inside each 8-lane half row: xor 1, xor 2,
+// mirror; afterwards every lane of the half row holds the winner.
+template <class T>
+__device__ __forceinline__ void argmax_step(T &v, int &i, T ov, int oi) {
+    if (ov > v || (ov == v && oi < i)) {
+        v = ov;
+        i = oi;
+    }
+}
+template <class T>
+__device__ __forceinline__ void argmax8(T &v, int &i) {
+    argmax_step(v, i, dpp<0xB1>(v), dpp<0xB1>(i));    // quad_perm [1,0,3,2]
+    argmax_step(v, i, dpp<0x4E>(v), dpp<0x4E>(i));    // quad_perm [2,3,0,1]
+    argmax_step(v, i, dpp<0x141>(v), dpp<0x141>(i));  // row_half_mirror
+}
+
+// ------------------------------------------------------------------ Connect4 bitboards
+__device__ __forceinline__ uint64_t drop_bit(uint64_t occ, int col) {
+    // c4_backend.play_move (:14-23): lowest empty row of `col`; a full column drops nothing.
+    const int s = 7 * col;
+    return (occ + (1ull << s)) & (0x3Full << s);
+}
+
+__device__ __forceinline__ int legal_mask(uint64_t occ) {
+    // c4_backend.get_legal_moves (:49-50): column c is legal while its top cell is empty.
+    // Gather bit 7c -> bit c with one multiply: the 49 partial products t_c * 2^(56-6i) land
+    // on distinct bit positions (7c - 6i is injective on 0..6 x 0..6), so nothing carries
+    // and bits 56..62 of the product are exactly t_0..t_6.
+    const uint64_t t = (~occ & kTop) >> 5;  // bit 7c
+    return (int)((t * 0x0104104104100000ull) >> 56) & 0x7F;
+}
+
+__device__ __forceinline__ bool has_four(uint64_t b) {
+    // c4_backend.check_win (:25-44) for one token: any horizontal, vertical or diagonal run.
+    uint64_t m = b & (b >> 7);
+    uint64_t r = m & (m >> 14);
+    m = b & (b >> 1);
+    r |= m & (m >> 2);
+    m = b & (b >> 6);
+    r |= m & (m >> 12);
+    m = b & (b >> 8);
+    r |= m & (m >> 16);
+    return r != 0;
+}
+
+// ------------------------------------------------------------------ CPython MT19937
+__device__ __forceinline__ uint32_t temper(uint32_t y) {
+    y ^= y >> 11;
+    y ^= (y << 7) & 0x9d2c5680u;
+    y ^= (y << 15) & 0xefc60000u;
+    y ^= y >> 18;
+    return y;
+}
+
+// The game's stream lives in a ring of RAW MT words x[p] (absolute position p, slot
+// p % kRingWords).  The recurrence x[p] = x[p-227] ^ twist(x[p-624], x[p-623]) regenerates
+// it kChunk words at a time, all lanes in parallel (every input is >= 227 words older).
+struct Rng {
+    uint32_t *ring;
+    uint32_t base;   // low 32 bits of the absolute position at the search's start (use0)
+    int32_t wrel;    // window start - use0 (a multiple of 64 in absolute terms; may be < 0)
+    uint32_t off;    // next word to consume = window start + off, off in [0, 64]
+    int32_t grel;    // words generated so far - use0
+    uint32_t wt;     // tempered x[window start + lane]
+    uint32_t wn;     // raw x[window start + 64 + lane], in flight until the window advances
+    __device__ __forceinline__ int32_t use() const { return wrel + (int32_t)off; }  // relative to use0
+    __device__ __forceinline__ uint32_t slot(int32_t rel) const { return (base + (uint32_t)rel) & kRingMask; }
+};
+
+__device__ __forceinline__ int32_t rng_generate(uint32_t *ring, uint32_t base, int32_t grel, int32_t target) {
+    const uint32_t lane = lane_id();
+    constexpr int K = kChunk / 64;
+    while (grel < target) {
+        // every input of the chunk is >= 227 words older than any output: load all, then store
+        uint32_t a[K], b[K], m[K];
+        const uint32_t p0 = base + (uint32_t)grel + lane;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const uint32_t p = p0 + 64u * k;
+            a[k] = ring[(p - 624) & kRingMask];
+            b[k] = ring[(p - 623) & kRingMask];
+            m[k] = ring[(p - 227) & kRingMask];
+        }
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const uint32_t p = p0 + 64u * k;
+            const uint32_t y = (a[k] & 0x80000000u) | (b[k] & 0x7fffffffu);
+            ring[p & kRingMask] = m[k] ^ (y >> 1) ^ ((b[k] & 1u) ? 0x9908b0dfu : 0u);
+        }
+        grel += kChunk;
+        wave_mem_order();
+    }
+    return grel;
+}
+
+__device__ __forceinline__ void rng_fill(Rng &r, int32_t target) {
+    if (r.grel < target) r.grel = rng_generate(r.ring, r.base, r.grel, target);
+}
+
+// use0 / gen0: absolute positions (words consumed / generated) from the game's rngpos.
+__device__ __forceinline__ void rng_open(Rng &r, uint32_t *ring, uint64_t use0, uint64_t gen0) {
+    r.ring = ring;
+    r.base = (uint32_t)use0;
+    r.grel = (int32_t)(gen0 - use0);
+    r.off = (uint32_t)use0 & (uint32_t)(kWin - 1);
+    r.wrel = -(int32_t)r.off;
+    rng_fill(r, r.wrel + 2 * kWin);
+    r.wt = temper(r.ring[r.slot(r.wrel + (int32_t)lane_id())]);
+    r.wn = r.ring[r.slot(r.wrel + kWin + (int32_t)lane_id())];
+}
+
+__device__ __forceinline__ void rng_advance(Rng &r) {
+    r.wrel += kWin;
+    r.off = 0;
+    r.wt = temper(r.wn);
+    if (r.grel < r.wrel + 2 * kWin) rng_fill(r, r.wrel + 2 * kWin);
+    r.wn = r.ring[r.slot(r.wrel + kWin + (int32_t)lane_id())];
+}
+
+// rngpos after the search: {use0 + use(), use0 + grel}
+__device__ __forceinline__ void rng_close(const Rng &r, uint64_t use0, uint64_t *rngpos) {
+    rngpos[0] = use0 + (uint64_t)(int64_t)r.use();
+    rngpos[1] = use0 + (uint64_t)(int64_t)r.grel;
+}
+
+// random._randbelow_with_getrandbits(n), 1 <= n <= 7: k = n.bit_length(); draw
+// getrandbits(k) = word >> (32-k) until < n.  All window words are tested at once; the
+// first accepted one (in stream order) is the draw, and everything before it is consumed.
+__device__ __forceinline__ uint32_t rng_below(Rng &r, uint32_t n) {
+    const uint32_t sh = (uint32_t)__clz(n);
+    const uint32_t lane = lane_id();
+    for (;;) {
+        if (r.off >= (uint32_t)kWin) rng_advance(r);
+        const uint32_t v = r.wt >> sh;
+        const uint64_t bal = __ballot(lane >= r.off && v < n);
+        if (bal) {
+            const int f = __builtin_ctzll(bal);
+            r.off = (uint32_t)f + 1;
+            return (uint32_t)__builtin_amdgcn_readlane((int)v, f);
+        }
+        r.off = kWin;
+    }
+}
+
+// Per-search counters, accumulated in lane 0 of VGPRs (off the scalar unit, no SGPRs).
+struct Counters {
+    int32_t expansions = 0, depth_sum = 0, plies = 0, blocks = 0;
+    __device__ __forceinline__ void add(int32_t &c, int32_t v) { c += (lane_id() == 0) ? v : 0; }
+};
+
+// A pending leaf, kept in LDS between the phases of a flush.
+struct Leaf {
+    uint64_t p0, p1;  // stones of 'X' / 'O'
+    uint32_t meta;    // node | depth << 16 | turn << 24 | legal mask << 25
+    int32_t val;      // rollout value from the leaf's side to move
+};
+
+// LDS copy of a node created in the current flush.  During selection the node lives only
+// here; its HBM record is written in one coalesced batch when the flush's leaves are chosen.
+struct Fresh {
+    uint32_t u;       // untried word (record +4)
+    uint32_t ow;      // packed move-list columns (record +12)
+    uint32_t link;    // parent | pact << 16 | depth << 24 (record +8)
+    uint32_t lmask;   // legal-column mask of the node's position
+    int32_t na;       // the edge INTO this node: Na (backup accumulates here, LDS atomics)
+    int32_t w;        //                          Wa
+    uint32_t pad1, pad2;
+    uint16_t ch[8];   // children (record +16)
+};
+static_assert(sizeof(Fresh) == 48, "Fresh is three 16-byte LDS slots");
+
+// ------------------------------------------------------------------ node records
+struct Tree {
+    uint8_t *nodes;  // this game's records
+    int32_t *W;      // this game's W rows
+    __device__ __forceinline__ uint8_t *rec(int nd) const { return nodes + (size_t)nd * kRecBytes; }
+    __device__ __forceinline__ uint32_t *hdr(int nd) const { return (uint32_t *)rec(nd); }
+    __device__ __forceinline__ uint16_t *child(int nd) const { return (uint16_t *)(rec(nd) + 16); }
+    __device__ __forceinline__ int32_t *na(int nd) const { return (int32_t *)(rec(nd) + 32); }
+    __device__ __forceinline__ double *q(int nd) const { return (double *)(rec(nd) + 64); }
+    __device__ __forceinline__ int32_t *w(int nd) const { return W + (size_t)nd * kSlots; }
+};
+
+// Node(state, legal_moves, parent, idx) (mcts.cpp:23-34): all moves untried, in list order.
+// Lanes 0..7 write slot `lane`; lane 0 writes the header.
+__device__ __forceinline__ void node_init(const Tree &t, int nd, int parent, int pact, int depth, uint32_t ow) {
+    const uint32_t lane = lane_id();
+    const uint32_t n = (ow >> 24) & 15u;
+    if (lane == 0) {
+        uint4 h;
+        h.x = 0;                                                                 // N
+        h.y = untried_init(n);                                                   // untried, #moves
+        h.z = (uint32_t)(parent & 0xFFFF) | ((uint32_t)(pact & 0xFF) << 16) | ((uint32_t)depth << 24);
+        h.w = ow;
+        *(uint4 *)t.rec(nd) = h;
+    }
+    if (lane < kSlots) {
+        t.child(nd)[lane] = 0xFFFF;
+        t.na(nd)[lane] = 0;
+        t.q(nd)[lane] = 0.0;
+        t.w(nd)[lane] = 0;
+    }
+}
+
+__device__ __forceinline__ bool valid_state(uint64_t p0, uint64_t p1, int turn) {
+    if ((p0 & p1) || ((p0 | p1) & ~kFull) || (turn & ~1)) return false;
+    const uint64_t occ = p0 | p1;
+#pragma unroll
+    for (int c = 0; c < 7; ++c) {
+        const uint64_t col = (occ >> (7 * c)) & 0x3Full;
+        if (col & (col + 1)) return false;  // stones must stack from the bottom
+    }
+    return true;
+}
+
+// ------------------------------------------------------------------ phase stamps (diagnostic)
+template <bool ON>
+struct Stamp {
+    uint64_t ph[kPhases];
+    uint64_t t;
+    __device__ __forceinline__ Stamp() : t(ON ? __builtin_amdgcn_s_memtime() : 0) {
+        for (int i = 0; i < kPhases; ++i) ph[i] = 0;
+    }
+    __device__ __forceinline__ void mark(int k) {
+        if (ON) {
+            const uint64_t now = __builtin_amdgcn_s_memtime();
+            ph[k] += now - t;
+            t = now;
+        }
+    }
+};
+
+using ConstDouble = const __attribute__((address_space(4))) double;
+
+// ------------------------------------------------------------------ selection of one flush
+// What a flush's selection leaves behind for its backup and publish steps.
+struct FlushSel {
+    int f0;          // first node created in this flush
+    int x0node, d0;  // X0: where the first walk stopped, and its depth
+    uint32_t ppath;  // lane l (l <= d0): level l of root..X0 = node | slot << 16
+    bool x0_dirty;   // X0 expanded during the flush (its record must be rewritten)
+    uint32_t x_u, x_ch;  // X0's untried word / child slot `lane & 7` as last seen
+};
+
+// select + expand of the nb leaves of one flush (mcts.cpp:129-147), shared by the fused
+// rollout search and the stepwise search.
+//
+// No backup happens inside a flush, so (1) the UCT path from the root to the node X0 where
+// the flush's first walk stops is shared by every leaf of the flush (each walk resumes where
+// the previous one expanded, always at or below X0), and (2) every node below X0 is created
+// in this flush ("fresh": id >= f0, Na = W = 0 on every edge).  The reference's walk from a
+// node without untried moves takes the first child with the largest UCT; an unvisited child
+// scores +inf, so below X0 that is simply the lowest slot holding a fresh child — no
+// arithmetic, no HBM.  Fresh nodes live in LDS (`fresh`) until the caller publishes them.
+// Leaf j goes to leaves[j] (board, node, depth, turn, legal mask) and its path (node ids of
+// levels 0..depth) to paths[j][*].
+//
+// QW = false: the record's +64 slots hold Q (rollout mode, W in the side array);
+// QW = true:  they hold W in fp64 and Q = W / Na is formed here — the same IEEE quotient
+//             mcts.cpp:95 stores, so the UCT inputs are bit-identical.
+template <bool QW, bool STAMP>
+__device__ __forceinline__ void select_flush(const Tree &t, Fresh *fresh, Leaf *leaves, uint16_t *paths,
+                                             const uint32_t *s_order, const uint8_t *s_sel, ConstDouble *logtab,
+                                             Rng &rng, Counters &cn, Stamp<STAMP> &stamp, int &nnodes, int &status,
+                                             uint64_t rp0, uint64_t rp1, int rturn, int done, int nb, double c,
+                                             FlushSel &fs) {
+    const uint32_t lane = lane_id();
+    const uint32_t k = lane & 7u;  // child slot handled by this lane (lanes 8.. mirror 0..7)
+    const int f0 = nnodes;
+    for (int i = (int)lane; i < nb; i += 64) {  // fresh slots: no children, zero in-edge counters
+        fresh[i].na = 0;
+        fresh[i].w = 0;
+        *(uint4 *)fresh[i].ch = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
+    }
+    int node = 0, depth = 0, turn = rturn, nN = done;  // nN = N(node) = Na of its in-edge
+    uint64_t b0 = rp0, b1 = rp1;
+    uint32_t pathv = (lane == 0) ? 0x00FF0000u : 0u;
+    uint32_t u, ow, ch;  // the current node's record (ch: slot k)
+    for (;;) {  // the first walk: select (mcts.cpp:47-63) over HBM records
+        const uint8_t *R = t.rec(node);
+        const uint4 h = *(const uint4 *)R;
+        ch = ((const uint16_t *)(R + 16))[k];
+        const int32_t na = ((const int32_t *)(R + 32))[k];
+        const double qw = ((const double *)(R + 64))[k];
+        const double lg = logtab[nN];  // log(N), glibc values tabulated on the host
+        u = uni(h.y);
+        ow = uni(h.w);
+        if (untried_count(u)) break;  // untried moves left: expand here
+        if (depth >= kMaxDepth - 2) {  // unreachable (a C4 tree is <= 42 deep); never spin
+            status = ZC_STATUS_INTERNAL;
+            u = 0;
+            break;
+        }
+        const uint32_t nm = u >> 28;
+        const bool valid = k < nm && ch != 0xFFFF;
+        int best;
+        const uint64_t unvisited = __ballot(valid && na == 0) & 0xFFull;
+        if (unvisited) {  // +inf beats everything; first such slot
+            best = __builtin_ctzll(unvisited);
+        } else {
+            // UCT (mcts.cpp:41-45) = fma(c, sqrt(log(N)/Na), Qa), first max in slot order
+            const double q = QW ? (valid ? qw / (double)na : 0.0) : qw;
+            double v = valid ? fma(c, sqrt(lg / (double)na), q) : -INFINITY;
+            int bi = (int)k;
+            argmax8(v, bi);
+            if ((__ballot(v == -INFINITY) & 1ull) != 0) break;  // no child: terminal leaf
+            best = uni(bi);
+        }
+        const int nxt = __builtin_amdgcn_readlane((int)ch, best);
+        nN = __builtin_amdgcn_readlane(na, best);
+        const uint64_t bit = drop_bit(b0 | b1, (int)((ow >> (3 * best)) & 7u));
+        if (turn) b1 |= bit; else b0 |= bit;
+        turn ^= 1;
+        node = nxt;
+        ++depth;
+        if (lane == (uint32_t)depth) pathv = (uint32_t)node | ((uint32_t)best << 16);
+    }
+    int cmask = legal_mask(b0 | b1);  // legal columns of the current node
+    const int x0node = node;
+    bool x0_dirty = false;
+    uint32_t x_u = u, x_ch = ch;
+    fs.f0 = f0;
+    fs.x0node = x0node;
+    fs.d0 = depth;
+    fs.ppath = pathv;
+    stamp.mark(1);
+
+    for (int j = 0; j < nb; ++j) {
+        // resume at `node` (fully described by u, ow, ch, cmask in registers)
+        for (;;) {
+            if (untried_count(u)) break;  // untried moves: expand here
+            const uint64_t fm = __ballot(k < (u >> 28) && ch != 0xFFFF && (int)ch >= f0) & 0xFFull;
+            if (!fm) break;  // no child at all: terminal, re-queued as its own leaf
+            const int s = __builtin_ctzll(fm);
+            const int child = __builtin_amdgcn_readlane((int)ch, s);
+            if (node == x0node) {  // leaving X0 for good (walks never go back up)
+                x_u = u;
+                x_ch = ch;
+            }
+            const uint64_t bit = drop_bit(b0 | b1, (int)((ow >> (3 * s)) & 7u));
+            if (turn) b1 |= bit; else b0 |= bit;
+            turn ^= 1;
+            ++depth;
+            if (lane == (uint32_t)depth) pathv = (uint32_t)child | ((uint32_t)s << 16);
+            node = child;
+            const uint4 fh = *(const uint4 *)&fresh[child - f0];  // u, ow, link, lmask
+            u = uni(fh.x);
+            ow = uni(fh.y);
+            cmask = uni((int)fh.w);
+            ch = fresh[child - f0].ch[k];
+        }
+        stamp.mark(2);
+        int leaf = node, ldepth = depth, lturn = turn, lmask = cmask;
+        uint64_t l0 = b0, l1 = b1;
+        const uint32_t cnt = untried_count(u);
+        if (cnt) {  // expand (mcts.cpp:65-78): policy = random.choice(untried)
+            const uint32_t r = rng_below(rng, cnt);
+            const int mi = (int)uni((uint32_t)s_sel[(u & 0x7Fu) * 8u + r]);
+            u &= ~(1u << mi);
+            const int col = (int)((ow >> (3 * mi)) & 7u);
+            const uint64_t bit = drop_bit(b0 | b1, col);
+            if (turn) l1 |= bit; else l0 |= bit;
+            lturn = turn ^ 1;
+            leaf = nnodes++;
+            ldepth = depth + 1;
+            if (bit & kTop) lmask &= ~(1 << col);  // the column just filled
+            const uint32_t low_ = uni(s_order[lmask]);
+            if (k == (uint32_t)mi) ch = (uint32_t)leaf;
+            if (node < f0) x0_dirty = true;  // X0 itself: written back when the flush is published
+            if (lane == 0) {
+                // Node(state, legal_moves) (mcts.cpp:23-34): all moves untried, no children
+                *(uint4 *)&fresh[leaf - f0] =
+                    make_uint4(untried_init((low_ >> 24) & 15u), low_,
+                               (uint32_t)node | ((uint32_t)mi << 16) | ((uint32_t)ldepth << 24), (uint32_t)lmask);
+                if (node >= f0) fresh[node - f0].u = u;  // the parent's copy in LDS
+            }
+            if (node >= f0 && lane == (uint32_t)mi) fresh[node - f0].ch[mi] = (uint16_t)leaf;
+            cn.add(cn.expansions, 1);
+            cn.add(cn.depth_sum, ldepth);
+        }
+        // the leaf's path: the walk's path plus the new node (the next walk resumes at `node`)
+        const uint32_t lpath = (cnt && lane == (uint32_t)ldepth) ? (uint32_t)leaf : pathv;
+        if (lane == 0) {
+            leaves[j].p0 = l0;
+            leaves[j].p1 = l1;
+            leaves[j].meta = (uint32_t)leaf | ((uint32_t)ldepth << 16) | ((uint32_t)lturn << 24) |
+                             ((uint32_t)lmask << 25);
+        }
+        if (lane < (uint32_t)kMaxDepth) paths[j * kMaxDepth + lane] = (uint16_t)lpath;
+        wave_mem_order();
+        stamp.mark(3);
+    }
+    if (node == x0node) {
+        x_u = u;
+        x_ch = ch;
+    }
+    fs.x0_dirty = x0_dirty;
+    fs.x_u = x_u;
+    fs.x_ch = x_ch;
+}
+
+}  // namespace
+}  // namespace zc

@@ -61,8 +61,8 @@ int dalloc(zc_engine *e, T **p, size_t count) {
 }
 
 void free_arena(zc::Arena &a) {
-    void *ptrs[] = {a.nodes, a.W, a.ring, a.rngpos,
-                    a.logtab, a.phase, a.roots, a.move, a.na, a.ids, a.stats};
+    void *ptrs[] = {a.nodes, a.W,     a.ring,  a.rngpos, a.logtab,  a.phase,    a.roots,    a.move,
+                    a.na,    a.ids,   a.stats, a.ext_ctl, a.ext_paths, a.ext_meta, a.ext_roots};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
     a = zc::Arena{};
@@ -116,6 +116,36 @@ zc::SearchParams make_params(zc_engine *e, int32_t first, int32_t n, const zc_c4
 
 }  // namespace
 
+// ---------------------------------------------------------------- stepwise search
+namespace {
+zc::ExtParams ext_params(zc_engine *e, int32_t first, int32_t n) {
+    zc::ExtParams p{};
+    p.first_game = first;
+    p.n_games = n;
+    p.sims = e->ext_sims;
+    p.bs = e->ext_bs;
+    p.M = e->M;
+    p.max_batch = e->cfg.max_batch;
+    p.c = e->ext_c;
+    p.a = e->a;
+    return p;
+}
+
+int check_ext_range(const zc_engine *e, int32_t first, int32_t n) {
+    if (!e->ext_active) return fail(ZC_EINVAL, "no stepwise search in progress (call zc_c4_ext_begin first)");
+    if (first < e->ext_first || n < 0 || (int64_t)first + n > (int64_t)e->ext_first + e->ext_n)
+        return fail(ZC_EINVAL, "games [%d, %d) outside the stepwise search's range [%d, %d)", first, first + n,
+                    e->ext_first, e->ext_first + e->ext_n);
+    return ZC_OK;
+}
+
+int check_flush(const zc_engine *e, int32_t flush) {
+    const int nflush = (e->ext_sims + e->ext_bs - 1) / e->ext_bs;
+    if (flush < 0 || flush >= nflush) return fail(ZC_EINVAL, "flush %d outside [0, %d)", flush, nflush);
+    return ZC_OK;
+}
+}  // namespace
+
 extern "C" {
 
 const char *zc_version(void) { return "zeroclone_amd 0.1.0 (gfx950)"; }
@@ -158,6 +188,11 @@ int zc_engine_create(const zc_engine_config *cfg, zc_engine **out) {
     if (!rc) rc = dalloc(e, &a.na, G * 7);
     if (!rc) rc = dalloc(e, &a.ids, G);
     if (!rc) rc = dalloc(e, &a.stats, G);
+    if (!rc) rc = dalloc(e, &a.ext_ctl, G * zc::kCtlWords);
+    if (!rc && hipMemset(a.ext_ctl, 0, G * zc::kCtlWords * sizeof(int32_t)) != hipSuccess) rc = fail(ZC_EHIP, "memset failed");
+    if (!rc) rc = dalloc(e, &a.ext_paths, G * (size_t)cfg->max_batch * zc::kMaxDepth);
+    if (!rc) rc = dalloc(e, &a.ext_meta, G * (size_t)cfg->max_batch);
+    if (!rc) rc = dalloc(e, &a.ext_roots, G);
     if (!rc && hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess)
         rc = fail(ZC_EHIP, "hipStreamCreate failed");
     if (!rc) {
@@ -363,6 +398,79 @@ int zc_c4_rollouts(zc_engine *eng, int32_t game, int32_t n, const zc_c4_state *s
     (void)hipFree(dv);
     (void)hipFree(dw);
     if (out_words) *out_words = words;
+    return ZC_OK;
+}
+
+
+int zc_c4_ext_begin(zc_engine *eng, int32_t first, int32_t n, const zc_c4_state *d_roots, int32_t sims, double c,
+                    int32_t bs, void *hip_stream) {
+    if (!eng || (n && !d_roots)) return fail(ZC_EINVAL, "null argument");
+    if (int r = check_search(eng, first, n, sims, c, bs)) return r;
+    std::lock_guard<std::mutex> lk(eng->mu);
+    ZC_HIP(hipSetDevice(eng->cfg.device));
+    eng->ext_first = first;
+    eng->ext_n = n;
+    eng->ext_sims = sims;
+    eng->ext_bs = bs;
+    eng->ext_c = c;
+    eng->ext_active = true;
+    if (!n) return ZC_OK;
+    zc::ExtParams p = ext_params(eng, first, n);
+    p.roots = d_roots;
+    zc::launch_c4_ext_begin(p, (hipStream_t)hip_stream);
+    ZC_HIP(hipGetLastError());
+    return ZC_OK;
+}
+
+int zc_c4_ext_select(zc_engine *eng, int32_t first, int32_t n, int32_t flush, zc_c4_state *d_leaves, void *d_planes,
+                     int32_t planes_dtype, int32_t *d_counts, void *hip_stream) {
+    if (!eng) return fail(ZC_EINVAL, "null argument");
+    if (planes_dtype != ZC_F32 && planes_dtype != ZC_F16) return fail(ZC_EINVAL, "planes_dtype must be ZC_F32 or ZC_F16");
+    std::lock_guard<std::mutex> lk(eng->mu);
+    if (int r = check_ext_range(eng, first, n)) return r;
+    if (int r = check_flush(eng, flush)) return r;
+    if (!n) return ZC_OK;
+    ZC_HIP(hipSetDevice(eng->cfg.device));
+    zc::ExtParams p = ext_params(eng, first, n);
+    p.flush = flush;
+    p.leaves = d_leaves;
+    p.planes = d_planes;
+    p.planes_f16 = planes_dtype == ZC_F16;
+    p.counts = d_counts;
+    zc::launch_c4_ext_select(p, (hipStream_t)hip_stream);
+    ZC_HIP(hipGetLastError());
+    return ZC_OK;
+}
+
+int zc_c4_ext_backup(zc_engine *eng, int32_t first, int32_t n, int32_t flush, const double *d_values,
+                     void *hip_stream) {
+    if (!eng || (n && !d_values)) return fail(ZC_EINVAL, "null argument");
+    std::lock_guard<std::mutex> lk(eng->mu);
+    if (int r = check_ext_range(eng, first, n)) return r;
+    if (int r = check_flush(eng, flush)) return r;
+    if (!n) return ZC_OK;
+    ZC_HIP(hipSetDevice(eng->cfg.device));
+    zc::ExtParams p = ext_params(eng, first, n);
+    p.flush = flush;
+    p.values = d_values;
+    zc::launch_c4_ext_backup(p, (hipStream_t)hip_stream);
+    ZC_HIP(hipGetLastError());
+    return ZC_OK;
+}
+
+int zc_c4_ext_end(zc_engine *eng, int32_t first, int32_t n, int32_t *d_move, int32_t *d_na, zc_game_stats *d_stats,
+                  void *hip_stream) {
+    if (!eng || (n && (!d_move || !d_na || !d_stats))) return fail(ZC_EINVAL, "null argument");
+    std::lock_guard<std::mutex> lk(eng->mu);
+    if (int r = check_ext_range(eng, first, n)) return r;
+    if (!n) return ZC_OK;
+    ZC_HIP(hipSetDevice(eng->cfg.device));
+    zc::ExtParams p = ext_params(eng, first, n);
+    p.out_move = d_move;
+    p.out_na = d_na;
+    p.out_stats = d_stats;
+    zc::launch_c4_ext_end(p, (hipStream_t)hip_stream);
+    ZC_HIP(hipGetLastError());
     return ZC_OK;
 }
 

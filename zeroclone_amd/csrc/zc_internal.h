@@ -17,19 +17,20 @@ namespace zc {
 // 128-byte line — everything selection reads for a node (mcts.cpp:10-39 Node, minus the
 // Python objects) — so the per-level load of the tree walk is one L2 line per game:
 //
-//   +0   u32  N            visit count of this node                   (Node::N)
-//   +4   u32  untried      bits 0..20: 3-bit move indices in order   (Node::untried)
-//                          bits 24..27: #untried, bits 28..31: #moves (Node::moves.size())
-//   +8   u16  parent       0xFFFF at the root                         (Node::parent)
-//   +10  u8   pact         index of this node in parent's moves       (parent_action_idx)
-//   +11  u8   depth        root = 0
-//   +12  u32  order        packed columns of the move list (CPython set order)
+//   +0   u32  (unused)     Node::N is not stored: it equals Na of the in-edge (root: the
+//                          number of leaves flushed so far)
+//   +4   u32  untried      bit i (i < 7) set while move i is untried    (Node::untried)
+//                          bits 28..31: #moves                          (Node::moves.size())
+//   +8   u32  link         parent (u16, 0xFFFF at the root) | pact << 16 | depth << 24
+//                                                  (Node::parent, parent_action_idx)
+//   +12  u32  order        packed 3-bit columns of the move list (CPython set order),
+//                          bits 24..27: #moves
 //   +16  u16  child[8]     0xFFFF = null                              (Node::children)
 //   +32  i32  Na[8]                                                    (Node::Na)
-//   +64  f64  Q[8]         Q[a] = W[a]/Na[a]; slot 7 holds log(N) of THIS node
-//                                                                      (Node::Qa)
-// Wa (integer in rollout mode) lives in a separate [game][M][8] i32 array: only backup
-// touches it.  Boards are not stored: the walk re-applies moves from the root.
+//   +64  f64  [8]          rollout search: Qa = Wa / Na                (Node::Qa)
+//                          stepwise search: Wa in fp64 (Qa is formed as Wa / Na when read)
+// In the rollout search Wa is an integer and lives in a separate [game][M][8] i32 array:
+// only backup touches it.  Boards are not stored: the walk re-applies moves from the root.
 constexpr int kRecBytes = 128;
 constexpr int kSlots = 8;
 constexpr int kMaxDepth = 44;          // levels 0..42 (a C4 game has at most 42 plies)
@@ -55,6 +56,25 @@ struct Arena {
     int32_t *na = nullptr;
     int32_t *ids = nullptr;
     zc_game_stats *stats = nullptr;
+    // stepwise (caller-valued) search: per-game control words and the pending flush
+    int32_t *ext_ctl = nullptr;       // [G][kCtlWords]
+    uint16_t *ext_paths = nullptr;    // [G][max_batch][kMaxDepth]  node ids of each leaf's path
+    uint32_t *ext_meta = nullptr;     // [G][max_batch]             leaf node | depth << 16 | turn << 24
+    zc_c4_state *ext_roots = nullptr; // [G]
+};
+
+// ext_ctl words of one game
+enum : int {
+    kCtlNodes = 0,   // nodes in the tree
+    kCtlF0 = 1,      // first node of the pending flush
+    kCtlD0 = 2,      // depth of the flush's X0
+    kCtlNb = 3,      // leaves in the pending flush
+    kCtlStatus = 5,  // ZC_STATUS_*
+    kCtlExp = 6,     // expansions so far
+    kCtlDepth = 7,   // sum of expansion depths
+    kCtlUse0 = 8,    // (2 words) RNG position at begin
+    kCtlPath = 16,   // [kMaxDepth] root..X0: node | slot << 16
+    kCtlWords = 64,
 };
 
 struct SearchParams {
@@ -69,7 +89,25 @@ struct SearchParams {
     int stamp;
 };
 
+struct ExtParams {
+    int first_game, n_games, sims, bs, M, max_batch, flush;
+    double c;
+    Arena a;
+    const zc_c4_state *roots;  // begin
+    zc_c4_state *leaves;       // select (optional)
+    void *planes;              // select (optional)
+    int planes_f16;
+    int32_t *counts;           // select (optional)
+    const double *values;      // backup
+    int32_t *out_move, *out_na;
+    zc_game_stats *out_stats;  // end
+};
+
 size_t c4_search_lds_bytes(int bs);
+void launch_c4_ext_begin(const ExtParams &p, hipStream_t s);
+void launch_c4_ext_select(const ExtParams &p, hipStream_t s);
+void launch_c4_ext_backup(const ExtParams &p, hipStream_t s);
+void launch_c4_ext_end(const ExtParams &p, hipStream_t s);
 void launch_c4_search(const SearchParams &p, hipStream_t s);
 void launch_c4_rollout_debug(const Arena &a, int M, int first_game, int n, const zc_c4_state *states,
                              int32_t *out_value, int64_t *out_words, hipStream_t s);
@@ -88,5 +126,9 @@ struct zc_engine {
     zc::Arena a;
     int64_t bytes = 0;
     int stamp = 0;
+    // the stepwise search in progress (zc_c4_ext_begin .. end)
+    int ext_first = 0, ext_n = 0, ext_sims = 0, ext_bs = 0, ext_flushes_done = 0;
+    double ext_c = 0;
+    bool ext_active = false;
     std::mutex mu;
 };

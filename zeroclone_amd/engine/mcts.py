@@ -9,11 +9,18 @@ stream is handed back advanced by exactly what the reference would have consumed
 `random.seed(s); get_move(...)` returns the reference's move and leaves `random` in the
 reference's state.  The GIL is released during the device call (ctypes).
 
-Supported plugin combination: the Connect4 backend (this package's c4_backend, or any
-module with the reference c4_backend's State layout), Policy('random') and
-Value('random_rollout').  Anything else raises NotImplementedError: there is no CPU search.
+Supported plugins: the Connect4 backend (this package's c4_backend, or any module with the
+reference c4_backend's State layout) and Policy('random').  Value('random_rollout') runs
+entirely on the device (zc_c4_search_games); any other value object runs through the
+stepwise search (zc_c4_ext_*, zeroclone_amd/valued.py): the tree stays on the GPU and
+value.batch(states, backend=backend) is called on the host once per flush, exactly where
+the reference calls it (mcts.cpp:116).  Such a value function must not draw from `random`
+(the reference's NN and crude-score values do not).  Anything else raises
+NotImplementedError: there is no CPU search.
 """
 from __future__ import annotations
+
+import numpy as np
 
 from . import _device
 
@@ -31,10 +38,13 @@ def _plugin_check(state, value, policy, backend):
     pname = getattr(policy, "name", None)
     if pname != "random":
         raise NotImplementedError(f"policy {pname!r}: only Policy('random') is implemented on the GPU")
-    vname = getattr(value, "name", None)
-    if vname != "random_rollout" or hasattr(value, "_req_q"):
-        raise NotImplementedError(f"value {vname!r}: only Value('random_rollout') is implemented on the GPU")
+    if not callable(getattr(value, "batch", None)):
+        raise NotImplementedError("value objects must provide .batch(states, backend=) (value_functions.py:20)")
     return c4
+
+
+def _device_rollouts(value) -> bool:
+    return getattr(value, "name", None) == "random_rollout" and not hasattr(value, "_req_q")
 
 
 def get_move(state, value, policy, backend, simulations=1000, c=1.4, batch_size=32):
@@ -49,7 +59,22 @@ def get_move(state, value, policy, backend, simulations=1000, c=1.4, batch_size=
         eng = ge.ensure(1, simulations, batch_size)
         mt, idx, ver, gauss = _device.python_random_state()
         eng.set_rng_state(0, mt, idx)
-        mv, _, _ = eng.c4_search_games([0], roots, simulations, c, batch_size)
+        if _device_rollouts(value):
+            mv, _, _ = eng.c4_search_games([0], roots, simulations, c, batch_size)
+        else:
+            mv = _valued_search(eng, roots, simulations, c, batch_size, value, backend)
         mt, idx = eng.get_rng_state(0)
         _device.set_python_random_state(mt, idx, ver, gauss)
     return (int(mv[0]), 0)
+
+
+def _valued_search(eng, roots, sims, c, bs, value, backend):
+    import torch
+    from ..valued import C4ValuedSearch, HostValue
+    vs = C4ValuedSearch(eng, 1, bs, planes=False)
+    r = torch.from_numpy(roots.view(np.int64).reshape(1, 3).copy()).to(vs.dev)
+    mv, _, st = vs.run(r, sims, c, HostValue(value, backend))
+    st = st.cpu().numpy()
+    if st[0, 5]:
+        raise ValueError(f"invalid root for the search (status {int(st[0, 5])})")
+    return mv.cpu().numpy()

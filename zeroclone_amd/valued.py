@@ -1,0 +1,126 @@
+"""Stepwise Connect4 search with caller-supplied leaf values (include/zeroclone.h zc_c4_ext_*).
+
+mcts.get_move (engine/mcts/src/mcts.cpp:102-160) pauses at every flush (:112-127) and hands
+the pending leaves to `value.batch` (engine/value_functions.py:16-32).  `C4ValuedSearch`
+drives the same loop for many games at once with the tree on the GPU:
+
+    begin -> [select(f) -> value_fn(leaves, planes, counts) -> backup(f)] * n_flush -> end
+
+`value_fn` returns one fp64 value per leaf slot (n_games * batch_size, leaf j of game i at
+i*batch_size + j) for the leaf's side to move.  Two value functions are provided:
+
+* `NetValue(model)` — the reference's network modes (value_functions.py:61-99, network.py):
+  the planes are built on the device in state_to_tensor layout and fed straight into the
+  fp16 model; no host round trip, so a whole move can be captured in one HIP graph
+  (`C4ValuedSearch.capture`).
+* `HostValue(value, backend)` — any reference-style Value object: the leaves go to the host
+  as c4_backend states and `value.batch(states, backend=backend)` is called once per game
+  per flush, as the reference does.  Slow, but it runs any plugin on the GPU tree search.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from . import _native
+
+
+def _stream(dev) -> int:
+    return torch.cuda.current_stream(dev).cuda_stream
+
+
+class C4ValuedSearch:
+    def __init__(self, eng: "_native.NativeEngine", n_games: int, batch_size: int = 32,
+                 planes_dtype: torch.dtype = torch.float16, leaves: bool = True, planes: bool = True):
+        if batch_size > eng.max_batch:
+            raise ValueError(f"batch_size {batch_size} > engine max_batch {eng.max_batch}")
+        if n_games > eng.max_games:
+            raise ValueError(f"{n_games} games > engine capacity {eng.max_games}")
+        if planes_dtype not in (torch.float16, torch.float32):
+            raise ValueError("planes_dtype must be float16 or float32")
+        self.eng, self.n, self.bs = eng, n_games, batch_size
+        self.dev = torch.device("cuda", eng.device)
+        L = n_games * batch_size
+        self.leaves = torch.zeros((L, 3), dtype=torch.int64, device=self.dev) if leaves else None
+        self.planes = torch.zeros((L, 2, 6, 7), dtype=planes_dtype, device=self.dev) if planes else None
+        self.counts = torch.zeros(n_games, dtype=torch.int32, device=self.dev)
+        self.values = torch.zeros(L, dtype=torch.float64, device=self.dev)
+        self.move = torch.zeros(n_games, dtype=torch.int32, device=self.dev)
+        self.na = torch.zeros((n_games, 7), dtype=torch.int32, device=self.dev)
+        self.stats = torch.zeros((n_games, _native.STATS_FIELDS), dtype=torch.int64, device=self.dev)
+
+    def _ptr(self, t):
+        return t.data_ptr() if t is not None else 0
+
+    def enqueue(self, roots: torch.Tensor, sims: int, c: float, value_fn, first_game: int = 0):
+        """Enqueue one whole move on torch's current stream (no host synchronisation unless
+        value_fn makes one)."""
+        if roots.shape != (self.n, 3) or roots.dtype != torch.int64 or not roots.is_contiguous():
+            raise ValueError("roots must be a contiguous int64 [n_games, 3] tensor of zc_c4_state rows")
+        if roots.device != self.dev:
+            raise ValueError("roots must live on the engine's device")
+        s = _stream(self.dev)
+        e, n = self.eng, self.n
+        e.c4_ext_begin(first_game, n, roots.data_ptr(), sims, c, self.bs, s)
+        for f in range((sims + self.bs - 1) // self.bs):
+            e.c4_ext_select(first_game, n, f, self._ptr(self.leaves), self._ptr(self.planes),
+                            self.planes is None or self.planes.dtype == torch.float16, self.counts.data_ptr(), s)
+            v = value_fn(self.leaves, self.planes, self.counts)
+            if v is not self.values:
+                self.values.copy_(v.reshape(-1))
+            e.c4_ext_backup(first_game, n, f, self.values.data_ptr(), _stream(self.dev))
+        e.c4_ext_end(first_game, n, self.move.data_ptr(), self.na.data_ptr(), self.stats.data_ptr(),
+                     _stream(self.dev))
+        return self.move, self.na, self.stats
+
+    def run(self, roots: torch.Tensor, sims: int, c: float, value_fn, first_game: int = 0):
+        self.enqueue(roots, sims, c, value_fn, first_game)
+        torch.cuda.current_stream(self.dev).synchronize()
+        return self.move, self.na, self.stats
+
+    def capture(self, roots: torch.Tensor, sims: int, c: float, value_fn, first_game: int = 0):
+        """Capture one move into a HIP graph (value_fn must be capturable, e.g. NetValue).
+        Returns the graph; graph.replay() re-runs the move on the current contents of
+        `roots` and of the games' RNG streams."""
+        side = torch.cuda.Stream(self.dev)
+        side.wait_stream(torch.cuda.current_stream(self.dev))
+        with torch.cuda.stream(side):  # warm the value function's kernels outside capture
+            value_fn(self.leaves, self.planes, self.counts)
+        torch.cuda.current_stream(self.dev).wait_stream(side)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self.enqueue(roots, sims, c, value_fn, first_game)
+        return g
+
+
+class NetValue:
+    """Value('network_*') (value_functions.py:61-99): model(planes) in the planes' dtype;
+    the [B, 1] output is the value for each leaf's side to move."""
+
+    def __init__(self, model: torch.nn.Module):
+        self.model = model
+
+    @torch.no_grad()
+    def __call__(self, leaves, planes, counts):
+        return self.model(planes).reshape(-1).to(torch.float64)
+
+
+class HostValue:
+    """Any reference-style Value object: value.batch(states, backend=backend) per game per
+    flush, on c4_backend states built from the device leaves."""
+
+    def __init__(self, value, backend):
+        self.value, self.backend = value, backend
+
+    def __call__(self, leaves, planes, counts):
+        from .engine.games.connect4 import c4_backend as zb
+        rows = leaves.cpu().numpy().view(np.uint64)
+        cnt = counts.cpu().numpy()
+        bs = rows.shape[0] // cnt.shape[0]
+        out = np.zeros(rows.shape[0], np.float64)
+        for i, k in enumerate(cnt):
+            if k == 0:
+                continue
+            states = [zb.from_zc(int(r[0]), int(r[1]), int(r[2]) & 1) for r in rows[i * bs: i * bs + k]]
+            out[i * bs: i * bs + k] = [float(v) for v in self.value.batch(states, backend=self.backend)]
+        return torch.from_numpy(out).to(leaves.device)
