@@ -57,6 +57,41 @@ def cpu_baseline(sims: int, bs: int, c: float, budget_s: float = 15.0):
                       f"batch {bs}, {threads} pthreads, oracle/c4_oracle.c, {dt:.1f}s"}
 
 
+MFMA_F16_PEAK_TFLOPS = 2500.0  # MI355X dense fp16 MFMA peak, ~2.5 PF (MI355X_MICROARCH.md; no sparsity)
+
+
+def net_mode(games: int, sims: int, bs: int, c: float, steps: int, dev) -> dict:
+    """C2(iii): the same search with a random-init value network instead of rollouts
+    (stepwise search zc_c4_ext_*, fp16 ValueNetwork(128, 8, in_planes=2) between the select
+    and backup kernels of every flush), one move per step captured in a HIP graph."""
+    from zeroclone_amd.nets import ValueNetwork, flops_per_position, for_inference
+    from zeroclone_amd.valued import C4ValuedSearch, NetValue
+    torch.manual_seed(0)
+    model = for_inference(ValueNetwork(128, 8, in_planes=2).eval(), dev, torch.float16)
+    eng = _native.NativeEngine(max_games=games, max_sims=sims, max_batch=bs, device=dev.index)
+    eng.seed(0, list(range(games)))
+    vs = C4ValuedSearch(eng, games, bs, leaves=False)
+    roots = torch.zeros((games, 3), dtype=torch.int64, device=dev)
+    g = vs.capture(roots, sims, c, NetValue(model))
+    g.replay()   # warm-up move
+    torch.cuda.synchronize(dev)
+    exp = 0
+    t = time.perf_counter()
+    for _ in range(steps):
+        g.replay()
+        exp += int(vs.stats[:, 0].sum().item())
+    dt = time.perf_counter() - t
+    flushes = (sims + bs - 1) // bs
+    fl = flops_per_position(128, 8, 2, 6, 7) * games * bs * flushes * steps
+    eng.close()
+    return {"value": round(exp / dt, 1), "unit": "expansions/s", "ms_per_move": round(dt / steps * 1e3, 1),
+            "net": "ValueNetwork(128, 8, in_planes=2) random init, fp16, BN folded, channels-last (MIOpen)",
+            "net_tflops_upper": round(fl / dt / 1e12, 1),
+            "mfma_frac_upper": round(fl / dt / 1e12 / MFMA_F16_PEAK_TFLOPS, 4),
+            "note": "TFLOP/s = network FLOPs / whole move time (search kernels included), so a lower bound "
+                    "on the network's own rate; stepwise search, per-flush leaf planes built on the device"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -68,6 +103,8 @@ def main():
     ap.add_argument("--c", type=float, default=1.4)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--net-steps", type=int, default=1,
+                    help="moves of the C2(iii) value-network mode reported under extra (0 = skip; N=1 only)")
     ap.add_argument("--traffic-bytes", type=float, default=None,
                     help="per-launch HBM bytes of the search kernel from a separate rocprofv3 --pmc pass")
     args = ap.parse_args()
@@ -182,6 +219,8 @@ def main():
             "extra": {"expansions": expansions, "leaves": leaves, "mean_depth": round(depth_sum / max(expansions, 1), 3),
                       "games_finished": finished, "search_ms_per_step": [round(x, 3) for x in kernel_ms]},
         }
+        if world == 1 and args.net_steps > 0:
+            out["extra"]["c2_value_net"] = net_mode(G, S, B, args.c, args.net_steps, dev)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(S, B, args.c)
         else:

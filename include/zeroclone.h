@@ -174,6 +174,50 @@ int zc_c4_to_rows(const zc_c4_state *s, char *rows42);
  * (bit c = column c playable); writes the columns to cols[0..n) and returns n (0..7). */
 int zc_c4_legal_order(int32_t mask, int32_t *cols);
 
+/* ---- Chess rules on the device (engine/games/chess/src/chess_backend.cpp) -----------
+ * A position in the reference's own encoding (include/state.h State, minus the history
+ * deques, which only check_draw's repetition test reads and which stay with the host State):
+ *   board[64]  State.board: ' ' empty, "PNBRQK" white, "pnbrqk" black; index 0 = a8 (row 0 =
+ *              rank 8), row-major
+ *   turn       0 = white to move; fifty = fifty_move_rule_counter (uint8, wraps like it)
+ *   castle     bit 0 w_ck, 1 w_cq, 2 b_ck, 3 b_cq
+ * A move is a uint16: from | to << 6 | capture value << 12, squares = row*8 + col, capture
+ * value = fabs(piece_val) of the captured piece (the Move tuple's double: 0,1,3,5,9).
+ * Move lists hold ZC_CHESS_MAX_MOVES slots per position, in the reference's order. */
+typedef struct zc_chess_state {
+    uint8_t board[64];
+    uint8_t turn;
+    uint8_t fifty;
+    uint8_t castle;
+    uint8_t reserved[5];
+} zc_chess_state;
+#define ZC_CHESS_MAX_MOVES 256
+#define ZC_CHESS_WIN 1        /* check_win: no legal move and in check                    */
+#define ZC_CHESS_STALEMATE 2  /* no legal move, not in check (check_draw)                  */
+#define ZC_CHESS_FIFTY 4      /* fifty_move_rule_counter >= 50 (check_draw)                */
+#define ZC_CHESS_OVERFLOW 8   /* more than ZC_CHESS_MAX_MOVES legal moves (never in chess) */
+
+/* get_legal_moves for n positions: d_moves[i*ZC_CHESS_MAX_MOVES + j], d_counts[i] (-1 =
+ * overflow).  Device pointers, enqueued on hip_stream (NULL = null stream). */
+int zc_chess_legal_moves_async(zc_engine *eng, int32_t n, const zc_chess_state *d_states, uint16_t *d_moves,
+                               int32_t *d_counts, void *hip_stream);
+/* play_move of every legal move: d_children[i*ZC_CHESS_MAX_MOVES + j] (and the moves, if
+ * d_moves is not NULL). */
+int zc_chess_children_async(zc_engine *eng, int32_t n, const zc_chess_state *d_states, zc_chess_state *d_children,
+                            uint16_t *d_moves, int32_t *d_counts, void *hip_stream);
+/* d_out[i] = play_move(d_in[i], d_moves[i]) (d_out may equal d_in). */
+int zc_chess_play_async(zc_engine *eng, int32_t n, const zc_chess_state *d_in, const uint16_t *d_moves,
+                        zc_chess_state *d_out, void *hip_stream);
+/* ZC_CHESS_* flags per position (check_win; check_draw without the repetition test). */
+int zc_chess_terminal_async(zc_engine *eng, int32_t n, const zc_chess_state *d_states, int32_t *d_flags,
+                            void *hip_stream);
+/* state_to_tensor: [n][17][8][8], planes_dtype ZC_F32 / ZC_F16. */
+int zc_chess_planes_async(zc_engine *eng, int32_t n, const zc_chess_state *d_states, void *d_planes,
+                          int32_t planes_dtype, void *hip_stream);
+/* state_from_fen (:525-556) / create_init_state (:446-457) on the host. */
+int zc_chess_from_fen(const char *fen, zc_chess_state *out);
+int zc_chess_init(zc_chess_state *out);
+
 /* ---- self-test hooks (used by the parity tests) -------------------------------------
  * UCT score exactly as the search kernel computes it (mcts.cpp:41-45), evaluated ON THE
  * DEVICE for n inputs: out[i] = na[i]==0 ? +inf : fma(c, sqrt(logn[i]/na[i]), q[i]). */

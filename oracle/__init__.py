@@ -163,3 +163,102 @@ def get_move_batch(boards: list[str], turns, seeds, sims: int, c: float = 1.4, b
                              sims, c, bs, threads, mv.ctypes.data_as(P(ctypes.c_int)),
                              na.ctypes.data_as(P(ctypes.c_int)), cons.ctypes.data_as(P(ctypes.c_uint64)))
     return mv, na, cons
+
+
+# ---------------------------------------------------------------- chess (chess_oracle.c)
+class ZccMove(ctypes.Structure):
+    _fields_ = [("fr", ctypes.c_uint8), ("fc", ctypes.c_uint8), ("tr", ctypes.c_uint8), ("tc", ctypes.c_uint8),
+                ("value", ctypes.c_double)]
+
+
+ZCC_HIST = 512
+ZCC_MAX_MOVES = 256
+
+
+class ZccState(ctypes.Structure):
+    _fields_ = [("board", ctypes.c_uint8 * 64), ("turn", ctypes.c_uint8), ("fifty", ctypes.c_uint8),
+                ("castle", ctypes.c_uint8), ("overflow", ctypes.c_uint8), ("nhw", ctypes.c_int), ("nhb", ctypes.c_int),
+                ("hw", ZccMove * ZCC_HIST), ("hb", ZccMove * ZCC_HIST)]
+
+
+def _chess_lib():
+    L = lib()
+    if not getattr(L, "_chess_ready", False):
+        P = ctypes.POINTER
+        L.zcc_init.argtypes = [P(ZccState)]
+        L.zcc_from_fen.argtypes = [ctypes.c_char_p, P(ZccState)]
+        L.zcc_legal_moves.argtypes = [P(ZccState), P(ZccMove)]
+        L.zcc_play.argtypes = [P(ZccState), P(ZccMove), P(ZccState)]
+        L.zcc_check_win.argtypes = [P(ZccState)]
+        L.zcc_check_draw.argtypes = [P(ZccState)]
+        L.zcc_state_to_tensor.argtypes = [P(ZccState), P(ctypes.c_float)]
+        L.zcc_perft.argtypes = [P(ZccState), ctypes.c_int]
+        L.zcc_perft.restype = ctypes.c_uint64
+        L._chess_ready = True
+    return L
+
+
+def _hist_moves(h: str):
+    return [(int(h[i]), int(h[i + 1]), int(h[i + 2]), int(h[i + 3]), float(h[i + 4])) for i in range(0, len(h), 5)]
+
+
+def chess_state(board: str, turn: int = 0, fifty: int = 0, castle: int = 0, hw: str = "", hb: str = "") -> ZccState:
+    """Fields as in tests/golden/chess_*.json (history strings: 5 digits per move)."""
+    s = ZccState()
+    s.board[:] = list(board.encode("latin-1"))
+    s.turn, s.fifty, s.castle = turn, fifty, castle
+    for name, h in (("hw", hw), ("hb", hb)):
+        ms = _hist_moves(h)
+        arr = getattr(s, name)
+        for i, m in enumerate(ms):
+            arr[i] = ZccMove(*m)
+        setattr(s, "n" + name, len(ms))
+    return s
+
+
+def chess_from_json(e: dict) -> ZccState:
+    return chess_state(e["board"], e["turn"], e["fifty"], e["castle"], e.get("hw", ""), e.get("hb", ""))
+
+
+def chess_init() -> ZccState:
+    s = ZccState()
+    _chess_lib().zcc_init(ctypes.byref(s))
+    return s
+
+
+def chess_from_fen(fen: str) -> ZccState:
+    s = ZccState()
+    if _chess_lib().zcc_from_fen(fen.encode(), ctypes.byref(s)):
+        raise ValueError(fen)
+    return s
+
+
+def chess_moves(s: ZccState):
+    out = (ZccMove * ZCC_MAX_MOVES)()
+    n = _chess_lib().zcc_legal_moves(ctypes.byref(s), out)
+    return [(m.fr, m.fc, m.tr, m.tc, m.value) for m in out[:n]]
+
+
+def chess_play(s: ZccState, move) -> ZccState:
+    o = ZccState()
+    _chess_lib().zcc_play(ctypes.byref(s), ctypes.byref(ZccMove(*move)), ctypes.byref(o))
+    return o
+
+
+def chess_win(s: ZccState) -> bool:
+    return bool(_chess_lib().zcc_check_win(ctypes.byref(s)))
+
+
+def chess_draw(s: ZccState) -> bool:
+    return bool(_chess_lib().zcc_check_draw(ctypes.byref(s)))
+
+
+def chess_tensor(s: ZccState):
+    import numpy as np
+    out = np.zeros(17 * 64, np.float32)
+    _chess_lib().zcc_state_to_tensor(ctypes.byref(s), out.ctypes.data_as(ctypes.POINTER(ctypes.c_float)))
+    return out.reshape(17, 8, 8)
+
+
+def chess_perft(s: ZccState, depth: int) -> int:
+    return int(_chess_lib().zcc_perft(ctypes.byref(s), depth))

@@ -1,0 +1,348 @@
+/* chess_oracle.c — TEST INFRASTRUCTURE ONLY: a plain-C restatement of the reference's chess
+ * rules (engine/games/chess/src/chess_backend.cpp), used by tests/ and bench.py's
+ * cpu_baseline to check the HIP move generator.  Never linked into the product.
+ *
+ * Every rule follows the reference, including its departures from standard chess:
+ *   - get_legal_moves (:184-360): an insufficient-material early exit (no P/R/Q of either
+ *     colour and at most one minor piece -> no moves); pseudo-legal moves in board-scan
+ *     order (index 0 = a8, row-major) and, per piece, in the reference's direction order;
+ *     the king can never be captured; no castling and no en passant are generated;
+ *     each move carries fabs(piece value) of the captured piece (0 otherwise);
+ *     legality = the mover's king is not attacked after play_move (:345-359), with the
+ *     king searched on the board (-1,-1 when absent, as find_king :70-83).
+ *   - play_move (:364-400): fifty counter (uint8, +1, reset on a pawn move or a capture),
+ *     castling rights cleared by K moves / R moves FROM column 7 or 0 (any rank), rook hop
+ *     for |dc| = 2 king moves, promotion to a queen on the last rank, move history pushed
+ *     to the FRONT of the mover's list.
+ *   - check_win (:404-412), check_draw (:416-441) with has_repeated_prefix (:148-180).
+ *   - state_to_tensor (:461-521), state_from_fen (:525-556).
+ * Pinned to the reference by tests/golden/chess_*.json (perft counts, ordered move lists
+ * with capture values, terminal flags, tensors, play_move results).
+ */
+#include "chess_oracle.h"
+
+#include <ctype.h>
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+
+static const int KN[8][2] = {{-2, -1}, {-2, 1}, {-1, -2}, {-1, 2}, {1, -2}, {1, 2}, {2, -1}, {2, 1}};
+static const int DIAG[4][2] = {{-1, -1}, {-1, 1}, {1, -1}, {1, 1}};
+static const int ORTH[4][2] = {{-1, 0}, {1, 0}, {0, -1}, {0, 1}};
+static const int ALL8[8][2] = {{-1, -1}, {-1, 1}, {1, -1}, {1, 1}, {-1, 0}, {1, 0}, {0, -1}, {0, 1}};
+
+static int inb(int r, int c) { return (unsigned)r < 8 && (unsigned)c < 8; }
+static int empty_sq(uint8_t x) { return x == ' ' || x == 0; }
+static int is_white(uint8_t x) { return x >= 'A' && x <= 'Z'; }
+static int enemy(uint8_t x, int turn) { return !empty_sq(x) && (turn == 0 ? !is_white(x) : is_white(x)); }
+static int value_of(uint8_t x) {
+    switch (toupper(x)) {
+        case 'P': return 1;
+        case 'N': return 3;
+        case 'B': return 3;
+        case 'R': return 5;
+        case 'Q': return 9;
+        case 'K': return 100;
+        default: return 0;
+    }
+}
+
+static void king_square(const zcc_state *s, int side, int *kr, int *kc) {
+    const uint8_t k = side == 0 ? 'K' : 'k';
+    for (int i = 0; i < 64; i++)
+        if (s->board[i] == k) {
+            *kr = i / 8;
+            *kc = i % 8;
+            return;
+        }
+    *kr = *kc = -1;
+}
+
+/* Is the king of side `t` (= s->turn in the reference) on (kr,kc) attacked? */
+static int attacked(const zcc_state *s, int t, int kr, int kc) {
+    const uint8_t *b = s->board;
+    const int pr = t == 0 ? kr - 1 : kr + 1;
+    const uint8_t pawn = t == 0 ? 'p' : 'P';
+    for (int dc = -1; dc <= 1; dc += 2)
+        if (inb(pr, kc + dc) && b[pr * 8 + kc + dc] == pawn) return 1;
+    const uint8_t kn = t ? 'N' : 'n';
+    for (int i = 0; i < 8; i++) {
+        const int r = kr + KN[i][0], c = kc + KN[i][1];
+        if (inb(r, c) && b[r * 8 + c] == kn) return 1;
+    }
+    const uint8_t q = t ? 'Q' : 'q', rk = t ? 'R' : 'r', bp = t ? 'B' : 'b';
+    for (int pass = 0; pass < 2; pass++) {
+        const int(*D)[2] = pass == 0 ? ORTH : DIAG;
+        const uint8_t p1 = pass == 0 ? rk : bp;
+        for (int i = 0; i < 4; i++) {
+            int r = kr + D[i][0], c = kc + D[i][1];
+            while (inb(r, c)) {
+                const uint8_t x = b[r * 8 + c];
+                if (!empty_sq(x)) {
+                    if (x == p1 || x == q) return 1;
+                    break;
+                }
+                r += D[i][0];
+                c += D[i][1];
+            }
+        }
+    }
+    const uint8_t kk = t ? 'K' : 'k';
+    for (int i = 0; i < 8; i++) {
+        const int r = kr + ALL8[i][0], c = kc + ALL8[i][1];
+        if (inb(r, c) && b[r * 8 + c] == kk) return 1;
+    }
+    return 0;
+}
+
+static void push(zcc_move *out, int *n, int fr, int fc, int tr, int tc, double v) {
+    out[*n].fr = (uint8_t)fr;
+    out[*n].fc = (uint8_t)fc;
+    out[*n].tr = (uint8_t)tr;
+    out[*n].tc = (uint8_t)tc;
+    out[*n].value = v;
+    (*n)++;
+}
+
+static int pseudo_moves(const zcc_state *s, zcc_move *out) {
+    const int t = s->turn;
+    int heavy = 0, minor = 0;
+    for (int i = 0; i < 64; i++) {
+        const int u = toupper(s->board[i]);
+        if (u == 'P' || u == 'R' || u == 'Q') heavy++;
+        if (u == 'B' || u == 'N') minor++;
+    }
+    if (heavy == 0 && minor <= 1) return 0;
+    int n = 0;
+    for (int idx = 0; idx < 64; idx++) {
+        const uint8_t pc = s->board[idx];
+        if (empty_sq(pc)) continue;
+        if ((t == 0) != (is_white(pc) != 0)) continue;
+        const int r = idx / 8, c = idx % 8, up = toupper(pc);
+        if (up == 'P') {
+            const int dir = pc == 'P' ? -1 : 1;
+            const int nr = r + dir;
+            if (inb(nr, c) && empty_sq(s->board[nr * 8 + c])) {
+                push(out, &n, r, c, nr, c, 0.0);
+                if (r == (pc == 'P' ? 6 : 1) && inb(nr + dir, c) && empty_sq(s->board[(nr + dir) * 8 + c]))
+                    push(out, &n, r, c, nr + dir, c, 0.0);
+            }
+            for (int dc = -1; dc <= 1; dc += 2) {
+                const int cc = c + dc;
+                if (!inb(nr, cc)) continue;
+                const uint8_t x = s->board[nr * 8 + cc];
+                if (enemy(x, t) && toupper(x) != 'K') push(out, &n, r, c, nr, cc, fabs((double)value_of(x)));
+            }
+        } else if (up == 'N' || up == 'K') {
+            const int(*D)[2] = up == 'N' ? KN : ALL8;
+            for (int i = 0; i < 8; i++) {
+                const int rr = r + D[i][0], cc = c + D[i][1];
+                if (!inb(rr, cc)) continue;
+                const uint8_t x = s->board[rr * 8 + cc];
+                if (empty_sq(x)) push(out, &n, r, c, rr, cc, 0.0);
+                else if (enemy(x, t) && toupper(x) != 'K') push(out, &n, r, c, rr, cc, fabs((double)value_of(x)));
+            }
+        } else if (up == 'B' || up == 'R' || up == 'Q') {
+            const int(*D)[2] = up == 'B' ? DIAG : up == 'R' ? ORTH : ALL8;
+            const int nd = up == 'Q' ? 8 : 4;
+            for (int i = 0; i < nd; i++) {
+                for (int k = 1;; k++) {
+                    const int rr = r + D[i][0] * k, cc = c + D[i][1] * k;
+                    if (!inb(rr, cc)) break;
+                    const uint8_t x = s->board[rr * 8 + cc];
+                    if (empty_sq(x)) {
+                        push(out, &n, r, c, rr, cc, 0.0);
+                        continue;
+                    }
+                    if (enemy(x, t) && toupper(x) != 'K') push(out, &n, r, c, rr, cc, fabs((double)value_of(x)));
+                    break;
+                }
+            }
+        }
+    }
+    return n;
+}
+
+void zcc_play(const zcc_state *s, const zcc_move *m, zcc_state *o) {
+    const int turn = s->turn;
+    if (o != s) memcpy(o, s, sizeof *o);
+    uint8_t *b = o->board;
+    o->turn = (uint8_t)(1 - turn);
+    o->fifty = (uint8_t)(o->fifty + 1);
+    if (turn == 0) {
+        if (o->nhw < ZCC_HIST) {
+            memmove(&o->hw[1], &o->hw[0], sizeof(zcc_move) * (size_t)o->nhw);
+            o->hw[0] = *m;
+            o->nhw++;
+        } else {
+            o->overflow = 1;
+        }
+    } else {
+        if (o->nhb < ZCC_HIST) {
+            memmove(&o->hb[1], &o->hb[0], sizeof(zcc_move) * (size_t)o->nhb);
+            o->hb[0] = *m;
+            o->nhb++;
+        } else {
+            o->overflow = 1;
+        }
+    }
+    const int fr = m->fr, fc = m->fc, tr = m->tr, tc = m->tc;
+    const uint8_t pc = b[fr * 8 + fc], trg = b[tr * 8 + tc];
+    if (pc == 'P' || pc == 'p' || !empty_sq(trg)) o->fifty = 0;
+    if (pc == 'K' || (pc == 'R' && fc == 7)) o->castle &= (uint8_t)~1u;
+    if (pc == 'K' || (pc == 'R' && fc == 0)) o->castle &= (uint8_t)~2u;
+    if (pc == 'k' || (pc == 'r' && fc == 7)) o->castle &= (uint8_t)~4u;
+    if (pc == 'k' || (pc == 'r' && fc == 0)) o->castle &= (uint8_t)~8u;
+    if (pc == 'K' && tc - fc == 2) { b[61] = 'R'; b[63] = ' '; }
+    if (pc == 'k' && tc - fc == 2) { b[5] = 'r'; b[7] = ' '; }
+    if (pc == 'K' && tc - fc == -2) { b[59] = 'R'; b[56] = ' '; }
+    if (pc == 'k' && tc - fc == -2) { b[3] = 'r'; b[0] = ' '; }
+    b[tr * 8 + tc] = pc;
+    b[fr * 8 + fc] = ' ';
+    if (tr == 0 && pc == 'P') b[tr * 8 + tc] = 'Q';
+    if (tr == 7 && pc == 'p') b[tr * 8 + tc] = 'q';
+}
+
+int zcc_legal_moves(const zcc_state *s, zcc_move *out) {
+    zcc_move ps[ZCC_MAX_MOVES];
+    const int np = pseudo_moves(s, ps);
+    int n = 0;
+    zcc_state t;
+    for (int i = 0; i < np; i++) {
+        /* only the board matters for the test: skip the history copy */
+        memcpy(t.board, s->board, 64);
+        t.turn = s->turn;
+        t.fifty = s->fifty;
+        t.castle = s->castle;
+        t.nhw = t.nhb = 0;
+        t.overflow = 0;
+        zcc_play(&t, &ps[i], &t);
+        int kr, kc;
+        king_square(&t, s->turn, &kr, &kc);
+        if (!attacked(&t, s->turn, kr, kc)) out[n++] = ps[i];
+    }
+    return n;
+}
+
+static int in_check(const zcc_state *s) {
+    int kr, kc;
+    king_square(s, s->turn, &kr, &kc);
+    return attacked(s, s->turn, kr, kc);
+}
+
+int zcc_check_win(const zcc_state *s) {
+    zcc_move m[ZCC_MAX_MOVES];
+    if (zcc_legal_moves(s, m)) return 0;
+    return in_check(s);
+}
+
+static int move_eq(const zcc_move *a, const zcc_move *b) {
+    return a->fr == b->fr && a->fc == b->fc && a->tr == b->tr && a->tc == b->tc && a->value == b->value;
+}
+
+/* has_repeated_prefix(L, 2, 3): some prefix of L (most recent move first) is a whole
+ * number >= 3 of repeats of a block of >= 2 moves (KMP prefix function). */
+int zcc_repeated_prefix(const zcc_move *L, int n) {
+    if (n < 6) return 0;
+    int *pi = (int *)calloc((size_t)n, sizeof(int));
+    int j = 0;
+    for (int i = 1; i < n; i++) {
+        while (j > 0 && !move_eq(&L[i], &L[j])) j = pi[j - 1];
+        if (move_eq(&L[i], &L[j])) ++j;
+        pi[i] = j;
+    }
+    int found = 0;
+    for (int i = 0; i < n && !found; i++) {
+        const int len = i + 1, p = len - pi[i];
+        if (p >= 2 && len % p == 0 && len / p >= 3) found = 1;
+    }
+    free(pi);
+    return found;
+}
+
+int zcc_check_draw(const zcc_state *s) {
+    zcc_move m[ZCC_MAX_MOVES];
+    if (zcc_legal_moves(s, m) == 0 && !in_check(s)) return 1;
+    if (s->fifty >= 50) return 1;
+    return zcc_repeated_prefix(s->hw, s->nhw) && zcc_repeated_prefix(s->hb, s->nhb);
+}
+
+void zcc_init(zcc_state *s) {
+    memset(s, 0, sizeof *s);
+    const char *back = "rnbqkbnr";
+    for (int i = 0; i < 8; i++) {
+        s->board[i] = (uint8_t)back[i];
+        s->board[8 + i] = 'p';
+        s->board[48 + i] = 'P';
+        s->board[56 + i] = (uint8_t)toupper(back[i]);
+    }
+    for (int i = 16; i < 48; i++) s->board[i] = ' ';
+    s->castle = 15;
+}
+
+int zcc_from_fen(const char *fen, zcc_state *s) {
+    memset(s, 0, sizeof *s);
+    int idx = 0;
+    const char *p = fen;
+    while (*p && *p != ' ') {
+        if (*p == '/') {
+        } else if (isdigit((unsigned char)*p)) {
+            for (int i = 0; i < *p - '0' && idx < 64; i++) s->board[idx++] = ' ';
+        } else if (idx < 64) {
+            s->board[idx++] = (uint8_t)*p;
+        }
+        p++;
+    }
+    if (idx != 64) return -1;
+    while (*p == ' ') p++;
+    s->turn = (p[0] == 'w' && (p[1] == ' ' || p[1] == 0)) ? 0 : 1;
+    while (*p && *p != ' ') p++;
+    while (*p == ' ') p++;
+    while (*p && *p != ' ') {
+        if (*p == 'K') s->castle |= 1;
+        if (*p == 'Q') s->castle |= 2;
+        if (*p == 'k') s->castle |= 4;
+        if (*p == 'q') s->castle |= 8;
+        p++;
+    }
+    while (*p == ' ') p++;
+    while (*p && *p != ' ') p++; /* en passant: ignored */
+    while (*p == ' ') p++;
+    s->fifty = (uint8_t)atoi(p);
+    return 0;
+}
+
+void zcc_state_to_tensor(const zcc_state *s, float *out) {
+    static const char pieces[12] = {'P', 'N', 'B', 'R', 'Q', 'K', 'p', 'n', 'b', 'r', 'q', 'k'};
+    memset(out, 0, sizeof(float) * 17 * 64);
+    for (int i = 0; i < 64; i++)
+        for (int k = 0; k < 12; k++)
+            if (s->board[i] == (uint8_t)pieces[k]) {
+                out[k * 64 + i] = 1.0f;
+                break;
+            }
+    for (int i = 0; i < 64; i++) {
+        out[12 * 64 + i] = s->turn == 0 ? 1.0f : 0.0f;
+        for (int k = 0; k < 4; k++) out[(13 + k) * 64 + i] = (s->castle >> k) & 1 ? 1.0f : 0.0f;
+    }
+}
+
+uint64_t zcc_perft(const zcc_state *s, int depth) {
+    if (depth == 0) return 1;
+    zcc_move m[ZCC_MAX_MOVES];
+    const int n = zcc_legal_moves(s, m);
+    if (depth == 1) return (uint64_t)n;
+    uint64_t total = 0;
+    zcc_state t;
+    for (int i = 0; i < n; i++) {
+        memcpy(t.board, s->board, 64);
+        t.turn = s->turn;
+        t.fifty = s->fifty;
+        t.castle = s->castle;
+        t.nhw = t.nhb = 0;
+        t.overflow = 0;
+        zcc_play(&t, &m[i], &t);
+        total += zcc_perft(&t, depth - 1);
+    }
+    return total;
+}

@@ -1,0 +1,149 @@
+"""GPU parity of the chess rules (chess.hip) with the reference's outputs
+(tests/golden/chess_*.json from engine/games/chess compiled unmodified): perft counts,
+ordered legal-move lists with capture values, play_move, terminal flags, planes."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+MAXM = 256
+
+
+@pytest.fixture(scope="module")
+def eng():
+    from zeroclone_amd._native import NativeEngine
+    e = NativeEngine(max_games=1, max_sims=1, max_batch=1)
+    yield e
+    e.close()
+
+
+def states_from_json(cases):
+    from zeroclone_amd._native import CHESS_STATE_DTYPE
+    a = np.zeros(len(cases), CHESS_STATE_DTYPE)
+    for i, e in enumerate(cases):
+        a[i]["board"] = np.frombuffer(e["board"].encode("latin-1"), np.uint8)
+        a[i]["turn"], a[i]["fifty"], a[i]["castle"] = e["turn"], e["fifty"], e["castle"]
+    return a
+
+
+def dev(a: np.ndarray):
+    return torch.from_numpy(a.view(np.uint8).reshape(len(a), -1).copy()).cuda()
+
+
+def legal(eng, st):
+    n = st.shape[0]
+    moves = torch.zeros((n, MAXM), dtype=torch.int16, device="cuda")
+    counts = torch.zeros(n, dtype=torch.int32, device="cuda")
+    eng.chess_legal_moves_async(n, st.data_ptr(), moves.data_ptr(), counts.data_ptr())
+    torch.cuda.synchronize()
+    return moves.cpu().numpy().view(np.uint16), counts.cpu().numpy()
+
+
+def decode(m):
+    from zeroclone_amd._native import unpack_chess_move
+    (fr, fc, tr, tc), v = unpack_chess_move(m)
+    return [fr, fc, tr, tc, v]
+
+
+def test_legal_move_lists_match_reference(eng, golden):
+    cases = golden("chess_movelists.json")["cases"]
+    st = dev(states_from_json([c["state"] for c in cases]))
+    moves, counts = legal(eng, st)
+    for i, c in enumerate(cases):
+        assert counts[i] == len(c["moves"]), i
+        assert [decode(m) for m in moves[i, :counts[i]]] == c["moves"], i
+
+
+def perft(eng, root: np.ndarray, depth: int) -> int:
+    from zeroclone_amd._native import CHESS_STATE_DTYPE
+    front = dev(np.array([root], CHESS_STATE_DTYPE))
+    for _ in range(depth - 1):
+        n = front.shape[0]
+        kids = torch.zeros((n * MAXM, 72), dtype=torch.uint8, device="cuda")
+        counts = torch.zeros(n, dtype=torch.int32, device="cuda")
+        eng.chess_children_async(n, front.data_ptr(), kids.data_ptr(), 0, counts.data_ptr())
+        keep = (torch.arange(MAXM, device="cuda")[None, :] < counts[:, None]).reshape(-1)
+        front = kids[keep].contiguous()
+    _, counts = legal(eng, front)
+    assert (counts >= 0).all()
+    return int(counts.sum())
+
+
+def test_perft_matches_reference(eng, golden):
+    from zeroclone_amd._native import chess_from_fen
+    for case in golden("chess_perft.json")["perft"]:
+        root = chess_from_fen(case["fen"])
+        for d, n in enumerate(case["counts"], start=1):
+            assert perft(eng, root, d) == n, (case["name"], d)
+
+
+def test_play_move_matches_reference(eng, golden):
+    from zeroclone_amd._native import CHESS_STATE_DTYPE, pack_chess_move
+    cases = golden("chess_play.json")["cases"]
+    st = dev(states_from_json([c["state"] for c in cases]))
+    mv = torch.tensor([pack_chess_move(*c["move"]) for c in cases], dtype=torch.int32).to(torch.int16).cuda()
+    out = torch.zeros_like(st)
+    eng.chess_play_async(len(cases), st.data_ptr(), mv.data_ptr(), out.data_ptr())
+    torch.cuda.synchronize()
+    got = out.cpu().numpy().reshape(-1).view(CHESS_STATE_DTYPE)
+    for i, c in enumerate(cases):
+        a = c["after"]
+        assert bytes(got[i]["board"]).decode("latin-1") == a["board"], i
+        assert (got[i]["turn"], got[i]["fifty"], got[i]["castle"]) == (a["turn"], a["fifty"], a["castle"]), i
+
+
+def test_terminal_flags_match_reference(eng, golden):
+    from zeroclone_amd._native import ZC_CHESS_FIFTY, ZC_CHESS_STALEMATE, ZC_CHESS_WIN
+    from zeroclone_amd.engine.games.chess.chess_backend import has_repeated_prefix, moves_from_hist
+    cases = golden("chess_terminal.json")["cases"]
+    st = dev(states_from_json([c["state"] for c in cases]))
+    flags = torch.zeros(len(cases), dtype=torch.int32, device="cuda")
+    eng.chess_terminal_async(len(cases), st.data_ptr(), flags.data_ptr())
+    f = flags.cpu().numpy()
+    for i, c in enumerate(cases):
+        assert bool(f[i] & ZC_CHESS_WIN) == c["win"], i
+        rep = has_repeated_prefix(moves_from_hist(c["state"]["hw"])) and \
+            has_repeated_prefix(moves_from_hist(c["state"]["hb"]))
+        assert (bool(f[i] & (ZC_CHESS_STALEMATE | ZC_CHESS_FIFTY)) or rep) == c["draw"], i
+
+
+def test_planes_match_state_to_tensor(eng, golden):
+    cases = golden("chess_tensor.json")["cases"]
+    st = dev(states_from_json([c["state"] for c in cases]))
+    for f16 in (False, True):
+        planes = torch.zeros((len(cases), 17, 8, 8), dtype=torch.float16 if f16 else torch.float32, device="cuda")
+        eng.chess_planes_async(len(cases), st.data_ptr(), planes.data_ptr(), f16)
+        p = planes.float().cpu().numpy()
+        for i, c in enumerate(cases):
+            bits = np.unpackbits(np.frombuffer(bytes.fromhex(c["bits"]), np.uint8))[: 17 * 64]
+            np.testing.assert_array_equal((p[i].reshape(-1) != 0).astype(np.uint8), bits)
+
+
+def test_backend_module_is_a_drop_in(golden):
+    """zeroclone_amd's chess_backend (reference API, rules on the device) on the
+    reference's own fixtures, including the repetition draw through move histories."""
+    from zeroclone_amd.engine.games.chess import chess_backend as cb
+    s = cb.create_init_state()
+    assert len(cb.get_legal_moves(s)) == 20 and not cb.check_win(s) and not cb.check_draw(s)
+    for c in golden("chess_movelists.json")["cases"][:40]:
+        e = c["state"]
+        st = cb.State(list(e["board"].encode("latin-1")), e["turn"], e["fifty"], e["castle"] & 1, e["castle"] & 2,
+                      e["castle"] & 4, e["castle"] & 8, [], [])
+        got = cb.get_legal_moves(st)
+        assert [list(m[0]) + [m[1]] for m in got] == c["moves"]
+    for c in golden("chess_terminal.json")["cases"]:
+        if "fen" in c:
+            st = cb.state_from_fen(c["fen"])
+            assert [cb.check_win(st), cb.check_draw(st)] == c["expect"]
+    # knight bounce: the repetition draw needs both histories periodic (test_cb.py style)
+    s = cb.create_init_state()
+    bounce = [((7, 6, 5, 5), 0.0), ((0, 6, 2, 5), 0.0), ((5, 5, 7, 6), 0.0), ((2, 5, 0, 6), 0.0)]
+    draws = []
+    for k in range(16):
+        s = cb.play_move(s, bounce[k % 4])
+        draws.append(cb.check_draw(s))
+    exp = [c["draw"] for c in golden("chess_terminal.json")["cases"] if c.get("note", "").startswith("knight")]
+    assert draws == exp and any(draws)
+    t = cb.state_to_tensor(cb.create_init_state())
+    assert t.shape == (17, 8, 8) and t[12].sum() == 64 and t[0, 6].sum() == 8

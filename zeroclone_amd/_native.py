@@ -46,6 +46,11 @@ C4_STATE_DTYPE = np.dtype([("stones", "<u8", (2,)), ("turn", "<i4"), ("reserved"
 STATS_DTYPE = np.dtype([("expansions", "<i8"), ("depth_sum", "<i8"), ("leaves", "<i8"),
                         ("rollout_plies", "<i8"), ("rng_words", "<i8"), ("status", "<i8"),
                         ("rollout_blocks", "<i8"), ("reserved", "<i8")])
+CHESS_STATE_DTYPE = np.dtype([("board", "u1", (64,)), ("turn", "u1"), ("fifty", "u1"), ("castle", "u1"),
+                              ("reserved", "u1", (5,))])
+CHESS_MAX_MOVES = 256
+ZC_CHESS_WIN, ZC_CHESS_STALEMATE, ZC_CHESS_FIFTY, ZC_CHESS_OVERFLOW = 1, 2, 4, 8
+assert CHESS_STATE_DTYPE.itemsize == 72
 assert C4_STATE_DTYPE.itemsize == ctypes.sizeof(C4State) == 24
 assert STATS_DTYPE.itemsize == ctypes.sizeof(GameStats) == 64
 STATS_FIELDS = 8
@@ -83,6 +88,18 @@ SIGNATURES = [
                                      ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     ("zc_c4_rollouts", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p,
                                       ctypes.c_void_p, P(ctypes.c_int64)]),
+    ("zc_chess_legal_moves_async", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p,
+                                                  ctypes.c_void_p, ctypes.c_void_p]),
+    ("zc_chess_children_async", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p,
+                                               ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    ("zc_chess_play_async", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p,
+                                           ctypes.c_void_p, ctypes.c_void_p]),
+    ("zc_chess_terminal_async", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p,
+                                               ctypes.c_void_p]),
+    ("zc_chess_planes_async", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p,
+                                             ctypes.c_int32, ctypes.c_void_p]),
+    ("zc_chess_from_fen", ctypes.c_int, [ctypes.c_char_p, ctypes.c_void_p]),
+    ("zc_chess_init", ctypes.c_int, [ctypes.c_void_p]),
     ("zc_c4_from_rows", ctypes.c_int, [ctypes.c_char_p, ctypes.c_int32, P(C4State)]),
     ("zc_c4_to_rows", ctypes.c_int, [P(C4State), ctypes.c_char_p]),
     ("zc_c4_legal_order", ctypes.c_int, [ctypes.c_int32, P(ctypes.c_int32)]),
@@ -154,6 +171,29 @@ def c4_legal_order(mask: int) -> list[int]:
     cols = (ctypes.c_int32 * 7)()
     n = check(lib().zc_c4_legal_order(int(mask), cols))
     return list(cols[:n])
+
+
+def chess_from_fen(fen: str) -> np.ndarray:
+    out = np.zeros(1, CHESS_STATE_DTYPE)
+    check(lib().zc_chess_from_fen(fen.encode(), _ptr(out)))
+    return out[0]
+
+
+def chess_init() -> np.ndarray:
+    out = np.zeros(1, CHESS_STATE_DTYPE)
+    check(lib().zc_chess_init(_ptr(out)))
+    return out[0]
+
+
+def unpack_chess_move(m: int):
+    """uint16 move -> ((fr, fc, tr, tc), capture value)."""
+    m = int(m)
+    f, t = m & 63, (m >> 6) & 63
+    return (f >> 3, f & 7, t >> 3, t & 7), float((m >> 12) & 15)
+
+
+def pack_chess_move(fr: int, fc: int, tr: int, tc: int, value: float) -> int:
+    return (fr * 8 + fc) | ((tr * 8 + tc) << 6) | (int(value) << 12)
 
 
 class NativeEngine:
@@ -257,6 +297,29 @@ class NativeEngine:
     def c4_ext_end(self, first_game: int, n: int, d_move: int, d_na: int, d_stats: int, stream: int = 0) -> None:
         check(lib().zc_c4_ext_end(self._h, first_game, n, ctypes.c_void_p(d_move), ctypes.c_void_p(d_na),
                                   ctypes.c_void_p(d_stats), ctypes.c_void_p(stream or None)))
+
+    # ---- chess rules (device pointers; stream 0 = null stream)
+    def chess_legal_moves_async(self, n: int, d_states: int, d_moves: int, d_counts: int, stream: int = 0):
+        check(lib().zc_chess_legal_moves_async(self._h, n, ctypes.c_void_p(d_states), ctypes.c_void_p(d_moves),
+                                               ctypes.c_void_p(d_counts), ctypes.c_void_p(stream or None)))
+
+    def chess_children_async(self, n: int, d_states: int, d_children: int, d_moves: int, d_counts: int,
+                             stream: int = 0):
+        check(lib().zc_chess_children_async(self._h, n, ctypes.c_void_p(d_states), ctypes.c_void_p(d_children),
+                                            ctypes.c_void_p(d_moves or None), ctypes.c_void_p(d_counts),
+                                            ctypes.c_void_p(stream or None)))
+
+    def chess_play_async(self, n: int, d_in: int, d_moves: int, d_out: int, stream: int = 0):
+        check(lib().zc_chess_play_async(self._h, n, ctypes.c_void_p(d_in), ctypes.c_void_p(d_moves),
+                                        ctypes.c_void_p(d_out), ctypes.c_void_p(stream or None)))
+
+    def chess_terminal_async(self, n: int, d_states: int, d_flags: int, stream: int = 0):
+        check(lib().zc_chess_terminal_async(self._h, n, ctypes.c_void_p(d_states), ctypes.c_void_p(d_flags),
+                                            ctypes.c_void_p(stream or None)))
+
+    def chess_planes_async(self, n: int, d_states: int, d_planes: int, f16: bool = False, stream: int = 0):
+        check(lib().zc_chess_planes_async(self._h, n, ctypes.c_void_p(d_states), ctypes.c_void_p(d_planes),
+                                          ZC_F16 if f16 else ZC_F32, ctypes.c_void_p(stream or None)))
 
     def c4_rollouts(self, states: np.ndarray, game: int = 0):
         """Sequential rollouts of `states` on one game's stream: (values[n], words consumed)."""

@@ -1,0 +1,219 @@
+// chess_device.h — the reference's chess rules (engine/games/chess/src/chess_backend.cpp)
+// as wave-level device functions for gfx950, shared by the chess kernels (chess.hip) and the
+// chess tree search.
+//
+// Execution model: ONE POSITION PER WAVE, ONE SQUARE PER LANE.  The board stays in the
+// reference's byte encoding (64 chars: ' ' empty, "PNBRQK" white, "pnbrqk" black, index 0 =
+// a8) in LDS, so every quirk of the reference — unknown characters, missing kings — behaves
+// identically.  get_legal_moves (:184-360) becomes:
+//   1. lane s counts the pseudo-legal moves of the piece on square s (reference order:
+//      pawn push / double push / captures dc=-1,+1; knight, bishop, rook, queen, king
+//      direction tables :17-34), an exclusive prefix sum over lanes gives each square its
+//      slot range — board-scan order is lane order — and lane s writes its moves there;
+//   2. lanes take the pseudo-legal moves 64 at a time and test the mover's king on the
+//      board after the move (:345-359) by reading LDS through a from/to override;
+//   3. ballot + mbcnt compact the legal moves, preserving order.
+// A move is packed in 16 bits: from square | to square << 6 | capture value << 12
+// (fabs(piece_val) of the captured piece: 0, 1, 3, 5 or 9).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace zc {
+namespace chessdev {
+namespace {
+
+constexpr int kMaxLegal = 256;   // the output capacity per position (real chess: <= 218)
+constexpr int kMaxPseudo = 512;  // pseudo-legal scratch per position
+
+__device__ __forceinline__ uint32_t lane() { return __lane_id(); }
+
+__device__ __forceinline__ bool empty_sq(uint32_t x) { return x == ' ' || x == 0; }
+__device__ __forceinline__ bool is_white(uint32_t x) { return x >= 'A' && x <= 'Z'; }
+__device__ __forceinline__ uint32_t upper(uint32_t x) { return (x >= 'a' && x <= 'z') ? x - 32u : x; }
+__device__ __forceinline__ bool enemy(uint32_t x, int t) { return !empty_sq(x) && (t == 0 ? !is_white(x) : is_white(x)); }
+__device__ __forceinline__ uint32_t piece_value(uint32_t x) {
+    switch (upper(x)) {
+        case 'P': return 1;
+        case 'N': return 3;
+        case 'B': return 3;
+        case 'R': return 5;
+        case 'Q': return 9;
+        default: return 0;  // K (100) never appears as a capture
+    }
+}
+__device__ __forceinline__ bool inb(int r, int c) { return (unsigned)r < 8u && (unsigned)c < 8u; }
+
+// direction tables (chess_backend.cpp:17-34)
+struct Dir {
+    int8_t dr, dc;
+};
+__constant__ Dir kKnight[8] = {{-2, -1}, {-2, 1}, {-1, -2}, {-1, 2}, {1, -2}, {1, 2}, {2, -1}, {2, 1}};
+__constant__ Dir kAll8[8] = {{-1, -1}, {-1, 1}, {1, -1}, {1, 1}, {-1, 0}, {1, 0}, {0, -1}, {0, 1}};
+// bishops use kAll8[0..4), rooks kAll8[4..8), queens and kings kAll8[0..8)
+
+__device__ __forceinline__ uint32_t pack_move(int from, int to, uint32_t v) {
+    return (uint32_t)from | ((uint32_t)to << 6) | (v << 12);
+}
+
+// Pseudo-legal moves of the piece `pc` on square s (row r, col c); F(from, to, value) is
+// called for each in the reference's order.  Returns nothing; the caller counts or stores.
+template <class F>
+__device__ __forceinline__ void piece_moves(const uint8_t *b, int t, int s, uint32_t pc, F &&emit) {
+    const int r = s >> 3, c = s & 7;
+    const uint32_t up = upper(pc);
+    if (up == 'P') {
+        const int dir = pc == 'P' ? -1 : 1;
+        const int nr = r + dir;
+        if (inb(nr, c) && empty_sq(b[nr * 8 + c])) {
+            emit(s, nr * 8 + c, 0u);
+            if (r == (pc == 'P' ? 6 : 1) && inb(nr + dir, c) && empty_sq(b[(nr + dir) * 8 + c]))
+                emit(s, (nr + dir) * 8 + c, 0u);
+        }
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const int cc = c + (k ? 1 : -1);
+            if (inb(nr, cc)) {
+                const uint32_t x = b[nr * 8 + cc];
+                if (enemy(x, t) && upper(x) != 'K') emit(s, nr * 8 + cc, piece_value(x));
+            }
+        }
+    } else if (up == 'N' || up == 'K') {
+        const Dir *D = up == 'N' ? kKnight : kAll8;
+        for (int i = 0; i < 8; ++i) {
+            const int rr = r + D[i].dr, cc = c + D[i].dc;
+            if (!inb(rr, cc)) continue;
+            const uint32_t x = b[rr * 8 + cc];
+            if (empty_sq(x)) emit(s, rr * 8 + cc, 0u);
+            else if (enemy(x, t) && upper(x) != 'K') emit(s, rr * 8 + cc, piece_value(x));
+        }
+    } else if (up == 'B' || up == 'R' || up == 'Q') {
+        const int d0 = up == 'R' ? 4 : 0, d1 = up == 'B' ? 4 : 8;
+        for (int i = d0; i < d1; ++i) {
+            const int dr = kAll8[i].dr, dc = kAll8[i].dc;
+            int rr = r + dr, cc = c + dc;
+            while (inb(rr, cc)) {
+                const uint32_t x = b[rr * 8 + cc];
+                if (empty_sq(x)) {
+                    emit(s, rr * 8 + cc, 0u);
+                } else {
+                    if (enemy(x, t) && upper(x) != 'K') emit(s, rr * 8 + cc, piece_value(x));
+                    break;
+                }
+                rr += dr;
+                cc += dc;
+            }
+        }
+    }
+}
+
+// king_attacked (:85-144) for the king of side t on (kr, kc) — (-1,-1) when absent, exactly
+// as the reference probes then — on the board b with square `from` emptied and `pc` on `to`
+// (the position after a non-castling move; promotion does not change the answer: the piece
+// on `to` is the mover's either way and only blocks).
+__device__ __forceinline__ bool attacked_after(const uint8_t *b, int t, int kr, int kc, int from, int to, uint32_t pc) {
+    auto at = [&](int r, int c) -> uint32_t {
+        const int s = r * 8 + c;
+        return s == to ? pc : (s == from ? (uint32_t)' ' : (uint32_t)b[s]);
+    };
+    const int pr = t == 0 ? kr - 1 : kr + 1;
+    const uint32_t pawn = t == 0 ? 'p' : 'P';
+    if (inb(pr, kc - 1) && at(pr, kc - 1) == pawn) return true;
+    if (inb(pr, kc + 1) && at(pr, kc + 1) == pawn) return true;
+    const uint32_t kn = t ? 'N' : 'n';
+    for (int i = 0; i < 8; ++i) {
+        const int rr = kr + kKnight[i].dr, cc = kc + kKnight[i].dc;
+        if (inb(rr, cc) && at(rr, cc) == kn) return true;
+    }
+    const uint32_t q = t ? 'Q' : 'q';
+    for (int i = 0; i < 8; ++i) {  // rook lines (kAll8[4..8)) first, then bishop lines: same answer
+        const int dr = kAll8[i].dr, dc = kAll8[i].dc;
+        const uint32_t p1 = i < 4 ? (t ? 'B' : 'b') : (t ? 'R' : 'r');
+        int rr = kr + dr, cc = kc + dc;
+        while (inb(rr, cc)) {
+            const uint32_t x = at(rr, cc);
+            if (!empty_sq(x)) {
+                if (x == p1 || x == q) return true;
+                break;
+            }
+            rr += dr;
+            cc += dc;
+        }
+    }
+    const uint32_t kk = t ? 'K' : 'k';
+    for (int i = 0; i < 8; ++i) {
+        const int rr = kr + kAll8[i].dr, cc = kc + kAll8[i].dc;
+        if (inb(rr, cc) && at(rr, cc) == kk) return true;
+    }
+    return false;
+}
+
+// Exclusive prefix sum over the wave (DPP row scan + row broadcasts).
+__device__ __forceinline__ uint32_t wave_excl_sum(uint32_t x, uint32_t &total) {
+    uint32_t v = x;
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false);
+    total = (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+    return v - x;
+}
+
+// Squares holding side's king (find_king :70-83 takes the first one; -1 when none).
+__device__ __forceinline__ uint64_t king_mask(const uint8_t *b, int side) {
+    return __ballot(b[lane()] == (side == 0 ? 'K' : 'k'));
+}
+
+// get_legal_moves for the board in LDS `b` (64 bytes) with side to move t.  Writes the
+// packed legal moves to out[0..n) (LDS or global), pseudo-legal scratch in LDS `ps`.
+// Returns n (wave-uniform), or -1 when the position has more than kMaxPseudo pseudo-legal
+// or kMaxLegal legal moves (never in reachable chess).
+__device__ __forceinline__ int legal_moves(const uint8_t *b, int t, uint16_t *out, uint16_t *ps) {
+    const uint32_t s = lane();
+    const uint32_t pc = b[s];
+    // insufficient material (:188-198): no P/R/Q of either colour and at most one minor
+    const uint32_t up = upper(pc);
+    const uint64_t heavy = __ballot(up == 'P' || up == 'R' || up == 'Q');
+    const int minor = __popcll(__ballot(up == 'B' || up == 'N'));
+    if (!heavy && minor <= 1) return 0;
+    const bool mine = !empty_sq(pc) && ((t == 0) == is_white(pc));
+    uint32_t cnt = 0;
+    if (mine) piece_moves(b, t, (int)s, pc, [&](int, int, uint32_t) { ++cnt; });
+    uint32_t total;
+    uint32_t off = wave_excl_sum(cnt, total);
+    if (total > (uint32_t)kMaxPseudo) return -1;
+    if (mine)
+        piece_moves(b, t, (int)s, pc, [&](int f, int to, uint32_t v) { ps[off++] = (uint16_t)pack_move(f, to, v); });
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    const uint64_t kings = king_mask(b, t);
+    const uint32_t kch = t == 0 ? 'K' : 'k';
+    int n = 0;
+    for (uint32_t base = 0; base < total; base += 64) {
+        const uint32_t i = base + s;
+        bool legal = false;
+        uint32_t m = 0;
+        if (i < total) {
+            m = ps[i];
+            const int from = (int)(m & 63u), to = (int)((m >> 6) & 63u);
+            const uint32_t mp = b[from];
+            // find_king on the board after the move: first square holding the mover's king
+            const uint64_t km = (kings & ~(1ull << from)) | (mp == kch ? (1ull << to) : 0ull);
+            const int k = km ? __builtin_ctzll(km) : -1;
+            const int kr = k >= 0 ? (k >> 3) : -1, kc = k >= 0 ? (k & 7) : -1;
+            legal = !attacked_after(b, t, kr, kc, from, to, mp);
+        }
+        const uint64_t L = __ballot(legal);
+        const int rank = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(L >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)L, 0u));
+        if (legal && n + rank < kMaxLegal) out[n + rank] = (uint16_t)m;
+        n += __popcll(L);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    return n > kMaxLegal ? -1 : n;
+}
+
+}  // namespace
+}  // namespace chessdev
+}  // namespace zc

@@ -4,6 +4,7 @@
 #include <math.h>
 #include <stdarg.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <vector>
@@ -472,6 +473,97 @@ int zc_c4_ext_end(zc_engine *eng, int32_t first, int32_t n, int32_t *d_move, int
     zc::launch_c4_ext_end(p, (hipStream_t)hip_stream);
     ZC_HIP(hipGetLastError());
     return ZC_OK;
+}
+
+// ---------------------------------------------------------------- chess rules
+#define ZC_CHESS_ENTRY(cond)                                                   \
+    if (!eng || n < 0 || (n && !(cond))) return fail(ZC_EINVAL, "bad argument"); \
+    if (!n) return ZC_OK;                                                      \
+    std::lock_guard<std::mutex> lk(eng->mu);                                   \
+    ZC_HIP(hipSetDevice(eng->cfg.device));
+
+int zc_chess_legal_moves_async(zc_engine *eng, int32_t n, const zc_chess_state *d_states, uint16_t *d_moves,
+                               int32_t *d_counts, void *hip_stream) {
+    ZC_CHESS_ENTRY(d_states && d_moves && d_counts)
+    zc::launch_chess_legal(n, d_states, d_moves, d_counts, (hipStream_t)hip_stream);
+    ZC_HIP(hipGetLastError());
+    return ZC_OK;
+}
+
+int zc_chess_children_async(zc_engine *eng, int32_t n, const zc_chess_state *d_states, zc_chess_state *d_children,
+                            uint16_t *d_moves, int32_t *d_counts, void *hip_stream) {
+    ZC_CHESS_ENTRY(d_states && d_children && d_counts)
+    zc::launch_chess_children(n, d_states, d_children, d_moves, d_counts, (hipStream_t)hip_stream);
+    ZC_HIP(hipGetLastError());
+    return ZC_OK;
+}
+
+int zc_chess_play_async(zc_engine *eng, int32_t n, const zc_chess_state *d_in, const uint16_t *d_moves,
+                        zc_chess_state *d_out, void *hip_stream) {
+    ZC_CHESS_ENTRY(d_in && d_moves && d_out)
+    zc::launch_chess_play(n, d_in, d_moves, d_out, (hipStream_t)hip_stream);
+    ZC_HIP(hipGetLastError());
+    return ZC_OK;
+}
+
+int zc_chess_terminal_async(zc_engine *eng, int32_t n, const zc_chess_state *d_states, int32_t *d_flags,
+                            void *hip_stream) {
+    ZC_CHESS_ENTRY(d_states && d_flags)
+    zc::launch_chess_terminal(n, d_states, d_flags, (hipStream_t)hip_stream);
+    ZC_HIP(hipGetLastError());
+    return ZC_OK;
+}
+
+int zc_chess_planes_async(zc_engine *eng, int32_t n, const zc_chess_state *d_states, void *d_planes,
+                          int32_t planes_dtype, void *hip_stream) {
+    if (planes_dtype != ZC_F32 && planes_dtype != ZC_F16) return fail(ZC_EINVAL, "planes_dtype must be ZC_F32 or ZC_F16");
+    ZC_CHESS_ENTRY(d_states && d_planes)
+    zc::launch_chess_planes(n, d_states, d_planes, planes_dtype == ZC_F16, (hipStream_t)hip_stream);
+    ZC_HIP(hipGetLastError());
+    return ZC_OK;
+}
+#undef ZC_CHESS_ENTRY
+
+int zc_chess_from_fen(const char *fen, zc_chess_state *out) {
+    // state_from_fen (chess_backend.cpp:525-556): placement, side, castling; en passant and
+    // the full-move number are ignored; the half-move clock becomes the fifty counter.
+    if (!fen || !out) return fail(ZC_EINVAL, "null argument");
+    zc_chess_state s{};
+    const char *p = fen;
+    int idx = 0;
+    for (; *p && *p != ' '; ++p) {
+        if (*p == '/') continue;
+        if (*p >= '0' && *p <= '9') {
+            for (int i = 0; i < *p - '0'; ++i) {
+                if (idx >= 64) return fail(ZC_EINVAL, "FEN placement longer than 64 squares");
+                s.board[idx++] = ' ';
+            }
+        } else {
+            if (idx >= 64) return fail(ZC_EINVAL, "FEN placement longer than 64 squares");
+            s.board[idx++] = (uint8_t)*p;
+        }
+    }
+    if (idx != 64) return fail(ZC_EINVAL, "FEN placement covers %d squares, not 64", idx);
+    while (*p == ' ') ++p;
+    s.turn = (p[0] == 'w' && (p[1] == ' ' || p[1] == 0)) ? 0 : 1;
+    while (*p && *p != ' ') ++p;
+    while (*p == ' ') ++p;
+    for (; *p && *p != ' '; ++p) {
+        if (*p == 'K') s.castle |= 1;
+        if (*p == 'Q') s.castle |= 2;
+        if (*p == 'k') s.castle |= 4;
+        if (*p == 'q') s.castle |= 8;
+    }
+    while (*p == ' ') ++p;
+    while (*p && *p != ' ') ++p;
+    while (*p == ' ') ++p;
+    s.fifty = (uint8_t)atoi(p);
+    *out = s;
+    return ZC_OK;
+}
+
+int zc_chess_init(zc_chess_state *out) {
+    return zc_chess_from_fen("rnbqkbnr/pppppppp/8/8/8/8/PPPPPPPP/RNBQKBNR w KQkq - 0 1", out);
 }
 
 int zc_c4_from_rows(const char *rows, int32_t turn, zc_c4_state *out) {

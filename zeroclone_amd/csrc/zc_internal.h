@@ -103,6 +103,13 @@ struct ExtParams {
     zc_game_stats *out_stats;  // end
 };
 
+void launch_chess_legal(int n, const zc_chess_state *s, uint16_t *moves, int32_t *counts, hipStream_t st);
+void launch_chess_children(int n, const zc_chess_state *s, zc_chess_state *children, uint16_t *moves,
+                           int32_t *counts, hipStream_t st);
+void launch_chess_play(int n, const zc_chess_state *in, const uint16_t *moves, zc_chess_state *out, hipStream_t st);
+void launch_chess_terminal(int n, const zc_chess_state *s, int32_t *flags, hipStream_t st);
+void launch_chess_planes(int n, const zc_chess_state *s, void *planes, int f16, hipStream_t st);
+
 size_t c4_search_lds_bytes(int bs);
 void launch_c4_ext_begin(const ExtParams &p, hipStream_t s);
 void launch_c4_ext_select(const ExtParams &p, hipStream_t s);
