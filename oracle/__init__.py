@@ -262,3 +262,46 @@ def chess_tensor(s: ZccState):
 
 def chess_perft(s: ZccState, depth: int) -> int:
     return int(_chess_lib().zcc_perft(ctypes.byref(s), depth))
+
+
+class ZccLight(ctypes.Structure):
+    _fields_ = [("board", ctypes.c_uint8 * 64), ("turn", ctypes.c_uint8), ("fifty", ctypes.c_uint8),
+                ("castle", ctypes.c_uint8), ("pad", ctypes.c_uint8)]
+
+
+CHESS_VALUE_FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ZccLight),
+                                  ctypes.POINTER(ctypes.c_double))
+
+
+def chess_light(s: ZccState) -> ZccLight:
+    l = ZccLight()
+    l.board[:] = list(s.board)
+    l.turn, l.fifty, l.castle = s.turn, s.fifty, s.castle
+    return l
+
+
+def chess_get_move(s: ZccState, mt: MT, sims: int, c: float, bs: int, policy: str = "random", freedom: float = 0.0,
+                   value_batch=None):
+    """mcts.get_move for chess (crude_chess_score unless value_batch(list of (board bytes,
+    turn, fifty, castle)) -> values is given).  Returns (best index, root moves, root visits)."""
+    L = _chess_lib()
+    L.zcc_get_move.argtypes = [ctypes.POINTER(ZccLight), ctypes.c_void_p, ctypes.c_int, ctypes.c_double, ctypes.c_int,
+                               ctypes.c_int, ctypes.c_double, CHESS_VALUE_FN, ctypes.c_void_p,
+                               ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ZccMove), ctypes.POINTER(ctypes.c_int)]
+    if value_batch is not None:
+        def cb(_ctx, n, leaves, out):
+            vals = value_batch([(bytes(leaves[j].board), leaves[j].turn, leaves[j].fifty, leaves[j].castle)
+                                for j in range(n)])
+            for j in range(n):
+                out[j] = float(vals[j])
+        fn = CHESS_VALUE_FN(cb)
+    else:
+        fn = ctypes.cast(None, CHESS_VALUE_FN)
+    na = (ctypes.c_int * ZCC_MAX_MOVES)()
+    mv = (ZccMove * ZCC_MAX_MOVES)()
+    n = ctypes.c_int(0)
+    best = L.zcc_get_move(ctypes.byref(chess_light(s)), ctypes.cast(ctypes.byref(mt.s), ctypes.c_void_p), sims, c, bs,
+                          1 if policy == "immediate_value" else 0, float(freedom), fn, None, na,
+                          mv, ctypes.byref(n))
+    moves = [(m.fr, m.fc, m.tr, m.tc, m.value) for m in mv[:n.value]]
+    return best, moves, list(na[:n.value])

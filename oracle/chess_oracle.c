@@ -346,3 +346,188 @@ uint64_t zcc_perft(const zcc_state *s, int depth) {
     }
     return total;
 }
+
+/* ------------------------------------------------------------- chess tree search (mcts.cpp) */
+/* mcts.get_move (engine/mcts/src/mcts.cpp:102-160) over the chess rules above, with
+ * Policy('random') or Policy('immediate_value') (engine/policy_functions.py:10-20) drawing
+ * from the CPython MT19937 stream of c4_oracle.c, and Value('crude_chess_score')
+ * (engine/value_functions.py:48-55) or a caller-supplied batch value function. */
+#include "c4_oracle.h"
+
+typedef struct {
+    zcc_light s;
+    int n, nu;
+    zcc_move *mv;
+    int *untried, *child, *Na;
+    double *Wa, *Qa;
+    int parent, pact, N;
+} cnode;
+
+static void light_to_state(const zcc_light *l, zcc_state *s) {
+    memcpy(s->board, l->board, 64);
+    s->turn = l->turn;
+    s->fifty = l->fifty;
+    s->castle = l->castle;
+    s->nhw = s->nhb = 0;
+    s->overflow = 0;
+}
+
+static int cnode_new(cnode *P, int *np, const zcc_light *l, int parent, int pact) {
+    cnode *x = &P[*np];
+    static __thread zcc_state tmp;
+    zcc_move buf[ZCC_MAX_MOVES];
+    light_to_state(l, &tmp);
+    x->s = *l;
+    x->n = zcc_legal_moves(&tmp, buf);
+    x->nu = x->n;
+    x->mv = (zcc_move *)malloc(sizeof(zcc_move) * (size_t)(x->n ? x->n : 1));
+    memcpy(x->mv, buf, sizeof(zcc_move) * (size_t)x->n);
+    x->untried = (int *)malloc(sizeof(int) * (size_t)(x->n ? x->n : 1));
+    x->child = (int *)malloc(sizeof(int) * (size_t)(x->n ? x->n : 1));
+    x->Na = (int *)calloc((size_t)(x->n ? x->n : 1), sizeof(int));
+    x->Wa = (double *)calloc((size_t)(x->n ? x->n : 1), sizeof(double));
+    x->Qa = (double *)calloc((size_t)(x->n ? x->n : 1), sizeof(double));
+    for (int i = 0; i < x->n; i++) {
+        x->untried[i] = i;
+        x->child[i] = -1;
+    }
+    x->parent = parent;
+    x->pact = pact;
+    x->N = 0;
+    return (*np)++;
+}
+
+double zcc_crude_score(const zcc_light *l) {   /* value_functions.py:48-55 */
+    static __thread zcc_state tmp;
+    light_to_state(l, &tmp);
+    if (zcc_check_win(&tmp)) return 1000.0;
+    int sum = 0;
+    for (int i = 0; i < 64; i++) {
+        switch (l->board[i]) {
+            case 'P': sum += 1; break;
+            case 'N': case 'B': sum += 3; break;
+            case 'R': sum += 5; break;
+            case 'Q': sum += 9; break;
+            case 'p': sum -= 1; break;
+            case 'n': case 'b': sum -= 3; break;
+            case 'r': sum -= 5; break;
+            case 'q': sum -= 9; break;
+            default: break;
+        }
+    }
+    const int factor = l->turn * -2 + 1;
+    return (double)(factor * sum);
+}
+
+static int cselect(const cnode *P, double c) {   /* mcts.cpp:47-63 */
+    int node = 0;
+    for (;;) {
+        const cnode *x = &P[node];
+        if (x->nu > 0) return node;
+        int best = -1;
+        double bv = -1e100;
+        for (int i = 0; i < x->n; i++) {
+            if (x->child[i] < 0) continue;
+            const double v = x->Na[i] == 0 ? INFINITY
+                                           : fma(c, sqrt(log((double)x->N) / (double)x->Na[i]), x->Qa[i]);
+            if (v > bv) { bv = v; best = i; }
+        }
+        if (best == -1) return node;
+        node = x->child[best];
+    }
+}
+
+static int cexpand(cnode *P, int *np, int node, zco_mt *r, int policy, double freedom) {   /* mcts.cpp:65-78 */
+    cnode *x = &P[node];
+    int local;
+    if (policy == 1) {   /* immediate_value: choice among untried moves scoring >= best - freedom */
+        double best = -INFINITY;
+        for (int i = 0; i < x->nu; i++)
+            if (x->mv[x->untried[i]].value > best) best = x->mv[x->untried[i]].value;
+        int cand[ZCC_MAX_MOVES], k = 0;
+        for (int i = 0; i < x->nu; i++)
+            if (x->mv[x->untried[i]].value >= best - freedom) cand[k++] = i;
+        local = cand[zco_randbelow(r, (uint32_t)k)];
+    } else {
+        local = (int)zco_randbelow(r, (uint32_t)x->nu);
+    }
+    const int move_idx = x->untried[local];
+    for (int i = local; i + 1 < x->nu; i++) x->untried[i] = x->untried[i + 1];
+    x->nu--;
+    zcc_state tmp;
+    light_to_state(&x->s, &tmp);
+    zcc_play(&tmp, &x->mv[move_idx], &tmp);
+    zcc_light l;
+    memcpy(l.board, tmp.board, 64);
+    l.turn = tmp.turn;
+    l.fifty = tmp.fifty;
+    l.castle = tmp.castle;
+    const int ch = cnode_new(P, np, &l, node, move_idx);
+    P[node].child[move_idx] = ch;
+    return ch;
+}
+
+static void cbackprop(cnode *P, int node, double v) {   /* mcts.cpp:80-100 */
+    for (;;) {
+        P[node].N += 1;
+        const int p = P[node].parent;
+        if (p < 0) break;
+        const int a = P[node].pact;
+        P[p].Na[a] += 1;
+        P[p].Wa[a] -= v;
+        P[p].Qa[a] = P[p].Wa[a] / (double)P[p].Na[a];
+        node = p;
+        v = -v;
+    }
+}
+
+int zcc_get_move(const zcc_light *root, void *rv, int sims, double c, int bs, int policy, double freedom,
+                 zcc_value_fn vfn, void *ctx, int *root_na, zcc_move *root_moves, int *n_root) {
+    zco_mt *r = (zco_mt *)rv;
+    if (bs < 1) bs = 1;
+    cnode *P = (cnode *)malloc(sizeof(cnode) * (size_t)(sims + 1));
+    int np = 0;
+    cnode_new(P, &np, root, -1, -1);
+    int *pend = (int *)malloc(sizeof(int) * (size_t)bs);
+    double *vals = (double *)malloc(sizeof(double) * (size_t)bs);
+    zcc_light *lv = (zcc_light *)malloc(sizeof(zcc_light) * (size_t)bs);
+    int npend = 0;
+    for (int i = 0; i < sims; i++) {
+        const int node = cselect(P, c);
+        const int leaf = P[node].nu > 0 ? cexpand(P, &np, node, r, policy, freedom) : node;
+        pend[npend++] = leaf;
+        if (npend >= bs || i == sims - 1) {
+            if (vfn) {
+                for (int j = 0; j < npend; j++) lv[j] = P[pend[j]].s;
+                vfn(ctx, npend, lv, vals);
+            } else {
+                for (int j = 0; j < npend; j++) vals[j] = zcc_crude_score(&P[pend[j]].s);
+            }
+            for (int j = 0; j < npend; j++) cbackprop(P, pend[j], vals[j]);
+            npend = 0;
+        }
+    }
+    int best = -1, bestN = -1;
+    for (int i = 0; i < P[0].n; i++) {
+        const int ch = P[0].child[i];
+        if (ch >= 0 && P[ch].N > bestN) { bestN = P[ch].N; best = i; }
+    }
+    if (n_root) *n_root = P[0].n;
+    for (int i = 0; i < P[0].n; i++) {
+        if (root_na) root_na[i] = P[0].Na[i];
+        if (root_moves) root_moves[i] = P[0].mv[i];
+    }
+    for (int i = 0; i < np; i++) {
+        free(P[i].mv);
+        free(P[i].untried);
+        free(P[i].child);
+        free(P[i].Na);
+        free(P[i].Wa);
+        free(P[i].Qa);
+    }
+    free(lv);
+    free(vals);
+    free(pend);
+    free(P);
+    return best;
+}

@@ -26,6 +26,12 @@ typedef struct {
     zcc_move hw[ZCC_HIST], hb[ZCC_HIST];
 } zcc_state;
 
+/* The position without history (what a search tree node holds). */
+typedef struct {
+    uint8_t board[64];
+    uint8_t turn, fifty, castle, pad;
+} zcc_light;
+
 void     zcc_init(zcc_state *s);                                       /* create_init_state */
 int      zcc_from_fen(const char *fen, zcc_state *s);                  /* state_from_fen    */
 int      zcc_legal_moves(const zcc_state *s, zcc_move *out);           /* get_legal_moves   */
@@ -35,6 +41,17 @@ int      zcc_check_draw(const zcc_state *s);
 int      zcc_repeated_prefix(const zcc_move *L, int n);               /* has_repeated_prefix(L,2,3) */
 void     zcc_state_to_tensor(const zcc_state *s, float *out);          /* [17][8][8]        */
 uint64_t zcc_perft(const zcc_state *s, int depth);
+
+/* Value('crude_chess_score') (value_functions.py:48-55). */
+double   zcc_crude_score(const zcc_light *l);
+/* mcts.get_move (mcts.cpp:102-160) for chess: policy 0 = Policy('random'), 1 =
+ * Policy('immediate_value', policy_freedom=freedom); vfn NULL = crude_chess_score, else
+ * vfn(ctx, n, leaves, out) is Value.batch over the flush's pending leaves.  r is a
+ * zco_mt* (c4_oracle.h).  Writes the root's moves and visits; returns the index of the
+ * chosen root move (-1 if none). */
+typedef void (*zcc_value_fn)(void *ctx, int n, const zcc_light *leaves, double *out);
+int      zcc_get_move(const zcc_light *root, void *r, int sims, double c, int bs, int policy, double freedom,
+                      zcc_value_fn vfn, void *ctx, int *root_na, zcc_move *root_moves, int *n_root);
 
 #ifdef __cplusplus
 }

@@ -56,3 +56,17 @@ def test_state_to_tensor(golden):
         bits = np.unpackbits(np.frombuffer(bytes.fromhex(case["bits"]), np.uint8))[: 17 * 64]
         np.testing.assert_array_equal((t.reshape(-1) != 0).astype(np.uint8), bits)
         assert list(t.shape) == case["shape"]
+
+
+def test_chess_search_matches_reference(golden):
+    """Chess get_move (crude_chess_score, immediate_value / random policy) vs the reference."""
+    for case in golden("chess_get_move.json")["cases"]:
+        s = oracle.chess_from_fen(case["fen"])
+        mt = oracle.MT(case["seed"])
+        best, moves, na = oracle.chess_get_move(s, mt, case["sims"], case["c"], case["bs"], case["policy"],
+                                                case["freedom"])
+        assert [list(m) for m in moves] == case["root_moves"]
+        assert na == case["root_na"], case["fen"]
+        assert list(moves[best]) == case["move"]
+        assert mt.drawn == case["consumed"]
+        assert mt.u32() == case["next_word"]
