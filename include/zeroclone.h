@@ -117,6 +117,7 @@ int zc_c4_play_async(zc_engine *eng, int32_t n_games, zc_c4_state *d_states, con
 #define ZC_STATUS_NO_MOVES 1     /* root has no legal move                                */
 #define ZC_STATUS_BAD_STATE 2    /* sentinel bits set / overlapping stones / bad turn    */
 #define ZC_STATUS_INTERNAL 3     /* search invariant violated (never expected)            */
+#define ZC_STATUS_CAPACITY 4     /* chess: child-slot pool or leaf depth (63) exhausted   */
 
 /* Value('random_rollout').batch(states, backend=c4_backend) (engine/value_functions.py:20-45)
  * on the device: the n states are rolled out IN ORDER on engine game `game`'s stream, as the
@@ -217,6 +218,36 @@ int zc_chess_planes_async(zc_engine *eng, int32_t n, const zc_chess_state *d_sta
 /* state_from_fen (:525-556) / create_init_state (:446-457) on the host. */
 int zc_chess_from_fen(const char *fen, zc_chess_state *out);
 int zc_chess_init(zc_chess_state *out);
+
+/* ---- Chess tree search: mcts.get_move (mcts.cpp:102-160) with the chess backend ---------
+ * Policy: ZC_POLICY_RANDOM = Policy('random'), ZC_POLICY_IMMEDIATE_VALUE =
+ * Policy('immediate_value', policy_freedom=freedom) (engine/policy_functions.py:10-20), both
+ * drawing from the game's CPython MT19937 stream.  Outputs (device):
+ *   d_out_move[i]                       chosen move (packed uint16, 0xFFFF if none)
+ *   d_out_root_na[i*ZC_CHESS_MAX_MOVES + j]  Na of root move j (the root's get_legal_moves order)
+ *   d_out_stats[i]                      counters; status ZC_STATUS_CAPACITY when the game's
+ *                                       child-slot pool (64 * (max_sims+1)) or the leaf depth
+ *                                       limit (63) was exhausted
+ * The engine allocates its chess tree arena on the first chess search.
+ * zc_chess_search_async evaluates leaves with Value('crude_chess_score')
+ * (value_functions.py:48-55, configs/crude_chess.yaml) inside the kernel; batch_size <= 256. */
+#define ZC_POLICY_RANDOM 0
+#define ZC_POLICY_IMMEDIATE_VALUE 1
+int zc_chess_search_async(zc_engine *eng, int32_t first_game, int32_t n_games, const zc_chess_state *d_roots,
+                          int32_t sims, double c, int32_t batch_size, int32_t policy, double freedom,
+                          uint16_t *d_out_move, int32_t *d_out_root_na, zc_game_stats *d_out_stats,
+                          void *hip_stream);
+/* Stepwise chess search with caller-supplied values, as zc_c4_ext_*: the leaves of flush f
+ * are exported as states (zc_chess_state) and state_to_tensor planes [n*bs][17][8][8]. */
+int zc_chess_ext_begin(zc_engine *eng, int32_t first_game, int32_t n_games, const zc_chess_state *d_roots,
+                       int32_t sims, double c, int32_t batch_size, int32_t policy, double freedom, void *hip_stream);
+int zc_chess_ext_select(zc_engine *eng, int32_t first_game, int32_t n_games, int32_t flush,
+                        zc_chess_state *d_leaves, void *d_planes, int32_t planes_dtype, int32_t *d_counts,
+                        void *hip_stream);
+int zc_chess_ext_backup(zc_engine *eng, int32_t first_game, int32_t n_games, int32_t flush, const double *d_values,
+                        void *hip_stream);
+int zc_chess_ext_end(zc_engine *eng, int32_t first_game, int32_t n_games, uint16_t *d_out_move,
+                     int32_t *d_out_root_na, zc_game_stats *d_out_stats, void *hip_stream);
 
 /* ---- self-test hooks (used by the parity tests) -------------------------------------
  * UCT score exactly as the search kernel computes it (mcts.cpp:41-45), evaluated ON THE

@@ -50,6 +50,8 @@ CHESS_STATE_DTYPE = np.dtype([("board", "u1", (64,)), ("turn", "u1"), ("fifty", 
                               ("reserved", "u1", (5,))])
 CHESS_MAX_MOVES = 256
 ZC_CHESS_WIN, ZC_CHESS_STALEMATE, ZC_CHESS_FIFTY, ZC_CHESS_OVERFLOW = 1, 2, 4, 8
+ZC_POLICY_RANDOM, ZC_POLICY_IMMEDIATE_VALUE = 0, 1
+ZC_STATUS_CAPACITY = 4
 assert CHESS_STATE_DTYPE.itemsize == 72
 assert C4_STATE_DTYPE.itemsize == ctypes.sizeof(C4State) == 24
 assert STATS_DTYPE.itemsize == ctypes.sizeof(GameStats) == 64
@@ -98,6 +100,20 @@ SIGNATURES = [
                                                ctypes.c_void_p]),
     ("zc_chess_planes_async", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p,
                                              ctypes.c_int32, ctypes.c_void_p]),
+    ("zc_chess_search_async", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p,
+                                             ctypes.c_int32, ctypes.c_double, ctypes.c_int32, ctypes.c_int32,
+                                             ctypes.c_double, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                             ctypes.c_void_p]),
+    ("zc_chess_ext_begin", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p,
+                                          ctypes.c_int32, ctypes.c_double, ctypes.c_int32, ctypes.c_int32,
+                                          ctypes.c_double, ctypes.c_void_p]),
+    ("zc_chess_ext_select", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                           ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p,
+                                           ctypes.c_void_p]),
+    ("zc_chess_ext_backup", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                           ctypes.c_void_p, ctypes.c_void_p]),
+    ("zc_chess_ext_end", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p,
+                                        ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     ("zc_chess_from_fen", ctypes.c_int, [ctypes.c_char_p, ctypes.c_void_p]),
     ("zc_chess_init", ctypes.c_int, [ctypes.c_void_p]),
     ("zc_c4_from_rows", ctypes.c_int, [ctypes.c_char_p, ctypes.c_int32, P(C4State)]),
@@ -320,6 +336,33 @@ class NativeEngine:
     def chess_planes_async(self, n: int, d_states: int, d_planes: int, f16: bool = False, stream: int = 0):
         check(lib().zc_chess_planes_async(self._h, n, ctypes.c_void_p(d_states), ctypes.c_void_p(d_planes),
                                           ZC_F16 if f16 else ZC_F32, ctypes.c_void_p(stream or None)))
+
+    # ---- chess tree search (device pointers)
+    def chess_search_async(self, first_game: int, n: int, d_roots: int, sims: int, c: float, batch_size: int,
+                           policy: int, freedom: float, d_move: int, d_na: int, d_stats: int, stream: int = 0):
+        check(lib().zc_chess_search_async(self._h, first_game, n, ctypes.c_void_p(d_roots), int(sims), float(c),
+                                          int(batch_size), int(policy), float(freedom), ctypes.c_void_p(d_move),
+                                          ctypes.c_void_p(d_na), ctypes.c_void_p(d_stats),
+                                          ctypes.c_void_p(stream or None)))
+
+    def chess_ext_begin(self, first_game: int, n: int, d_roots: int, sims: int, c: float, batch_size: int,
+                        policy: int = 0, freedom: float = 0.0, stream: int = 0):
+        check(lib().zc_chess_ext_begin(self._h, first_game, n, ctypes.c_void_p(d_roots), int(sims), float(c),
+                                       int(batch_size), int(policy), float(freedom), ctypes.c_void_p(stream or None)))
+
+    def chess_ext_select(self, first_game: int, n: int, flush: int, d_leaves: int = 0, d_planes: int = 0,
+                         planes_f16: bool = True, d_counts: int = 0, stream: int = 0):
+        check(lib().zc_chess_ext_select(self._h, first_game, n, int(flush), ctypes.c_void_p(d_leaves or None),
+                                        ctypes.c_void_p(d_planes or None), ZC_F16 if planes_f16 else ZC_F32,
+                                        ctypes.c_void_p(d_counts or None), ctypes.c_void_p(stream or None)))
+
+    def chess_ext_backup(self, first_game: int, n: int, flush: int, d_values: int, stream: int = 0):
+        check(lib().zc_chess_ext_backup(self._h, first_game, n, int(flush), ctypes.c_void_p(d_values),
+                                        ctypes.c_void_p(stream or None)))
+
+    def chess_ext_end(self, first_game: int, n: int, d_move: int, d_na: int, d_stats: int, stream: int = 0):
+        check(lib().zc_chess_ext_end(self._h, first_game, n, ctypes.c_void_p(d_move), ctypes.c_void_p(d_na),
+                                     ctypes.c_void_p(d_stats), ctypes.c_void_p(stream or None)))
 
     def c4_rollouts(self, states: np.ndarray, game: int = 0):
         """Sequential rollouts of `states` on one game's stream: (values[n], words consumed)."""

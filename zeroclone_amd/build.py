@@ -13,7 +13,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libzeroclone_amd.so")
-SOURCES = ["engine.hip", "c4_search.hip", "c4_ext.hip", "chess.hip"]
+SOURCES = ["engine.hip", "c4_search.hip", "c4_ext.hip", "chess.hip", "chess_search.hip"]
 HEADERS = ["zc_internal.h", "c4_order_table.h", "c4_device.h", "chess_device.h", os.path.join("..", "..", "include", "zeroclone.h")]
 ARCH = os.environ.get("ZC_OFFLOAD_ARCH", "gfx950")
 
@@ -33,15 +33,30 @@ def _stale() -> bool:
     return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
 
 
+FLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math", "-Wall"]
+
+
 def build(force: bool = False, verbose: bool = False) -> str:
+    """Compile every source to an object in parallel, then link the shared library."""
     if not force and not _stale():
         return LIB
-    srcs = [os.path.join(CSRC, s) for s in SOURCES]
-    tmp = LIB + ".tmp"
+    from concurrent.futures import ThreadPoolExecutor
+    objdir = os.path.join(HERE, "build_obj")
+    os.makedirs(objdir, exist_ok=True)
     # -ffp-contract=off: the UCT arithmetic must round exactly like the reference's
     # (explicit fma only where GCC emitted one for mcts.cpp:44).
-    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-ffp-contract=off", "-fno-fast-math", "-Wall", "-o", tmp] + srcs
+    def compile_one(src):
+        obj = os.path.join(objdir, os.path.splitext(src)[0] + ".o")
+        cmd = [hipcc(), f"--offload-arch={ARCH}", *FLAGS, "-c", os.path.join(CSRC, src), "-o", obj]
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        subprocess.run(cmd, check=True)
+        return obj
+    jobs = min(len(SOURCES), int(os.environ.get("MAX_JOBS", "8")))
+    with ThreadPoolExecutor(jobs) as ex:
+        objs = list(ex.map(compile_one, SOURCES))
+    tmp = LIB + ".tmp"
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)

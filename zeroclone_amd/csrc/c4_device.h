@@ -193,7 +193,7 @@ __device__ __forceinline__ void rng_close(const Rng &r, uint64_t use0, uint64_t 
     rngpos[1] = use0 + (uint64_t)(int64_t)r.grel;
 }
 
-// random._randbelow_with_getrandbits(n), 1 <= n <= 7: k = n.bit_length(); draw
+// random._randbelow_with_getrandbits(n), 1 <= n < 2**31: k = n.bit_length(); draw
 // getrandbits(k) = word >> (32-k) until < n.  All window words are tested at once; the
 // first accepted one (in stream order) is the draw, and everything before it is consumed.
 __device__ __forceinline__ uint32_t rng_below(Rng &r, uint32_t n) {

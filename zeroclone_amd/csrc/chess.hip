@@ -13,36 +13,6 @@ namespace {
 
 using namespace chessdev;
 
-// play_move (:364-400) without the history deques (those stay with the host State).
-__device__ __forceinline__ void apply_move(zc_chess_state &o, uint32_t m) {
-    const int from = (int)(m & 63u), to = (int)((m >> 6) & 63u);
-    const int fc = from & 7, tc = to & 7, tr = to >> 3;
-    uint8_t *b = o.board;
-    const uint8_t pc = b[from], trg = b[to];
-    const int turn = o.turn;
-    o.turn = (uint8_t)(1 - turn);
-    o.fifty = (uint8_t)(o.fifty + 1);
-    if (pc == 'P' || pc == 'p' || !(trg == ' ' || trg == 0)) o.fifty = 0;
-    if (pc == 'K' || (pc == 'R' && fc == 7)) o.castle &= (uint8_t)~1u;
-    if (pc == 'K' || (pc == 'R' && fc == 0)) o.castle &= (uint8_t)~2u;
-    if (pc == 'k' || (pc == 'r' && fc == 7)) o.castle &= (uint8_t)~4u;
-    if (pc == 'k' || (pc == 'r' && fc == 0)) o.castle &= (uint8_t)~8u;
-    if (pc == 'K' && tc - fc == 2) { b[61] = 'R'; b[63] = ' '; }
-    if (pc == 'k' && tc - fc == 2) { b[5] = 'r'; b[7] = ' '; }
-    if (pc == 'K' && tc - fc == -2) { b[59] = 'R'; b[56] = ' '; }
-    if (pc == 'k' && tc - fc == -2) { b[3] = 'r'; b[0] = ' '; }
-    b[to] = pc;
-    b[from] = ' ';
-    if (tr == 0 && pc == 'P') b[to] = 'Q';
-    if (tr == 7 && pc == 'p') b[to] = 'q';
-}
-
-struct WaveScratch {
-    uint8_t board[64];
-    uint16_t legal[kMaxLegal];
-    uint16_t pseudo[kMaxPseudo];
-};
-
 __device__ __forceinline__ void load_board(uint8_t *sb, const zc_chess_state &s) {
     sb[lane()] = s.board[lane()];
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -50,7 +20,7 @@ __device__ __forceinline__ void load_board(uint8_t *sb, const zc_chess_state &s)
 
 __global__ __launch_bounds__(64) void chess_legal_kernel(int n, const zc_chess_state *states, uint16_t *moves,
                                                         int32_t *counts) {
-    __shared__ WaveScratch S;
+    __shared__ ChessScratch S;
     const int i = blockIdx.x;
     if (i >= n) return;
     load_board(S.board, states[i]);
@@ -64,7 +34,7 @@ __global__ __launch_bounds__(64) void chess_legal_kernel(int n, const zc_chess_s
 __global__ __launch_bounds__(64) void chess_children_kernel(int n, const zc_chess_state *states,
                                                            zc_chess_state *children, uint16_t *moves,
                                                            int32_t *counts) {
-    __shared__ WaveScratch S;
+    __shared__ ChessScratch S;
     const int i = blockIdx.x;
     if (i >= n) return;
     const zc_chess_state st = states[i];
@@ -91,7 +61,7 @@ __global__ void chess_play_kernel(int n, const zc_chess_state *in, const uint16_
 // check_win (:404-412): no legal move and the side to move is in check; check_draw
 // (:416-441) minus the history test: stalemate, or fifty counter >= 50.
 __global__ __launch_bounds__(64) void chess_terminal_kernel(int n, const zc_chess_state *states, int32_t *flags) {
-    __shared__ WaveScratch S;
+    __shared__ ChessScratch S;
     const int i = blockIdx.x;
     if (i >= n) return;
     const zc_chess_state st = states[i];

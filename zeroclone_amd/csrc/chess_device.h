@@ -20,6 +20,8 @@
 
 #include <cstdint>
 
+#include "../../include/zeroclone.h"
+
 namespace zc {
 namespace chessdev {
 namespace {
@@ -213,6 +215,36 @@ __device__ __forceinline__ int legal_moves(const uint8_t *b, int t, uint16_t *ou
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     return n > kMaxLegal ? -1 : n;
 }
+
+// play_move (:364-400) without the history deques (those stay with the host State).
+__device__ __forceinline__ void apply_move(zc_chess_state &o, uint32_t m) {
+    const int from = (int)(m & 63u), to = (int)((m >> 6) & 63u);
+    const int fc = from & 7, tc = to & 7, tr = to >> 3;
+    uint8_t *b = o.board;
+    const uint8_t pc = b[from], trg = b[to];
+    const int turn = o.turn;
+    o.turn = (uint8_t)(1 - turn);
+    o.fifty = (uint8_t)(o.fifty + 1);
+    if (pc == 'P' || pc == 'p' || !(trg == ' ' || trg == 0)) o.fifty = 0;
+    if (pc == 'K' || (pc == 'R' && fc == 7)) o.castle &= (uint8_t)~1u;
+    if (pc == 'K' || (pc == 'R' && fc == 0)) o.castle &= (uint8_t)~2u;
+    if (pc == 'k' || (pc == 'r' && fc == 7)) o.castle &= (uint8_t)~4u;
+    if (pc == 'k' || (pc == 'r' && fc == 0)) o.castle &= (uint8_t)~8u;
+    if (pc == 'K' && tc - fc == 2) { b[61] = 'R'; b[63] = ' '; }
+    if (pc == 'k' && tc - fc == 2) { b[5] = 'r'; b[7] = ' '; }
+    if (pc == 'K' && tc - fc == -2) { b[59] = 'R'; b[56] = ' '; }
+    if (pc == 'k' && tc - fc == -2) { b[3] = 'r'; b[0] = ' '; }
+    b[to] = pc;
+    b[from] = ' ';
+    if (tr == 0 && pc == 'P') b[to] = 'Q';
+    if (tr == 7 && pc == 'p') b[to] = 'q';
+}
+
+struct ChessScratch {
+    uint8_t board[64];
+    uint16_t legal[kMaxLegal];
+    uint16_t pseudo[kMaxPseudo];
+};
 
 }  // namespace
 }  // namespace chessdev

@@ -1,0 +1,500 @@
+// chess_search.hip — batched chess tree search for gfx950: mcts.get_move
+// (engine/mcts/src/mcts.cpp:102-160) with the chess backend (chess.hip rules), Policy('random')
+// or Policy('immediate_value') (engine/policy_functions.py:10-20) on each game's CPython
+// MT19937 stream, and either Value('crude_chess_score') evaluated in the kernel
+// (engine/value_functions.py:48-55; configs/crude_chess.yaml) or values supplied by the
+// caller at every flush (the network modes, value_functions.py:61-99; configs/chess_value.yaml).
+//
+// One game per wave.  The tree lives in HBM (zc_internal.h ChessNode + SoA child slots);
+// every node keeps its position, so selection never replays moves.  Lanes take:
+//   - the UCT scan: up to 256 child slots, 64 per pass, fp64 fma(c, sqrt(log N / Na), Q)
+//     with the reference's first-maximum rule (a butterfly argmax over the wave);
+//   - node creation: the legal-move generator of chess_device.h (one square per lane);
+//   - the policy's candidate filter and the untried-list erase;
+//   - backup: lane l updates the edge into level l of the leaf's path.
+// Backups are applied leaf by leaf in pending order, so every Wa receives its fp64
+// subtractions in the reference's order.
+#include <hip/hip_fp16.h>
+
+#include "c4_device.h"
+#include "chess_device.h"
+
+namespace zc {
+namespace {
+
+using chessdev::ChessScratch;
+
+struct CTree {
+    ChessNode *nodes;
+    uint16_t *mv;
+    uint8_t *ut;
+    uint16_t *ch;
+    int32_t *na;
+    double *w;
+    int64_t S;
+};
+
+__device__ __forceinline__ CTree ctree(const ChessParams &p, int g) {
+    const ChessArena &a = p.ca;
+    const size_t so = (size_t)g * (size_t)a.S;
+    return CTree{a.nodes + (size_t)g * p.M, a.mv + so, a.ut + so, a.ch + so, a.na + so, a.w + so, a.S};
+}
+
+enum : int { cNodes = 0, cSlots = 1, cStatus = 2, cNb = 3, cExp = 4, cDepth = 5, cUse0 = 6 };
+
+struct CLds {
+    ChessScratch s;
+    zc_chess_state st;  // staging: the position of the node being created
+};
+
+__device__ __forceinline__ void wave_sync_mem() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); }
+
+__device__ __forceinline__ int32_t piece_material(uint32_t x) {
+    switch (x) {
+        case 'P': return 1;
+        case 'N': case 'B': return 3;
+        case 'R': return 5;
+        case 'Q': return 9;
+        case 'p': return -1;
+        case 'n': case 'b': return -3;
+        case 'r': return -5;
+        case 'q': return -9;
+        default: return 0;
+    }
+}
+
+__device__ __forceinline__ int32_t wave_sum(int32_t x) {
+    for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
+    return x;
+}
+
+// Node(state, get_legal_moves(state), parent, idx) (mcts.cpp:23-34) for the position in
+// L.st: moves in the reference order into fresh slots, all untried, no children.
+__device__ void create_node(const CTree &t, CLds &L, int id, int parent, int pact, int depth, int &slots, int &status) {
+    const uint32_t lane = lane_id();
+    L.s.board[lane] = L.st.board[lane];
+    wave_sync_mem();
+    const int turn = uni((int)L.st.turn);
+    int n = chessdev::legal_moves(L.s.board, turn, L.s.legal, L.s.pseudo);
+    if (n < 0) {
+        status = ZC_STATUS_CAPACITY;
+        n = 0;
+    }
+    const int32_t mat = wave_sum(piece_material(L.s.board[lane]));
+    const uint64_t km = __ballot(L.s.board[lane] == (turn == 0 ? 'K' : 'k'));
+    const int ks = km ? __builtin_ctzll(km) : -1;
+    const bool check = chessdev::attacked_after(L.s.board, turn, ks >= 0 ? ks >> 3 : -1, ks >= 0 ? ks & 7 : -1, -1,
+                                                -1, 0);
+    const int base = slots;
+    if ((int64_t)base + n > t.S) {
+        status = ZC_STATUS_CAPACITY;
+        n = 0;
+    }
+    slots = base + n;
+    for (int j = (int)lane; j < n; j += 64) {
+        t.mv[base + j] = L.s.legal[j];
+        t.ut[base + j] = (uint8_t)j;
+        t.ch[base + j] = 0xFFFF;
+        t.na[base + j] = 0;
+        t.w[base + j] = 0.0;
+    }
+    ChessNode *N = &t.nodes[id];
+    if (lane < 18) ((uint32_t *)&N->st)[lane] = ((const uint32_t *)&L.st)[lane];
+    if (lane == 0) {
+        N->base = (uint32_t)base;
+        N->nmoves = (uint16_t)n;
+        N->nu = (uint16_t)n;
+        N->parent = (uint16_t)parent;
+        N->pact = (uint16_t)pact;
+        N->depth = (uint16_t)depth;
+        N->material = (int16_t)mat;
+        N->check = check ? 1 : 0;
+    }
+    wave_sync_mem();
+}
+
+__device__ __forceinline__ void argmax64(double &v, int &i) {
+    for (int o = 32; o > 0; o >>= 1) {
+        const double ov = __shfl_xor(v, o);
+        const int oi = __shfl_xor(i, o);
+        if (ov > v || (ov == v && oi < i)) {
+            v = ov;
+            i = oi;
+        }
+    }
+}
+
+// The r-th set position (in index order) of a predicate over [0, n), 64 per pass.
+template <class Pred>
+__device__ __forceinline__ int nth_true(int n, uint32_t r, Pred pred) {
+    const uint32_t lane = lane_id();
+    for (int b = 0; b < n; b += 64) {
+        const int j = b + (int)lane;
+        const uint64_t m = __ballot(j < n && pred(j));
+        const uint32_t c = (uint32_t)__popcll(m);
+        if (r < c) {
+            const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+            const uint64_t hit = __ballot(((m >> lane) & 1ull) && rank == r);
+            return b + __builtin_ctzll(hit);
+        }
+        r -= c;
+    }
+    return -1;
+}
+
+// select + expand + record of ONE simulation (mcts.cpp:129-147).  Returns the leaf node;
+// its depth in `ldepth`; lane l of `pathv` holds the slot of the edge into level l.
+__device__ int simulate(const ChessParams &p, const CTree &t, CLds &L, ConstDouble *logtab, Rng &rng, int done,
+                        int &nnodes, int &slots, int &status, int &ldepth, uint32_t &pathv, Counters &cn) {
+    const uint32_t lane = lane_id();
+    int node = 0, depth = 0, nN = done;
+    pathv = 0;
+    for (;;) {  // select (mcts.cpp:47-63)
+        const ChessNode *N = &t.nodes[node];
+        const uint32_t base = uni(N->base);
+        const int nm = uni((int)N->nmoves), nu = uni((int)N->nu);
+        if (nu > 0 || nm == 0) break;
+        if (depth >= kChessPath - 2) {
+            status = ZC_STATUS_CAPACITY;
+            break;
+        }
+        const double lg = logtab[nN];
+        int first_unv = 0x7FFFFFFF;
+        double bv = -INFINITY;
+        int bi = 0x7FFFFFFF;
+        for (int b = 0; b < nm; b += 64) {
+            const int j = b + (int)lane;
+            bool valid = false;
+            int32_t na = 0;
+            double w = 0.0;
+            if (j < nm) {
+                valid = t.ch[base + j] != 0xFFFF;
+                na = t.na[base + j];
+                w = t.w[base + j];
+            }
+            const uint64_t unv = __ballot(valid && na == 0);
+            if (unv && first_unv == 0x7FFFFFFF) first_unv = b + __builtin_ctzll(unv);
+            if (valid && na > 0) {
+                // UCT (mcts.cpp:41-45): fma(c, sqrt(log(N)/Na), Qa), Qa = Wa / Na (:95)
+                const double v = fma(p.c, sqrt(lg / (double)na), w / (double)na);
+                if (v > bv) {
+                    bv = v;
+                    bi = j;
+                }
+            }
+        }
+        int best;
+        if (first_unv != 0x7FFFFFFF) {
+            best = first_unv;
+        } else {
+            argmax64(bv, bi);
+            if (bi == 0x7FFFFFFF) break;  // no child at all (cannot happen with nu == 0, nm > 0)
+            best = uni(bi);
+        }
+        const int nxt = uni((int)t.ch[base + best]);
+        nN = uni(t.na[base + best]);
+        ++depth;
+        if (lane == (uint32_t)depth) pathv = base + (uint32_t)best;
+        node = nxt;
+    }
+    ChessNode *N = &t.nodes[node];
+    const int nu = uni((int)N->nu);
+    ldepth = depth;
+    if (nu == 0 || status) return node;
+
+    // expand (mcts.cpp:65-78): the policy picks among the untried moves, in untried order
+    const uint32_t base = uni(N->base);
+    int local;
+    if (p.policy == 1) {
+        // Policy('immediate_value') (policy_functions.py:14-17): random.choice over the
+        // untried moves whose capture value >= max - policy_freedom
+        int best = -1;
+        for (int b = 0; b < nu; b += 64) {
+            const int i = b + (int)lane;
+            int v = -1;
+            if (i < nu) v = (int)(t.mv[base + t.ut[base + i]] >> 12);
+            for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o));
+            best = max(best, v);
+        }
+        const double thr = (double)best - p.freedom;
+        auto cand = [&](int i) { return (double)(t.mv[base + t.ut[base + i]] >> 12) >= thr; };
+        uint32_t k = 0;
+        for (int b = 0; b < nu; b += 64) {
+            const int i = b + (int)lane;
+            k += (uint32_t)__popcll(__ballot(i < nu && cand(i)));
+        }
+        const uint32_t r = rng_below(rng, k);
+        local = nth_true(nu, r, cand);
+    } else {
+        local = (int)rng_below(rng, (uint32_t)nu);  // Policy('random'): random.choice(untried)
+    }
+    const int midx = uni((int)t.ut[base + local]);
+    // untried.erase(begin + local): shift the tail down, 64 entries per pass (each pass
+    // reads entries the previous pass has not overwritten)
+    for (int b = local; b < nu - 1; b += 64) {
+        const int i = b + (int)lane;
+        uint8_t v = 0;
+        if (i < nu - 1) v = t.ut[base + i + 1];
+        wave_sync_mem();
+        if (i < nu - 1) t.ut[base + i] = v;
+    }
+    if (lane == 0) N->nu = (uint16_t)(nu - 1);
+    const uint32_t m = uni((uint32_t)t.mv[base + midx]);
+    if (lane < 18) ((uint32_t *)&L.st)[lane] = ((const uint32_t *)&N->st)[lane];
+    wave_sync_mem();
+    if (lane == 0) chessdev::apply_move(L.st, m);
+    wave_sync_mem();
+    const int child = nnodes++;
+    if (child >= p.M) {
+        status = ZC_STATUS_INTERNAL;
+        return node;
+    }
+    create_node(t, L, child, node, midx, depth + 1, slots, status);
+    if (lane == 0) t.ch[base + midx] = (uint16_t)child;
+    ++depth;
+    if (lane == (uint32_t)depth) pathv = base + (uint32_t)midx;
+    ldepth = depth;
+    cn.add(cn.expansions, 1);
+    cn.add(cn.depth_sum, depth);
+    wave_sync_mem();
+    return child;
+}
+
+// backprop of leaf j (mcts.cpp:80-100): Na += 1, Wa -= (-1)^(d-l) v on the edge into level l.
+__device__ __forceinline__ void backup_leaf(const CTree &t, const uint32_t *path, int d, double v) {
+    const uint32_t lane = lane_id();
+    if (lane >= 1 && lane <= (uint32_t)d) {
+        const uint32_t s = path[lane];
+        const double r = ((d - (int)lane) & 1) ? -v : v;
+        t.na[s] += 1;
+        t.w[s] -= r;
+    }
+}
+
+__device__ void root_init(const ChessParams &p, const CTree &t, CLds &L, int gl, int g, int32_t *ctl) {
+    const uint32_t lane = lane_id();
+    if (lane < 18) {
+        const uint32_t w = ((const uint32_t *)&p.roots[gl])[lane];
+        ((uint32_t *)&L.st)[lane] = w;
+        ((uint32_t *)&p.ca.roots[g])[lane] = w;
+    }
+    wave_sync_mem();
+    int slots = 0, status = 0;
+    create_node(t, L, 0, 0xFFFF, 0xFFFF, 0, slots, status);
+    if (!status && uni((int)t.nodes[0].nmoves) == 0) status = ZC_STATUS_NO_MOVES;
+    const uint64_t use0 = p.a.rngpos[2 * (size_t)g];
+    if (lane == 0) {
+        ctl[cNodes] = 1;
+        ctl[cSlots] = slots;
+        ctl[cStatus] = status;
+        ctl[cNb] = 0;
+        ctl[cExp] = 0;
+        ctl[cDepth] = 0;
+        ctl[cUse0] = (int32_t)(uint32_t)use0;
+        ctl[cUse0 + 1] = (int32_t)(uint32_t)(use0 >> 32);
+    }
+    wave_sync_mem();
+}
+
+__device__ void finish(const ChessParams &p, const CTree &t, int gl, int g, const int32_t *ctl) {
+    const uint32_t lane = lane_id();
+    const int status = uni(ctl[cStatus]);
+    const ChessNode *R = &t.nodes[0];
+    const int nm = status == ZC_STATUS_NO_MOVES ? 0 : uni((int)R->nmoves);
+    const uint32_t base = uni(R->base);
+    // first max of child N over the root's moves (mcts.cpp:150-155)
+    int bv = -1, bi = 0x7FFFFFFF;
+    for (int b = 0; b < nm; b += 64) {
+        const int j = b + (int)lane;
+        if (j < nm && t.ch[base + j] != 0xFFFF) {
+            const int na = t.na[base + j];
+            if (na > bv) {
+                bv = na;
+                bi = j;
+            }
+        }
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        const int ov = __shfl_xor(bv, o), oi = __shfl_xor(bi, o);
+        if (ov > bv || (ov == bv && oi < bi)) {
+            bv = ov;
+            bi = oi;
+        }
+    }
+    for (int j = (int)lane; j < ZC_CHESS_MAX_MOVES; j += 64)
+        p.out_na[(size_t)gl * ZC_CHESS_MAX_MOVES + j] = j < nm ? t.na[base + j] : 0;
+    if (lane == 0) {
+        p.out_move[gl] = (bi != 0x7FFFFFFF && !status) ? t.mv[base + bi] : (uint16_t)0xFFFF;
+        zc_game_stats st{};
+        st.status = status;
+        st.expansions = ctl[cExp];
+        st.depth_sum = ctl[cDepth];
+        st.leaves = p.sims;
+        const uint64_t use0 = (uint64_t)(uint32_t)ctl[cUse0] | ((uint64_t)(uint32_t)ctl[cUse0 + 1] << 32);
+        st.rng_words = (int64_t)(p.a.rngpos[2 * (size_t)g] - use0);
+        p.out_stats[gl] = st;
+    }
+}
+
+// select + expand of one flush; leaf records to the arena (meta, paths).  Returns nb.
+__device__ int chess_select_flush(const ChessParams &p, const CTree &t, CLds &L, ConstDouble *logtab, int g, int32_t *ctl,
+                            int done, int nb) {
+    const uint32_t lane = lane_id();
+    int nnodes = uni(ctl[cNodes]), slots = uni(ctl[cSlots]), status = uni(ctl[cStatus]);
+    Rng rng;
+    const uint64_t use_now = uni64(p.a.rngpos[2 * (size_t)g]);
+    rng_open(rng, p.a.ring + (size_t)g * kRingWords, use_now, uni64(p.a.rngpos[2 * (size_t)g + 1]));
+    Counters cn;
+    uint32_t *paths = p.ca.paths + (size_t)g * p.max_batch * kChessPath;
+    uint32_t *meta = p.ca.meta + (size_t)g * p.max_batch;
+    int j = 0;
+    for (; j < nb && !status; ++j) {
+        int d = 0;
+        uint32_t pathv = 0;
+        const int leaf = simulate(p, t, L, logtab, rng, done, nnodes, slots, status, d, pathv, cn);
+        if (lane < (uint32_t)kChessPath) paths[(size_t)j * kChessPath + lane] = pathv;
+        if (lane == 0) meta[j] = (uint32_t)leaf | ((uint32_t)d << 16);
+    }
+    wave_sync_mem();
+    if (lane == 0) {
+        ctl[cNodes] = nnodes;
+        ctl[cSlots] = slots;
+        ctl[cStatus] = status;
+        ctl[cNb] = status ? 0 : nb;
+        ctl[cExp] += cn.expansions;
+        ctl[cDepth] += cn.depth_sum;
+        rng_close(rng, use_now, p.a.rngpos + 2 * (size_t)g);
+    }
+    wave_sync_mem();
+    return status ? 0 : nb;
+}
+
+__device__ void chess_backup_flush(const ChessParams &p, const CTree &t, int g, const int32_t *ctl, const double *vals,
+                             int nb) {
+    const uint32_t *paths = p.ca.paths + (size_t)g * p.max_batch * kChessPath;
+    const uint32_t *meta = p.ca.meta + (size_t)g * p.max_batch;
+    for (int j = 0; j < nb; ++j) {
+        const uint32_t m = uni(meta[j]);
+        const double v = __hiloint2double(uni(__double2hiint(vals[j])), uni(__double2loint(vals[j])));
+        backup_leaf(t, paths + (size_t)j * kChessPath, (int)(m >> 16), v);
+        wave_sync_mem();
+    }
+}
+
+// ---------------------------------------------------------------- fused: crude_chess_score
+__global__ __launch_bounds__(64) void chess_search_kernel(ChessParams p) {
+    __shared__ CLds L;
+    __shared__ double s_vals[256];
+    const int gl = blockIdx.x;
+    if (gl >= p.n_games) return;
+    const int g = p.first_game + gl;
+    const CTree t = ctree(p, g);
+    int32_t *ctl = p.ca.ctl + (size_t)g * kCtlWords;
+    ConstDouble *logtab = (ConstDouble *)p.a.logtab;
+    root_init(p, t, L, gl, g, ctl);
+    const uint32_t *meta = p.ca.meta + (size_t)g * p.max_batch;
+    for (int done = 0; done < p.sims && !uni(ctl[cStatus]);) {
+        const int nb = chess_select_flush(p, t, L, logtab, g, ctl, done, min(p.bs, p.sims - done));
+        // value.batch: crude_chess_score of every pending leaf (mcts.cpp:116-118)
+        for (int j = (int)lane_id(); j < nb; j += 64) {
+            const ChessNode *N = &t.nodes[meta[j] & 0xFFFFu];
+            const int nm = N->nmoves, chk = N->check, turn = N->st.turn, mat = N->material;
+            s_vals[j] = (nm == 0 && chk) ? 1000.0 : (double)((turn * -2 + 1) * mat);
+        }
+        wave_sync_mem();
+        chess_backup_flush(p, t, g, ctl, s_vals, nb);
+        done += nb;
+    }
+    finish(p, t, gl, g, ctl);
+}
+
+// ---------------------------------------------------------------- stepwise (caller values)
+__global__ __launch_bounds__(64) void chess_ext_begin_kernel(ChessParams p) {
+    __shared__ CLds L;
+    const int gl = blockIdx.x;
+    if (gl >= p.n_games) return;
+    const int g = p.first_game + gl;
+    root_init(p, ctree(p, g), L, gl, g, p.ca.ctl + (size_t)g * kCtlWords);
+}
+
+__global__ __launch_bounds__(64) void chess_ext_select_kernel(ChessParams p) {
+    __shared__ CLds L;
+    const int gl = blockIdx.x;
+    if (gl >= p.n_games) return;
+    const int g = p.first_game + gl;
+    const CTree t = ctree(p, g);
+    int32_t *ctl = p.ca.ctl + (size_t)g * kCtlWords;
+    const uint32_t lane = lane_id();
+    int nb = 0;
+    if (!uni(ctl[cStatus])) {
+        const int done = p.flush * p.bs;
+        nb = chess_select_flush(p, t, L, (ConstDouble *)p.a.logtab, g, ctl, done, min(p.bs, p.sims - done));
+    } else if (lane == 0) {
+        ctl[cNb] = 0;
+    }
+    if (lane == 0 && p.counts) p.counts[gl] = nb;
+    const uint32_t *meta = p.ca.meta + (size_t)g * p.max_batch;
+    const size_t obase = (size_t)gl * p.bs;
+    for (int j = 0; j < nb; ++j) {
+        const ChessNode *N = &t.nodes[uni(meta[j]) & 0xFFFFu];
+        if (p.leaves && lane < 18) ((uint32_t *)&p.leaves[obase + j])[lane] = ((const uint32_t *)&N->st)[lane];
+        if (p.planes) {
+            // state_to_tensor (chess_backend.cpp:461-521): lane = square
+            const uint32_t pc = N->st.board[lane];
+            const char pieces[12] = {'P', 'N', 'B', 'R', 'Q', 'K', 'p', 'n', 'b', 'r', 'q', 'k'};
+            int which = -1;
+            for (int k = 0; k < 12; ++k)
+                if (pc == (uint8_t)pieces[k]) {
+                    which = k;
+                    break;
+                }
+            const int turn = N->st.turn, castle = N->st.castle;
+            for (int k = 0; k < 17; ++k) {
+                float v;
+                if (k < 12) v = k == which ? 1.0f : 0.0f;
+                else if (k == 12) v = turn == 0 ? 1.0f : 0.0f;
+                else v = (castle >> (k - 13)) & 1 ? 1.0f : 0.0f;
+                const size_t o = ((obase + j) * 17 + k) * 64 + lane;
+                if (p.planes_f16) ((__half *)p.planes)[o] = __float2half(v);
+                else ((float *)p.planes)[o] = v;
+            }
+        }
+    }
+}
+
+__global__ __launch_bounds__(64) void chess_ext_backup_kernel(ChessParams p) {
+    const int gl = blockIdx.x;
+    if (gl >= p.n_games) return;
+    const int g = p.first_game + gl;
+    const int32_t *ctl = p.ca.ctl + (size_t)g * kCtlWords;
+    const int nb = uni(ctl[cNb]);
+    if (uni(ctl[cStatus]) || nb == 0) return;
+    chess_backup_flush(p, ctree(p, g), g, ctl, p.values + (size_t)gl * p.bs, nb);
+}
+
+__global__ __launch_bounds__(64) void chess_ext_end_kernel(ChessParams p) {
+    const int gl = blockIdx.x;
+    if (gl >= p.n_games) return;
+    const int g = p.first_game + gl;
+    finish(p, ctree(p, g), gl, g, p.ca.ctl + (size_t)g * kCtlWords);
+}
+
+}  // namespace
+
+void launch_chess_search(const ChessParams &p, hipStream_t s) {
+    hipLaunchKernelGGL(chess_search_kernel, dim3(p.n_games), dim3(64), 0, s, p);
+}
+void launch_chess_ext_begin(const ChessParams &p, hipStream_t s) {
+    hipLaunchKernelGGL(chess_ext_begin_kernel, dim3(p.n_games), dim3(64), 0, s, p);
+}
+void launch_chess_ext_select(const ChessParams &p, hipStream_t s) {
+    hipLaunchKernelGGL(chess_ext_select_kernel, dim3(p.n_games), dim3(64), 0, s, p);
+}
+void launch_chess_ext_backup(const ChessParams &p, hipStream_t s) {
+    hipLaunchKernelGGL(chess_ext_backup_kernel, dim3(p.n_games), dim3(64), 0, s, p);
+}
+void launch_chess_ext_end(const ChessParams &p, hipStream_t s) {
+    hipLaunchKernelGGL(chess_ext_end_kernel, dim3(p.n_games), dim3(64), 0, s, p);
+}
+
+}  // namespace zc

@@ -61,6 +61,13 @@ int dalloc(zc_engine *e, T **p, size_t count) {
     return ZC_OK;
 }
 
+void free_chess(zc::ChessArena &c) {
+    void *ptrs[] = {c.nodes, c.mv, c.ut, c.ch, c.na, c.w, c.ctl, c.paths, c.meta, c.roots};
+    for (void *p : ptrs)
+        if (p) (void)hipFree(p);
+    c = zc::ChessArena{};
+}
+
 void free_arena(zc::Arena &a) {
     void *ptrs[] = {a.nodes, a.W,     a.ring,  a.rngpos, a.logtab,  a.phase,    a.roots,    a.move,
                     a.na,    a.ids,   a.stats, a.ext_ctl, a.ext_paths, a.ext_meta, a.ext_roots};
@@ -223,6 +230,7 @@ int zc_engine_destroy(zc_engine *eng) {
         (void)hipSetDevice(eng->cfg.device);
         (void)hipStreamSynchronize(eng->stream);
         free_arena(eng->a);
+        free_chess(eng->ca);
         (void)hipStreamDestroy(eng->stream);
     }
     delete eng;
@@ -523,6 +531,174 @@ int zc_chess_planes_async(zc_engine *eng, int32_t n, const zc_chess_state *d_sta
     return ZC_OK;
 }
 #undef ZC_CHESS_ENTRY
+
+// ---------------------------------------------------------------- chess tree search
+}  // extern "C"
+
+namespace {
+int ensure_chess(zc_engine *e) {
+    zc::ChessArena &c = e->ca;
+    if (c.nodes) return ZC_OK;
+    const size_t G = (size_t)e->cfg.max_games, M = (size_t)e->M;
+    const size_t S = M * zc::kChessSlotsPerNode;
+    zc::ChessArena n{};
+    n.S = (int64_t)S;
+    int rc = ZC_OK;
+    if (!rc) rc = dalloc(e, &n.nodes, G * M);
+    if (!rc) rc = dalloc(e, &n.mv, G * S);
+    if (!rc) rc = dalloc(e, &n.ut, G * S);
+    if (!rc) rc = dalloc(e, &n.ch, G * S);
+    if (!rc) rc = dalloc(e, &n.na, G * S);
+    if (!rc) rc = dalloc(e, &n.w, G * S);
+    if (!rc) rc = dalloc(e, &n.ctl, G * zc::kCtlWords);
+    if (!rc) rc = dalloc(e, &n.paths, G * (size_t)e->cfg.max_batch * zc::kChessPath);
+    if (!rc) rc = dalloc(e, &n.meta, G * (size_t)e->cfg.max_batch);
+    if (!rc) rc = dalloc(e, &n.roots, G);
+    if (!rc && hipMemset(n.ctl, 0, G * zc::kCtlWords * sizeof(int32_t)) != hipSuccess) rc = fail(ZC_EHIP, "memset failed");
+    if (rc) {
+        free_chess(n);
+        return rc;
+    }
+    c = n;
+    return ZC_OK;
+}
+
+zc::ChessParams chess_params(zc_engine *e, int32_t first, int32_t n, int32_t sims, double c, int32_t bs, int32_t policy,
+                             double freedom) {
+    zc::ChessParams p{};
+    p.first_game = first;
+    p.n_games = n;
+    p.sims = sims;
+    p.bs = bs;
+    p.M = e->M;
+    p.max_batch = e->cfg.max_batch;
+    p.c = c;
+    p.policy = policy;
+    p.freedom = freedom;
+    p.a = e->a;
+    p.ca = e->ca;
+    return p;
+}
+
+int check_chess(zc_engine *e, int32_t first, int32_t n, int32_t sims, double c, int32_t bs, int32_t policy,
+                double freedom) {
+    if (int r = check_search(e, first, n, sims, c, bs)) return r;
+    if (policy != ZC_POLICY_RANDOM && policy != ZC_POLICY_IMMEDIATE_VALUE)
+        return fail(ZC_EINVAL, "policy must be ZC_POLICY_RANDOM or ZC_POLICY_IMMEDIATE_VALUE");
+    if (!isfinite(freedom)) return fail(ZC_EINVAL, "policy_freedom must be finite");
+    return ZC_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int zc_chess_search_async(zc_engine *eng, int32_t first, int32_t n, const zc_chess_state *d_roots, int32_t sims,
+                          double c, int32_t bs, int32_t policy, double freedom, uint16_t *d_move, int32_t *d_na,
+                          zc_game_stats *d_stats, void *hip_stream) {
+    if (!eng || (n && (!d_roots || !d_move || !d_na || !d_stats))) return fail(ZC_EINVAL, "null argument");
+    if (int r = check_chess(eng, first, n, sims, c, bs, policy, freedom)) return r;
+    if (bs > 256) return fail(ZC_EINVAL, "batch_size %d > 256 (crude-score chess search)", bs);
+    if (!n) return ZC_OK;
+    std::lock_guard<std::mutex> lk(eng->mu);
+    ZC_HIP(hipSetDevice(eng->cfg.device));
+    if (int r = ensure_chess(eng)) return r;
+    zc::ChessParams p = chess_params(eng, first, n, sims, c, bs, policy, freedom);
+    p.roots = d_roots;
+    p.out_move = d_move;
+    p.out_na = d_na;
+    p.out_stats = d_stats;
+    zc::launch_chess_search(p, (hipStream_t)hip_stream);
+    ZC_HIP(hipGetLastError());
+    return ZC_OK;
+}
+
+int zc_chess_ext_begin(zc_engine *eng, int32_t first, int32_t n, const zc_chess_state *d_roots, int32_t sims, double c,
+                       int32_t bs, int32_t policy, double freedom, void *hip_stream) {
+    if (!eng || (n && !d_roots)) return fail(ZC_EINVAL, "null argument");
+    if (int r = check_chess(eng, first, n, sims, c, bs, policy, freedom)) return r;
+    std::lock_guard<std::mutex> lk(eng->mu);
+    ZC_HIP(hipSetDevice(eng->cfg.device));
+    if (int r = ensure_chess(eng)) return r;
+    eng->cx_first = first;
+    eng->cx_n = n;
+    eng->cx_sims = sims;
+    eng->cx_bs = bs;
+    eng->cx_c = c;
+    eng->cx_policy = policy;
+    eng->cx_freedom = freedom;
+    eng->cx_active = true;
+    if (!n) return ZC_OK;
+    zc::ChessParams p = chess_params(eng, first, n, sims, c, bs, policy, freedom);
+    p.roots = d_roots;
+    zc::launch_chess_ext_begin(p, (hipStream_t)hip_stream);
+    ZC_HIP(hipGetLastError());
+    return ZC_OK;
+}
+
+}  // extern "C"
+
+namespace {
+int check_cx(zc_engine *e, int32_t first, int32_t n, int32_t flush, bool need_flush) {
+    if (!e->cx_active) return fail(ZC_EINVAL, "no chess stepwise search in progress (call zc_chess_ext_begin first)");
+    if (first < e->cx_first || n < 0 || (int64_t)first + n > (int64_t)e->cx_first + e->cx_n)
+        return fail(ZC_EINVAL, "games [%d, %d) outside the stepwise search's range", first, first + n);
+    const int nflush = (e->cx_sims + e->cx_bs - 1) / e->cx_bs;
+    if (need_flush && (flush < 0 || flush >= nflush)) return fail(ZC_EINVAL, "flush %d outside [0, %d)", flush, nflush);
+    return ZC_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int zc_chess_ext_select(zc_engine *eng, int32_t first, int32_t n, int32_t flush, zc_chess_state *d_leaves,
+                        void *d_planes, int32_t planes_dtype, int32_t *d_counts, void *hip_stream) {
+    if (!eng) return fail(ZC_EINVAL, "null argument");
+    if (planes_dtype != ZC_F32 && planes_dtype != ZC_F16) return fail(ZC_EINVAL, "planes_dtype must be ZC_F32 or ZC_F16");
+    std::lock_guard<std::mutex> lk(eng->mu);
+    if (int r = check_cx(eng, first, n, flush, true)) return r;
+    if (!n) return ZC_OK;
+    ZC_HIP(hipSetDevice(eng->cfg.device));
+    zc::ChessParams p = chess_params(eng, first, n, eng->cx_sims, eng->cx_c, eng->cx_bs, eng->cx_policy, eng->cx_freedom);
+    p.flush = flush;
+    p.leaves = d_leaves;
+    p.planes = d_planes;
+    p.planes_f16 = planes_dtype == ZC_F16;
+    p.counts = d_counts;
+    zc::launch_chess_ext_select(p, (hipStream_t)hip_stream);
+    ZC_HIP(hipGetLastError());
+    return ZC_OK;
+}
+
+int zc_chess_ext_backup(zc_engine *eng, int32_t first, int32_t n, int32_t flush, const double *d_values,
+                        void *hip_stream) {
+    if (!eng || (n && !d_values)) return fail(ZC_EINVAL, "null argument");
+    std::lock_guard<std::mutex> lk(eng->mu);
+    if (int r = check_cx(eng, first, n, flush, true)) return r;
+    if (!n) return ZC_OK;
+    ZC_HIP(hipSetDevice(eng->cfg.device));
+    zc::ChessParams p = chess_params(eng, first, n, eng->cx_sims, eng->cx_c, eng->cx_bs, eng->cx_policy, eng->cx_freedom);
+    p.flush = flush;
+    p.values = d_values;
+    zc::launch_chess_ext_backup(p, (hipStream_t)hip_stream);
+    ZC_HIP(hipGetLastError());
+    return ZC_OK;
+}
+
+int zc_chess_ext_end(zc_engine *eng, int32_t first, int32_t n, uint16_t *d_move, int32_t *d_na, zc_game_stats *d_stats,
+                     void *hip_stream) {
+    if (!eng || (n && (!d_move || !d_na || !d_stats))) return fail(ZC_EINVAL, "null argument");
+    std::lock_guard<std::mutex> lk(eng->mu);
+    if (int r = check_cx(eng, first, n, 0, false)) return r;
+    if (!n) return ZC_OK;
+    ZC_HIP(hipSetDevice(eng->cfg.device));
+    zc::ChessParams p = chess_params(eng, first, n, eng->cx_sims, eng->cx_c, eng->cx_bs, eng->cx_policy, eng->cx_freedom);
+    p.out_move = d_move;
+    p.out_na = d_na;
+    p.out_stats = d_stats;
+    zc::launch_chess_ext_end(p, (hipStream_t)hip_stream);
+    ZC_HIP(hipGetLastError());
+    return ZC_OK;
+}
 
 int zc_chess_from_fen(const char *fen, zc_chess_state *out) {
     // state_from_fen (chess_backend.cpp:525-556): placement, side, castling; en passant and

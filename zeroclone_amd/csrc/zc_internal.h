@@ -103,6 +103,65 @@ struct ExtParams {
     zc_game_stats *out_stats;  // end
 };
 
+// ---------------------------------------------------------------- chess tree search
+// Per game: M node records (ChessNode) and a pool of S child slots; node i's moves occupy
+// slots [base, base + nmoves) in the reference's move order.  Slot arrays are SoA so the
+// UCT scan over a node's children is a coalesced read per array.
+constexpr int kChessPath = 64;      // deepest leaf a flush may hold (levels 0..63)
+constexpr int kChessSlotsPerNode = 64;
+
+struct ChessNode {
+    zc_chess_state st;   // 72 B: the position (board bytes, turn, fifty, castling)
+    uint32_t base;       // first child slot
+    uint16_t nmoves;     // legal moves (Node::moves.size())
+    uint16_t nu;         // untried moves left (Node::untried.size())
+    uint16_t parent;     // 0xFFFF at the root
+    uint16_t pact;       // slot index in the parent's move list (parent_action_idx)
+    uint16_t depth;
+    int16_t material;    // sum of piece values, white positive (crude_chess_score)
+    uint8_t check;       // side to move in check
+    uint8_t pad[7];
+};
+static_assert(sizeof(ChessNode) == 96, "ChessNode is 96 bytes");
+
+struct ChessArena {
+    ChessNode *nodes = nullptr;  // [G][M]
+    uint16_t *mv = nullptr;      // [G][S] packed move (from | to << 6 | value << 12)
+    uint8_t *ut = nullptr;       // [G][S] untried list: indices into the node's moves, in order
+    uint16_t *ch = nullptr;      // [G][S] child node, 0xFFFF = null
+    int32_t *na = nullptr;       // [G][S] Na
+    double *w = nullptr;         // [G][S] Wa (fp64, summed in pending order)
+    int32_t *ctl = nullptr;      // [G][kCtlWords]
+    uint32_t *paths = nullptr;   // [G][max_batch][kChessPath] slot of the edge into each level
+    uint32_t *meta = nullptr;    // [G][max_batch] leaf node | depth << 16
+    zc_chess_state *roots = nullptr;  // [G]
+    int64_t S = 0;
+};
+
+struct ChessParams {
+    int first_game, n_games, sims, bs, M, max_batch, flush;
+    double c;
+    int policy;        // 0 = Policy('random'), 1 = Policy('immediate_value')
+    double freedom;    // policy_freedom
+    Arena a;           // RNG ring / positions and the log table
+    ChessArena ca;
+    const zc_chess_state *roots;
+    zc_chess_state *leaves;
+    void *planes;
+    int planes_f16;
+    int32_t *counts;
+    const double *values;
+    uint16_t *out_move;
+    int32_t *out_na;   // [n][ZC_CHESS_MAX_MOVES]
+    zc_game_stats *out_stats;
+};
+
+void launch_chess_search(const ChessParams &p, hipStream_t s);     // crude_chess_score, whole move
+void launch_chess_ext_begin(const ChessParams &p, hipStream_t s);
+void launch_chess_ext_select(const ChessParams &p, hipStream_t s);
+void launch_chess_ext_backup(const ChessParams &p, hipStream_t s);
+void launch_chess_ext_end(const ChessParams &p, hipStream_t s);
+
 void launch_chess_legal(int n, const zc_chess_state *s, uint16_t *moves, int32_t *counts, hipStream_t st);
 void launch_chess_children(int n, const zc_chess_state *s, zc_chess_state *children, uint16_t *moves,
                            int32_t *counts, hipStream_t st);
@@ -133,6 +192,11 @@ struct zc_engine {
     zc::Arena a;
     int64_t bytes = 0;
     int stamp = 0;
+    zc::ChessArena ca;  // allocated on the first chess search
+    // the chess stepwise search in progress
+    int cx_first = 0, cx_n = 0, cx_sims = 0, cx_bs = 0, cx_policy = 0;
+    double cx_c = 0, cx_freedom = 0;
+    bool cx_active = false;
     // the stepwise search in progress (zc_c4_ext_begin .. end)
     int ext_first = 0, ext_n = 0, ext_sims = 0, ext_bs = 0, ext_flushes_done = 0;
     double ext_c = 0;

@@ -124,3 +124,53 @@ class HostValue:
             states = [zb.from_zc(int(r[0]), int(r[1]), int(r[2]) & 1) for r in rows[i * bs: i * bs + k]]
             out[i * bs: i * bs + k] = [float(v) for v in self.value.batch(states, backend=self.backend)]
         return torch.from_numpy(out).to(leaves.device)
+
+
+class ChessValuedSearch:
+    """Stepwise chess search (zc_chess_ext_*): the configs/chess_value.yaml path — a value
+    network evaluates every flush's leaves (planes [n*bs, 17, 8, 8]) between the select and
+    backup kernels.  Same protocol and value_fn contract as C4ValuedSearch."""
+
+    def __init__(self, eng: "_native.NativeEngine", n_games: int, batch_size: int = 32,
+                 planes_dtype: torch.dtype = torch.float16, leaves: bool = True, planes: bool = True,
+                 policy: int = _native.ZC_POLICY_RANDOM, freedom: float = 0.0):
+        if batch_size > eng.max_batch:
+            raise ValueError(f"batch_size {batch_size} > engine max_batch {eng.max_batch}")
+        if n_games > eng.max_games:
+            raise ValueError(f"{n_games} games > engine capacity {eng.max_games}")
+        self.eng, self.n, self.bs, self.policy, self.freedom = eng, n_games, batch_size, policy, freedom
+        self.dev = torch.device("cuda", eng.device)
+        L = n_games * batch_size
+        self.leaves = torch.zeros((L, 72), dtype=torch.uint8, device=self.dev) if leaves else None
+        self.planes = torch.zeros((L, 17, 8, 8), dtype=planes_dtype, device=self.dev) if planes else None
+        self.counts = torch.zeros(n_games, dtype=torch.int32, device=self.dev)
+        self.values = torch.zeros(L, dtype=torch.float64, device=self.dev)
+        self.move = torch.zeros(n_games, dtype=torch.int16, device=self.dev)
+        self.na = torch.zeros((n_games, _native.CHESS_MAX_MOVES), dtype=torch.int32, device=self.dev)
+        self.stats = torch.zeros((n_games, _native.STATS_FIELDS), dtype=torch.int64, device=self.dev)
+
+    def enqueue(self, roots: torch.Tensor, sims: int, c: float, value_fn, first_game: int = 0):
+        if roots.shape != (self.n, 72) or roots.dtype != torch.uint8 or not roots.is_contiguous():
+            raise ValueError("roots must be a contiguous uint8 [n_games, 72] tensor of zc_chess_state rows")
+        e, n = self.eng, self.n
+        p = lambda t: t.data_ptr() if t is not None else 0  # noqa: E731
+        e.chess_ext_begin(first_game, n, roots.data_ptr(), sims, c, self.bs, self.policy, self.freedom,
+                          _stream(self.dev))
+        for f in range((sims + self.bs - 1) // self.bs):
+            e.chess_ext_select(first_game, n, f, p(self.leaves), p(self.planes),
+                               self.planes is None or self.planes.dtype == torch.float16, self.counts.data_ptr(),
+                               _stream(self.dev))
+            v = value_fn(self.leaves, self.planes, self.counts)
+            if v is not self.values:
+                self.values.copy_(v.reshape(-1))
+            e.chess_ext_backup(first_game, n, f, self.values.data_ptr(), _stream(self.dev))
+        e.chess_ext_end(first_game, n, self.move.data_ptr(), self.na.data_ptr(), self.stats.data_ptr(),
+                        _stream(self.dev))
+        return self.move, self.na, self.stats
+
+    def run(self, roots: torch.Tensor, sims: int, c: float, value_fn, first_game: int = 0):
+        self.enqueue(roots, sims, c, value_fn, first_game)
+        torch.cuda.current_stream(self.dev).synchronize()
+        return self.move, self.na, self.stats
+
+    capture = C4ValuedSearch.capture
