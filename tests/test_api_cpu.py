@@ -62,10 +62,12 @@ def test_engine_surface_without_gpu():
 def test_unsupported_plugins_fail_loudly():
     from zeroclone_amd.engine import Policy, Value, mcts
     with pytest.raises(NotImplementedError):
-        Value("network_latest", model_type="chess_value")
+        Value("mystery_value")
     v = Value("random_rollout")
     with pytest.raises(NotImplementedError):
-        mcts.get_move(c4.create_init_state(), v, Policy("immediate_value"), c4, 10)
+        mcts.get_move(c4.create_init_state(), v, Policy("mystery_policy"), c4, 10)
+    with pytest.raises(NotImplementedError):   # chess value on a Connect4 game
+        mcts.get_move(c4.create_init_state(), Value("crude_chess_score"), Policy("random"), c4, 10)
 
     class Other:
         __name__ = "chess_backend"

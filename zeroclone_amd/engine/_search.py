@@ -1,0 +1,135 @@
+"""Dispatch of a batched search to the right device path, by game and plugin kind.
+
+    game      value object                         device path
+    connect4  Value('random_rollout')              zc_c4_search_games (fused rollouts)
+    connect4  network Value / any .batch object    zc_c4_ext_* + NetValue / HostValue
+    chess     Value('crude_chess_score')           zc_chess_search_async (value in-kernel)
+    chess     network Value / any .batch object    zc_chess_ext_* + NetValue / HostValue
+
+Policy('random') and Policy('immediate_value', policy_freedom=f) run on the device for
+chess; Connect4 moves carry no capture value, so for Connect4 immediate_value picks among
+all untried moves exactly like random (policy_functions.py:14-17 with all values 0) and both
+map to the same device policy.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from .. import _native
+
+
+def game_of(backend, state) -> str:
+    g = getattr(backend, "ZC_GAME", None)
+    if g:
+        return g
+    name = getattr(backend, "__name__", "") or type(backend).__name__
+    if name.endswith("c4_backend"):
+        return "connect4"
+    if name.endswith("chess_backend"):
+        return "chess"
+    if hasattr(state, "fifty_move_rule_counter"):
+        return "chess"
+    from .games.connect4 import c4_backend as c4
+    if c4.is_state(state):
+        return "connect4"
+    raise NotImplementedError(f"backend {name!r}: only Connect4 and chess run on the MI355X search path")
+
+
+def policy_of(policy):
+    name = getattr(policy, "name", None) or "random"
+    if name == "random":
+        return _native.ZC_POLICY_RANDOM, 0.0
+    if name == "immediate_value":
+        return _native.ZC_POLICY_IMMEDIATE_VALUE, float(getattr(policy, "args", {}).get("policy_freedom", 0))
+    raise NotImplementedError(f"policy {name!r}: only Policy('random') and Policy('immediate_value') run on the GPU")
+
+
+def value_kind(value) -> str:
+    name = getattr(value, "name", None)
+    if name == "random_rollout" and not hasattr(value, "_req_q"):
+        return "rollout"
+    if name == "crude_chess_score":
+        return "crude"
+    if getattr(value, "zc_model", None) is not None:
+        return "net"
+    if callable(getattr(value, "batch", None)):
+        return "host"
+    raise NotImplementedError("value objects must provide .batch(states, backend=) (value_functions.py:20)")
+
+
+def chess_roots(states) -> np.ndarray:
+    from .games.chess import chess_backend as cb
+    return np.stack([cb.to_zc(s) for s in states]).astype(_native.CHESS_STATE_DTYPE)
+
+
+def chess_moves(eng, ids, states, sims, c, bs, value, policy, backend):
+    """Search chess games `ids` (engine game indices) from `states`; returns list of moves
+    ((fr, fc, tr, tc), capture_value), None for a game with no legal move."""
+    import torch
+    pol, freedom = policy_of(policy)
+    kind = value_kind(value)
+    n = len(ids)
+    dev = torch.device("cuda", eng.device)
+    first = int(ids[0])
+    if list(ids) != list(range(first, first + n)):
+        raise ValueError("chess searches take a contiguous range of engine games")
+    roots = torch.from_numpy(chess_roots(states).view(np.uint8).reshape(n, 72).copy()).to(dev)
+    if kind == "crude":
+        mv = torch.zeros(n, dtype=torch.int16, device=dev)
+        na = torch.zeros((n, _native.CHESS_MAX_MOVES), dtype=torch.int32, device=dev)
+        st = torch.zeros((n, _native.STATS_FIELDS), dtype=torch.int64, device=dev)
+        s = torch.cuda.current_stream(dev).cuda_stream
+        eng.chess_search_async(first, n, roots.data_ptr(), sims, c, bs, pol, freedom,
+                               mv.data_ptr(), na.data_ptr(), st.data_ptr(), s)
+        torch.cuda.current_stream(dev).synchronize()
+    else:
+        from ..valued import ChessValuedSearch, NetValue
+        vs = ChessValuedSearch(eng, n, bs, policy=pol, freedom=freedom, planes=(kind == "net"))
+        fn = NetValue(value.zc_model) if kind == "net" else _ChessHostValue(value, backend)
+        mv, na, st = vs.run(roots, sims, c, fn, first_game=first)
+    st = st.cpu().numpy()
+    bad = st[:, 5]
+    if (bad == _native.ZC_STATUS_CAPACITY).any():
+        raise RuntimeError("chess search exceeded the tree's child-slot pool or depth limit")
+    mv = mv.cpu().numpy().view(np.uint16)
+    return [None if m == 0xFFFF else _native.unpack_chess_move(m) for m in mv]
+
+
+class _ChessHostValue:
+    def __init__(self, value, backend):
+        self.value, self.backend = value, backend
+
+    def __call__(self, leaves, planes, counts):
+        import torch
+        from .games.chess import chess_backend as cb
+        rows = leaves.cpu().numpy()
+        cnt = counts.cpu().numpy()
+        bs = rows.shape[0] // cnt.shape[0]
+        out = np.zeros(rows.shape[0], np.float64)
+        for i, k in enumerate(cnt):
+            if k:
+                states = [cb.from_zc(r.view(_native.CHESS_STATE_DTYPE)[0]) for r in rows[i * bs: i * bs + k]]
+                out[i * bs: i * bs + k] = [float(v) for v in self.value.batch(states, backend=self.backend)]
+        return torch.from_numpy(out).to(leaves.device)
+
+
+def c4_moves(eng, ids, roots, sims, c, bs, value, backend):
+    """Connect4: fused rollouts for Value('random_rollout'), stepwise otherwise."""
+    kind = value_kind(value)
+    if kind == "rollout":
+        mv, _, st = eng.c4_search_games(ids, roots, sims, c, bs)
+        return [(int(m), 0) for m in mv]
+    import torch
+    from ..valued import C4ValuedSearch, HostValue, NetValue
+    n = len(ids)
+    first = int(ids[0])
+    if list(ids) != list(range(first, first + n)):
+        raise ValueError("stepwise searches take a contiguous range of engine games")
+    vs = C4ValuedSearch(eng, n, bs, planes=(kind == "net"))
+    r = torch.from_numpy(roots.view(np.int64).reshape(n, 3).copy()).to(vs.dev)
+    fn = NetValue(value.zc_model) if kind == "net" else HostValue(value, backend)
+    mv, _, st = vs.run(r, sims, c, fn, first_game=first)
+    st = st.cpu().numpy()
+    if st[:, 5].any():
+        raise ValueError(f"invalid root for the search (status {int(st[:, 5].max())})")
+    return [(int(m), 0) for m in mv.cpu().numpy()]

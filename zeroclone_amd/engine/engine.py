@@ -13,6 +13,8 @@ all deliberate and documented in DESIGN.md:
   game in index order — the reference's serial behaviour.
 * `play_move` accepts Connect4 moves: the reference's `_is_legal` unpacks `mv[0]` as a chess
   4-tuple and raises TypeError for `(col, 0)` (engine.py:155-157).
+* Chess games search on the device too (crude_chess_score in-kernel; network values between
+  the select and backup kernels); the game's move histories stay on the host State.
 """
 from __future__ import annotations
 
@@ -152,26 +154,55 @@ class Engine:
         except (TypeError, IndexError):
             return False
 
-    def _check_search_plugins(self):
-        from .mcts import _plugin_check
-        _plugin_check(self.states[0], self.values[0], self.policy, self.backend)
-        if any(getattr(v, "name", None) != "random_rollout" for v in self.values):
-            raise NotImplementedError("both value functions must be Value('random_rollout') on the GPU path")
-
     def _search(self, idxs, simulations, c, batch_size):
-        self._check_search_plugins()
-        roots = _device.c4_roots([self.states[i] for i in idxs], self.backend)
+        from . import _search
+        from .mcts import _plugin_check, get_move
+        game = None
+        for v in {id(v): v for v in self.values}.values():
+            game = _plugin_check(self.states[idxs[0]], v, self.policy, self.backend)
         if self.rng_mode == "global":
-            from .mcts import get_move
             return {i: get_move(self.states[i], self.values[self.states[i].turn], self.policy, self.backend,
                                 simulations, c, batch_size) for i in idxs}
         need = max(idxs) + 1
         if self._dev is None:
             self._dev = _device.GrowingEngine(max(need, 64), simulations, batch_size, self.device)
+        moves = {}
         with self._dev.lock:
             eng = self._dev.ensure(need, simulations, batch_size)
             if need > self._seeded:
                 eng.seed(self._seeded, [self.seed + g for g in range(self._seeded, need)])
                 self._seeded = need
-            mv, _, _ = eng.c4_search_games(idxs, roots, simulations, c, batch_size)
-        return {i: (int(m), 0) for i, m in zip(idxs, mv)}
+            # Engine.play_mcts uses values[state.turn] (engine.py:126): one device search per
+            # value object, over contiguous runs of game indices
+            groups = {}
+            for i in sorted(idxs):
+                v = self.values[self.states[i].turn]
+                groups.setdefault(id(v), (v, []))[1].append(i)
+            for value, ids in groups.values():
+                if game == "connect4" and _search.value_kind(value) == "rollout":
+                    roots = _device.c4_roots([self.states[i] for i in ids], self.backend)
+                    moves.update(zip(ids, _search.c4_moves(eng, ids, roots, simulations, c, batch_size, value,
+                                                           self.backend)))
+                    continue
+                for run in _runs(ids):
+                    st = [self.states[i] for i in run]
+                    if game == "connect4":
+                        mv = _search.c4_moves(eng, run, _device.c4_roots(st, self.backend), simulations, c,
+                                              batch_size, value, self.backend)
+                    else:
+                        mv = _search.chess_moves(eng, run, st, simulations, c, batch_size, value, self.policy,
+                                                 self.backend)
+                    moves.update(zip(run, mv))
+        return moves
+
+
+def _runs(ids):
+    out, cur = [], [ids[0]]
+    for i in ids[1:]:
+        if i == cur[-1] + 1:
+            cur.append(i)
+        else:
+            out.append(cur)
+            cur = [i]
+    out.append(cur)
+    return out

@@ -1,27 +1,41 @@
 """Leaf evaluators with the reference's interface (engine/value_functions.py:8-130).
 
-`Value('random_rollout')` runs on the GPU: `batch(states, backend=)` rolls the states out
-in order on one CPython-compatible MT19937 stream taken from (and returned to) Python's
-global `random` module — the same numbers, consumed in the same order, as the reference's
-`[self(s) for s in states]` (value_functions.py:20-22, 35-45).  Inside `mcts.get_move` /
-`Engine` the value object is not called at all: its name selects the fused on-device
-rollout of the search kernel.
+Inside `mcts.get_move` / `Engine` the value object selects the device path (_search.py):
+`random_rollout` (Connect4) and `crude_chess_score` (chess) are evaluated inside the search
+kernels; the network modes hand the device-built leaf planes to the model between the
+select and backup kernels.  Called directly, `Value` behaves as the reference's:
+
+* `random_rollout`: `batch(states, backend=)` rolls the states out IN ORDER on the GPU on a
+  CPython-compatible MT19937 stream taken from (and returned to) Python's global `random`
+  — the numbers the reference's `[self(s) for s in states]` would draw (:20-22, 35-45).
+* `crude_chess_score` (:48-55): 1000 if check_win(state), else (turn*-2+1) * material.
+* `network_latest` / `network_at_path` (:61-130): the reference's ValueNetwork template
+  (zeroclone_amd.nets) for `model_type` (chess_value: 17 planes; connect4: 2 planes), in fp16
+  on the GPU; weights from `path` / models/<model_type>/latest.pth when present (state_dict,
+  loaded with weights_only=True), else the random init, as the reference.
 """
 from __future__ import annotations
 
+import os
+
 from . import _device
 
-SUPPORTED = ("random_rollout",)
+SUPPORTED = ("random_rollout", "crude_chess_score", "network_latest", "network_at_path")
+_PIECES = {"P": 1, "N": 3, "B": 3, "R": 5, "Q": 9, "p": -1, "n": -3, "b": -3, "r": -5, "q": -9}
+MODEL_PLANES = {"chess_value": 17, "connect4_value": 2}
 
 
 class Value:
     def __init__(self, name, **kwargs):
         self.name = name
         self.init_args = kwargs
+        self.zc_model = None
         if name not in SUPPORTED:
             raise NotImplementedError(
-                f"value function {name!r} is not implemented on the MI355X path yet "
-                f"(supported: {', '.join(SUPPORTED)}); see DESIGN.md 'Out of scope / next'")
+                f"value function {name!r} is not implemented on the MI355X path "
+                f"(supported: {', '.join(SUPPORTED)}); see DESIGN.md")
+        if name.startswith("network"):
+            self._init_network()
 
     def __call__(self, state, **kwargs):
         return self.batch([state], **kwargs)[0]
@@ -30,6 +44,7 @@ class Value:
         backend = (self.init_args | kwargs).get("backend")
         return getattr(self, self.name)(list(states), backend)
 
+    # ---------------------------------------------------------------- random_rollout
     def random_rollout(self, states, backend):
         if getattr(backend, "ZC_GAME", None) != "connect4" and not _looks_like_c4(backend, states):
             raise NotImplementedError("random_rollout is implemented for the Connect4 backend only")
@@ -45,6 +60,43 @@ class Value:
             mt, idx = eng.get_rng_state(0)
             _device.set_python_random_state(mt, idx, ver, gauss)
         return [int(v) for v in vals]
+
+    # ---------------------------------------------------------------- crude_chess_score
+    def crude_chess_score(self, states, backend):
+        out = []
+        for s in states:
+            if backend.check_win(s):
+                out.append(1000)
+                continue
+            factor = s.turn * -2 + 1
+            out.append(factor * sum(_PIECES.get(chr(p), 0) for p in s.board))
+        return out
+
+    # ---------------------------------------------------------------- network modes
+    def _init_network(self):
+        import torch
+        from ..nets import ValueNetwork, for_inference
+        mt = self.init_args.get("model_type", "chess_value")
+        net = ValueNetwork(in_planes=MODEL_PLANES.get(mt, 17))
+        path = self.init_args.get("path") if self.name == "network_at_path" else \
+            os.path.join("models", mt, "latest.pth")
+        if path and os.path.exists(path):
+            sd = torch.load(path, map_location="cpu", weights_only=True)
+            net.load_state_dict(sd.state_dict() if hasattr(sd, "state_dict") else sd)
+        self.zc_model = for_inference(net.eval(), "cuda", torch.float16)
+        self.batch_size = self.init_args.get("batch_size", 1)
+
+    def _network(self, states, backend):
+        import numpy as np
+        import torch
+        if not states:
+            return []
+        x = torch.from_numpy(np.stack([backend.state_to_tensor(s) for s in states]).astype(np.float32))
+        with torch.no_grad():
+            return [float(v) for v in self.zc_model(x.cuda().half()).float().reshape(-1).cpu()]
+
+    network_latest = _network
+    network_at_path = _network
 
 
 def _looks_like_c4(backend, states):
