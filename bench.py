@@ -86,10 +86,59 @@ def net_mode(games: int, sims: int, bs: int, c: float, steps: int, dev) -> dict:
     eng.close()
     return {"value": round(exp / dt, 1), "unit": "expansions/s", "ms_per_move": round(dt / steps * 1e3, 1),
             "net": "ValueNetwork(128, 8, in_planes=2) random init, fp16, BN folded, channels-last (MIOpen)",
-            "net_tflops_upper": round(fl / dt / 1e12, 1),
-            "mfma_frac_upper": round(fl / dt / 1e12 / MFMA_F16_PEAK_TFLOPS, 4),
+            "net_tflops_lower": round(fl / dt / 1e12, 1),
+            "mfma_frac_lower": round(fl / dt / 1e12 / MFMA_F16_PEAK_TFLOPS, 4),
             "note": "TFLOP/s = network FLOPs / whole move time (search kernels included), so a lower bound "
                     "on the network's own rate; stepwise search, per-flush leaf planes built on the device"}
+
+
+def chess_modes(steps: int, dev) -> dict:
+    """BASELINE configs[3] (C4): chess, 1024 games, 400 sims/move — the crude-score search
+    (configs/crude_chess.yaml, value in the kernel) and the value-network search
+    (configs/chess_value.yaml: ValueNetwork(128, 8) random init, fp16, one move per HIP graph)."""
+    import numpy as np
+    from zeroclone_amd.nets import ValueNetwork, flops_per_position, for_inference
+    from zeroclone_amd.valued import ChessValuedSearch, NetValue
+    G, S, B = 1024, 400, 32
+    eng = _native.NativeEngine(max_games=G, max_sims=S, max_batch=B, device=dev.index)
+    eng.seed(0, list(range(G)))
+    rows = np.array([_native.chess_init()] * G, _native.CHESS_STATE_DTYPE).view(np.uint8).reshape(G, 72)
+    roots = torch.from_numpy(rows.copy()).to(dev)
+    mv = torch.zeros(G, dtype=torch.int16, device=dev)
+    na = torch.zeros((G, _native.CHESS_MAX_MOVES), dtype=torch.int32, device=dev)
+    st = torch.zeros((G, _native.STATS_FIELDS), dtype=torch.int64, device=dev)
+    s = torch.cuda.current_stream(dev).cuda_stream
+    crude = lambda: eng.chess_search_async(0, G, roots.data_ptr(), S, 1.4, B, _native.ZC_POLICY_IMMEDIATE_VALUE,  # noqa
+                                           3.0, mv.data_ptr(), na.data_ptr(), st.data_ptr(), s)
+    crude()
+    torch.cuda.synchronize(dev)
+    t = time.perf_counter()
+    exp = 0
+    for _ in range(steps):
+        crude()
+        exp += int(st[:, 0].sum().item())
+    dt = time.perf_counter() - t
+    out = {"crude": {"value": round(exp / dt, 1), "unit": "expansions/s", "ms_per_move": round(dt / steps * 1e3, 2),
+                     "config": "1024 games x 400 sims, crude_chess_score, immediate_value(3), from the opening"}}
+    torch.manual_seed(0)
+    model = for_inference(ValueNetwork(128, 8).eval(), dev, torch.float16)
+    vs = ChessValuedSearch(eng, G, B, leaves=False)
+    g = vs.capture(roots, S, 1.4, NetValue(model))
+    g.replay()
+    torch.cuda.synchronize(dev)
+    t = time.perf_counter()
+    exp = 0
+    for _ in range(steps):
+        g.replay()
+        exp += int(vs.stats[:, 0].sum().item())
+    dt = time.perf_counter() - t
+    fl = flops_per_position(128, 8, 17, 8, 8) * G * B * ((S + B - 1) // B) * steps
+    out["value_net"] = {"value": round(exp / dt, 1), "unit": "expansions/s", "ms_per_move": round(dt / steps * 1e3, 1),
+                        "config": "1024 games x 400 sims, ValueNetwork(128, 8) random init fp16, random policy",
+                        "net_tflops_lower": round(fl / dt / 1e12, 1),
+                        "mfma_frac_lower": round(fl / dt / 1e12 / MFMA_F16_PEAK_TFLOPS, 4)}
+    eng.close()
+    return out
 
 
 def main():
@@ -221,6 +270,7 @@ def main():
         }
         if world == 1 and args.net_steps > 0:
             out["extra"]["c2_value_net"] = net_mode(G, S, B, args.c, args.net_steps, dev)
+            out["extra"]["c4_chess"] = chess_modes(args.net_steps, dev)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(S, B, args.c)
         else:

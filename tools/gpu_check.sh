@@ -22,9 +22,9 @@ for st in "$@"; do
             if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi ;;
     smoke)  run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit $? ;;
     bench)  run bench 900 python bench.py || exit $? ;;
-    benchq) run benchq 600 python bench.py --steps 3 --warmup 1 --no-cpu-baseline || exit $? ;;
+    benchq) run benchq 600 python bench.py --steps 3 --warmup 1 --no-cpu-baseline --net-steps 0 || exit $? ;;
     prof)   run prof 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv \
-                -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline || exit $? ;;
+                -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --net-steps 0 || exit $? ;;
     diag)   run diag 600 python tools/diag_c4.py || exit $? ;;
     pmc)    run pmc 600 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/pmc -o pmc \
                 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY \
