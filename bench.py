@@ -85,7 +85,7 @@ def net_mode(games: int, sims: int, bs: int, c: float, steps: int, dev) -> dict:
     fl = flops_per_position(128, 8, 2, 6, 7) * games * bs * flushes * steps
     eng.close()
     return {"value": round(exp / dt, 1), "unit": "expansions/s", "ms_per_move": round(dt / steps * 1e3, 1),
-            "net": "ValueNetwork(128, 8, in_planes=2) random init, fp16, BN folded, channels-last (MIOpen)",
+            "net": "ValueNetwork(128, 8, in_planes=2) random init, fp16, BN folded, this package's MFMA conv kernels",
             "net_tflops_lower": round(fl / dt / 1e12, 1),
             "mfma_frac_lower": round(fl / dt / 1e12 / MFMA_F16_PEAK_TFLOPS, 4),
             "note": "TFLOP/s = network FLOPs / whole move time (search kernels included), so a lower bound "
@@ -134,7 +134,7 @@ def chess_modes(steps: int, dev) -> dict:
     dt = time.perf_counter() - t
     fl = flops_per_position(128, 8, 17, 8, 8) * G * B * ((S + B - 1) // B) * steps
     out["value_net"] = {"value": round(exp / dt, 1), "unit": "expansions/s", "ms_per_move": round(dt / steps * 1e3, 1),
-                        "config": "1024 games x 400 sims, ValueNetwork(128, 8) random init fp16, random policy",
+                        "config": "1024 games x 400 sims, ValueNetwork(128, 8) random init fp16 (MFMA kernels), random policy",
                         "net_tflops_lower": round(fl / dt / 1e12, 1),
                         "mfma_frac_lower": round(fl / dt / 1e12 / MFMA_F16_PEAK_TFLOPS, 4)}
     eng.close()

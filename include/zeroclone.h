@@ -249,6 +249,24 @@ int zc_chess_ext_backup(zc_engine *eng, int32_t first_game, int32_t n_games, int
 int zc_chess_ext_end(zc_engine *eng, int32_t first_game, int32_t n_games, uint16_t *d_out_move,
                      int32_t *d_out_root_na, zc_game_stats *d_out_stats, void *hip_stream);
 
+/* ---- Value-network layers on the matrix cores (models/chess_value/network.py:24-45) -----
+ * The residual tower of ValueNetwork with BatchNorm folded into the convolutions, NHWC fp16
+ * activations ([n][h][w][c], a pixel's channels contiguous), 128 output channels.
+ *   zc_net_conv3x3_async: out = act(conv3x3(in, weight) + bias (+ residual)), padding 1;
+ *     weight [9][128][cin] fp16 (tap = ky*3+kx, then output channel, then input channel),
+ *     bias [128] f32, residual NULL or [n][h][w][128] fp16, relu 0/1.  Shapes: (h, w) in
+ *     {(8, 8), (6, 7)}, cin in {32, 128}; others are ZC_EINVAL.
+ *   zc_net_planes_to_nhwc_async: state_to_tensor planes [n][cin][h*w] fp16 -> [n][h*w][cpad].
+ *   zc_net_value_head_async: mean over pixels -> dot(fc_w[128]) + fc_b -> tanh, as fp64
+ *     values[n] (the input of zc_*_ext_backup).
+ * Device pointers, enqueued on hip_stream (NULL = null stream); no engine needed. */
+int zc_net_conv3x3_async(int32_t n_boards, int32_t h, int32_t w, int32_t cin, const void *d_in, const void *d_weight,
+                         const float *d_bias, const void *d_residual, void *d_out, int32_t relu, void *hip_stream);
+int zc_net_planes_to_nhwc_async(int32_t n, int32_t cin, int32_t hw, int32_t cpad, const void *d_planes, void *d_out,
+                                void *hip_stream);
+int zc_net_value_head_async(int32_t n, int32_t hw, const void *d_act, const float *d_fc_w, float fc_b, double *d_values,
+                            void *hip_stream);
+
 /* ---- self-test hooks (used by the parity tests) -------------------------------------
  * UCT score exactly as the search kernel computes it (mcts.cpp:41-45), evaluated ON THE
  * DEVICE for n inputs: out[i] = na[i]==0 ? +inf : fma(c, sqrt(logn[i]/na[i]), q[i]). */

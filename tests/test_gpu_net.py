@@ -1,0 +1,59 @@
+"""The value network on this package's MFMA kernels (csrc/net_conv.hip) against the same
+folded network in PyTorch fp32 on the GPU (tolerance: fp16 activations and weights,
+fp32 accumulation)."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _net(in_planes, seed, channels=128, blocks=8):
+    from zeroclone_amd.nets import ValueNetwork
+    torch.manual_seed(seed)
+    net = ValueNetwork(channels, blocks, in_planes=in_planes)
+    for m in net.modules():   # non-trivial folded BN
+        if isinstance(m, torch.nn.BatchNorm2d):
+            m.running_mean.uniform_(-0.1, 0.1)
+            m.running_var.uniform_(0.5, 1.5)
+            m.weight.data.uniform_(0.5, 1.5)
+            m.bias.data.uniform_(-0.1, 0.1)
+    return net.eval()
+
+
+@pytest.mark.parametrize("shape", [(17, 8, 8), (2, 6, 7)])
+@pytest.mark.parametrize("n", [1, 7, 301])
+def test_mfma_network_matches_torch(shape, n):
+    from zeroclone_amd.nets import FoldedValueNetwork, MfmaValueNetwork
+    c, h, w = shape
+    net = _net(c, seed=n)
+    ref = FoldedValueNetwork(net).cuda().float().eval()
+    x = (torch.rand(n, c, h, w, device="cuda") < 0.3).half()
+    with torch.no_grad():
+        want = ref(x.float()).reshape(-1).double()
+    got = MfmaValueNetwork(net)(x).clone()
+    torch.cuda.synchronize()
+    assert got.dtype == torch.float64 and got.shape == (n,)
+    np.testing.assert_allclose(got.cpu().numpy(), want.cpu().numpy(), rtol=0, atol=2e-2)
+
+
+def test_single_conv_layer_exactness():
+    """One conv layer with small-integer data is exact in fp32 accumulation: checks the
+    MFMA operand/accumulator layouts, the tap shifts and the board edges bit for bit."""
+    from zeroclone_amd import _native
+    L = _native.lib()
+    for (h, w, cin) in [(8, 8, 128), (6, 7, 32), (8, 8, 32), (6, 7, 128)]:
+        n = 13
+        g = torch.Generator().manual_seed(h * 100 + cin)
+        x = torch.randint(-2, 3, (n, h, w, cin), generator=g).half().cuda()
+        wt = torch.randint(-2, 3, (128, cin, 3, 3), generator=g).float()
+        bias = torch.randint(-3, 4, (128,), generator=g).float().cuda()
+        res = torch.randint(-2, 3, (n, h, w, 128), generator=g).half().cuda()
+        wk = wt.permute(2, 3, 0, 1).reshape(9, 128, cin).contiguous().half().cuda()
+        out = torch.empty((n, h, w, 128), dtype=torch.float16, device="cuda")
+        _native.check(L.zc_net_conv3x3_async(n, h, w, cin, x.data_ptr(), wk.data_ptr(), bias.data_ptr(),
+                                             res.data_ptr(), out.data_ptr(), 1, None))
+        torch.cuda.synchronize()
+        ref = torch.nn.functional.conv2d(x.permute(0, 3, 1, 2).float().cpu(), wt, bias.cpu(), padding=1)
+        ref = torch.relu(ref + res.permute(0, 3, 1, 2).float().cpu()).permute(0, 2, 3, 1)
+        assert torch.equal(out.float().cpu(), ref), (h, w, cin)

@@ -36,22 +36,26 @@ def main():
     ap.add_argument("--find", action="store_true", help="MIOpen exhaustive kernel search (cudnn.benchmark)")
     ap.add_argument("--nchw", action="store_true")
     ap.add_argument("--net-only", action="store_true")
+    ap.add_argument("--mfma", action="store_true", help="this package's MFMA conv kernels instead of MIOpen")
+    ap.add_argument("--planes", type=int, default=2)
+    ap.add_argument("--hw", default="6x7")
     a = ap.parse_args()
     torch.backends.cudnn.benchmark = a.find
     torch.manual_seed(0)
-    net = ValueNetwork(a.channels, a.blocks, in_planes=2).eval()
-    model = for_inference(net, "cuda", torch.float16)
+    H, W = (int(v) for v in a.hw.split("x"))
+    net = ValueNetwork(a.channels, a.blocks, in_planes=a.planes).eval()
+    model = for_inference(net, "cuda", torch.float16, backend="mfma" if a.mfma else "torch")
     if a.nchw:
         model = model.to(memory_format=torch.contiguous_format)
         model.forward = lambda x, m=model: _nchw_forward(m, x)
     eng = _native.NativeEngine(max_games=a.games, max_sims=a.sims, max_batch=a.bs)
     eng.seed(0, list(range(a.games)))
     vs = C4ValuedSearch(eng, a.games, a.bs, leaves=False)
-    value = NetValue(model)
+    value = NetValue(model) if not a.mfma else (lambda leaves, planes, counts: model(planes))
     roots = torch.zeros((a.games, 3), dtype=torch.int64, device="cuda")
     L = a.games * a.bs
     # network alone
-    x = (torch.rand(L, 2, 6, 7, device="cuda") < 0.3).half()
+    x = (torch.rand(L, a.planes, H, W, device="cuda") < 0.3).half()
     with torch.no_grad():
         for _ in range(2):
             model(x)
@@ -61,7 +65,7 @@ def main():
             model(x)
         torch.cuda.synchronize()
         net_ms = (time.perf_counter() - t) / 5 * 1e3
-    fl = flops_per_position(a.channels, a.blocks, 2, 6, 7)
+    fl = flops_per_position(a.channels, a.blocks, a.planes, H, W)
     out = {"net_ms_per_flush": round(net_ms, 3), "positions_per_flush": L,
            "net_tflops": round(fl * L / net_ms / 1e9, 1), "flops_per_position": fl}
     if a.net_only:

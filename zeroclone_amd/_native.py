@@ -114,6 +114,13 @@ SIGNATURES = [
                                            ctypes.c_void_p, ctypes.c_void_p]),
     ("zc_chess_ext_end", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p,
                                         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    ("zc_net_conv3x3_async", ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                            ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p]),
+    ("zc_net_planes_to_nhwc_async", ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                                   ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    ("zc_net_value_head_async", ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p,
+                                               ctypes.c_float, ctypes.c_void_p, ctypes.c_void_p]),
     ("zc_chess_from_fen", ctypes.c_int, [ctypes.c_char_p, ctypes.c_void_p]),
     ("zc_chess_init", ctypes.c_int, [ctypes.c_void_p]),
     ("zc_c4_from_rows", ctypes.c_int, [ctypes.c_char_p, ctypes.c_int32, P(C4State)]),

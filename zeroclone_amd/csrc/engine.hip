@@ -700,6 +700,36 @@ int zc_chess_ext_end(zc_engine *eng, int32_t first, int32_t n, uint16_t *d_move,
     return ZC_OK;
 }
 
+// ---------------------------------------------------------------- value-network layers
+int zc_net_conv3x3_async(int32_t n, int32_t h, int32_t w, int32_t cin, const void *d_in, const void *d_weight,
+                         const float *d_bias, const void *d_residual, void *d_out, int32_t relu, void *hip_stream) {
+    if (n < 0 || (n && (!d_in || !d_weight || !d_bias || !d_out))) return fail(ZC_EINVAL, "bad argument");
+    if (!n) return ZC_OK;
+    if (!zc::launch_net_conv3x3(n, h, w, cin, d_in, d_weight, d_bias, d_residual, d_out, relu ? 1 : 0,
+                                (hipStream_t)hip_stream))
+        return fail(ZC_EINVAL, "conv3x3 shape (h %d, w %d, cin %d) not supported", h, w, cin);
+    ZC_HIP(hipGetLastError());
+    return ZC_OK;
+}
+
+int zc_net_planes_to_nhwc_async(int32_t n, int32_t cin, int32_t hw, int32_t cpad, const void *d_planes, void *d_out,
+                                void *hip_stream) {
+    if (n < 0 || cin < 1 || hw < 1 || cpad < cin || (n && (!d_planes || !d_out))) return fail(ZC_EINVAL, "bad argument");
+    if (!n) return ZC_OK;
+    zc::launch_net_planes_to_nhwc(n, cin, hw, cpad, d_planes, d_out, (hipStream_t)hip_stream);
+    ZC_HIP(hipGetLastError());
+    return ZC_OK;
+}
+
+int zc_net_value_head_async(int32_t n, int32_t hw, const void *d_act, const float *d_fc_w, float fc_b,
+                            double *d_values, void *hip_stream) {
+    if (n < 0 || hw < 1 || (n && (!d_act || !d_fc_w || !d_values))) return fail(ZC_EINVAL, "bad argument");
+    if (!n) return ZC_OK;
+    zc::launch_net_value_head(n, hw, d_act, d_fc_w, fc_b, d_values, (hipStream_t)hip_stream);
+    ZC_HIP(hipGetLastError());
+    return ZC_OK;
+}
+
 int zc_chess_from_fen(const char *fen, zc_chess_state *out) {
     // state_from_fen (chess_backend.cpp:525-556): placement, side, castling; en passant and
     // the full-move number are ignored; the half-move clock becomes the fifty counter.

@@ -1,0 +1,276 @@
+// net_conv.hip — the value network's residual tower on gfx950 matrix cores.
+//
+// ValueNetwork (models/chess_value/network.py:24-45) with BatchNorm folded into the
+// convolutions (zeroclone_amd/nets.py) is 17 conv3x3 layers of 128 channels on tiny boards
+// (8x8 chess, 6x7 Connect4) plus a pooled linear head.  Each layer is an implicit GEMM
+//   D[cout][pixel] = sum_{tap, cin} Wt[tap][cout][cin] * X[pixel shifted by tap][cin]
+// with M = 128 output channels, N = the pixels of a tile of boards, K = 9 taps x cin, on
+// v_mfma_f32_32x32x16_f16.  Activations are NHWC fp16 (a pixel's channels contiguous).
+//
+// One workgroup = 4 waves = one tile of BPW boards (<= 256 pixels; 4 chess boards, 6
+// Connect4 boards).  The tile's input pixels are staged ONCE in LDS (rows padded by 16 B so
+// the 32 lanes reading 32 pixels hit different banks); the 9 shifted views of a tap are
+// just different LDS rows (zero outside the board), so no im2col ever touches HBM.  The
+// weights of one tap (128 x cin) sit in one of two LDS buffers; the next tap's weights are
+// fetched into registers while the current tap computes.  Wave w owns all 128 channels x
+// 64 pixels (4 x 2 MFMA tiles): per 16-deep k-step it reads 4 weight and 2 activation
+// fragments (ds_read_b128) for 8 MFMAs, 0.75 KB of LDS per MFMA.  The epilogue adds the
+// folded-BN bias, the residual and ReLU in fp32 and stores 4 channels (8 B) per lane per
+// row group.
+#include <hip/hip_fp16.h>
+#include <hip/hip_runtime.h>
+
+#include "zc_internal.h"
+
+namespace zc {
+namespace {
+
+typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+typedef float f16x __attribute__((ext_vector_type(16)));
+
+constexpr int kCout = 128;
+constexpr int kTilePix = 256;
+
+template <int H, int W, int BPW, int CIN>
+__global__ __launch_bounds__(256) void conv3x3_kernel(int nboards, const _Float16 *__restrict__ in,
+                                                      const _Float16 *__restrict__ wt, const float *__restrict__ bias,
+                                                      const _Float16 *__restrict__ res, _Float16 *__restrict__ out,
+                                                      int relu) {
+    constexpr int HW = H * W;
+    constexpr int PIX = BPW * HW;
+    static_assert(PIX <= kTilePix, "tile too large");
+    constexpr int LD = CIN + 8;                // padded LDS row, halves
+    constexpr int C8 = CIN / 8;
+    constexpr int WCH = kCout * C8 / 256;      // 16-byte weight chunks per thread per tap
+    constexpr int NI = kTilePix * C8 / 256;    // 16-byte input chunks per thread
+    extern __shared__ __attribute__((aligned(16))) _Float16 lds[];
+    _Float16 *const sin = lds;                         // [kTilePix + 1][LD]; the last row is zero
+    _Float16 *const swb = lds + (kTilePix + 1) * LD;  // [2][kCout][LD]: weights of even / odd taps
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int b0 = blockIdx.x * BPW;
+    const int npix = min(BPW, nboards - b0) * HW;
+    const h8 zero = {0, 0, 0, 0, 0, 0, 0, 0};
+    h8 wpre[WCH];
+    {
+        // stage the tile's input and tap 0's weights: every load in flight before the first
+        // LDS store
+        h8 v[NI];
+#pragma unroll
+        for (int q = 0; q < NI; ++q) {
+            const int i = tid + q * 256, row = i / C8, c8 = i - row * C8;
+            v[q] = row < npix ? *(const h8 *)(in + ((size_t)b0 * HW + row) * CIN + c8 * 8) : zero;
+        }
+#pragma unroll
+        for (int q = 0; q < WCH; ++q) {
+            const int i = tid + q * 256, row = i / C8, c8 = i - row * C8;
+            wpre[q] = *(const h8 *)(wt + (size_t)row * CIN + c8 * 8);
+        }
+#pragma unroll
+        for (int q = 0; q < NI; ++q) {
+            const int i = tid + q * 256, row = i / C8, c8 = i - row * C8;
+            *(h8 *)(sin + row * LD + c8 * 8) = v[q];
+        }
+        if (tid < C8) *(h8 *)(sin + kTilePix * LD + tid * 8) = zero;  // the off-board row
+#pragma unroll
+        for (int q = 0; q < WCH; ++q) {
+            const int i = tid + q * 256, row = i / C8, c8 = i - row * C8;
+            *(h8 *)(swb + row * LD + c8 * 8) = wpre[q];
+        }
+    }
+
+    // wave w: all 128 output channels x pixels [64w, 64w+64) (2 tiles of 32)
+    const int r = lane & 31, hh = lane >> 5;
+    int pb[2], py[2], px[2];
+    bool pv[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+        const int P = wave * 64 + t * 32 + r;
+        pv[t] = P < npix;
+        pb[t] = P / HW;
+        const int rem = P - pb[t] * HW;
+        py[t] = rem / W;
+        px[t] = rem - py[t] * W;
+    }
+    f16x acc[4][2];
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+            for (int k = 0; k < 16; ++k) acc[m][t][k] = 0.0f;
+
+    for (int tap = 0; tap < 9; ++tap) {
+        __syncthreads();  // this tap's weights (and, at tap 0, the input tile) are in LDS
+        if (tap + 1 < 9) {
+#pragma unroll
+            for (int q = 0; q < WCH; ++q) {
+                const int i = tid + q * 256, row = i / C8, c8 = i - row * C8;
+                wpre[q] = *(const h8 *)(wt + ((size_t)(tap + 1) * kCout + row) * CIN + c8 * 8);
+            }
+        }
+        const _Float16 *sw = swb + (tap & 1) * kCout * LD;
+        const int dy = tap / 3 - 1, dx = tap % 3 - 1;
+        const _Float16 *xb[2];
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+            const int sy = py[t] + dy, sx = px[t] + dx;
+            const bool sv = pv[t] && (unsigned)sy < (unsigned)H && (unsigned)sx < (unsigned)W;
+            xb[t] = sin + (sv ? pb[t] * HW + sy * W + sx : kTilePix) * LD + hh * 8;  // off-board: zeros
+        }
+        const _Float16 *wa = sw + r * LD + hh * 8;
+        // software-pipelined k loop: the fragments of step kc+1 are read from LDS while the
+        // 8 MFMAs of step kc run (one wave per SIMD has nobody else to hide LDS latency)
+        h8 a[4], x[2], an[4], xn[2];
+#pragma unroll
+        for (int t = 0; t < 2; ++t) x[t] = *(const h8 *)(xb[t]);
+#pragma unroll
+        for (int m = 0; m < 4; ++m) a[m] = *(const h8 *)(wa + m * 32 * LD);
+#pragma unroll
+        for (int kc = 0; kc < CIN / 16; ++kc) {
+            if (kc + 1 < CIN / 16) {
+#pragma unroll
+                for (int t = 0; t < 2; ++t) xn[t] = *(const h8 *)(xb[t] + (kc + 1) * 16);
+#pragma unroll
+                for (int m = 0; m < 4; ++m) an[m] = *(const h8 *)(wa + m * 32 * LD + (kc + 1) * 16);
+            }
+#pragma unroll
+            for (int m = 0; m < 4; ++m)
+#pragma unroll
+                for (int t = 0; t < 2; ++t)
+                    acc[m][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[m], x[t], acc[m][t], 0, 0, 0);
+            if (kc + 1 < CIN / 16) {
+                // interleave: one LDS read of step kc+1 behind each MFMA of step kc
+#pragma unroll
+                for (int q = 0; q < 6; ++q) {
+                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // 1 MFMA
+                    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // 1 DS read
+                }
+                __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);      // the last 2 MFMAs
+#pragma unroll
+                for (int m = 0; m < 4; ++m) a[m] = an[m];
+#pragma unroll
+                for (int t = 0; t < 2; ++t) x[t] = xn[t];
+            }
+        }
+        if (tap + 1 < 9) {
+            _Float16 *dst = swb + ((tap + 1) & 1) * kCout * LD;
+#pragma unroll
+            for (int q = 0; q < WCH; ++q) {
+                const int i = tid + q * 256, row = i / C8, c8 = i - row * C8;
+                *(h8 *)(dst + row * LD + c8 * 8) = wpre[q];
+            }
+        }
+    }
+
+    // epilogue: D[cout][pixel], pixel = lane & 31, cout rows (reg&3) + 8*(reg>>2) + 4*hh.
+    // All residual loads are issued before any is used.
+    h4 rv[2][4][4];
+    if (res) {
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+            const int P = min(wave * 64 + t * 32 + r, max(npix - 1, 0));
+            const size_t orow = ((size_t)b0 * HW + P) * kCout;
+#pragma unroll
+            for (int m = 0; m < 4; ++m)
+#pragma unroll
+                for (int g = 0; g < 4; ++g) rv[t][m][g] = *(const h4 *)(res + orow + m * 32 + 8 * g + 4 * hh);
+        }
+    }
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+        const int P = wave * 64 + t * 32 + r;
+        const size_t orow = ((size_t)b0 * HW + P) * kCout;
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const int co = m * 32 + 8 * g + 4 * hh;
+                const float4 bb = *(const float4 *)(bias + co);
+                float v0 = acc[m][t][4 * g + 0] + bb.x, v1 = acc[m][t][4 * g + 1] + bb.y;
+                float v2 = acc[m][t][4 * g + 2] + bb.z, v3 = acc[m][t][4 * g + 3] + bb.w;
+                if (res) {
+                    v0 += (float)rv[t][m][g][0];
+                    v1 += (float)rv[t][m][g][1];
+                    v2 += (float)rv[t][m][g][2];
+                    v3 += (float)rv[t][m][g][3];
+                }
+                if (relu) {
+                    v0 = fmaxf(v0, 0.0f);
+                    v1 = fmaxf(v1, 0.0f);
+                    v2 = fmaxf(v2, 0.0f);
+                    v3 = fmaxf(v3, 0.0f);
+                }
+                h4 o;
+                o[0] = (_Float16)v0;
+                o[1] = (_Float16)v1;
+                o[2] = (_Float16)v2;
+                o[3] = (_Float16)v3;
+                if (P < npix) *(h4 *)(out + orow + co) = o;
+            }
+    }
+}
+
+// planes [n][cin][H*W] (state_to_tensor layout, fp16) -> NHWC [n][H*W][cpad], zero padded.
+__global__ void planes_to_nhwc_kernel(int n, int cin, int hw, int cpad, const _Float16 *__restrict__ planes,
+                                      _Float16 *__restrict__ out) {
+    const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= (int64_t)n * hw) return;
+    const int i = (int)(g / hw), p = (int)(g - (int64_t)i * hw);
+    _Float16 *o = out + g * cpad;
+    for (int c = 0; c < cpad; ++c) o[c] = c < cin ? planes[((size_t)i * cin + c) * hw + p] : (_Float16)0.0f;
+}
+
+// head (network.py:37-42): global average pool -> Linear(128, 1) -> tanh, in fp32; one wave
+// per position, lane l owns channels 2l and 2l+1.  Writes the fp64 value the backup takes.
+__global__ __launch_bounds__(256) void value_head_kernel(int n, int hw, const _Float16 *__restrict__ act,
+                                                         const float *__restrict__ fcw, float fcb,
+                                                         double *__restrict__ values) {
+    const int i = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+    const int lane = threadIdx.x & 63;
+    if (i >= n) return;
+    const _Float16 *a = act + (size_t)i * hw * kCout + 2 * lane;
+    float s0 = 0.0f, s1 = 0.0f;
+    for (int p = 0; p < hw; ++p) {
+        s0 += (float)a[(size_t)p * kCout];
+        s1 += (float)a[(size_t)p * kCout + 1];
+    }
+    float d = (s0 * fcw[2 * lane] + s1 * fcw[2 * lane + 1]) / (float)hw;
+    for (int o = 32; o > 0; o >>= 1) d += __shfl_xor(d, o);
+    if (lane == 0) values[i] = (double)tanhf(d + fcb);
+}
+
+template <int H, int W, int BPW, int CIN>
+void launch_conv(int n, const void *in, const void *wt, const float *bias, const void *res, void *out, int relu,
+                 hipStream_t s) {
+    const size_t lds = (size_t)(kTilePix + 1 + 2 * kCout) * (CIN + 8) * sizeof(_Float16);
+    hipLaunchKernelGGL((conv3x3_kernel<H, W, BPW, CIN>), dim3((n + BPW - 1) / BPW), dim3(256), lds, s, n,
+                       (const _Float16 *)in, (const _Float16 *)wt, bias, (const _Float16 *)res, (_Float16 *)out,
+                       relu);
+}
+
+}  // namespace
+
+bool launch_net_conv3x3(int n, int h, int w, int cin, const void *in, const void *wt, const float *bias,
+                        const void *res, void *out, int relu, hipStream_t s) {
+    if (h == 8 && w == 8 && cin == 128) launch_conv<8, 8, 4, 128>(n, in, wt, bias, res, out, relu, s);
+    else if (h == 8 && w == 8 && cin == 32) launch_conv<8, 8, 4, 32>(n, in, wt, bias, res, out, relu, s);
+    else if (h == 6 && w == 7 && cin == 128) launch_conv<6, 7, 6, 128>(n, in, wt, bias, res, out, relu, s);
+    else if (h == 6 && w == 7 && cin == 32) launch_conv<6, 7, 6, 32>(n, in, wt, bias, res, out, relu, s);
+    else return false;
+    return true;
+}
+
+void launch_net_planes_to_nhwc(int n, int cin, int hw, int cpad, const void *planes, void *out, hipStream_t s) {
+    const int64_t total = (int64_t)n * hw;
+    hipLaunchKernelGGL(planes_to_nhwc_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, n, cin, hw, cpad,
+                       (const _Float16 *)planes, (_Float16 *)out);
+}
+
+void launch_net_value_head(int n, int hw, const void *act, const float *fcw, float fcb, double *values, hipStream_t s) {
+    hipLaunchKernelGGL(value_head_kernel, dim3((unsigned)(((int64_t)n * 64 + 255) / 256)), dim3(256), 0, s, n, hw,
+                       (const _Float16 *)act, fcw, fcb, values);
+}
+
+}  // namespace zc

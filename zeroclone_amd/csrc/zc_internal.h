@@ -169,6 +169,11 @@ void launch_chess_play(int n, const zc_chess_state *in, const uint16_t *moves, z
 void launch_chess_terminal(int n, const zc_chess_state *s, int32_t *flags, hipStream_t st);
 void launch_chess_planes(int n, const zc_chess_state *s, void *planes, int f16, hipStream_t st);
 
+bool launch_net_conv3x3(int n, int h, int w, int cin, const void *in, const void *wt, const float *bias,
+                        const void *res, void *out, int relu, hipStream_t s);
+void launch_net_planes_to_nhwc(int n, int cin, int hw, int cpad, const void *planes, void *out, hipStream_t s);
+void launch_net_value_head(int n, int hw, const void *act, const float *fcw, float fcb, double *values, hipStream_t s);
+
 size_t c4_search_lds_bytes(int bs);
 void launch_c4_ext_begin(const ExtParams &p, hipStream_t s);
 void launch_c4_ext_select(const ExtParams &p, hipStream_t s);

@@ -101,6 +101,88 @@ class FoldedValueNetwork(nn.Module):
         return torch.tanh(self.fc(x))
 
 
-def for_inference(net: ValueNetwork, device, dtype=torch.float16) -> nn.Module:
+def mfma_supported(net: ValueNetwork) -> bool:
+    """Shapes the hand-written MFMA tower covers: 128 channels, <= 32 input planes."""
+    conv = net.stem[0]
+    return conv.out_channels == 128 and conv.in_channels <= 32
+
+
+def for_inference(net: ValueNetwork, device, dtype=torch.float16, backend: str = "auto"):
+    """The network as the search evaluates it.  backend "mfma" (default when the shape is
+    covered and the device is a GPU): this package's MFMA kernels (MfmaValueNetwork);
+    "torch": the folded module in fp16, channels-last, on PyTorch-ROCm (MIOpen)."""
+    use_mfma = backend == "mfma" or (backend == "auto" and dtype == torch.float16 and mfma_supported(net)
+                                     and torch.device(device).type == "cuda")
+    if use_mfma:
+        return MfmaValueNetwork(net, device)
     m = FoldedValueNetwork(net).to(device=device, dtype=dtype)
     return m.to(memory_format=torch.channels_last).eval()
+
+
+class MfmaValueNetwork:
+    """The folded ValueNetwork on this package's own MFMA kernels (csrc/net_conv.hip):
+    NHWC fp16 activations, implicit-GEMM conv3x3 on v_mfma_f32_32x32x16_f16 with the
+    bias / residual / ReLU epilogue fused, and the pooled tanh head writing fp64 values.
+    Call with state_to_tensor planes [n, in_planes, H, W] fp16 (as the stepwise search
+    exports them); returns fp64 values [n].  Buffers are cached per batch size, so a call
+    can be captured in a HIP graph."""
+
+    def __init__(self, net: ValueNetwork, device="cuda"):
+        import torch
+        f = FoldedValueNetwork(net)
+        self.dev = torch.device(device)
+        self.in_planes = f.stem.in_channels
+        self.cpad = 32
+        if self.in_planes > self.cpad or f.stem.out_channels != 128:
+            raise ValueError("MFMA path: in_planes <= 32 and 128 channels")
+        convs = [(f.stem, self.cpad)] + [(c, 128) for b in f.res for c in (b.c1, b.c2)]
+        self.w, self.b = [], []
+        for conv, cin in convs:
+            wt = conv.weight.detach().float()                      # [128][ci][3][3]
+            wp = torch.zeros(128, cin, 3, 3)
+            wp[:, : wt.shape[1]] = wt
+            self.w.append(wp.permute(2, 3, 0, 1).reshape(9, 128, cin).contiguous().to(self.dev, torch.float16))
+            self.b.append(conv.bias.detach().float().contiguous().to(self.dev))
+        self.fcw = f.fc.weight.detach().float().reshape(-1).contiguous().to(self.dev)
+        self.fcb = float(f.fc.bias.detach().float().item())
+        self._bufs = {}
+
+    def _buffers(self, n, hw):
+        import torch
+        key = (n, hw)
+        if key not in self._bufs:
+            mk = lambda c: torch.empty((n, hw, c), dtype=torch.float16, device=self.dev)  # noqa: E731
+            self._bufs[key] = (mk(self.cpad), mk(128), mk(128), mk(128),
+                               torch.empty(n, dtype=torch.float64, device=self.dev))
+        return self._bufs[key]
+
+    def __call__(self, planes):
+        import torch
+        from . import _native
+        L = _native.lib()
+        n, c, h, w = planes.shape
+        if c != self.in_planes or planes.dtype != torch.float16:
+            raise ValueError("planes must be fp16 [n, in_planes, h, w]")
+        planes = planes.contiguous()
+        hw = h * w
+        x0, a, t, b, vals = self._buffers(n, hw)
+        s = ctypes_stream(self.dev)
+        _native.check(L.zc_net_planes_to_nhwc_async(n, c, hw, self.cpad, planes.data_ptr(), x0.data_ptr(), s))
+
+        def conv(i, src, dst, res):
+            _native.check(L.zc_net_conv3x3_async(n, h, w, src.shape[2], src.data_ptr(), self.w[i].data_ptr(),
+                                                 self.b[i].data_ptr(), res.data_ptr() if res is not None else None,
+                                                 dst.data_ptr(), 1, s))
+        conv(0, x0, a, None)
+        for k in range((len(self.w) - 1) // 2):
+            conv(1 + 2 * k, a, t, None)
+            conv(2 + 2 * k, t, b, a)
+            a, b = b, a
+        _native.check(L.zc_net_value_head_async(n, hw, a.data_ptr(), self.fcw.data_ptr(), self.fcb, vals.data_ptr(), s))
+        return vals
+
+
+def ctypes_stream(dev):
+    import ctypes
+    import torch
+    return ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream or None)
