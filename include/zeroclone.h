@@ -249,6 +249,28 @@ int zc_chess_ext_backup(zc_engine *eng, int32_t first_game, int32_t n_games, int
 int zc_chess_ext_end(zc_engine *eng, int32_t first_game, int32_t n_games, uint16_t *d_out_move,
                      int32_t *d_out_root_na, zc_game_stats *d_out_stats, void *hip_stream);
 
+/* ---- Chess PUCT search (AlphaZero-style; no reference counterpart) -------
+ * Selection by Q + c_puct * P * sqrt(sum N) / (1 + N) with priors P from a policy network,
+ * virtual loss within a flush, Dirichlet(alpha) noise of weight eps on the root priors
+ * (Philox stream keyed by seed and game).  Flush 0 evaluates the root alone; then
+ * ceil((sims - 1) / batch_size) flushes of up to batch_size leaves: zc_chess_puct_flushes.
+ * select exports leaves/planes as zc_chess_ext_select; backup takes per leaf slot the value
+ * for the leaf's side to move and 4096 policy logits indexed from*64 + to (logits_dtype
+ * ZC_F32 / ZC_F16); end picks the move with the most visits (temperature 0) or samples
+ * proportionally to N^(1/temperature), and writes root visits (and, optionally, the root
+ * priors after noise, float [n][ZC_CHESS_MAX_MOVES]). */
+int zc_chess_puct_flushes(int32_t sims, int32_t batch_size);
+int zc_chess_puct_begin(zc_engine *eng, int32_t first_game, int32_t n_games, const zc_chess_state *d_roots,
+                        int32_t sims, double c_puct, int32_t batch_size, float dirichlet_alpha, float dirichlet_eps,
+                        uint64_t seed, void *hip_stream);
+int zc_chess_puct_select(zc_engine *eng, int32_t first_game, int32_t n_games, int32_t flush,
+                         zc_chess_state *d_leaves, void *d_planes, int32_t planes_dtype, int32_t *d_counts,
+                         void *hip_stream);
+int zc_chess_puct_backup(zc_engine *eng, int32_t first_game, int32_t n_games, int32_t flush, const double *d_values,
+                         const void *d_logits, int32_t logits_dtype, void *hip_stream);
+int zc_chess_puct_end(zc_engine *eng, int32_t first_game, int32_t n_games, float temperature, uint16_t *d_out_move,
+                      int32_t *d_out_root_na, float *d_out_root_prior, zc_game_stats *d_out_stats, void *hip_stream);
+
 /* ---- Value-network layers on the matrix cores (models/chess_value/network.py:24-45) -----
  * The residual tower of ValueNetwork with BatchNorm folded into the convolutions, NHWC fp16
  * activations ([n][h][w][c], a pixel's channels contiguous), 128 output channels.

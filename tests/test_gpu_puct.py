@@ -1,0 +1,124 @@
+"""GPU checks of the PUCT search (chess_puct.hip; SURVEY §8 a21, no reference counterpart):
+exact agreement with its plain-Python specification (tests/puct_ref.py) on uniform priors
+and deterministic values, Dirichlet root noise properties, the policy+value network on the
+MFMA kernels against PyTorch fp32, and a full search with that network."""
+import numpy as np
+import pytest
+import torch
+
+import oracle
+import puct_ref
+
+pytestmark = pytest.mark.gpu
+
+FENS = ["rnbqkbnr/pppppppp/8/8/8/8/PPPPPPPP/RNBQKBNR w KQkq - 0 1",
+        "r3k2r/p1ppqpb1/bn2pnp1/3PN3/1p2P3/2N2Q1p/PPPBBPPP/R3K2R w KQkq - 0 1",
+        "8/2p5/3p4/KP5r/1R3p1k/8/4P1P1/8 w - - 0 1",
+        "r1bqkbnr/pppp1ppp/2n5/4p3/2B1P3/5Q2/PPPP1PPP/RNB1K1NR w KQkq - 2 3",
+        "6k1/5ppp/8/8/8/8/5PPP/3R2K1 w - - 0 1"]
+M64 = (1 << 64) - 1
+
+
+def hv(board: bytes, turn: int) -> float:
+    h = 0x84222325CBF29CE4
+    for b in board:
+        h = ((h ^ b) * 0x100000001B3) & M64
+    h = (h ^ (turn * 0x9E3779B97F4A7C15)) & M64
+    h ^= h >> 31
+    return ((h % 400001) - 200000) / 200003.0
+
+
+@pytest.fixture(scope="module")
+def eng():
+    from zeroclone_amd._native import NativeEngine
+    e = NativeEngine(max_games=64, max_sims=300, max_batch=32)
+    yield e
+    e.close()
+
+
+def roots_of(fens):
+    from zeroclone_amd._native import CHESS_STATE_DTYPE, chess_from_fen
+    a = np.array([chess_from_fen(f) for f in fens], CHESS_STATE_DTYPE)
+    return torch.from_numpy(a.view(np.uint8).reshape(len(fens), 72).copy()).cuda()
+
+
+def decode(m):
+    from zeroclone_amd._native import unpack_chess_move
+    (fr, fc, tr, tc), v = unpack_chess_move(int(m) & 0xFFFF)
+    return (fr, fc, tr, tc, v)
+
+
+def hash_net(leaves, planes, counts):
+    rows = leaves.cpu().numpy()
+    v = torch.tensor([hv(bytes(r[:64]), int(r[64])) for r in rows], dtype=torch.float64).cuda()
+    return v, torch.zeros((rows.shape[0], 4096), dtype=torch.float32, device="cuda")
+
+
+@pytest.mark.parametrize("sims,bs,c", [(65, 8, 1.5), (129, 16, 2.5), (40, 32, 1.0)])
+def test_puct_matches_its_specification(eng, sims, bs, c):
+    from zeroclone_amd.valued import ChessPuctSearch
+    fens = FENS * 2
+    ps = ChessPuctSearch(eng, len(fens), bs, c_puct=c, dirichlet_eps=0.0)
+    mv, na, st = ps.run(roots_of(fens), sims, hash_net)
+    mv, na, st = mv.cpu().numpy(), na.cpu().numpy(), st.cpu().numpy()
+    for i, fen in enumerate(fens):
+        moves, N, best = puct_ref.search(oracle.chess_from_fen(fen), sims, bs, c,
+                                         lambda s: hv(bytes(s.board), s.turn),
+                                         lambda node: [float(np.float32(1.0) / np.float32(len(node.moves)))] * len(node.moves))
+        assert st[i, 5] == 0
+        assert list(na[i, :len(moves)]) == N, fen
+        assert sum(N) == sims - 1
+        assert decode(mv[i]) == moves[best]
+
+
+def test_dirichlet_root_noise(eng):
+    from zeroclone_amd.valued import ChessPuctSearch
+    n = 64
+    fens = [FENS[0]] * n
+    pri = []
+    for seed in (1, 1, 2):
+        ps = ChessPuctSearch(eng, n, 8, dirichlet_alpha=0.3, dirichlet_eps=0.25, seed=seed)
+        ps.run(roots_of(fens), 9, hash_net)
+        pri.append(ps.prior.cpu().numpy()[:, :20].astype(np.float64))
+    assert np.array_equal(pri[0], pri[1])          # same seed: same noise
+    assert not np.array_equal(pri[0], pri[2])      # another seed: another draw
+    p = pri[0]
+    np.testing.assert_allclose(p.sum(axis=1), 1.0, atol=1e-5)
+    assert (p.min(axis=1) >= 0.75 / 20 - 1e-6).all()   # (1 - eps) * uniform + eps * noise
+    assert len({tuple(np.round(r, 6)) for r in p}) == n   # every game its own draw
+    np.testing.assert_allclose(p.mean(axis=0), 1 / 20, atol=0.02)   # E[noise] = uniform
+
+
+def test_policy_value_network_mfma_matches_torch():
+    from zeroclone_amd.nets import MfmaPolicyValueNetwork, PolicyValueNetwork
+    torch.manual_seed(0)
+    net = PolicyValueNetwork().eval()
+    for m in net.modules():
+        if isinstance(m, torch.nn.BatchNorm2d):
+            m.running_mean.uniform_(-0.1, 0.1)
+            m.running_var.uniform_(0.5, 1.5)
+    x = (torch.rand(37, 17, 8, 8) < 0.2).float()
+    with torch.no_grad():
+        v_ref, l_ref = net(x)
+    v, l = MfmaPolicyValueNetwork(net)(x.cuda().half())
+    np.testing.assert_allclose(v.cpu().numpy(), v_ref.reshape(-1).double().numpy(), atol=2e-2)
+    np.testing.assert_allclose(l.float().cpu().numpy(), l_ref.numpy(), atol=5e-2, rtol=2e-2)
+
+
+def test_puct_with_the_network_end_to_end(eng):
+    from zeroclone_amd.nets import MfmaPolicyValueNetwork, PolicyValueNetwork
+    from zeroclone_amd.valued import ChessPuctSearch
+    torch.manual_seed(1)
+    net = MfmaPolicyValueNetwork(PolicyValueNetwork().eval())
+    fens = FENS * 4
+    ps = ChessPuctSearch(eng, len(fens), 32, seed=7)
+    mv, na, st = ps.run(roots_of(fens), 161, lambda leaves, planes, counts: net(planes), temperature=1.0)
+    na, st = na.cpu().numpy(), st.cpu().numpy()
+    assert (st[:, 5] == 0).all()
+    assert (na.sum(axis=1) == 160).all()
+    for i, fen in enumerate(fens):
+        assert decode(mv.cpu().numpy()[i]) in oracle.chess_moves(oracle.chess_from_fen(fen))
+    g = ps.capture(roots_of(fens), 161, lambda leaves, planes, counts: net(planes))
+    g.replay()
+    torch.cuda.synchronize()
+    assert (ps.na.cpu().numpy().sum(axis=1) == 160).all()

@@ -114,6 +114,18 @@ SIGNATURES = [
                                            ctypes.c_void_p, ctypes.c_void_p]),
     ("zc_chess_ext_end", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p,
                                         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    ("zc_chess_puct_flushes", ctypes.c_int, [ctypes.c_int32, ctypes.c_int32]),
+    ("zc_chess_puct_begin", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p,
+                                           ctypes.c_int32, ctypes.c_double, ctypes.c_int32, ctypes.c_float,
+                                           ctypes.c_float, ctypes.c_uint64, ctypes.c_void_p]),
+    ("zc_chess_puct_select", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p,
+                                            ctypes.c_void_p]),
+    ("zc_chess_puct_backup", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p]),
+    ("zc_chess_puct_end", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_float,
+                                         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                         ctypes.c_void_p]),
     ("zc_net_conv3x3_async", ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
                                             ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                             ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p]),
@@ -370,6 +382,27 @@ class NativeEngine:
     def chess_ext_end(self, first_game: int, n: int, d_move: int, d_na: int, d_stats: int, stream: int = 0):
         check(lib().zc_chess_ext_end(self._h, first_game, n, ctypes.c_void_p(d_move), ctypes.c_void_p(d_na),
                                      ctypes.c_void_p(d_stats), ctypes.c_void_p(stream or None)))
+
+    # ---- chess PUCT search (device pointers)
+    def chess_puct_begin(self, first_game, n, d_roots, sims, c_puct, batch_size, alpha, eps, seed, stream=0):
+        check(lib().zc_chess_puct_begin(self._h, first_game, n, ctypes.c_void_p(d_roots), int(sims), float(c_puct),
+                                        int(batch_size), float(alpha), float(eps), int(seed) & (2**64 - 1),
+                                        ctypes.c_void_p(stream or None)))
+
+    def chess_puct_select(self, first_game, n, flush, d_leaves=0, d_planes=0, planes_f16=True, d_counts=0, stream=0):
+        check(lib().zc_chess_puct_select(self._h, first_game, n, int(flush), ctypes.c_void_p(d_leaves or None),
+                                         ctypes.c_void_p(d_planes or None), ZC_F16 if planes_f16 else ZC_F32,
+                                         ctypes.c_void_p(d_counts or None), ctypes.c_void_p(stream or None)))
+
+    def chess_puct_backup(self, first_game, n, flush, d_values, d_logits, logits_f16=False, stream=0):
+        check(lib().zc_chess_puct_backup(self._h, first_game, n, int(flush), ctypes.c_void_p(d_values),
+                                         ctypes.c_void_p(d_logits), ZC_F16 if logits_f16 else ZC_F32,
+                                         ctypes.c_void_p(stream or None)))
+
+    def chess_puct_end(self, first_game, n, temperature, d_move, d_na, d_prior, d_stats, stream=0):
+        check(lib().zc_chess_puct_end(self._h, first_game, n, float(temperature), ctypes.c_void_p(d_move),
+                                      ctypes.c_void_p(d_na), ctypes.c_void_p(d_prior or None),
+                                      ctypes.c_void_p(d_stats), ctypes.c_void_p(stream or None)))
 
     def c4_rollouts(self, states: np.ndarray, game: int = 0):
         """Sequential rollouts of `states` on one game's stream: (values[n], words consumed)."""

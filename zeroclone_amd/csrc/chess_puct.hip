@@ -1,0 +1,410 @@
+// chess_puct.hip — AlphaZero-style PUCT search for chess on gfx950 (SURVEY.md §8 a21, config
+// C5: a policy + value network, Dirichlet root noise).  The reference has no counterpart
+// (its search is plain UCT with one-at-a-time expansion, mcts.cpp:41-78); this extension
+// reuses its tree, rules and flush protocol and changes the selection rule:
+//
+//   select  a = first argmax  Q(a) + c_puct * P(a) * sqrt(sum_b N(b)) / (1 + N(a)),
+//           Q(a) = W(a) / N(a) (0 when N(a) = 0), P from the policy head of the node's own
+//           evaluation; the walk stops at an edge without a child (the child is created and
+//           is the leaf), at a terminal node, or at a node still waiting for its evaluation;
+//   virtual loss: every edge of a pending leaf's path counts as one visit lost by the
+//           parent's mover (N += 1, W -= 1) until the flush is backed up, so the leaves of a
+//           flush spread over the tree instead of repeating one path;
+//   backup  per leaf in pending order: the node's priors = softmax of the policy logits over
+//           its legal moves (first evaluation only), then each edge undoes its virtual loss
+//           and takes the value (W += 1 - r, N already counted), r alternating in sign;
+//           a terminal leaf's value is -1 (side to move mated) or 0 (no moves otherwise);
+//   root    flush 0 evaluates the root alone; its priors get Dirichlet(alpha) noise with
+//           weight eps, drawn with a counter-based Philox4x32-10 stream keyed by (seed, game).
+//
+// Launches (one wave per game): begin (root node), select (flush f's leaves, planes),
+// backup (priors + values), end (move by visits or temperature sampling, visit counts).
+#include <hip/hip_fp16.h>
+
+#include "chess_tree.h"
+
+namespace zc {
+namespace {
+
+// ---------------------------------------------------------------- Philox4x32-10
+__device__ __forceinline__ uint4 philox(uint4 c, uint2 k) {
+#pragma unroll
+    for (int i = 0; i < 10; ++i) {
+        const uint64_t p0 = (uint64_t)0xD2511F53u * c.x, p1 = (uint64_t)0xCD9E8D57u * c.z;
+        const uint32_t h0 = (uint32_t)(p0 >> 32), l0 = (uint32_t)p0, h1 = (uint32_t)(p1 >> 32), l1 = (uint32_t)p1;
+        c = make_uint4(h1 ^ c.y ^ k.x, l1, h0 ^ c.w ^ k.y, l0);
+        k.x += 0x9E3779B9u;
+        k.y += 0xBB67AE85u;
+    }
+    return c;
+}
+__device__ __forceinline__ float u01(uint32_t x) { return ((float)(x >> 8) + 0.5f) * (1.0f / 16777216.0f); }
+
+// Gamma(alpha, 1) by Marsaglia-Tsang (alpha < 1 via Gamma(alpha + 1) * U^(1/alpha)); the
+// draws of (game, move j) come from Philox counters (j, attempt, game, tag).
+__device__ float gamma_draw(float alpha, uint2 key, uint32_t game, uint32_t j) {
+    const bool boost = alpha < 1.0f;
+    const float a = boost ? alpha + 1.0f : alpha;
+    const float d = a - 1.0f / 3.0f, cc = 1.0f / sqrtf(9.0f * d);
+    float g = 0.0f;
+    for (uint32_t att = 0; att < 64; ++att) {
+        const uint4 r = philox(make_uint4(j, att, game, 0x6A09E667u), key);
+        // Box-Muller normal from two uniforms
+        const float z = sqrtf(-2.0f * logf(u01(r.x))) * cospif(2.0f * u01(r.y));
+        const float v1 = 1.0f + cc * z;
+        if (v1 <= 0.0f) continue;
+        const float v = v1 * v1 * v1, u = u01(r.z);
+        if (logf(u) < 0.5f * z * z + d - d * v + d * logf(v)) {
+            g = d * v;
+            if (boost) g *= powf(u01(r.w), 1.0f / alpha);
+            break;
+        }
+    }
+    return g;
+}
+
+__device__ __forceinline__ double wave_sum_d(double x) {
+    for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
+    return x;
+}
+__device__ __forceinline__ float wave_max_f(float x) {
+    for (int o = 32; o > 0; o >>= 1) x = fmaxf(x, __shfl_xor(x, o));
+    return x;
+}
+__device__ __forceinline__ float wave_sum_f(float x) {
+    for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
+    return x;
+}
+
+// flushes: 0 = the root alone, then batches of bs
+__device__ __forceinline__ int flush_leaves(const ChessParams &p, int f) {
+    if (f == 0) return 1;
+    return max(0, min(p.bs, p.sims - 1 - (f - 1) * p.bs));
+}
+
+// One PUCT walk + expansion; returns the leaf, its depth, and the edge slots of its path
+// in lanes 1..depth of pathv.  Applies the virtual loss on every edge it takes.
+__device__ int puct_walk(const ChessParams &p, const CTree &t, CLds &L, int &nnodes, int &slots, int &status,
+                         int &ldepth, uint32_t &pathv, Counters &cn) {
+    const uint32_t lane = lane_id();
+    int node = 0, depth = 0;
+    pathv = 0;
+    for (;;) {
+        ChessNode *N = &t.nodes[node];
+        const int nm = uni((int)N->nmoves);
+        if (nm == 0 || !uni((int)N->evaluated)) break;  // terminal, or a leaf still pending
+        if (depth >= kChessPath - 2) {
+            status = ZC_STATUS_CAPACITY;
+            break;
+        }
+        const uint32_t base = uni(N->base);
+        double tot = 0.0;
+        for (int b = 0; b < nm; b += 64) {
+            const int j = b + (int)lane;
+            tot += j < nm ? (double)t.na[base + j] : 0.0;
+        }
+        const double sq = sqrt(wave_sum_d(tot));
+        double bv = -INFINITY;
+        int bi = 0x7FFFFFFF;
+        for (int b = 0; b < nm; b += 64) {
+            const int j = b + (int)lane;
+            if (j < nm) {
+                const int32_t na = t.na[base + j];
+                const double q = na > 0 ? t.w[base + j] / (double)na : 0.0;
+                const double u = p.c * (double)t.pr[base + j] * sq / (double)(1 + na);
+                const double v = q + u;
+                if (v > bv) {
+                    bv = v;
+                    bi = j;
+                }
+            }
+        }
+        argmax64(bv, bi);
+        const int best = uni(bi);
+        const uint32_t s = base + (uint32_t)best;
+        if (lane == 0) {  // virtual loss: one visit lost by this node's mover
+            t.na[s] += 1;
+            t.w[s] -= 1.0;
+        }
+        ++depth;
+        if (lane == (uint32_t)depth) pathv = s;
+        const int child = uni((int)t.ch[s]);
+        if (child != 0xFFFF) {
+            node = child;
+            continue;
+        }
+        // expand the edge: the child position, its legal moves, no priors yet
+        const uint32_t m = uni((uint32_t)t.mv[s]);
+        if (lane < 18) ((uint32_t *)&L.st)[lane] = ((const uint32_t *)&N->st)[lane];
+        wave_sync_mem();
+        if (lane == 0) chessdev::apply_move(L.st, m);
+        wave_sync_mem();
+        const int id = nnodes++;
+        if (id >= p.M) {
+            status = ZC_STATUS_CAPACITY;
+            break;
+        }
+        create_node(t, L, id, node, best, depth, slots, status);
+        if (lane == 0) t.ch[s] = (uint16_t)id;
+        cn.add(cn.expansions, 1);
+        cn.add(cn.depth_sum, depth);
+        wave_sync_mem();
+        node = id;
+        break;
+    }
+    ldepth = depth;
+    return node;
+}
+
+__global__ __launch_bounds__(64) void puct_begin_kernel(ChessParams p) {
+    __shared__ CLds L;
+    const int gl = blockIdx.x;
+    if (gl >= p.n_games) return;
+    const int g = p.first_game + gl;
+    const CTree t = ctree(p, g);
+    int32_t *ctl = p.ca.ctl + (size_t)g * kCtlWords;
+    const uint32_t lane = lane_id();
+    if (lane < 18) {
+        const uint32_t w = ((const uint32_t *)&p.roots[gl])[lane];
+        ((uint32_t *)&L.st)[lane] = w;
+        ((uint32_t *)&p.ca.roots[g])[lane] = w;
+    }
+    wave_sync_mem();
+    int slots = 0, status = 0;
+    create_node(t, L, 0, 0xFFFF, 0xFFFF, 0, slots, status);
+    if (!status && uni((int)t.nodes[0].nmoves) == 0) status = ZC_STATUS_NO_MOVES;
+    if (lane == 0) {
+        ctl[cNodes] = 1;
+        ctl[cSlots] = slots;
+        ctl[cStatus] = status;
+        ctl[cNb] = 0;
+        ctl[cExp] = 0;
+        ctl[cDepth] = 0;
+    }
+}
+
+__global__ __launch_bounds__(64) void puct_select_kernel(ChessParams p) {
+    __shared__ CLds L;
+    const int gl = blockIdx.x;
+    if (gl >= p.n_games) return;
+    const int g = p.first_game + gl;
+    const CTree t = ctree(p, g);
+    int32_t *ctl = p.ca.ctl + (size_t)g * kCtlWords;
+    const uint32_t lane = lane_id();
+    int status = uni(ctl[cStatus]);
+    int nb = status ? 0 : flush_leaves(p, p.flush);
+    int nnodes = uni(ctl[cNodes]), slots = uni(ctl[cSlots]);
+    uint32_t *paths = p.ca.paths + (size_t)g * p.max_batch * kChessPath;
+    uint32_t *meta = p.ca.meta + (size_t)g * p.max_batch;
+    Counters cn;
+    int j = 0;
+    for (; j < nb && !status; ++j) {
+        int d = 0;
+        uint32_t pathv = 0;
+        const int leaf = p.flush == 0 ? 0 : puct_walk(p, t, L, nnodes, slots, status, d, pathv, cn);
+        if (lane < (uint32_t)kChessPath) paths[(size_t)j * kChessPath + lane] = pathv;
+        if (lane == 0) meta[j] = (uint32_t)leaf | ((uint32_t)d << 16);
+    }
+    if (status) nb = 0;
+    wave_sync_mem();
+    if (lane == 0) {
+        ctl[cNodes] = nnodes;
+        ctl[cSlots] = slots;
+        ctl[cStatus] = status;
+        ctl[cNb] = nb;
+        ctl[cExp] += cn.expansions;
+        ctl[cDepth] += cn.depth_sum;
+        if (p.counts) p.counts[gl] = nb;
+    }
+    const size_t obase = (size_t)gl * p.bs;
+    for (int k = 0; k < nb; ++k) {
+        const ChessNode *N = &t.nodes[uni(meta[k]) & 0xFFFFu];
+        if (p.leaves && lane < 18) ((uint32_t *)&p.leaves[obase + k])[lane] = ((const uint32_t *)&N->st)[lane];
+        if (p.planes) {
+            const uint32_t pc = N->st.board[lane];
+            const char pieces[12] = {'P', 'N', 'B', 'R', 'Q', 'K', 'p', 'n', 'b', 'r', 'q', 'k'};
+            int which = -1;
+            for (int q = 0; q < 12; ++q)
+                if (pc == (uint8_t)pieces[q]) {
+                    which = q;
+                    break;
+                }
+            const int turn = N->st.turn, castle = N->st.castle;
+            for (int q = 0; q < 17; ++q) {
+                float v;
+                if (q < 12) v = q == which ? 1.0f : 0.0f;
+                else if (q == 12) v = turn == 0 ? 1.0f : 0.0f;
+                else v = (castle >> (q - 13)) & 1 ? 1.0f : 0.0f;
+                const size_t o = ((obase + k) * 17 + q) * 64 + lane;
+                if (p.planes_f16) ((__half *)p.planes)[o] = __float2half(v);
+                else ((float *)p.planes)[o] = v;
+            }
+        }
+    }
+}
+
+__global__ __launch_bounds__(64) void puct_backup_kernel(ChessParams p) {
+    const int gl = blockIdx.x;
+    if (gl >= p.n_games) return;
+    const int g = p.first_game + gl;
+    const CTree t = ctree(p, g);
+    const int32_t *ctl = p.ca.ctl + (size_t)g * kCtlWords;
+    const uint32_t lane = lane_id();
+    const int nb = uni(ctl[cNb]);
+    if (uni(ctl[cStatus]) || nb == 0) return;
+    const uint32_t *paths = p.ca.paths + (size_t)g * p.max_batch * kChessPath;
+    const uint32_t *meta = p.ca.meta + (size_t)g * p.max_batch;
+    const uint2 key = make_uint2((uint32_t)p.seed, (uint32_t)(p.seed >> 32));
+    for (int j = 0; j < nb; ++j) {
+        const uint32_t mt = uni(meta[j]);
+        const int node = (int)(mt & 0xFFFFu), d = (int)(mt >> 16);
+        ChessNode *N = &t.nodes[node];
+        const int nm = uni((int)N->nmoves);
+        const size_t li = (size_t)gl * p.bs + j;
+        double v;
+        if (nm == 0) {
+            v = uni((int)N->check) ? -1.0 : 0.0;  // checkmated side to move / no moves
+        } else {
+            v = __hiloint2double(uni(__double2hiint(p.values[li])), uni(__double2loint(p.values[li])));
+            if (!uni((int)N->evaluated)) {
+                // priors: softmax of the logits of this node's legal moves (from*64 + to)
+                const uint32_t base = uni(N->base);
+                float lg[4];
+                float mx = -INFINITY;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int k = q * 64 + (int)lane;
+                    lg[q] = -INFINITY;
+                    if (k < nm) {
+                        const uint32_t m = t.mv[base + k];
+                        const size_t o = li * 4096 + (m & 63u) * 64 + ((m >> 6) & 63u);
+                        lg[q] = p.logits_f16 ? __half2float(((const __half *)p.logits)[o]) : ((const float *)p.logits)[o];
+                        mx = fmaxf(mx, lg[q]);
+                    }
+                }
+                mx = wave_max_f(mx);
+                float e[4], sum = 0.0f;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    e[q] = q * 64 + (int)lane < nm ? expf(lg[q] - mx) : 0.0f;
+                    sum += e[q];
+                }
+                sum = wave_sum_f(sum);
+                float pr[4];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) pr[q] = e[q] / sum;
+                if (node == 0 && p.dir_eps > 0.0f) {
+                    // Dirichlet(alpha) noise on the root priors
+                    float gm[4], gs = 0.0f;
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const int k = q * 64 + (int)lane;
+                        gm[q] = k < nm ? gamma_draw(p.dir_alpha, key, (uint32_t)g, (uint32_t)k) : 0.0f;
+                        gs += gm[q];
+                    }
+                    gs = wave_sum_f(gs);
+#pragma unroll
+                    for (int q = 0; q < 4; ++q)
+                        pr[q] = (1.0f - p.dir_eps) * pr[q] + p.dir_eps * (gs > 0.0f ? gm[q] / gs : 0.0f);
+                }
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int k = q * 64 + (int)lane;
+                    if (k < nm) t.pr[base + k] = pr[q];
+                }
+                if (lane == 0) N->evaluated = 1;
+            }
+        }
+        wave_sync_mem();
+        // backup with the virtual loss undone: W += 1 - r on the edge into level l
+        if (lane >= 1 && lane <= (uint32_t)d) {
+            const uint32_t s = paths[(size_t)j * kChessPath + lane];
+            const double r = ((d - (int)lane) & 1) ? -v : v;
+            t.w[s] = t.w[s] + 1.0 - r;
+        }
+        wave_sync_mem();
+    }
+}
+
+__global__ __launch_bounds__(64) void puct_end_kernel(ChessParams p) {
+    const int gl = blockIdx.x;
+    if (gl >= p.n_games) return;
+    const int g = p.first_game + gl;
+    const CTree t = ctree(p, g);
+    const int32_t *ctl = p.ca.ctl + (size_t)g * kCtlWords;
+    const uint32_t lane = lane_id();
+    const int status = uni(ctl[cStatus]);
+    const ChessNode *R = &t.nodes[0];
+    const int nm = status == ZC_STATUS_NO_MOVES ? 0 : uni((int)R->nmoves);
+    const uint32_t base = uni(R->base);
+    for (int j = (int)lane; j < ZC_CHESS_MAX_MOVES; j += 64) {
+        p.out_na[(size_t)gl * ZC_CHESS_MAX_MOVES + j] = j < nm ? t.na[base + j] : 0;
+        if (p.out_prior) p.out_prior[(size_t)gl * ZC_CHESS_MAX_MOVES + j] = j < nm ? t.pr[base + j] : 0.0f;
+    }
+    int best = -1;
+    if (nm > 0) {
+        if (p.temperature <= 0.0f) {  // most visits, first maximum
+            int bv = -1, bi = 0x7FFFFFFF;
+            for (int b = 0; b < nm; b += 64) {
+                const int j = b + (int)lane;
+                if (j < nm && t.na[base + j] > bv) {
+                    bv = t.na[base + j];
+                    bi = j;
+                }
+            }
+            for (int o = 32; o > 0; o >>= 1) {
+                const int ov = __shfl_xor(bv, o), oi = __shfl_xor(bi, o);
+                if (ov > bv || (ov == bv && oi < bi)) {
+                    bv = ov;
+                    bi = oi;
+                }
+            }
+            best = uni(bi);
+        } else {  // sample proportional to Na^(1/T): inverse CDF over the moves in order
+            double tot = 0.0;
+            for (int b = 0; b < nm; b += 64) {
+                const int j = b + (int)lane;
+                tot += j < nm ? pow((double)t.na[base + j], 1.0 / (double)p.temperature) : 0.0;
+            }
+            tot = wave_sum_d(tot);
+            const uint4 r = philox(make_uint4((uint32_t)g, 0x5BE0CD19u, 0, 0),
+                                   make_uint2((uint32_t)p.seed, (uint32_t)(p.seed >> 32)));
+            const double target = (double)u01(r.x) * tot;
+            double run = 0.0;
+            best = nm - 1;
+            for (int j = 0; j < nm; ++j) {  // serial scan in move order (<= 256 steps, once per move)
+                run += pow((double)uni(t.na[base + j]), 1.0 / (double)p.temperature);
+                if (run > target) {
+                    best = j;
+                    break;
+                }
+            }
+        }
+    }
+    if (lane == 0) {
+        p.out_move[gl] = (best >= 0 && !status) ? t.mv[base + best] : (uint16_t)0xFFFF;
+        zc_game_stats st{};
+        st.status = status;
+        st.expansions = ctl[cExp];
+        st.depth_sum = ctl[cDepth];
+        st.leaves = p.sims;
+        p.out_stats[gl] = st;
+    }
+}
+
+}  // namespace
+
+void launch_chess_puct_begin(const ChessParams &p, hipStream_t s) {
+    hipLaunchKernelGGL(puct_begin_kernel, dim3(p.n_games), dim3(64), 0, s, p);
+}
+void launch_chess_puct_select(const ChessParams &p, hipStream_t s) {
+    hipLaunchKernelGGL(puct_select_kernel, dim3(p.n_games), dim3(64), 0, s, p);
+}
+void launch_chess_puct_backup(const ChessParams &p, hipStream_t s) {
+    hipLaunchKernelGGL(puct_backup_kernel, dim3(p.n_games), dim3(64), 0, s, p);
+}
+void launch_chess_puct_end(const ChessParams &p, hipStream_t s) {
+    hipLaunchKernelGGL(puct_end_kernel, dim3(p.n_games), dim3(64), 0, s, p);
+}
+
+}  // namespace zc

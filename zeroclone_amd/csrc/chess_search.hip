@@ -16,131 +16,10 @@
 // subtractions in the reference's order.
 #include <hip/hip_fp16.h>
 
-#include "c4_device.h"
-#include "chess_device.h"
+#include "chess_tree.h"
 
 namespace zc {
 namespace {
-
-using chessdev::ChessScratch;
-
-struct CTree {
-    ChessNode *nodes;
-    uint16_t *mv;
-    uint8_t *ut;
-    uint16_t *ch;
-    int32_t *na;
-    double *w;
-    int64_t S;
-};
-
-__device__ __forceinline__ CTree ctree(const ChessParams &p, int g) {
-    const ChessArena &a = p.ca;
-    const size_t so = (size_t)g * (size_t)a.S;
-    return CTree{a.nodes + (size_t)g * p.M, a.mv + so, a.ut + so, a.ch + so, a.na + so, a.w + so, a.S};
-}
-
-enum : int { cNodes = 0, cSlots = 1, cStatus = 2, cNb = 3, cExp = 4, cDepth = 5, cUse0 = 6 };
-
-struct CLds {
-    ChessScratch s;
-    zc_chess_state st;  // staging: the position of the node being created
-};
-
-__device__ __forceinline__ void wave_sync_mem() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); }
-
-__device__ __forceinline__ int32_t piece_material(uint32_t x) {
-    switch (x) {
-        case 'P': return 1;
-        case 'N': case 'B': return 3;
-        case 'R': return 5;
-        case 'Q': return 9;
-        case 'p': return -1;
-        case 'n': case 'b': return -3;
-        case 'r': return -5;
-        case 'q': return -9;
-        default: return 0;
-    }
-}
-
-__device__ __forceinline__ int32_t wave_sum(int32_t x) {
-    for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
-    return x;
-}
-
-// Node(state, get_legal_moves(state), parent, idx) (mcts.cpp:23-34) for the position in
-// L.st: moves in the reference order into fresh slots, all untried, no children.
-__device__ void create_node(const CTree &t, CLds &L, int id, int parent, int pact, int depth, int &slots, int &status) {
-    const uint32_t lane = lane_id();
-    L.s.board[lane] = L.st.board[lane];
-    wave_sync_mem();
-    const int turn = uni((int)L.st.turn);
-    int n = chessdev::legal_moves(L.s.board, turn, L.s.legal, L.s.pseudo);
-    if (n < 0) {
-        status = ZC_STATUS_CAPACITY;
-        n = 0;
-    }
-    const int32_t mat = wave_sum(piece_material(L.s.board[lane]));
-    const uint64_t km = __ballot(L.s.board[lane] == (turn == 0 ? 'K' : 'k'));
-    const int ks = km ? __builtin_ctzll(km) : -1;
-    const bool check = chessdev::attacked_after(L.s.board, turn, ks >= 0 ? ks >> 3 : -1, ks >= 0 ? ks & 7 : -1, -1,
-                                                -1, 0);
-    const int base = slots;
-    if ((int64_t)base + n > t.S) {
-        status = ZC_STATUS_CAPACITY;
-        n = 0;
-    }
-    slots = base + n;
-    for (int j = (int)lane; j < n; j += 64) {
-        t.mv[base + j] = L.s.legal[j];
-        t.ut[base + j] = (uint8_t)j;
-        t.ch[base + j] = 0xFFFF;
-        t.na[base + j] = 0;
-        t.w[base + j] = 0.0;
-    }
-    ChessNode *N = &t.nodes[id];
-    if (lane < 18) ((uint32_t *)&N->st)[lane] = ((const uint32_t *)&L.st)[lane];
-    if (lane == 0) {
-        N->base = (uint32_t)base;
-        N->nmoves = (uint16_t)n;
-        N->nu = (uint16_t)n;
-        N->parent = (uint16_t)parent;
-        N->pact = (uint16_t)pact;
-        N->depth = (uint16_t)depth;
-        N->material = (int16_t)mat;
-        N->check = check ? 1 : 0;
-    }
-    wave_sync_mem();
-}
-
-__device__ __forceinline__ void argmax64(double &v, int &i) {
-    for (int o = 32; o > 0; o >>= 1) {
-        const double ov = __shfl_xor(v, o);
-        const int oi = __shfl_xor(i, o);
-        if (ov > v || (ov == v && oi < i)) {
-            v = ov;
-            i = oi;
-        }
-    }
-}
-
-// The r-th set position (in index order) of a predicate over [0, n), 64 per pass.
-template <class Pred>
-__device__ __forceinline__ int nth_true(int n, uint32_t r, Pred pred) {
-    const uint32_t lane = lane_id();
-    for (int b = 0; b < n; b += 64) {
-        const int j = b + (int)lane;
-        const uint64_t m = __ballot(j < n && pred(j));
-        const uint32_t c = (uint32_t)__popcll(m);
-        if (r < c) {
-            const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-            const uint64_t hit = __ballot(((m >> lane) & 1ull) && rank == r);
-            return b + __builtin_ctzll(hit);
-        }
-        r -= c;
-    }
-    return -1;
-}
 
 // select + expand + record of ONE simulation (mcts.cpp:129-147).  Returns the leaf node;
 // its depth in `ldepth`; lane l of `pathv` holds the slot of the edge into level l.

@@ -62,7 +62,7 @@ int dalloc(zc_engine *e, T **p, size_t count) {
 }
 
 void free_chess(zc::ChessArena &c) {
-    void *ptrs[] = {c.nodes, c.mv, c.ut, c.ch, c.na, c.w, c.ctl, c.paths, c.meta, c.roots};
+    void *ptrs[] = {c.nodes, c.mv, c.ut, c.ch, c.na, c.w, c.prior, c.ctl, c.paths, c.meta, c.roots};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
     c = zc::ChessArena{};
@@ -550,6 +550,7 @@ int ensure_chess(zc_engine *e) {
     if (!rc) rc = dalloc(e, &n.ch, G * S);
     if (!rc) rc = dalloc(e, &n.na, G * S);
     if (!rc) rc = dalloc(e, &n.w, G * S);
+    if (!rc) rc = dalloc(e, &n.prior, G * S);
     if (!rc) rc = dalloc(e, &n.ctl, G * zc::kCtlWords);
     if (!rc) rc = dalloc(e, &n.paths, G * (size_t)e->cfg.max_batch * zc::kChessPath);
     if (!rc) rc = dalloc(e, &n.meta, G * (size_t)e->cfg.max_batch);
@@ -696,6 +697,116 @@ int zc_chess_ext_end(zc_engine *eng, int32_t first, int32_t n, uint16_t *d_move,
     p.out_na = d_na;
     p.out_stats = d_stats;
     zc::launch_chess_ext_end(p, (hipStream_t)hip_stream);
+    ZC_HIP(hipGetLastError());
+    return ZC_OK;
+}
+
+// ---------------------------------------------------------------- chess PUCT search
+int zc_chess_puct_flushes(int32_t sims, int32_t bs) {
+    if (sims < 2 || bs < 1) return fail(ZC_EINVAL, "PUCT search needs sims >= 2 and batch_size >= 1");
+    return 1 + (sims - 1 + bs - 1) / bs;
+}
+
+}  // extern "C"
+
+namespace {
+zc::ChessParams puct_params(zc_engine *e, int32_t first, int32_t n) {
+    zc::ChessParams p = chess_params(e, first, n, e->px_sims, e->px_c, e->px_bs, 0, 0.0);
+    p.dir_alpha = e->px_alpha;
+    p.dir_eps = e->px_eps;
+    p.seed = e->px_seed;
+    return p;
+}
+int check_px(zc_engine *e, int32_t first, int32_t n, int32_t flush, bool need_flush) {
+    if (!e->px_active) return fail(ZC_EINVAL, "no PUCT search in progress (call zc_chess_puct_begin first)");
+    if (first < e->px_first || n < 0 || (int64_t)first + n > (int64_t)e->px_first + e->px_n)
+        return fail(ZC_EINVAL, "games [%d, %d) outside the PUCT search's range", first, first + n);
+    const int nflush = 1 + (e->px_sims - 1 + e->px_bs - 1) / e->px_bs;
+    if (need_flush && (flush < 0 || flush >= nflush)) return fail(ZC_EINVAL, "flush %d outside [0, %d)", flush, nflush);
+    return ZC_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int zc_chess_puct_begin(zc_engine *eng, int32_t first, int32_t n, const zc_chess_state *d_roots, int32_t sims,
+                        double c_puct, int32_t bs, float alpha, float eps, uint64_t seed, void *hip_stream) {
+    if (!eng || (n && !d_roots)) return fail(ZC_EINVAL, "null argument");
+    if (int r = check_search(eng, first, n, sims, c_puct, bs)) return r;
+    if (sims < 2) return fail(ZC_EINVAL, "PUCT search needs sims >= 2 (flush 0 evaluates the root)");
+    if (!(alpha > 0.0f) || !(eps >= 0.0f && eps <= 1.0f)) return fail(ZC_EINVAL, "need alpha > 0 and 0 <= eps <= 1");
+    std::lock_guard<std::mutex> lk(eng->mu);
+    ZC_HIP(hipSetDevice(eng->cfg.device));
+    if (int r = ensure_chess(eng)) return r;
+    eng->px_first = first;
+    eng->px_n = n;
+    eng->px_sims = sims;
+    eng->px_bs = bs;
+    eng->px_c = c_puct;
+    eng->px_alpha = alpha;
+    eng->px_eps = eps;
+    eng->px_seed = seed;
+    eng->px_active = true;
+    if (!n) return ZC_OK;
+    zc::ChessParams p = puct_params(eng, first, n);
+    p.roots = d_roots;
+    zc::launch_chess_puct_begin(p, (hipStream_t)hip_stream);
+    ZC_HIP(hipGetLastError());
+    return ZC_OK;
+}
+
+int zc_chess_puct_select(zc_engine *eng, int32_t first, int32_t n, int32_t flush, zc_chess_state *d_leaves,
+                         void *d_planes, int32_t planes_dtype, int32_t *d_counts, void *hip_stream) {
+    if (!eng) return fail(ZC_EINVAL, "null argument");
+    if (planes_dtype != ZC_F32 && planes_dtype != ZC_F16) return fail(ZC_EINVAL, "planes_dtype must be ZC_F32 or ZC_F16");
+    std::lock_guard<std::mutex> lk(eng->mu);
+    if (int r = check_px(eng, first, n, flush, true)) return r;
+    if (!n) return ZC_OK;
+    ZC_HIP(hipSetDevice(eng->cfg.device));
+    zc::ChessParams p = puct_params(eng, first, n);
+    p.flush = flush;
+    p.leaves = d_leaves;
+    p.planes = d_planes;
+    p.planes_f16 = planes_dtype == ZC_F16;
+    p.counts = d_counts;
+    zc::launch_chess_puct_select(p, (hipStream_t)hip_stream);
+    ZC_HIP(hipGetLastError());
+    return ZC_OK;
+}
+
+int zc_chess_puct_backup(zc_engine *eng, int32_t first, int32_t n, int32_t flush, const double *d_values,
+                         const void *d_logits, int32_t logits_dtype, void *hip_stream) {
+    if (!eng || (n && (!d_values || !d_logits))) return fail(ZC_EINVAL, "null argument");
+    if (logits_dtype != ZC_F32 && logits_dtype != ZC_F16) return fail(ZC_EINVAL, "logits_dtype must be ZC_F32 or ZC_F16");
+    std::lock_guard<std::mutex> lk(eng->mu);
+    if (int r = check_px(eng, first, n, flush, true)) return r;
+    if (!n) return ZC_OK;
+    ZC_HIP(hipSetDevice(eng->cfg.device));
+    zc::ChessParams p = puct_params(eng, first, n);
+    p.flush = flush;
+    p.values = d_values;
+    p.logits = d_logits;
+    p.logits_f16 = logits_dtype == ZC_F16;
+    zc::launch_chess_puct_backup(p, (hipStream_t)hip_stream);
+    ZC_HIP(hipGetLastError());
+    return ZC_OK;
+}
+
+int zc_chess_puct_end(zc_engine *eng, int32_t first, int32_t n, float temperature, uint16_t *d_move, int32_t *d_na,
+                      float *d_prior, zc_game_stats *d_stats, void *hip_stream) {
+    if (!eng || (n && (!d_move || !d_na || !d_stats))) return fail(ZC_EINVAL, "null argument");
+    if (!(temperature >= 0.0f)) return fail(ZC_EINVAL, "temperature must be >= 0");
+    std::lock_guard<std::mutex> lk(eng->mu);
+    if (int r = check_px(eng, first, n, 0, false)) return r;
+    if (!n) return ZC_OK;
+    ZC_HIP(hipSetDevice(eng->cfg.device));
+    zc::ChessParams p = puct_params(eng, first, n);
+    p.temperature = temperature;
+    p.out_move = d_move;
+    p.out_na = d_na;
+    p.out_prior = d_prior;
+    p.out_stats = d_stats;
+    zc::launch_chess_puct_end(p, (hipStream_t)hip_stream);
     ZC_HIP(hipGetLastError());
     return ZC_OK;
 }

@@ -120,7 +120,8 @@ struct ChessNode {
     uint16_t depth;
     int16_t material;    // sum of piece values, white positive (crude_chess_score)
     uint8_t check;       // side to move in check
-    uint8_t pad[7];
+    uint8_t evaluated;   // PUCT search: the network's priors are in the slots
+    uint8_t pad[6];
 };
 static_assert(sizeof(ChessNode) == 96, "ChessNode is 96 bytes");
 
@@ -131,6 +132,7 @@ struct ChessArena {
     uint16_t *ch = nullptr;      // [G][S] child node, 0xFFFF = null
     int32_t *na = nullptr;       // [G][S] Na
     double *w = nullptr;         // [G][S] Wa (fp64, summed in pending order)
+    float *prior = nullptr;      // [G][S] P (PUCT search: the policy network's prior)
     int32_t *ctl = nullptr;      // [G][kCtlWords]
     uint32_t *paths = nullptr;   // [G][max_batch][kChessPath] slot of the edge into each level
     uint32_t *meta = nullptr;    // [G][max_batch] leaf node | depth << 16
@@ -154,6 +156,13 @@ struct ChessParams {
     uint16_t *out_move;
     int32_t *out_na;   // [n][ZC_CHESS_MAX_MOVES]
     zc_game_stats *out_stats;
+    // PUCT search (chess_puct.hip)
+    float dir_alpha, dir_eps;   // Dirichlet root noise
+    uint64_t seed;              // counter-based RNG key (noise, temperature sampling)
+    float temperature;          // end: 0 = most visits, > 0 = sample proportional to Na^(1/T)
+    const void *logits;         // backup: [n*bs][4096] policy logits (from*64 + to)
+    int logits_f16;
+    float *out_prior;           // end (optional): root priors after noise [n][ZC_CHESS_MAX_MOVES]
 };
 
 void launch_chess_search(const ChessParams &p, hipStream_t s);     // crude_chess_score, whole move
@@ -161,6 +170,11 @@ void launch_chess_ext_begin(const ChessParams &p, hipStream_t s);
 void launch_chess_ext_select(const ChessParams &p, hipStream_t s);
 void launch_chess_ext_backup(const ChessParams &p, hipStream_t s);
 void launch_chess_ext_end(const ChessParams &p, hipStream_t s);
+
+void launch_chess_puct_begin(const ChessParams &p, hipStream_t s);
+void launch_chess_puct_select(const ChessParams &p, hipStream_t s);
+void launch_chess_puct_backup(const ChessParams &p, hipStream_t s);
+void launch_chess_puct_end(const ChessParams &p, hipStream_t s);
 
 void launch_chess_legal(int n, const zc_chess_state *s, uint16_t *moves, int32_t *counts, hipStream_t st);
 void launch_chess_children(int n, const zc_chess_state *s, zc_chess_state *children, uint16_t *moves,
@@ -198,6 +212,12 @@ struct zc_engine {
     int64_t bytes = 0;
     int stamp = 0;
     zc::ChessArena ca;  // allocated on the first chess search
+    // the chess PUCT search in progress
+    int px_first = 0, px_n = 0, px_sims = 0, px_bs = 0;
+    double px_c = 0;
+    float px_alpha = 0, px_eps = 0;
+    uint64_t px_seed = 0;
+    bool px_active = false;
     // the chess stepwise search in progress
     int cx_first = 0, cx_n = 0, cx_sims = 0, cx_bs = 0, cx_policy = 0;
     double cx_c = 0, cx_freedom = 0;

@@ -156,7 +156,8 @@ class MfmaValueNetwork:
                                torch.empty(n, dtype=torch.float64, device=self.dev))
         return self._bufs[key]
 
-    def __call__(self, planes):
+    def tower(self, planes):
+        """Stem + residual blocks: the final activation, NHWC fp16 [n, h*w, 128]."""
         import torch
         from . import _native
         L = _native.lib()
@@ -178,7 +179,14 @@ class MfmaValueNetwork:
             conv(1 + 2 * k, a, t, None)
             conv(2 + 2 * k, t, b, a)
             a, b = b, a
-        _native.check(L.zc_net_value_head_async(n, hw, a.data_ptr(), self.fcw.data_ptr(), self.fcb, vals.data_ptr(), s))
+        return a, vals
+
+    def __call__(self, planes):
+        from . import _native
+        a, vals = self.tower(planes)
+        n, hw = a.shape[0], a.shape[1]
+        _native.check(_native.lib().zc_net_value_head_async(n, hw, a.data_ptr(), self.fcw.data_ptr(), self.fcb,
+                                                            vals.data_ptr(), ctypes_stream(self.dev)))
         return vals
 
 
@@ -186,3 +194,66 @@ def ctypes_stream(dev):
     import ctypes
     import torch
     return ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream or None)
+
+
+class PolicyValueNetwork(nn.Module):
+    """The PUCT search's network (no reference counterpart): the
+    ValueNetwork tower and value head plus a policy head — conv1x1 to `policy_planes`, BN,
+    ReLU, Linear to one logit per (from, to) square pair (index from*64 + to; the reference's
+    rules promote to a queen only, so from/to identifies a move)."""
+
+    def __init__(self, channels: int = 128, blocks: int = 8, in_planes: int = 17, board=(8, 8),
+                 policy_planes: int = 32, n_logits: int = 4096):
+        super().__init__()
+        base = ValueNetwork(channels, blocks, in_planes)
+        self.stem, self.res, self.head = base.stem, base.res, base.head
+        h, w = board
+        self.policy = nn.Sequential(
+            nn.Conv2d(channels, policy_planes, 1, bias=False),
+            nn.BatchNorm2d(policy_planes),
+            nn.ReLU(inplace=True),
+            nn.Flatten(),
+            nn.Linear(policy_planes * h * w, n_logits),
+        )
+
+    def value_network(self) -> ValueNetwork:
+        v = ValueNetwork(self.stem[0].out_channels, len(self.res), self.stem[0].in_channels)
+        v.stem, v.res, v.head = self.stem, self.res, self.head
+        return v
+
+    def forward(self, x):
+        t = self.res(self.stem(x))
+        return self.head(t), self.policy(t)
+
+
+class MfmaPolicyValueNetwork:
+    """PolicyValueNetwork for inference: the tower and value head on the MFMA kernels, the
+    policy head (BN folded; a 128->P channel matmul and one Linear) as two fp16 GEMMs on
+    PyTorch-ROCm reading the tower's NHWC activation in place.  Returns (fp64 values [n],
+    fp16 logits [n, 4096])."""
+
+    def __init__(self, net: PolicyValueNetwork, device="cuda"):
+        import torch
+        self.tower = MfmaValueNetwork(net.value_network(), device)
+        conv, bn, lin = net.policy[0], net.policy[1], net.policy[4]
+        folded = _fold(conv, bn)
+        P = conv.out_channels
+        self.w1 = folded.weight.detach().float().reshape(P, -1).t().contiguous().to(device, torch.float16)  # [C, P]
+        self.b1 = folded.bias.detach().float().to(device, torch.float16)
+        hw = lin.in_features // P
+        # torch flattens [P, h, w] channel-major; the NHWC activation is pixel-major
+        wl = lin.weight.detach().float().reshape(lin.out_features, P, hw).permute(0, 2, 1).reshape(lin.out_features, -1)
+        self.w2 = wl.t().contiguous().to(device, torch.float16)  # [hw*P, n_logits]
+        self.b2 = lin.bias.detach().float().to(device, torch.float16)
+
+    def __call__(self, planes):
+        import torch
+        from . import _native
+        a, vals = self.tower.tower(planes)
+        n, hw = a.shape[0], a.shape[1]
+        _native.check(_native.lib().zc_net_value_head_async(n, hw, a.data_ptr(), self.tower.fcw.data_ptr(),
+                                                            self.tower.fcb, vals.data_ptr(),
+                                                            ctypes_stream(self.tower.dev)))
+        p = torch.relu(torch.addmm(self.b1, a.reshape(n * hw, -1), self.w1)).reshape(n, -1)
+        logits = torch.addmm(self.b2, p, self.w2)
+        return vals, logits

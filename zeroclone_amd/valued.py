@@ -174,3 +174,64 @@ class ChessValuedSearch:
         return self.move, self.na, self.stats
 
     capture = C4ValuedSearch.capture
+
+
+class ChessPuctSearch:
+    """AlphaZero-style PUCT search for chess (zc_chess_puct_*).
+
+    net_fn(leaves, planes, counts) -> (values fp64 [n*bs], logits [n*bs, 4096] fp32/fp16,
+    index from*64 + to).  Flush 0 evaluates the roots; Dirichlet(alpha) noise of weight eps
+    goes on the root priors; end() picks by visits (temperature 0) or samples."""
+
+    def __init__(self, eng: "_native.NativeEngine", n_games: int, batch_size: int = 32, c_puct: float = 1.5,
+                 dirichlet_alpha: float = 0.3, dirichlet_eps: float = 0.25, seed: int = 0,
+                 planes_dtype: torch.dtype = torch.float16, leaves: bool = True):
+        if batch_size > eng.max_batch:
+            raise ValueError(f"batch_size {batch_size} > engine max_batch {eng.max_batch}")
+        self.eng, self.n, self.bs = eng, n_games, batch_size
+        self.c, self.alpha, self.eps, self.seed = c_puct, dirichlet_alpha, dirichlet_eps, seed
+        self.dev = torch.device("cuda", eng.device)
+        L = n_games * batch_size
+        self.leaves = torch.zeros((L, 72), dtype=torch.uint8, device=self.dev) if leaves else None
+        self.planes = torch.zeros((L, 17, 8, 8), dtype=planes_dtype, device=self.dev)
+        self.counts = torch.zeros(n_games, dtype=torch.int32, device=self.dev)
+        self.values = torch.zeros(L, dtype=torch.float64, device=self.dev)
+        self.move = torch.zeros(n_games, dtype=torch.int16, device=self.dev)
+        self.na = torch.zeros((n_games, _native.CHESS_MAX_MOVES), dtype=torch.int32, device=self.dev)
+        self.prior = torch.zeros((n_games, _native.CHESS_MAX_MOVES), dtype=torch.float32, device=self.dev)
+        self.stats = torch.zeros((n_games, _native.STATS_FIELDS), dtype=torch.int64, device=self.dev)
+
+    def enqueue(self, roots: torch.Tensor, sims: int, net_fn, temperature: float = 0.0, first_game: int = 0):
+        e, n = self.eng, self.n
+        p = lambda t: t.data_ptr() if t is not None else 0  # noqa: E731
+        nfl = _native.check(_native.lib().zc_chess_puct_flushes(int(sims), int(self.bs)))
+        e.chess_puct_begin(first_game, n, roots.data_ptr(), sims, self.c, self.bs, self.alpha, self.eps, self.seed,
+                           _stream(self.dev))
+        for f in range(nfl):
+            e.chess_puct_select(first_game, n, f, p(self.leaves), p(self.planes),
+                                self.planes.dtype == torch.float16, self.counts.data_ptr(), _stream(self.dev))
+            v, logits = net_fn(self.leaves, self.planes, self.counts)
+            if v is not self.values:
+                self.values.copy_(v.reshape(-1))
+            logits = logits.contiguous()
+            e.chess_puct_backup(first_game, n, f, self.values.data_ptr(), logits.data_ptr(),
+                                logits.dtype == torch.float16, _stream(self.dev))
+        e.chess_puct_end(first_game, n, temperature, self.move.data_ptr(), self.na.data_ptr(), self.prior.data_ptr(),
+                         self.stats.data_ptr(), _stream(self.dev))
+        return self.move, self.na, self.stats
+
+    def run(self, roots, sims, net_fn, temperature: float = 0.0, first_game: int = 0):
+        self.enqueue(roots, sims, net_fn, temperature, first_game)
+        torch.cuda.current_stream(self.dev).synchronize()
+        return self.move, self.na, self.stats
+
+    def capture(self, roots, sims, net_fn, temperature: float = 0.0, first_game: int = 0):
+        side = torch.cuda.Stream(self.dev)
+        side.wait_stream(torch.cuda.current_stream(self.dev))
+        with torch.cuda.stream(side):
+            net_fn(self.leaves, self.planes, self.counts)
+        torch.cuda.current_stream(self.dev).wait_stream(side)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self.enqueue(roots, sims, net_fn, temperature, first_game)
+        return g
