@@ -141,6 +141,39 @@ def chess_modes(steps: int, dev) -> dict:
     return out
 
 
+def puct_mode(steps: int, dev) -> dict:
+    """BASELINE configs[4] (C5) per GPU: chess PUCT self-play search, 1024 games x 1600 sims,
+    policy + value ResNet (128 x 8, random init, fp16; tower on the MFMA kernels), Dirichlet
+    root noise, one move per HIP graph."""
+    import numpy as np
+    from zeroclone_amd.nets import MfmaPolicyValueNetwork, PolicyValueNetwork, flops_per_position
+    from zeroclone_amd.valued import ChessPuctSearch
+    G, S, B = 1024, 1600, 32
+    eng = _native.NativeEngine(max_games=G, max_sims=S, max_batch=B, device=dev.index)
+    rows = np.array([_native.chess_init()] * G, _native.CHESS_STATE_DTYPE).view(np.uint8).reshape(G, 72)
+    roots = torch.from_numpy(rows.copy()).to(dev)
+    torch.manual_seed(0)
+    net = MfmaPolicyValueNetwork(PolicyValueNetwork().eval(), dev)
+    ps = ChessPuctSearch(eng, G, B, seed=1, leaves=False)
+    fn = lambda leaves, planes, counts: net(planes)  # noqa: E731
+    g = ps.capture(roots, S, fn, temperature=1.0)
+    g.replay()
+    torch.cuda.synchronize(dev)
+    t = time.perf_counter()
+    exp = 0
+    for _ in range(steps):
+        g.replay()
+        exp += int(ps.stats[:, 0].sum().item())
+    dt = time.perf_counter() - t
+    nfl = _native.check(_native.lib().zc_chess_puct_flushes(S, B))
+    fl = flops_per_position(128, 8, 17, 8, 8) * G * B * nfl * steps
+    eng.close()
+    return {"value": round(exp / dt, 1), "unit": "expansions/s", "ms_per_move": round(dt / steps * 1e3, 1),
+            "config": "C5 per GPU: 1024 games x 1600 sims, PUCT c 1.5, Dirichlet(0.3, 0.25), policy+value ResNet "
+                      "128x8 random init fp16 (MFMA tower), temperature 1",
+            "net_tflops_lower": round(fl / dt / 1e12, 1), "mfma_frac_lower": round(fl / dt / 1e12 / MFMA_F16_PEAK_TFLOPS, 4)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -271,6 +304,7 @@ def main():
         if world == 1 and args.net_steps > 0:
             out["extra"]["c2_value_net"] = net_mode(G, S, B, args.c, args.net_steps, dev)
             out["extra"]["c4_chess"] = chess_modes(args.net_steps, dev)
+            out["extra"]["c5_chess_puct"] = puct_mode(args.net_steps, dev)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(S, B, args.c)
         else:

@@ -233,6 +233,9 @@ int zc_chess_init(zc_chess_state *out);
  * (value_functions.py:48-55, configs/crude_chess.yaml) inside the kernel; batch_size <= 256. */
 #define ZC_POLICY_RANDOM 0
 #define ZC_POLICY_IMMEDIATE_VALUE 1
+/* Allocate the chess tree arena now (it is otherwise allocated by the first chess search —
+ * which must then not be inside a HIP-graph capture). */
+int zc_chess_reserve(zc_engine *eng);
 int zc_chess_search_async(zc_engine *eng, int32_t first_game, int32_t n_games, const zc_chess_state *d_roots,
                           int32_t sims, double c, int32_t batch_size, int32_t policy, double freedom,
                           uint16_t *d_out_move, int32_t *d_out_root_na, zc_game_stats *d_out_stats,

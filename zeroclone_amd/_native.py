@@ -100,6 +100,7 @@ SIGNATURES = [
                                                ctypes.c_void_p]),
     ("zc_chess_planes_async", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p,
                                              ctypes.c_int32, ctypes.c_void_p]),
+    ("zc_chess_reserve", ctypes.c_int, [ctypes.c_void_p]),
     ("zc_chess_search_async", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p,
                                              ctypes.c_int32, ctypes.c_double, ctypes.c_int32, ctypes.c_int32,
                                              ctypes.c_double, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
@@ -357,6 +358,9 @@ class NativeEngine:
                                           ZC_F16 if f16 else ZC_F32, ctypes.c_void_p(stream or None)))
 
     # ---- chess tree search (device pointers)
+    def chess_reserve(self):
+        check(lib().zc_chess_reserve(self._h))
+
     def chess_search_async(self, first_game: int, n: int, d_roots: int, sims: int, c: float, batch_size: int,
                            policy: int, freedom: float, d_move: int, d_na: int, d_stats: int, stream: int = 0):
         check(lib().zc_chess_search_async(self._h, first_game, n, ctypes.c_void_p(d_roots), int(sims), float(c),

@@ -593,6 +593,13 @@ int check_chess(zc_engine *e, int32_t first, int32_t n, int32_t sims, double c, 
 
 extern "C" {
 
+int zc_chess_reserve(zc_engine *eng) {
+    if (!eng) return fail(ZC_EINVAL, "null argument");
+    std::lock_guard<std::mutex> lk(eng->mu);
+    ZC_HIP(hipSetDevice(eng->cfg.device));
+    return ensure_chess(eng);
+}
+
 int zc_chess_search_async(zc_engine *eng, int32_t first, int32_t n, const zc_chess_state *d_roots, int32_t sims,
                           double c, int32_t bs, int32_t policy, double freedom, uint16_t *d_move, int32_t *d_na,
                           zc_game_stats *d_stats, void *hip_stream) {

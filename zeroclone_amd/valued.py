@@ -139,6 +139,7 @@ class ChessValuedSearch:
         if n_games > eng.max_games:
             raise ValueError(f"{n_games} games > engine capacity {eng.max_games}")
         self.eng, self.n, self.bs, self.policy, self.freedom = eng, n_games, batch_size, policy, freedom
+        eng.chess_reserve()   # the tree arena exists before any graph capture
         self.dev = torch.device("cuda", eng.device)
         L = n_games * batch_size
         self.leaves = torch.zeros((L, 72), dtype=torch.uint8, device=self.dev) if leaves else None
@@ -190,6 +191,7 @@ class ChessPuctSearch:
             raise ValueError(f"batch_size {batch_size} > engine max_batch {eng.max_batch}")
         self.eng, self.n, self.bs = eng, n_games, batch_size
         self.c, self.alpha, self.eps, self.seed = c_puct, dirichlet_alpha, dirichlet_eps, seed
+        eng.chess_reserve()   # the tree arena exists before any graph capture
         self.dev = torch.device("cuda", eng.device)
         L = n_games * batch_size
         self.leaves = torch.zeros((L, 72), dtype=torch.uint8, device=self.dev) if leaves else None
