@@ -35,7 +35,7 @@ __device__ __forceinline__ uint32_t mbcnt(uint64_t m) {  // set bits of m in lan
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
-// Inclusive prefix SUM over the 64 lanes (same DPP pattern as scan_or32).
+// Inclusive prefix SUM over the 64 lanes (DPP: row_shr 1,2,4,8, then row_bcast 15 / 31).
 __device__ __forceinline__ uint32_t scan_add32(uint32_t x) {
     x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, false);
     x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, false);
@@ -46,18 +46,25 @@ __device__ __forceinline__ uint32_t scan_add32(uint32_t x) {
     return x;
 }
 
-// Inclusive prefix OR over the 64 lanes (DPP: row_shr 1,2,4,8, then row_bcast 15 / 31).
-__device__ __forceinline__ uint32_t scan_or32(uint32_t x) {
+// LDS words of the rollout's compaction scratch: 64 compacted plies + 96 for lanes not written
+constexpr int kPermWords = 160;
+
+// Inclusive prefix OR within each 16-lane row (DPP row_shr 1, 2, 4, 8): four independent
+// 16-lane scans per wave.
+__device__ __forceinline__ uint32_t scan_or16(uint32_t x) {
     x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, false);
     x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, false);
     x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, false);
     x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, false);
-    x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false);
-    x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false);
     return x;
 }
-__device__ __forceinline__ uint64_t scan_or(uint64_t x) {
-    return ((uint64_t)scan_or32((uint32_t)(x >> 32)) << 32) | (uint64_t)scan_or32((uint32_t)x);
+
+// has_four restricted to two directions d1, d2 (per lane): a run of four along d exists
+// iff (m = b & b>>d) & (m >> 2d) != 0.
+__device__ __forceinline__ bool four_along(uint64_t b, uint32_t d1, uint32_t d2) {
+    const uint64_t m1 = b & (b >> d1);
+    const uint64_t m2 = b & (b >> d2);
+    return ((m1 & (m1 >> (2 * d1))) | (m2 & (m2 >> (2 * d2)))) != 0;
 }
 
 // Value.random_rollout (value_functions.py:35-45) for the nb pending leaves of one flush, in
@@ -69,13 +76,23 @@ __device__ __forceinline__ uint64_t scan_or(uint64_t x) {
 // Plies are simulated a BLOCK at a time.  While the legal set is unchanged (no column has
 // filled), the draws are exactly the window words w with (w >> (32-k)) < n, in stream
 // order — so one ballot yields the moves of every ply the window covers.  Lane k (an
-// accepted word) is ply q_k = #accepted lanes below it; its stone's row is the column
-// height plus #earlier accepted lanes in the same column; prefix-OR scans over the lanes
-// build each player's stones after every ply, and every lane tests check_win / full board
-// / column filled for ITS ply.  The first lane with an event ends the block (a fill changes
-// the legal set, so the next block restarts from the following word).
-__device__ void c4_rollouts(Leaf *L, int nb, Rng &rng, const uint32_t *s_order, Counters &cn) {
+// accepted word) is ply q_k = #accepted lanes below it; its column comes from the move
+// order, its row from the column height plus #earlier accepted lanes in the same column
+// (packed 4-bit per-column prefix sums).  The block ends at its first column fill or at the
+// board-full ply (both known without the win test), at its 32nd ply, or at the window's end.
+//
+// The win test runs on a COMPACTED copy of the block's plies: ply q goes (through 64 dwords
+// of LDS) to lane (q & 1)*16 + q/2 and to that lane + 32, so rows 0 and 2 hold the first
+// mover's plies in order, rows 1 and 3 the other side's.  One 16-lane prefix-OR scan per
+// row then gives every ply its mover's new stones (instead of two full-wave scans of both
+// parities), and the copy lets rows 0/1 test the vertical and horizontal directions while
+// rows 2/3 test the diagonals.  The first winning ply (if any) ends the rollout.
+__device__ void c4_rollouts(Leaf *L, int nb, Rng &rng, const uint32_t *s_order, uint32_t *s_perm, Counters &cn) {
     const uint32_t lane = lane_id();
+    const uint32_t lrow = lane >> 4;
+    const uint32_t myply = 2u * (lane & 15u) + (lrow & 1u);  // ply of this lane in the compacted layout
+    const bool first_row = (lrow & 1u) == 0;                  // rows 0, 2: the block's first mover
+    const uint32_t d1 = lrow < 2 ? 1u : 6u, d2 = lrow < 2 ? 7u : 8u;
     for (int j = 0; j < nb; ++j) {
         const uint64_t x0 = uni64(L[j].p0);
         const uint64_t x1 = uni64(L[j].p1);
@@ -111,19 +128,46 @@ __device__ void c4_rollouts(Leaf *L, int nb, Rng &rng, const uint32_t *s_order, 
                 const uint32_t same = ((scan_add32(one) - one) >> (4 * col)) & 15u;
                 const uint64_t occ = me | op;
                 const uint32_t h0 = (uint32_t)__popcll((occ >> (7 * col)) & 0x3Full);
-                const uint32_t row = min(h0 + same, 6u);
-                const uint64_t bit = acc ? (1ull << (7 * col + row)) : 0ull;
-                const bool even = (qk & 1u) == 0;
-                const uint64_t E = scan_or(even ? bit : 0ull);  // stones of the block's first mover
-                const uint64_t O = scan_or(even ? 0ull : bit);  // stones of the other side
-                const bool win = has_four(even ? (me | E) : (op | O));
-                const bool full = stones + (int)qk + 1 == 42;
-                const uint64_t W = __ballot(acc && win);
-                const uint64_t EV = W | __ballot(acc && (full || row == 5));
-                const int kend = EV ? __builtin_ctzll(EV) : 63 - __builtin_clzll(A);
-                const int np = __builtin_amdgcn_readlane((int)qk, kend) + 1;  // plies in this block
-                const uint64_t a2 = me | readlane64(E, kend);
-                const uint64_t b2 = op | readlane64(O, kend);
+                const uint32_t row = h0 + same;  // exact up to the block's first fill
+                // the block's last ply (before wins): its first column fill, the board-full
+                // ply, ply 31, or else the last accepted word
+                const uint32_t cap = min((uint32_t)(41 - stones), 31u);
+                const uint64_t E0 = __ballot(acc && (row == 5 || qk >= cap));
+                const uint32_t l0 = E0 ? (uint32_t)__builtin_ctzll(E0) : 0u;
+                const uint32_t last = E0 ? (uint32_t)__builtin_amdgcn_readlane((int)qk, (int)l0)
+                                         : (uint32_t)__popcll(A) - 1u;
+                // compact plies 0..last by parity (and a copy 32 lanes up); other lanes
+                // write to a scratch area above
+                const bool keep = acc && qk <= last;
+                const uint32_t t = keep ? (qk & 1u) * 16u + (qk >> 1) : 64u + lane;
+                const uint32_t b = 7u * col + row + 1u;
+                s_perm[t] = b;
+                s_perm[t + 32] = b;
+                wave_mem_order();
+                const uint32_t pb = s_perm[lane];
+                const bool valid = myply <= last;
+                const uint64_t bit = valid ? (1ull << (pb - 1u)) : 0ull;
+                const uint64_t mine = ((uint64_t)scan_or16((uint32_t)(bit >> 32)) << 32) |
+                                      (uint64_t)scan_or16((uint32_t)bit);  // this row's stones so far
+                const bool four = four_along((first_row ? me : op) | mine, d1, d2);
+                const uint64_t W = __ballot((int)valid & (int)four);
+                // back to word order: the accepted lane of ply qk won if its compacted lane did
+                const uint32_t W32 = (uint32_t)W | (uint32_t)(W >> 32);
+                const bool won_k = keep && ((W32 >> ((qk & 1u) * 16u + (qk >> 1))) & 1u);
+                const uint64_t E = __ballot(won_k) | (E0 & (~E0 + 1ull));
+                uint32_t endply, endlane = 0;
+                if (E) {
+                    endlane = (uint32_t)__builtin_ctzll(E);
+                    endply = (uint32_t)__builtin_amdgcn_readlane((int)qk, (int)endlane);
+                    rng.off = endlane + 1u;
+                } else {  // no event: the whole window is consumed
+                    endply = last;
+                    rng.off = kWin;
+                }
+                // both sides' stones after ply endply
+                const uint64_t a2 = me | readlane64(mine, (int)(endply >> 1));
+                const uint64_t b2 = endply ? op | readlane64(mine, 16 + (int)((endply - 1) >> 1)) : op;
+                const int np = (int)endply + 1;
                 if (np & 1) {
                     me = b2;
                     op = a2;
@@ -133,9 +177,7 @@ __device__ void c4_rollouts(Leaf *L, int nb, Rng &rng, const uint32_t *s_order, 
                 }
                 q += np;
                 stones += np;
-                rng.off = EV ? (uint32_t)kend + 1 : (uint32_t)kWin;
-                if (!EV) continue;
-                if ((W >> kend) & 1ull) {  // the ply's mover completed four
+                if (W) {  // the ply's mover completed four
                     val = (q & 1) ? 1 : -1;
                     break;
                 }
@@ -143,17 +185,21 @@ __device__ void c4_rollouts(Leaf *L, int nb, Rng &rng, const uint32_t *s_order, 
                     val = 0;
                     break;
                 }
-                // a column filled: the legal set (and its CPython order) changes
-                mask &= ~(1 << __builtin_amdgcn_readlane((int)col, kend));
-                ow = uni(s_order[mask]);
-                n = (ow >> 24) & 15u;
+                if (E) {
+                    const uint32_t rc = (uint32_t)__builtin_amdgcn_readlane((int)((row << 3) | col), (int)endlane);
+                    if ((rc >> 3) == 5u) {
+                        // a column filled: the legal set (and its CPython order) changes
+                        mask &= ~(1 << (rc & 7u));
+                        ow = uni(s_order[mask]);
+                        n = (ow >> 24) & 15u;
+                    }
+                }
             }
         }
         if (lane == 0) L[j].val = val;
         cn.add(cn.plies, q);
     }
 }
-
 
 // ------------------------------------------------------------------ the search kernel
 // STAMP = diagnostic build: lane 0 adds s_memtime deltas per phase into p.a.phase[g][0..7] =
@@ -169,6 +215,8 @@ __global__ __launch_bounds__(kBlock) void c4_search_kernel(SearchParams p) {
     Fresh *const fresh = (Fresh *)(s_dyn + kTabBytes);
     Leaf *const leaves = (Leaf *)(s_dyn + kTabBytes + sizeof(Fresh) * (size_t)p.bs);
     uint16_t *const paths = (uint16_t *)(s_dyn + kTabBytes + (sizeof(Fresh) + sizeof(Leaf)) * (size_t)p.bs);
+    uint32_t *const s_perm = (uint32_t *)(s_dyn + kTabBytes +
+                                          (sizeof(Fresh) + sizeof(Leaf) + sizeof(uint16_t) * kMaxDepth) * (size_t)p.bs);
     load_tables(s_order, s_sel);
     __syncthreads();
     // log(N) table read through the constant address space: uniform index -> scalar loads,
@@ -230,7 +278,7 @@ __global__ __launch_bounds__(kBlock) void c4_search_kernel(SearchParams p) {
         const int f0 = fs.f0, d0 = fs.d0;
 
         // ---- value.batch: random rollouts in pending order (mcts.cpp:112-124) ---------------
-        c4_rollouts(leaves, nb, rng, s_order, cn);
+        c4_rollouts(leaves, nb, rng, s_order, s_perm, cn);
         wave_mem_order();
         stamp.mark(4);
 
@@ -356,6 +404,7 @@ __global__ __launch_bounds__(kBlock) void c4_rollout_debug_kernel(Arena a, int f
     __shared__ Leaf s_leaf[1];
     __shared__ uint32_t s_order[128];
     __shared__ uint8_t s_sel[1024];
+    __shared__ uint32_t s_perm[kPermWords];
     load_tables(s_order, s_sel);
     __syncthreads();
     const uint32_t lane = lane_id();
@@ -373,7 +422,7 @@ __global__ __launch_bounds__(kBlock) void c4_rollout_debug_kernel(Arena a, int f
     }
     wave_mem_order();
     Counters cn;
-    c4_rollouts(s_leaf, 1, rng, s_order, cn);
+    c4_rollouts(s_leaf, 1, rng, s_order, s_perm, cn);
     wave_mem_order();
     if (lane == 0) {
         out_value[gl] = s_leaf[0].val;
@@ -388,6 +437,7 @@ __global__ __launch_bounds__(kBlock) void c4_rollout_seq_kernel(Arena a, int g, 
     __shared__ Leaf s_leaf[kBlock];
     __shared__ uint32_t s_order[128];
     __shared__ uint8_t s_sel[1024];
+    __shared__ uint32_t s_perm[kPermWords];
     load_tables(s_order, s_sel);
     __syncthreads();
     const uint32_t lane = lane_id();
@@ -405,7 +455,7 @@ __global__ __launch_bounds__(kBlock) void c4_rollout_seq_kernel(Arena a, int g, 
         }
         wave_mem_order();
         rng_fill(rng, rng.use() + kLookahead);
-        c4_rollouts(s_leaf, cnt, rng, s_order, cn);
+        c4_rollouts(s_leaf, cnt, rng, s_order, s_perm, cn);
         wave_mem_order();
         if ((int)lane < cnt) out_value[base + lane] = s_leaf[lane].val;
         wave_mem_order();
@@ -446,7 +496,7 @@ __global__ void uct_debug_kernel(int n, const double *logn, const int32_t *na, c
 }  // namespace
 
 size_t c4_search_lds_bytes(int bs) {
-    return kTabBytes + (sizeof(Leaf) + sizeof(Fresh) + sizeof(uint16_t) * kMaxDepth) * (size_t)bs;
+    return kTabBytes + (sizeof(Leaf) + sizeof(Fresh) + sizeof(uint16_t) * kMaxDepth) * (size_t)bs + kPermWords * sizeof(uint32_t);
 }
 
 void launch_c4_search(const SearchParams &p, hipStream_t s) {
