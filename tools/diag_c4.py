@@ -13,7 +13,7 @@ import numpy as np  # noqa: E402
 from zeroclone_amd import _native  # noqa: E402
 
 
-def timed(eng, G, S, B, reps=3):
+def timed(eng, G, S, B, reps=7):
     roots = np.zeros(G, _native.C4_STATE_DTYPE)
     eng.seed(0, list(range(G)))
     eng.c4_search(roots, S, 1.4, B)  # warm
@@ -22,7 +22,8 @@ def timed(eng, G, S, B, reps=3):
         t = time.perf_counter()
         mv, na, st = eng.c4_search(roots, S, 1.4, B)
         ts.append(time.perf_counter() - t)
-    return min(ts), st
+    ts.sort()
+    return ts[len(ts) // 2], st
 
 
 def main():
@@ -36,13 +37,16 @@ def main():
                   "words_per_leaf": round(st["rng_words"].sum() / st["leaves"].sum(), 2),
                   "blocks_per_leaf": round(st["rollout_blocks"].sum() / st["leaves"].sum(), 3)}
         print(G, res[G], flush=True)
-    eng.phase_cycles(True)
-    roots = np.zeros(4096, _native.C4_STATE_DTYPE)
-    eng.c4_search(roots, S, 1.4, B)
-    ph = eng.phase_cycles(False)
-    tot = sum(ph.values())
-    print("phase shares (4096 games, stamped build):", {k: round(v / tot, 4) for k, v in ph.items()},
-          "cycles/game/sim:", round(tot / 4096 / S, 1), flush=True)
+    for G in (4096, 256):
+        eng.phase_cycles(True)
+        roots = np.zeros(G, _native.C4_STATE_DTYPE)
+        eng.seed(0, list(range(G)))
+        eng.c4_search(roots, S, 1.4, B)
+        ph = eng.phase_cycles(False)
+        tot = sum(ph.values())
+        print(f"phase shares ({G} games, stamped build):", {k: round(v / tot, 4) for k, v in ph.items()},
+              "cycles/game/sim:", round(tot / G / S, 1),
+              "per phase:", {k: round(v / G / S, 1) for k, v in ph.items()}, flush=True)
     print(json.dumps(res))
 
 

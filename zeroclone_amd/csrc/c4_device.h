@@ -16,28 +16,18 @@ constexpr uint32_t kRingMask = kRingWords - 1;
 constexpr uint64_t kBottom = 0x0000040810204081ull;  // bit 7c: bottom cell of column c
 constexpr uint64_t kFull = kBottom * 0x3Full;        // the 42 playable cells
 constexpr uint64_t kTop = kBottom << 5;              // top playable cell of each column
-constexpr int kTabBytes = 128 * 4 + 128 * 8;  // LDS tables: move-list order[128], select[128][8]
+constexpr int kTabBytes = 128 * 4;  // LDS table: move-list order[128]
 
 // Untried moves of a node (record +4 / Fresh.u): bit i (i < 7) set while move i of the
 // node's move list is untried; bits 28..31 = number of moves.  The reference keeps the
 // untried INDICES in list order and lets random.choice pick the r-th (mcts.cpp:67-72); the
-// r-th remaining index is the r-th set bit of the mask (table sel[mask][r]).
+// r-th remaining index is the r-th set bit of the mask (one ballot over lanes 0..6).
 __device__ __forceinline__ uint32_t untried_init(uint32_t n) { return ((1u << n) - 1u) | (n << 28); }
 __device__ __forceinline__ uint32_t untried_count(uint32_t u) { return (uint32_t)__popc(u & 0x7Fu); }
 
-// Fill the LDS tables (whole wave): s_order = d_order, s_sel[m*8 + r] = r-th set bit of m.
-__device__ __forceinline__ void load_tables(uint32_t *s_order, uint8_t *s_sel) {
+// Fill the LDS table (whole workgroup): s_order = d_order.
+__device__ __forceinline__ void load_tables(uint32_t *s_order) {
     for (int i = (int)threadIdx.x; i < 128; i += blockDim.x) s_order[i] = d_order[i];
-    for (int i = (int)threadIdx.x; i < 1024; i += blockDim.x) {
-        const uint32_t m = (uint32_t)i >> 3, r = (uint32_t)i & 7u;
-        uint32_t x = m, c = 0, bitpos = 7;
-        for (uint32_t b = 0; b < 7; ++b)
-            if ((x >> b) & 1u) {
-                if (c == r) { bitpos = b; break; }
-                ++c;
-            }
-        s_sel[i] = (uint8_t)bitpos;
-    }
 }
 constexpr int kWin = 64;                             // RNG window: one word per lane
 
@@ -330,7 +320,7 @@ struct FlushSel {
 //             mcts.cpp:95 stores, so the UCT inputs are bit-identical.
 template <bool QW, bool STAMP>
 __device__ __forceinline__ void select_flush(const Tree &t, Fresh *fresh, Leaf *leaves, uint16_t *paths,
-                                             const uint32_t *s_order, const uint8_t *s_sel, ConstDouble *logtab,
+                                             const uint32_t *s_order, ConstDouble *logtab,
                                              Rng &rng, Counters &cn, Stamp<STAMP> &stamp, int &nnodes, int &status,
                                              uint64_t rp0, uint64_t rp1, int rturn, int done, int nb, double c,
                                              FlushSel &fs) {
@@ -425,7 +415,10 @@ __device__ __forceinline__ void select_flush(const Tree &t, Fresh *fresh, Leaf *
         const uint32_t cnt = untried_count(u);
         if (cnt) {  // expand (mcts.cpp:65-78): policy = random.choice(untried)
             const uint32_t r = rng_below(rng, cnt);
-            const int mi = (int)uni((uint32_t)s_sel[(u & 0x7Fu) * 8u + r]);
+            // the r-th untried move in bit order (lane b holds bit b of the untried mask)
+            const uint32_t um = u & 0x7Fu;
+            const int mi = __builtin_ctzll(
+                __ballot(lane < 7u && ((um >> (lane & 7u)) & 1u) && (uint32_t)__popc(um & ((1u << (lane & 7u)) - 1u)) == r));
             u &= ~(1u << mi);
             const int col = (int)((ow >> (3 * mi)) & 7u);
             const uint64_t bit = drop_bit(b0 | b1, col);
@@ -433,8 +426,11 @@ __device__ __forceinline__ void select_flush(const Tree &t, Fresh *fresh, Leaf *
             lturn = turn ^ 1;
             leaf = nnodes++;
             ldepth = depth + 1;
-            if (bit & kTop) lmask &= ~(1 << col);  // the column just filled
-            const uint32_t low_ = uni(s_order[lmask]);
+            uint32_t low_ = ow;  // the leaf's legal set is the node's unless the column filled
+            if (bit & kTop) {
+                lmask &= ~(1 << col);
+                low_ = uni(s_order[lmask]);
+            }
             if (k == (uint32_t)mi) ch = (uint32_t)leaf;
             if (node < f0) x0_dirty = true;  // X0 itself: written back when the flush is published
             if (lane == 0) {

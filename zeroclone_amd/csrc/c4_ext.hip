@@ -53,11 +53,10 @@ __global__ __launch_bounds__(kBlock) void c4_ext_begin_kernel(ExtParams p) {
 __global__ __launch_bounds__(kBlock) void c4_ext_select_kernel(ExtParams p) {
     extern __shared__ __attribute__((aligned(16))) uint8_t s_dyn[];
     uint32_t *const s_order = (uint32_t *)s_dyn;
-    uint8_t *const s_sel = s_dyn + 512;
     Fresh *const fresh = (Fresh *)(s_dyn + kTabBytes);
     Leaf *const leaves = (Leaf *)(s_dyn + kTabBytes + sizeof(Fresh) * (size_t)p.bs);
     uint16_t *const paths = (uint16_t *)(s_dyn + kTabBytes + (sizeof(Fresh) + sizeof(Leaf)) * (size_t)p.bs);
-    load_tables(s_order, s_sel);
+    load_tables(s_order);
     __syncthreads();
     ConstDouble *logtab = (ConstDouble *)p.a.logtab;
 
@@ -87,7 +86,7 @@ __global__ __launch_bounds__(kBlock) void c4_ext_select_kernel(ExtParams p) {
     Stamp<false> stamp;
     FlushSel fs;
     const zc_c4_state root = a.ext_roots[g];
-    select_flush<true, false>(t, fresh, leaves, paths, s_order, s_sel, logtab, rng, cn, stamp, nnodes, status,
+    select_flush<true, false>(t, fresh, leaves, paths, s_order, logtab, rng, cn, stamp, nnodes, status,
                               uni64(root.stones[0]), uni64(root.stones[1]), uni(root.turn), done, nb, p.c, fs);
     const int f0 = fs.f0;
 

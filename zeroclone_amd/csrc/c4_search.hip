@@ -31,6 +31,17 @@ __device__ __forceinline__ uint64_t readlane64(uint64_t x, int l) {
            (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)x, l);
 }
 
+// lane-wise select by a wave mask in SGPRs: bit `lane` of m set -> b, else a (or 0)
+__device__ __forceinline__ uint32_t mask_sel(uint64_t m, uint32_t a, uint32_t b) {
+    uint32_t r;
+    __asm__("v_cndmask_b32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(m));
+    return r;
+}
+__device__ __forceinline__ uint32_t mask_sel0(uint64_t m, uint32_t b) {
+    uint32_t r;
+    __asm__("v_cndmask_b32 %0, 0, %1, %2" : "=v"(r) : "v"(b), "s"(m));
+    return r;
+}
 __device__ __forceinline__ uint32_t mbcnt(uint64_t m) {  // set bits of m in lanes below this one
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
@@ -59,12 +70,25 @@ __device__ __forceinline__ uint32_t scan_or16(uint32_t x) {
     return x;
 }
 
-// has_four restricted to two directions d1, d2 (per lane): a run of four along d exists
-// iff (m = b & b>>d) & (m >> 2d) != 0.
-__device__ __forceinline__ bool four_along(uint64_t b, uint32_t d1, uint32_t d2) {
-    const uint64_t m1 = b & (b >> d1);
-    const uint64_t m2 = b & (b >> d2);
-    return ((m1 & (m1 >> (2 * d1))) | (m2 & (m2 >> (2 * d2)))) != 0;
+// Values that are the same in every lane but should live in VGPRs (worked on by the VALU):
+// the scalar unit is shared by the CU's four SIMDs and is the busier of the two here.
+__device__ __forceinline__ uint64_t in_vgpr(uint64_t x) {
+    __asm__("" : "+v"(x));
+    return x;
+}
+__device__ __forceinline__ uint32_t in_vgpr(uint32_t x) {
+    __asm__("" : "+v"(x));
+    return x;
+}
+// first set bit of a wave mask, 0xFFFFFFFF when empty (s_ff1_i32_b64)
+__device__ __forceinline__ uint32_t ff1(uint64_t m) {
+    uint32_t r;
+    __asm__("s_ff1_i32_b64 %0, %1" : "=s"(r) : "s"(m));
+    return r;
+}
+// DPP row_shr:1 with zero fill: the value of the previous lane of the 16-lane row (0 at its start)
+__device__ __forceinline__ uint32_t row_prev(uint32_t x) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, false);
 }
 
 // Value.random_rollout (value_functions.py:35-45) for the nb pending leaves of one flush, in
@@ -79,41 +103,50 @@ __device__ __forceinline__ bool four_along(uint64_t b, uint32_t d1, uint32_t d2)
 // accepted word) is ply q_k = #accepted lanes below it; its column comes from the move
 // order, its row from the column height plus #earlier accepted lanes in the same column
 // (packed 4-bit per-column prefix sums).  The block ends at its first column fill or at the
-// board-full ply (both known without the win test), at its 32nd ply, or at the window's end.
+// board-full ply (both known without the win test), at its 31st ply, or at its last
+// accepted word.
 //
 // The win test runs on a COMPACTED copy of the block's plies: ply q goes (through 64 dwords
 // of LDS) to lane (q & 1)*16 + q/2 and to that lane + 32, so rows 0 and 2 hold the first
 // mover's plies in order, rows 1 and 3 the other side's.  One 16-lane prefix-OR scan per
-// row then gives every ply its mover's new stones (instead of two full-wave scans of both
-// parities), and the copy lets rows 0/1 test the vertical and horizontal directions while
-// rows 2/3 test the diagonals.  The first winning ply (if any) ends the rollout.
+// row then gives every ply its mover's new stones, and the copy lets rows 0/1 test the
+// vertical and horizontal directions while rows 2/3 test the diagonals.  The first winning
+// ply (if any) ends the rollout.
+//
+// Work is placed for the scalar unit's sake: the boards are uniform values kept in VGPRs,
+// lane conditions are single compares whose ballots are used as v_cndmask masks, and the
+// scalar unit only handles the masks, the block's end and the loop control.
 __device__ void c4_rollouts(Leaf *L, int nb, Rng &rng, const uint32_t *s_order, uint32_t *s_perm, Counters &cn) {
     const uint32_t lane = lane_id();
     const uint32_t lrow = lane >> 4;
     const uint32_t myply = 2u * (lane & 15u) + (lrow & 1u);  // ply of this lane in the compacted layout
     const bool first_row = (lrow & 1u) == 0;                  // rows 0, 2: the block's first mover
     const uint32_t d1 = lrow < 2 ? 1u : 6u, d2 = lrow < 2 ? 7u : 8u;
+    const uint32_t hd = (0x08070601u >> (8u * (lane & 3u))) & 0xFFu;  // lanes 0..3: one direction each
     for (int j = 0; j < nb; ++j) {
-        const uint64_t x0 = uni64(L[j].p0);
-        const uint64_t x1 = uni64(L[j].p1);
         const uint32_t lm = uni(L[j].meta);
-        const int tn = (int)((lm >> 24) & 1u);
+        const uint64_t x0 = in_vgpr(L[j].p0);
+        const uint64_t x1 = in_vgpr(L[j].p1);
+        const bool tn = (lm >> 24) & 1u;
         uint64_t me = tn ? x1 : x0;  // side to move
         uint64_t op = tn ? x0 : x1;  // last mover
         int val = 0;
         int q = 0;  // plies played in this rollout
-        if (has_four(op)) {
+        const uint64_t hm = op & (op >> hd);
+        const int room0 = 41 - (int)uni((uint32_t)__popcll(me | op));  // 41 - stones
+        if (__ballot(lane < 4u && (hm & (hm >> (2u * hd))) != 0)) {  // has_four(last mover)
             val = -1;
-        } else if ((me | op) != kFull) {
+        } else if (room0 >= 0) {  // not check_draw
+            int room = room0;
             int mask = (int)(lm >> 25);
             uint32_t ow = uni(s_order[mask]);
             uint32_t n = (ow >> 24) & 15u;
-            int stones = __popcll(me | op);
+            uint32_t sh = (uint32_t)__clz(n);
             for (;;) {
                 if (rng.off >= (uint32_t)kWin) rng_advance(rng);
-                const uint32_t v = rng.wt >> __clz(n);
-                const bool acc = lane >= rng.off && v < n;
-                const uint64_t A = __ballot(acc);
+                const uint32_t v = rng.wt >> sh;
+                // accepted words: v < n, at or after the next unconsumed word
+                const uint64_t A = __ballot((v | ((lane - rng.off) & 0x80000000u)) < n);
                 if (!A) {
                     rng.off = kWin;
                     continue;
@@ -124,75 +157,69 @@ __device__ void c4_rollouts(Leaf *L, int nb, Rng &rng, const uint32_t *s_order, 
                 // earlier plies in the same column: 4-bit per-column counters, prefix-summed
                 // (a nibble can only overflow past 15 plies in one column, i.e. after that
                 // column filled — beyond the block's first event, so never read)
-                const uint32_t one = acc ? (1u << (4 * col)) : 0u;
+                const uint32_t one = mask_sel0(A, 1u << (4 * col));
                 const uint32_t same = ((scan_add32(one) - one) >> (4 * col)) & 15u;
-                const uint64_t occ = me | op;
-                const uint32_t h0 = (uint32_t)__popcll((occ >> (7 * col)) & 0x3Full);
+                const uint32_t h0 = (uint32_t)__popcll(((me | op) >> (7 * col)) & 0x3Full);
                 const uint32_t row = h0 + same;  // exact up to the block's first fill
-                // the block's last ply (before wins): its first column fill, the board-full
-                // ply, ply 31, or else the last accepted word
-                const uint32_t cap = min((uint32_t)(41 - stones), 31u);
-                const uint64_t E0 = __ballot(acc && (row == 5 || qk >= cap));
-                const uint32_t l0 = E0 ? (uint32_t)__builtin_ctzll(E0) : 0u;
-                const uint32_t last = E0 ? (uint32_t)__builtin_amdgcn_readlane((int)qk, (int)l0)
-                                         : (uint32_t)__popcll(A) - 1u;
+                // the block's last ply before any win: its first column fill, the board-full
+                // ply, ply 30, or its last accepted word (so there always is one)
+                const uint32_t nacc = (uint32_t)__popc(in_vgpr((uint32_t)A)) + (uint32_t)__popc(in_vgpr((uint32_t)(A >> 32)));
+                const uint32_t cap = min(min((uint32_t)room, 30u), nacc - 1u);
+                const bool fills = row == 5u;
+                const uint64_t R5 = __ballot(fills);
+                const uint64_t E0 = __ballot(mask_sel0(A, (fills ? 63u : qk) + 1u) > cap);
+                const uint32_t l0 = (uint32_t)__builtin_ctzll(E0);
+                const uint32_t last = (uint32_t)__builtin_amdgcn_readlane((int)qk, (int)l0);
+                const uint64_t K = __ballot(mask_sel(A, 255u, qk) <= last);  // lanes of plies 0..last
                 // compact plies 0..last by parity (and a copy 32 lanes up); other lanes
                 // write to a scratch area above
-                const bool keep = acc && qk <= last;
-                const uint32_t t = keep ? (qk & 1u) * 16u + (qk >> 1) : 64u + lane;
+                const uint32_t c = (qk & 1u) * 16u + (qk >> 1);
+                const uint32_t t = mask_sel(K, 64u + lane, c);
                 const uint32_t b = 7u * col + row + 1u;
                 s_perm[t] = b;
                 s_perm[t + 32] = b;
                 wave_mem_order();
                 const uint32_t pb = s_perm[lane];
-                const bool valid = myply <= last;
-                const uint64_t bit = valid ? (1ull << (pb - 1u)) : 0ull;
-                const uint64_t mine = ((uint64_t)scan_or16((uint32_t)(bit >> 32)) << 32) |
-                                      (uint64_t)scan_or16((uint32_t)bit);  // this row's stones so far
-                const bool four = four_along((first_row ? me : op) | mine, d1, d2);
-                const uint64_t W = __ballot((int)valid & (int)four);
+                const uint64_t V = __ballot(myply <= last);  // lanes holding plies 0..last
+                const uint64_t bit = 1ull << (pb - 1u);
+                const uint32_t blo = scan_or16(mask_sel0(V, (uint32_t)bit));
+                const uint32_t bhi = scan_or16(mask_sel0(V, (uint32_t)(bit >> 32)));
+                const uint64_t mine = ((uint64_t)bhi << 32) | blo;  // this row's stones so far
+                const uint64_t bd = (first_row ? me : op) | mine;
+                const uint64_t m1 = bd & (bd >> d1), m2 = bd & (bd >> d2);
+                const uint64_t f4 = (m1 & (m1 >> (2 * d1))) | (m2 & (m2 >> (2 * d2)));
+                const uint64_t W = __ballot(mask_sel0(V, (uint32_t)f4 | (uint32_t)(f4 >> 32)) != 0u);
                 // back to word order: the accepted lane of ply qk won if its compacted lane did
                 const uint32_t W32 = (uint32_t)W | (uint32_t)(W >> 32);
-                const bool won_k = keep && ((W32 >> ((qk & 1u) * 16u + (qk >> 1))) & 1u);
-                const uint64_t E = __ballot(won_k) | (E0 & (~E0 + 1ull));
-                uint32_t endply, endlane = 0;
-                if (E) {
-                    endlane = (uint32_t)__builtin_ctzll(E);
-                    endply = (uint32_t)__builtin_amdgcn_readlane((int)qk, (int)endlane);
-                    rng.off = endlane + 1u;
-                } else {  // no event: the whole window is consumed
-                    endply = last;
-                    rng.off = kWin;
-                }
-                // both sides' stones after ply endply
+                const uint64_t Ew = __ballot(mask_sel0(K, (W32 >> c) & 1u) != 0u);
+                const uint32_t endlane = min(ff1(Ew), l0);
+                const uint32_t endply = (uint32_t)__builtin_amdgcn_readlane((int)qk, (int)endlane);
+                rng.off = endlane + 1u;  // words through the block's last ply are consumed
+                // both sides' stones after ply endply: first mover through ply 2*(endply/2)
+                // (row 0, inclusive), second mover through the odd plies <= endply (row 1,
+                // exclusive: lane 16 + (endply+1)/2; zero at the row's start)
+                const uint64_t prev = ((uint64_t)row_prev(bhi) << 32) | row_prev(blo);
                 const uint64_t a2 = me | readlane64(mine, (int)(endply >> 1));
-                const uint64_t b2 = endply ? op | readlane64(mine, 16 + (int)((endply - 1) >> 1)) : op;
-                const int np = (int)endply + 1;
-                if (np & 1) {
-                    me = b2;
-                    op = a2;
-                } else {
-                    me = a2;
-                    op = b2;
-                }
-                q += np;
-                stones += np;
-                if (W) {  // the ply's mover completed four
+                const uint64_t b2 = op | readlane64(prev, (int)((endply + 33u) >> 1));
+                const bool odd = endply & 1u;  // an even number of plies: the first mover is to move again
+                me = odd ? a2 : b2;
+                op = odd ? b2 : a2;
+                q += (int)endply + 1;
+                room -= (int)endply + 1;
+                if (Ew) {  // the ply's mover completed four
                     val = (q & 1) ? 1 : -1;
                     break;
                 }
-                if (stones >= 42) {  // check_draw: board full
+                if (room < 0) {  // check_draw: board full
                     val = 0;
                     break;
                 }
-                if (E) {
-                    const uint32_t rc = (uint32_t)__builtin_amdgcn_readlane((int)((row << 3) | col), (int)endlane);
-                    if ((rc >> 3) == 5u) {
-                        // a column filled: the legal set (and its CPython order) changes
-                        mask &= ~(1 << (rc & 7u));
-                        ow = uni(s_order[mask]);
-                        n = (ow >> 24) & 15u;
-                    }
+                if ((R5 >> endlane) & 1u) {
+                    // a column filled: the legal set (and its CPython order) changes
+                    mask &= ~(1 << __builtin_amdgcn_readlane((int)col, (int)endlane));
+                    ow = uni(s_order[mask]);
+                    n = (ow >> 24) & 15u;
+                    sh = (uint32_t)__clz(n);
                 }
             }
         }
@@ -208,16 +235,15 @@ __device__ void c4_rollouts(Leaf *L, int nb, Rng &rng, const uint32_t *s_order, 
 template <bool STAMP>
 __global__ __launch_bounds__(kBlock) void c4_search_kernel(SearchParams p) {
     extern __shared__ __attribute__((aligned(16))) uint8_t s_dyn[];
-    // LDS: tables (order[128] u32, sel[128][8] u8), fresh[bs] (48 B), leaves[bs] (24 B),
+    // LDS: order[128] u32, fresh[bs] (48 B), leaves[bs] (24 B),
     //      paths[bs][kMaxDepth] (u16 node ids)
     uint32_t *const s_order = (uint32_t *)s_dyn;
-    uint8_t *const s_sel = s_dyn + 512;
     Fresh *const fresh = (Fresh *)(s_dyn + kTabBytes);
     Leaf *const leaves = (Leaf *)(s_dyn + kTabBytes + sizeof(Fresh) * (size_t)p.bs);
     uint16_t *const paths = (uint16_t *)(s_dyn + kTabBytes + (sizeof(Fresh) + sizeof(Leaf)) * (size_t)p.bs);
     uint32_t *const s_perm = (uint32_t *)(s_dyn + kTabBytes +
                                           (sizeof(Fresh) + sizeof(Leaf) + sizeof(uint16_t) * kMaxDepth) * (size_t)p.bs);
-    load_tables(s_order, s_sel);
+    load_tables(s_order);
     __syncthreads();
     // log(N) table read through the constant address space: uniform index -> scalar loads,
     // which do not sit in the vector-memory counter the walk and the RNG window wait on.
@@ -271,7 +297,7 @@ __global__ __launch_bounds__(kBlock) void c4_search_kernel(SearchParams p) {
         {
             // the root position, re-read every flush rather than held in registers
             const zc_c4_state root = p.roots[gl];
-            select_flush<false, STAMP>(t, fresh, leaves, paths, s_order, s_sel, logtab, rng, cn, stamp, nnodes,
+            select_flush<false, STAMP>(t, fresh, leaves, paths, s_order, logtab, rng, cn, stamp, nnodes,
                                        status, uni64(root.stones[0]), uni64(root.stones[1]), uni(root.turn), done,
                                        nb, p.c, fs);
         }
@@ -403,9 +429,8 @@ __global__ __launch_bounds__(kBlock) void c4_rollout_debug_kernel(Arena a, int f
                                                                   int64_t *out_words) {
     __shared__ Leaf s_leaf[1];
     __shared__ uint32_t s_order[128];
-    __shared__ uint8_t s_sel[1024];
     __shared__ uint32_t s_perm[kPermWords];
-    load_tables(s_order, s_sel);
+    load_tables(s_order);
     __syncthreads();
     const uint32_t lane = lane_id();
     const int gl = blockIdx.x;
@@ -436,9 +461,8 @@ __global__ __launch_bounds__(kBlock) void c4_rollout_seq_kernel(Arena a, int g, 
                                                                 int32_t *out_value, int64_t *out_words) {
     __shared__ Leaf s_leaf[kBlock];
     __shared__ uint32_t s_order[128];
-    __shared__ uint8_t s_sel[1024];
     __shared__ uint32_t s_perm[kPermWords];
-    load_tables(s_order, s_sel);
+    load_tables(s_order);
     __syncthreads();
     const uint32_t lane = lane_id();
     Rng rng;
