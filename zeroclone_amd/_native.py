@@ -428,8 +428,8 @@ class NativeEngine:
     def phase_cycles(self, enable: bool):
         out = (ctypes.c_int64 * 8)()
         check(lib().zc_debug_phase_cycles(self._h, int(bool(enable)), out))
-        return dict(zip(["rng", "walk_first", "walk_resumed", "expand", "rollout", "backup", "publish"],
-                        list(out)[:7]))
+        return dict(zip(["rng", "walk_first", "walk_resumed", "expand", "rollout", "backup", "publish", "sub"],
+                        list(out)))
 
     def debug_c4_rollout(self, states: np.ndarray, first_game: int = 0):
         states = np.ascontiguousarray(states, dtype=C4_STATE_DTYPE)

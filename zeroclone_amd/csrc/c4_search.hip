@@ -61,13 +61,17 @@ __device__ __forceinline__ uint32_t scan_add32(uint32_t x) {
 constexpr int kPermWords = 160;
 
 // Inclusive prefix OR within each 16-lane row (DPP row_shr 1, 2, 4, 8): four independent
-// 16-lane scans per wave.
-__device__ __forceinline__ uint32_t scan_or16(uint32_t x) {
+// 16-lane scans per wave, of two values at once (the two halves of a bitboard), interleaved
+// so that each DPP read finds its operand written two instructions earlier.
+__device__ __forceinline__ void scan_or16x2(uint32_t &x, uint32_t &y) {
     x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, false);
+    y |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)y, 0x111, 0xF, 0xF, false);
     x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, false);
+    y |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)y, 0x112, 0xF, 0xF, false);
     x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, false);
+    y |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)y, 0x114, 0xF, 0xF, false);
     x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, false);
-    return x;
+    y |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)y, 0x118, 0xF, 0xF, false);
 }
 
 // Values that are the same in every lane but should live in VGPRs (worked on by the VALU):
@@ -182,8 +186,8 @@ __device__ void c4_rollouts(Leaf *L, int nb, Rng &rng, const uint32_t *s_order, 
                 const uint32_t pb = s_perm[lane];
                 const uint64_t V = __ballot(myply <= last);  // lanes holding plies 0..last
                 const uint64_t bit = 1ull << (pb - 1u);
-                const uint32_t blo = scan_or16(mask_sel0(V, (uint32_t)bit));
-                const uint32_t bhi = scan_or16(mask_sel0(V, (uint32_t)(bit >> 32)));
+                uint32_t blo = mask_sel0(V, (uint32_t)bit), bhi = mask_sel0(V, (uint32_t)(bit >> 32));
+                scan_or16x2(blo, bhi);
                 const uint64_t mine = ((uint64_t)bhi << 32) | blo;  // this row's stones so far
                 const uint64_t bd = (first_row ? me : op) | mine;
                 const uint64_t m1 = bd & (bd >> d1), m2 = bd & (bd >> d2);
