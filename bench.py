@@ -174,6 +174,28 @@ def puct_mode(steps: int, dev) -> dict:
             "net_tflops_lower": round(fl / dt / 1e12, 1), "mfma_frac_lower": round(fl / dt / 1e12 / MFMA_F16_PEAK_TFLOPS, 4)}
 
 
+def philox_mode(eng, step, evs, acc, args, G: int, dev) -> dict:
+    """C2(ii): the same self-play steps with ZC_ROLLOUT_PHILOX (leaf-parallel rollouts on
+    per-leaf Philox-seeded streams; statistical parity, tests/test_gpu_philox.py)."""
+    eng.c4_rollout_mode("philox", args.seed + 0xC2)
+    try:
+        step()
+        torch.cuda.synchronize(dev)
+        acc.zero_()
+        t0 = time.perf_counter()
+        for k in range(args.steps):
+            step(evs[k])
+        torch.cuda.synchronize(dev)
+        dt = time.perf_counter() - t0
+    finally:
+        eng.c4_rollout_mode("exact")
+    kernel_ms = [a.elapsed_time(b) for a, b in evs]
+    expansions = int(acc[0].item())
+    return {"value": round(expansions / dt, 1), "unit": "expansions/s", "ms_per_step": round(dt / args.steps * 1e3, 3),
+            "search_ms_per_step": [round(x, 3) for x in kernel_ms], "expansions": expansions,
+            "config": f"C2(ii) {G} games x {args.sims} sims, batch {args.batch}: Philox rollout mode"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -301,7 +323,26 @@ def main():
             "extra": {"expansions": expansions, "leaves": leaves, "mean_depth": round(depth_sum / max(expansions, 1), 3),
                       "games_finished": finished, "search_ms_per_step": [round(x, 3) for x in kernel_ms]},
         }
+        # per-phase times (s_memtime stamps, one extra search with the stamped
+        # kernel; shares applied to the unstamped launch time) and the tree-walk-only roofline
+        # (select + expand-write + backup + publish; rollouts are integer VALU, not HBM).
+        eng.phase_cycles(True)
+        eng.c4_search_async(roots.data_ptr(), G, S, args.c, B, moves.data_ptr(), na.data_ptr(), stats.data_ptr(),
+                            stream=torch_stream.cuda_stream)
+        torch.cuda.synchronize(dev)
+        ph = eng.phase_cycles(False)
+        tot_c = max(sum(ph.values()), 1)
+        share = {k: v / tot_c for k, v in ph.items() if k != "sub"}
+        walk = sum(share[k] for k in ("rng", "walk_first", "walk_resumed", "expand", "backup", "publish"))
+        out["extra"]["phases"] = {
+            "share": {k: round(v, 4) for k, v in share.items()},
+            "ms_per_launch": {k: round(v * avg_kernel_s * 1e3, 3) for k, v in share.items()},
+            "walk_roofline": {"t_walk_ms": round(walk * avg_kernel_s * 1e3, 3),
+                              "achieved": round(bytes_launch / (walk * avg_kernel_s) / 1e9, 2),
+                              "frac": round(bytes_launch / (walk * avg_kernel_s) / 1e9 / HBM_PEAK_GBS, 5),
+                              "note": "SURVEY §8(d) roofline definition: model bytes / tree-walk time only"}}
         if world == 1 and args.net_steps > 0:
+            out["extra"]["c2_philox"] = philox_mode(eng, step, evs, acc, args, G, dev)
             out["extra"]["c2_value_net"] = net_mode(G, S, B, args.c, args.net_steps, dev)
             out["extra"]["c4_chess"] = chess_modes(args.net_steps, dev)
             out["extra"]["c5_chess_puct"] = puct_mode(args.net_steps, dev)

@@ -103,6 +103,20 @@ int zc_c4_search_async(zc_engine *eng, int32_t first_game, int32_t n_games, cons
                        int32_t *d_out_move, int32_t *d_out_root_na, zc_game_stats *d_out_stats,
                        void *hip_stream);
 
+/* Random source of the Connect4 search's rollouts (all zc_c4_search* calls that follow):
+ *   ZC_ROLLOUT_EXACT (default) — the game's CPython MT19937 stream in the reference's order;
+ *     results are bit-identical to mcts.get_move.
+ *   ZC_ROLLOUT_PHILOX — SURVEY §8(d) C2(ii) "rollout fast mode": the same random playout
+ *     (uniform legal moves until a win or a full board, value_functions.py:35-45), but each
+ *     leaf draws from its own xoshiro128** stream seeded by Philox4x32-10(counter = (leaf's
+ *     simulation index, game's MT position at the search's start, game, 0x0C4F0A57), key =
+ *     seed), so a flush's leaves roll out in parallel.  Expansion draws still come from the
+ *     game's MT stream.  Statistical parity with the reference only (same distribution of
+ *     playouts, different numbers); specification: tests/c4_philox_ref.py. */
+#define ZC_ROLLOUT_EXACT 0
+#define ZC_ROLLOUT_PHILOX 1
+int zc_c4_set_rollout_mode(zc_engine *eng, int32_t mode, uint64_t seed);
+
 /* Engine.play_move + Engine._evaluate on the device for n games (engine/engine.py:98-108,
  * 148-153): states[i] = c4_backend.play_move(states[i], (moves[i], 0)) and
  *   results[i] = turn*2-1 if check_win (i.e. +1 when 'X' just won), 0 if check_draw, else

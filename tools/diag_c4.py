@@ -37,6 +37,20 @@ def main():
                   "words_per_leaf": round(st["rng_words"].sum() / st["leaves"].sum(), 2),
                   "blocks_per_leaf": round(st["rollout_blocks"].sum() / st["leaves"].sum(), 3)}
         print(G, res[G], flush=True)
+    eng.c4_rollout_mode("philox", 12345)
+    for G in (4096, 16384):
+        t, st = timed(eng, G, S, B)
+        print("philox", G, {"ms": round(t * 1e3, 3), "Mexp_s": round(st["expansions"].sum() / t / 1e6, 2),
+                            "plies_per_leaf": round(st["rollout_plies"].sum() / st["leaves"].sum(), 2)}, flush=True)
+    eng.phase_cycles(True)
+    roots = np.zeros(4096, _native.C4_STATE_DTYPE)
+    eng.seed(0, list(range(4096)))
+    eng.c4_search(roots, S, 1.4, B)
+    ph = eng.phase_cycles(False)
+    tot = sum(ph.values())
+    print("philox phase shares (4096 games):", {k: round(v / tot, 4) for k, v in ph.items()},
+          "cycles/game/sim:", round(tot / 4096 / S, 1), flush=True)
+    eng.c4_rollout_mode("exact")
     for G in (4096, 256):
         eng.phase_cycles(True)
         roots = np.zeros(G, _native.C4_STATE_DTYPE)

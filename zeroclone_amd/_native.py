@@ -22,6 +22,8 @@ ZC_ECAPACITY = -4
 ZC_EDEVICE = -5
 ZC_C4_ONGOING = 2
 ZC_STATUS_NO_MOVES = 1
+ROLLOUT_EXACT = 0   # ZC_ROLLOUT_EXACT
+ROLLOUT_PHILOX = 1  # ZC_ROLLOUT_PHILOX
 ZC_STATUS_BAD_STATE = 2
 ZC_F32 = 0
 ZC_F16 = 1
@@ -74,6 +76,7 @@ SIGNATURES = [
     ("zc_c4_search_games", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p,
                                           ctypes.c_int32, ctypes.c_double, ctypes.c_int32, ctypes.c_void_p,
                                           ctypes.c_void_p, ctypes.c_void_p]),
+    ("zc_c4_set_rollout_mode", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_uint64]),
     ("zc_c4_search_async", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p,
                                           ctypes.c_int32, ctypes.c_double, ctypes.c_int32, ctypes.c_void_p,
                                           ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
@@ -301,6 +304,12 @@ class NativeEngine:
         check(lib().zc_c4_search_games(self._h, n, _ptr(ids), _ptr(roots), int(sims), float(c), int(batch_size),
                                        _ptr(mv), _ptr(na), _ptr(st)))
         return mv, na, st
+
+    def c4_rollout_mode(self, mode: str = "exact", seed: int = 0) -> None:
+        """"exact" (the game's MT19937 stream, bit-identical to the reference) or "philox"
+        (leaf-parallel rollouts on per-leaf counter-based streams; statistical parity only)."""
+        m = {"exact": ROLLOUT_EXACT, "philox": ROLLOUT_PHILOX}[mode]
+        check(lib().zc_c4_set_rollout_mode(self._h, m, int(seed) & (2**64 - 1)))
 
     def c4_search_async(self, d_roots: int, n: int, sims: int, c: float, batch_size: int, d_move: int, d_na: int,
                         d_stats: int, stream: int = 0, first_game: int = 0) -> None:

@@ -21,6 +21,7 @@
 // The whole move (every flush of `batch_size` leaves) runs in one launch; games never
 // synchronise with each other.
 #include "c4_device.h"
+#include "counter_rng.h"
 
 namespace zc {
 namespace {
@@ -232,11 +233,85 @@ __device__ void c4_rollouts(Leaf *L, int nb, Rng &rng, const uint32_t *s_order, 
     }
 }
 
+// Philox rollout mode ("rollout fast mode", statistical parity only).
+// Value.random_rollout's game (value_functions.py:35-45) — uniform random legal moves until
+// check_win (last mover) or check_draw — with the random numbers taken from a per-leaf
+// counter-based stream instead of the game's one MT19937 stream.  Leaves no longer depend on
+// each other, so the flush's leaves roll out in parallel, one per lane.  Leaf j of the flush
+// that starts at simulation `leaf0` seeds xoshiro128** with Philox4x32-10(counter = (leaf0 +
+// j, tag, game, 0x0C4F0A57), key = seed), tag = the game's MT position at the search's start
+// (a different stream every move); each ply takes one draw u and plays the k-th legal column
+// in ascending order, k = (u * n) >> 32.  Specification: tests/c4_philox_ref.py.
+__device__ void c4_rollouts_philox(Leaf *L, int nb, const uint8_t *s_sel, uint2 key, uint32_t leaf0, uint32_t tag,
+                                   uint32_t game, Counters &cn) {
+    const uint32_t lane = lane_id();
+    for (int base = 0; base < nb; base += kBlock) {
+        const int j = base + (int)lane;
+        int val = 0, q = 0;
+        if (j < nb) {
+            const uint64_t x0 = L[j].p0, x1 = L[j].p1;
+            const bool tn = (L[j].meta >> 24) & 1u;
+            uint64_t me = tn ? x1 : x0;  // side to move
+            uint64_t op = tn ? x0 : x1;  // last mover
+            int stones = __popcll(me | op);
+            if (has_four(op)) {
+                val = -1;
+            } else if (stones < 42) {
+                uint32_t legal = (uint32_t)legal_mask(me | op);
+                const uint4 sd = philox(make_uint4(leaf0 + (uint32_t)j, tag, game, 0x0C4F0A57u), key);
+                Xoshiro128 x{sd.x | ((sd.x | sd.y | sd.z | sd.w) == 0u), sd.y, sd.z, sd.w};
+                for (;;) {
+                    const uint32_t n = (uint32_t)__popc(legal);
+                    const uint32_t k = __umulhi(x.next(), n);
+                    const uint32_t col = s_sel[legal * 8u + k];
+                    const uint32_t h = (uint32_t)__popcll(((me | op) >> (7u * col)) & 0x3Full);
+                    me |= 1ull << (7u * col + h);
+                    ++q;
+                    ++stones;
+                    if (h == 5u) legal &= ~(1u << col);
+                    if (has_four(me)) {  // the ply's mover completed four
+                        val = (q & 1) ? 1 : -1;
+                        break;
+                    }
+                    if (stones == 42) {  // check_draw
+                        val = 0;
+                        break;
+                    }
+                    const uint64_t t = me;
+                    me = op;
+                    op = t;
+                }
+            }
+            L[j].val = val;
+        }
+        int tot = q;
+        for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o);
+        cn.add(cn.plies, tot);
+    }
+}
+
+// s_sel[m*8 + r] = the r-th set bit of the 7-bit column mask m (Philox mode's move pick).
+__device__ __forceinline__ void load_sel(uint8_t *s_sel) {
+    for (int i = (int)threadIdx.x; i < 1024; i += blockDim.x) {
+        const uint32_t m = (uint32_t)i >> 3, r = (uint32_t)i & 7u;
+        uint32_t c = 0, pos = 7;
+        for (uint32_t b = 0; b < 7; ++b)
+            if ((m >> b) & 1u) {
+                if (c == r) {
+                    pos = b;
+                    break;
+                }
+                ++c;
+            }
+        s_sel[i] = (uint8_t)pos;
+    }
+}
+
 // ------------------------------------------------------------------ the search kernel
 // STAMP = diagnostic build: lane 0 adds s_memtime deltas per phase into p.a.phase[g][0..7] =
 // {rng generation at flush start, first walk of a flush, resumed walks, expansion + leaf
 //  bookkeeping, rollouts, backup, publish, -}.
-template <bool STAMP>
+template <bool STAMP, bool PHILOX>
 __global__ __launch_bounds__(kBlock) void c4_search_kernel(SearchParams p) {
     extern __shared__ __attribute__((aligned(16))) uint8_t s_dyn[];
     // LDS: order[128] u32, fresh[bs] (48 B), leaves[bs] (24 B),
@@ -247,7 +322,9 @@ __global__ __launch_bounds__(kBlock) void c4_search_kernel(SearchParams p) {
     uint16_t *const paths = (uint16_t *)(s_dyn + kTabBytes + (sizeof(Fresh) + sizeof(Leaf)) * (size_t)p.bs);
     uint32_t *const s_perm = (uint32_t *)(s_dyn + kTabBytes +
                                           (sizeof(Fresh) + sizeof(Leaf) + sizeof(uint16_t) * kMaxDepth) * (size_t)p.bs);
+    uint8_t *const s_sel = (uint8_t *)(s_perm + kPermWords);  // Philox mode only
     load_tables(s_order);
+    if (PHILOX) load_sel(s_sel);
     __syncthreads();
     // log(N) table read through the constant address space: uniform index -> scalar loads,
     // which do not sit in the vector-memory counter the walk and the RNG window wait on.
@@ -280,6 +357,7 @@ __global__ __launch_bounds__(kBlock) void c4_search_kernel(SearchParams p) {
 
     Rng rng;
     rng_open(rng, a.ring + (size_t)g * kRingWords, uni64(a.rngpos[2 * (size_t)g]), uni64(a.rngpos[2 * (size_t)g + 1]));
+    const uint32_t tag = uni((uint32_t)a.rngpos[2 * (size_t)g]);  // Philox mode: stream per move
     Counters cn;
     int status = 0;
 
@@ -308,7 +386,11 @@ __global__ __launch_bounds__(kBlock) void c4_search_kernel(SearchParams p) {
         const int f0 = fs.f0, d0 = fs.d0;
 
         // ---- value.batch: random rollouts in pending order (mcts.cpp:112-124) ---------------
-        c4_rollouts(leaves, nb, rng, s_order, s_perm, cn);
+        if (PHILOX)
+            c4_rollouts_philox(leaves, nb, s_sel, make_uint2((uint32_t)p.philox_seed, (uint32_t)(p.philox_seed >> 32)),
+                               (uint32_t)done, tag, (uint32_t)g, cn);
+        else
+            c4_rollouts(leaves, nb, rng, s_order, s_perm, cn);
         wave_mem_order();
         stamp.mark(4);
 
@@ -528,11 +610,19 @@ size_t c4_search_lds_bytes(int bs) {
 }
 
 void launch_c4_search(const SearchParams &p, hipStream_t s) {
-    const size_t lds = c4_search_lds_bytes(p.bs);
-    if (p.stamp)
-        hipLaunchKernelGGL(c4_search_kernel<true>, dim3(p.n_games), dim3(kBlock), lds, s, p);
-    else
-        hipLaunchKernelGGL(c4_search_kernel<false>, dim3(p.n_games), dim3(kBlock), lds, s, p);
+    const size_t lds = c4_search_lds_bytes(p.bs) + (p.philox ? 1024 : 0);
+    const dim3 grid(p.n_games), block(kBlock);
+    if (p.philox) {
+        if (p.stamp)
+            hipLaunchKernelGGL((c4_search_kernel<true, true>), grid, block, lds, s, p);
+        else
+            hipLaunchKernelGGL((c4_search_kernel<false, true>), grid, block, lds, s, p);
+    } else {
+        if (p.stamp)
+            hipLaunchKernelGGL((c4_search_kernel<true, false>), grid, block, lds, s, p);
+        else
+            hipLaunchKernelGGL((c4_search_kernel<false, false>), grid, block, lds, s, p);
+    }
 }
 
 void launch_c4_rollout_debug(const Arena &a, int M, int first_game, int n, const zc_c4_state *states,

@@ -22,22 +22,12 @@
 #include <hip/hip_fp16.h>
 
 #include "chess_tree.h"
+#include "counter_rng.h"
 
 namespace zc {
 namespace {
 
-// ---------------------------------------------------------------- Philox4x32-10
-__device__ __forceinline__ uint4 philox(uint4 c, uint2 k) {
-#pragma unroll
-    for (int i = 0; i < 10; ++i) {
-        const uint64_t p0 = (uint64_t)0xD2511F53u * c.x, p1 = (uint64_t)0xCD9E8D57u * c.z;
-        const uint32_t h0 = (uint32_t)(p0 >> 32), l0 = (uint32_t)p0, h1 = (uint32_t)(p1 >> 32), l1 = (uint32_t)p1;
-        c = make_uint4(h1 ^ c.y ^ k.x, l1, h0 ^ c.w ^ k.y, l0);
-        k.x += 0x9E3779B9u;
-        k.y += 0xBB67AE85u;
-    }
-    return c;
-}
+// ---------------------------------------------------------------- Philox draws
 __device__ __forceinline__ float u01(uint32_t x) { return ((float)(x >> 8) + 0.5f) * (1.0f / 16777216.0f); }
 
 // Gamma(alpha, 1) by Marsaglia-Tsang (alpha < 1 via Gamma(alpha + 1) * U^(1/alpha)); the

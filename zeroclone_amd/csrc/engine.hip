@@ -119,6 +119,8 @@ zc::SearchParams make_params(zc_engine *e, int32_t first, int32_t n, const zc_c4
     p.a = e->a;
     p.max_batch = e->cfg.max_batch;
     p.stamp = e->stamp;
+    p.philox = e->rollout_mode == ZC_ROLLOUT_PHILOX;
+    p.philox_seed = e->rollout_seed;
     return p;
 }
 
@@ -345,6 +347,15 @@ int search_sync(zc_engine *eng, int32_t first, int32_t n, const int32_t *ids, co
     return ZC_OK;
 }
 }  // namespace
+
+int zc_c4_set_rollout_mode(zc_engine *eng, int32_t mode, uint64_t seed) {
+    if (!eng) return fail(ZC_EINVAL, "null argument");
+    if (mode != ZC_ROLLOUT_EXACT && mode != ZC_ROLLOUT_PHILOX) return fail(ZC_EINVAL, "unknown rollout mode %d", mode);
+    std::lock_guard<std::mutex> lk(eng->mu);
+    eng->rollout_mode = mode;
+    eng->rollout_seed = seed;
+    return ZC_OK;
+}
 
 int zc_c4_search(zc_engine *eng, int32_t first, int32_t n, const zc_c4_state *roots, int32_t sims, double c,
                  int32_t bs, int32_t *out_move, int32_t *out_na, zc_game_stats *out_stats) {

@@ -87,6 +87,8 @@ struct SearchParams {
     Arena a;
     int max_batch;
     int stamp;
+    int philox;            // rollouts: 0 = the game's MT19937 stream (exact), 1 = Philox mode
+    uint64_t philox_seed;  // Philox key of the Philox rollout mode
 };
 
 struct ExtParams {
@@ -211,6 +213,8 @@ struct zc_engine {
     zc::Arena a;
     int64_t bytes = 0;
     int stamp = 0;
+    int rollout_mode = 0;        // ZC_ROLLOUT_EXACT / ZC_ROLLOUT_PHILOX
+    uint64_t rollout_seed = 0;
     zc::ChessArena ca;  // allocated on the first chess search
     // the chess PUCT search in progress
     int px_first = 0, px_n = 0, px_sims = 0, px_bs = 0;
