@@ -29,6 +29,9 @@ for st in "$@"; do
     pmc)    run pmc 600 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/pmc -o pmc \
                 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY \
                 -- python3 tools/one_search.py --reps 2 || exit $? ;;
+    pmcx)   run pmcx 600 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/pmcx -o pmc \
+                --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY \
+                -- python3 tools/one_search.py --reps 2 --mode philox || exit $? ;;
     hbm)    run hbm_fetch 600 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/hbm -o fetch \
                 --pmc FETCH_SIZE -- python3 tools/one_search.py --reps 2 || exit $?
             run hbm_write 600 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/hbm -o write \

@@ -17,8 +17,10 @@ ap.add_argument("--games", type=int, default=4096)
 ap.add_argument("--sims", type=int, default=800)
 ap.add_argument("--batch", type=int, default=32)
 ap.add_argument("--reps", type=int, default=3)
+ap.add_argument("--mode", default="exact", choices=["exact", "philox"])
 a = ap.parse_args()
 eng = _native.NativeEngine(max_games=a.games, max_sims=a.sims, max_batch=a.batch)
+eng.c4_rollout_mode(a.mode, 7)
 roots = np.zeros(a.games, _native.C4_STATE_DTYPE)
 tot = 0
 for r in range(a.reps):

@@ -7,6 +7,8 @@
 // with M = 128 output channels, N = the pixels of a tile of boards, K = 9 taps x cin, on
 // v_mfma_f32_32x32x16_f16.  Activations are NHWC fp16 (a pixel's channels contiguous).
 //
+// Two forms (bit-identical results; tools/ab_conv.py): the default half-tile kernel below
+// (128-pixel tiles, 70 KB of LDS, two workgroups per CU) and this one (ZC_CONV_IMPL=tile).
 // One workgroup = 4 waves = one tile of BPW boards (<= 256 pixels; 4 chess boards, 6
 // Connect4 boards).  The tile's input pixels are staged ONCE in LDS (rows padded by 16 B so
 // the 32 lanes reading 32 pixels hit different banks); the 9 shifted views of a tap are
@@ -19,6 +21,10 @@
 // row group.
 #include <hip/hip_fp16.h>
 #include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
 
 #include "zc_internal.h"
 
@@ -212,6 +218,187 @@ __global__ __launch_bounds__(256) void conv3x3_kernel(int nboards, const _Float1
     }
 }
 
+// Half-tile form: 128-pixel tiles with ONE weight buffer, 70 KB of LDS, so two workgroups
+// share a CU and one's staging, barriers and epilogue run under the other's MFMAs.  Wave w
+// owns output channels [64 (w & 1), +64) x pixels [64 (w >> 1), +64) (2 x 2 MFMA tiles).
+// Per tap: the next tap's weights are fetched into registers during the MFMAs, then
+// barrier -> store -> barrier.  Same accumulation order as conv3x3_kernel (bit-identical).
+constexpr int kHalfPix = 128;
+
+template <int H, int W, int BPW, int CIN>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void conv3x3_half_kernel(int nboards, const _Float16 *__restrict__ in,
+                                                              const _Float16 *__restrict__ wt,
+                                                              const float *__restrict__ bias,
+                                                              const _Float16 *__restrict__ res,
+                                                              _Float16 *__restrict__ out, int relu) {
+    constexpr int HW = H * W;
+    constexpr int PIX = BPW * HW;
+    static_assert(PIX <= kHalfPix, "tile too large");
+    constexpr int LD = CIN + 8;
+    constexpr int C8 = CIN / 8;
+    constexpr int WCH = kCout * C8 / 256;
+    constexpr int NI = kHalfPix * C8 / 256;
+    extern __shared__ __attribute__((aligned(16))) _Float16 lds[];
+    _Float16 *const sin = lds;                         // [kHalfPix + 1][LD]; the last row is zero
+    _Float16 *const sw = lds + (kHalfPix + 1) * LD;   // [kCout][LD]: the current tap's weights
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int b0 = blockIdx.x * BPW;
+    const int npix = min(BPW, nboards - b0) * HW;
+    const h8 zero = {0, 0, 0, 0, 0, 0, 0, 0};
+    h8 wpre[WCH];
+    {
+        h8 v[NI];
+        const _Float16 *src = in + (size_t)b0 * HW * CIN;
+#pragma unroll
+        for (int q = 0; q < NI; ++q) {
+            const int i = tid + q * 256, row = i / C8, c8 = i - row * C8;
+            const h8 t = *(const h8 *)(src + min(row, npix - 1) * CIN + c8 * 8);
+            v[q] = row < npix ? t : zero;
+        }
+#pragma unroll
+        for (int q = 0; q < WCH; ++q) {
+            const int i = tid + q * 256, row = i / C8, c8 = i - row * C8;
+            wpre[q] = *(const h8 *)(wt + (size_t)row * CIN + c8 * 8);
+        }
+#pragma unroll
+        for (int q = 0; q < NI; ++q) {
+            const int i = tid + q * 256, row = i / C8, c8 = i - row * C8;
+            *(h8 *)(sin + row * LD + c8 * 8) = v[q];
+        }
+        if (tid < C8) *(h8 *)(sin + kHalfPix * LD + tid * 8) = zero;  // the off-board row
+#pragma unroll
+        for (int q = 0; q < WCH; ++q) {
+            const int i = tid + q * 256, row = i / C8, c8 = i - row * C8;
+            *(h8 *)(sw + row * LD + c8 * 8) = wpre[q];
+        }
+    }
+
+    const int r = lane & 31, hh = lane >> 5;
+    const int m0 = 2 * (wave & 1), p0 = 64 * (wave >> 1);
+    int pb[2], py[2], px[2];
+    bool pv[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+        const int P = p0 + t * 32 + r;
+        pv[t] = P < npix;
+        pb[t] = P / HW;
+        const int rem = P - pb[t] * HW;
+        py[t] = rem / W;
+        px[t] = rem - py[t] * W;
+    }
+    f16x acc[2][2];
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+            for (int k = 0; k < 16; ++k) acc[m][t][k] = 0.0f;
+
+    for (int tap = 0; tap < 9; ++tap) {
+        __syncthreads();  // this tap's weights (and, at tap 0, the input tile) are in LDS
+        if (tap + 1 < 9) {
+#pragma unroll
+            for (int q = 0; q < WCH; ++q) {
+                const int i = tid + q * 256, row = i / C8, c8 = i - row * C8;
+                wpre[q] = *(const h8 *)(wt + ((size_t)(tap + 1) * kCout + row) * CIN + c8 * 8);
+            }
+        }
+        const int dy = tap / 3 - 1, dx = tap % 3 - 1;
+        const _Float16 *xb[2];
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+            const int sy = py[t] + dy, sx = px[t] + dx;
+            const bool sv = pv[t] && (unsigned)sy < (unsigned)H && (unsigned)sx < (unsigned)W;
+            xb[t] = sin + (sv ? pb[t] * HW + sy * W + sx : kHalfPix) * LD + hh * 8;  // off-board: zeros
+        }
+        const _Float16 *wa = sw + (m0 * 32 + r) * LD + hh * 8;
+        h8 a[2], x[2], an[2], xn[2];
+#pragma unroll
+        for (int t = 0; t < 2; ++t) x[t] = *(const h8 *)(xb[t]);
+#pragma unroll
+        for (int m = 0; m < 2; ++m) a[m] = *(const h8 *)(wa + m * 32 * LD);
+#pragma unroll
+        for (int kc = 0; kc < CIN / 16; ++kc) {
+            if (kc + 1 < CIN / 16) {
+#pragma unroll
+                for (int t = 0; t < 2; ++t) xn[t] = *(const h8 *)(xb[t] + (kc + 1) * 16);
+#pragma unroll
+                for (int m = 0; m < 2; ++m) an[m] = *(const h8 *)(wa + m * 32 * LD + (kc + 1) * 16);
+            }
+#pragma unroll
+            for (int m = 0; m < 2; ++m)
+#pragma unroll
+                for (int t = 0; t < 2; ++t)
+                    acc[m][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[m], x[t], acc[m][t], 0, 0, 0);
+            if (kc + 1 < CIN / 16) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // 1 MFMA
+                    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // 1 DS read
+                }
+#pragma unroll
+                for (int m = 0; m < 2; ++m) a[m] = an[m];
+#pragma unroll
+                for (int t = 0; t < 2; ++t) x[t] = xn[t];
+            }
+        }
+        if (tap + 1 < 9) {
+            __syncthreads();  // every wave is done with this tap's weights
+#pragma unroll
+            for (int q = 0; q < WCH; ++q) {
+                const int i = tid + q * 256, row = i / C8, c8 = i - row * C8;
+                *(h8 *)(sw + row * LD + c8 * 8) = wpre[q];
+            }
+        }
+    }
+
+    h4 rv[2][2][4];
+    if (res) {
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+            const int P = min(p0 + t * 32 + r, max(npix - 1, 0));
+            const size_t orow = ((size_t)b0 * HW + P) * kCout;
+#pragma unroll
+            for (int m = 0; m < 2; ++m)
+#pragma unroll
+                for (int g = 0; g < 4; ++g) rv[t][m][g] = *(const h4 *)(res + orow + (m0 + m) * 32 + 8 * g + 4 * hh);
+        }
+    }
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+        const int P = p0 + t * 32 + r;
+        const size_t orow = ((size_t)b0 * HW + P) * kCout;
+#pragma unroll
+        for (int m = 0; m < 2; ++m)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const int co = (m0 + m) * 32 + 8 * g + 4 * hh;
+                const float4 bb = *(const float4 *)(bias + co);
+                float v0 = acc[m][t][4 * g + 0] + bb.x, v1 = acc[m][t][4 * g + 1] + bb.y;
+                float v2 = acc[m][t][4 * g + 2] + bb.z, v3 = acc[m][t][4 * g + 3] + bb.w;
+                if (res) {
+                    v0 += (float)rv[t][m][g][0];
+                    v1 += (float)rv[t][m][g][1];
+                    v2 += (float)rv[t][m][g][2];
+                    v3 += (float)rv[t][m][g][3];
+                }
+                if (relu) {
+                    v0 = fmaxf(v0, 0.0f);
+                    v1 = fmaxf(v1, 0.0f);
+                    v2 = fmaxf(v2, 0.0f);
+                    v3 = fmaxf(v3, 0.0f);
+                }
+                h4 o;
+                o[0] = (_Float16)v0;
+                o[1] = (_Float16)v1;
+                o[2] = (_Float16)v2;
+                o[3] = (_Float16)v3;
+                if (P < npix) *(h4 *)(out + orow + co) = o;
+            }
+    }
+}
+
 // planes [n][cin][H*W] (state_to_tensor layout, fp16) -> NHWC [n][H*W][cpad], zero padded.
 __global__ void planes_to_nhwc_kernel(int n, int cin, int hw, int cpad, const _Float16 *__restrict__ planes,
                                       _Float16 *__restrict__ out) {
@@ -241,23 +428,38 @@ __global__ __launch_bounds__(256) void value_head_kernel(int n, int hw, const _F
     if (lane == 0) values[i] = (double)tanhf(d + fcb);
 }
 
-template <int H, int W, int BPW, int CIN>
+int conv_impl() {  // ZC_CONV_IMPL=tile: 256-pixel tiles, one workgroup per CU; default: half tiles
+    static const int v = [] {
+        const char *e = getenv("ZC_CONV_IMPL");
+        return e && !strcmp(e, "tile") ? 0 : 1;
+    }();
+    return v;
+}
+
+template <int H, int W, int BPW, int BPH, int CIN>
 void launch_conv(int n, const void *in, const void *wt, const float *bias, const void *res, void *out, int relu,
                  hipStream_t s) {
-    const size_t lds = (size_t)(kTilePix + 1 + 2 * kCout) * (CIN + 8) * sizeof(_Float16);
-    hipLaunchKernelGGL((conv3x3_kernel<H, W, BPW, CIN>), dim3((n + BPW - 1) / BPW), dim3(256), lds, s, n,
-                       (const _Float16 *)in, (const _Float16 *)wt, bias, (const _Float16 *)res, (_Float16 *)out,
-                       relu);
+    if (conv_impl() == 1) {
+        const size_t lds = (size_t)(kHalfPix + 1 + kCout) * (CIN + 8) * sizeof(_Float16);
+        hipLaunchKernelGGL((conv3x3_half_kernel<H, W, BPH, CIN>), dim3((n + BPH - 1) / BPH), dim3(256), lds, s, n,
+                           (const _Float16 *)in, (const _Float16 *)wt, bias, (const _Float16 *)res, (_Float16 *)out,
+                           relu);
+    } else {
+        const size_t lds = (size_t)(kTilePix + 1 + 2 * kCout) * (CIN + 8) * sizeof(_Float16);
+        hipLaunchKernelGGL((conv3x3_kernel<H, W, BPW, CIN>), dim3((n + BPW - 1) / BPW), dim3(256), lds, s, n,
+                           (const _Float16 *)in, (const _Float16 *)wt, bias, (const _Float16 *)res, (_Float16 *)out,
+                           relu);
+    }
 }
 
 }  // namespace
 
 bool launch_net_conv3x3(int n, int h, int w, int cin, const void *in, const void *wt, const float *bias,
                         const void *res, void *out, int relu, hipStream_t s) {
-    if (h == 8 && w == 8 && cin == 128) launch_conv<8, 8, 4, 128>(n, in, wt, bias, res, out, relu, s);
-    else if (h == 8 && w == 8 && cin == 32) launch_conv<8, 8, 4, 32>(n, in, wt, bias, res, out, relu, s);
-    else if (h == 6 && w == 7 && cin == 128) launch_conv<6, 7, 6, 128>(n, in, wt, bias, res, out, relu, s);
-    else if (h == 6 && w == 7 && cin == 32) launch_conv<6, 7, 6, 32>(n, in, wt, bias, res, out, relu, s);
+    if (h == 8 && w == 8 && cin == 128) launch_conv<8, 8, 4, 2, 128>(n, in, wt, bias, res, out, relu, s);
+    else if (h == 8 && w == 8 && cin == 32) launch_conv<8, 8, 4, 2, 32>(n, in, wt, bias, res, out, relu, s);
+    else if (h == 6 && w == 7 && cin == 128) launch_conv<6, 7, 6, 3, 128>(n, in, wt, bias, res, out, relu, s);
+    else if (h == 6 && w == 7 && cin == 32) launch_conv<6, 7, 6, 3, 32>(n, in, wt, bias, res, out, relu, s);
     else return false;
     return true;
 }
