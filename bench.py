@@ -326,21 +326,22 @@ def main():
         # per-phase times (s_memtime stamps, one extra search with the stamped
         # kernel; shares applied to the unstamped launch time) and the tree-walk-only roofline
         # (select + expand-write + backup + publish; rollouts are integer VALU, not HBM).
-        eng.phase_cycles(True)
-        eng.c4_search_async(roots.data_ptr(), G, S, args.c, B, moves.data_ptr(), na.data_ptr(), stats.data_ptr(),
-                            stream=torch_stream.cuda_stream)
-        torch.cuda.synchronize(dev)
-        ph = eng.phase_cycles(False)
-        tot_c = max(sum(ph.values()), 1)
-        share = {k: v / tot_c for k, v in ph.items() if k != "sub"}
-        walk = sum(share[k] for k in ("rng", "walk_first", "walk_resumed", "expand", "backup", "publish"))
-        out["extra"]["phases"] = {
-            "share": {k: round(v, 4) for k, v in share.items()},
-            "ms_per_launch": {k: round(v * avg_kernel_s * 1e3, 3) for k, v in share.items()},
-            "walk_roofline": {"t_walk_ms": round(walk * avg_kernel_s * 1e3, 3),
-                              "achieved": round(bytes_launch / (walk * avg_kernel_s) / 1e9, 2),
-                              "frac": round(bytes_launch / (walk * avg_kernel_s) / 1e9 / HBM_PEAK_GBS, 5),
-                              "note": "SURVEY §8(d) roofline definition: model bytes / tree-walk time only"}}
+        if world == 1:
+            eng.phase_cycles(True)
+            eng.c4_search_async(roots.data_ptr(), G, S, args.c, B, moves.data_ptr(), na.data_ptr(), stats.data_ptr(),
+                                stream=torch_stream.cuda_stream)
+            torch.cuda.synchronize(dev)
+            ph = eng.phase_cycles(False)
+            tot_c = max(sum(ph.values()), 1)
+            share = {k: v / tot_c for k, v in ph.items() if k != "sub"}
+            walk = sum(share[k] for k in ("rng", "walk_first", "walk_resumed", "expand", "backup", "publish"))
+            out["extra"]["phases"] = {
+                "share": {k: round(v, 4) for k, v in share.items()},
+                "ms_per_launch": {k: round(v * avg_kernel_s * 1e3, 3) for k, v in share.items()},
+                "walk_roofline": {"t_walk_ms": round(walk * avg_kernel_s * 1e3, 3),
+                                  "achieved": round(bytes_launch / (walk * avg_kernel_s) / 1e9, 2),
+                                  "frac": round(bytes_launch / (walk * avg_kernel_s) / 1e9 / HBM_PEAK_GBS, 5),
+                                  "note": "SURVEY §8(d) roofline definition: model bytes / tree-walk time only"}}
         if world == 1 and args.net_steps > 0:
             out["extra"]["c2_philox"] = philox_mode(eng, step, evs, acc, args, G, dev)
             out["extra"]["c2_value_net"] = net_mode(G, S, B, args.c, args.net_steps, dev)

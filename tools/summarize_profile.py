@@ -15,7 +15,7 @@ import collections
 import csv
 import json
 
-KERNEL = "c4_search_kernel"
+KERNEL = "c4_search_kernel<false, false>"  # the product kernel (not the stamped diagnostic build)
 
 
 def per_launch(path, counter):
