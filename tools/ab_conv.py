@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""A/B of the conv3x3 implementations (ZC_CONV_IMPL=tile vs the default persistent form):
+"""A/B of the conv3x3 implementations (ZC_CONV_IMPL = tile / half / w8; argv picks them):
 bit-identical outputs and per-layer time.  Runs each impl in a child process."""
 import json
 import os
@@ -36,16 +36,17 @@ for (h, w, n) in [(8, 8, 32768), (6, 7, 131072), (8, 8, 1000), (6, 7, 777)]:
                         "hash": int((o.view(torch.int16).to(torch.int64) * torch.arange(o.numel(), device="cuda").view(o.shape) % 1000003).sum().item())}
 print(json.dumps(out))
 '''
+IMPLS = sys.argv[1:] or ["tile", "half"]
 res = {}
-for impl in ("tile", "persistent"):
+for impl in IMPLS:
     env = dict(os.environ, ZC_CONV_IMPL=impl)
     r = subprocess.run([sys.executable, "-c", CHILD, HERE], env=env, capture_output=True, text=True, timeout=600)
     if r.returncode:
         print(r.stderr[-3000:])
         sys.exit(r.returncode)
     res[impl] = json.loads(r.stdout.strip().splitlines()[-1])
-same = all(res["tile"][k]["hash"] == res["persistent"][k]["hash"] for k in res["tile"])
-for k in res["tile"]:
-    print(f'{k:32s} tile {res["tile"][k]["ms"]:8.4f} ms {res["tile"][k]["tflops"]:7.1f} TF | persistent '
-          f'{res["persistent"][k]["ms"]:8.4f} ms {res["persistent"][k]["tflops"]:7.1f} TF | same={res["tile"][k]["hash"] == res["persistent"][k]["hash"]}')
+base = IMPLS[0]
+same = all(res[i][k]["hash"] == res[base][k]["hash"] for i in IMPLS for k in res[base])
+for k in res[base]:
+    print(f"{k:30s}" + " | ".join(f"{i} {res[i][k]['ms']:7.4f} ms {res[i][k]['tflops']:6.1f} TF" for i in IMPLS))
 print("bit-identical:", same)
