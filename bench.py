@@ -292,6 +292,25 @@ def main():
                 traffic = hbm["bytes_per_launch"]
                 traffic_src = os.path.relpath(prof[-1], HERE)
 
+    # C3's one exchange: the all-gather of finished trajectories into the
+    # replay buffer — here a payload of the right shape, this rank's K steps x G positions
+    # (24-B zc_c4_state rows), through selfplay.gather_positions (RCCL over xGMI).  Off the
+    # expansions/s clock, reported beside it.
+    gather = None
+    if world > 1:
+        from zeroclone_amd.selfplay import gather_positions
+        local = roots.repeat(args.steps, 1)
+        gather_positions(local)  # warm the communicator
+        dist.barrier()
+        torch.cuda.synchronize(dev)
+        tg = time.perf_counter()
+        allpos = gather_positions(local)
+        torch.cuda.synchronize(dev)
+        gms = torch.tensor([(time.perf_counter() - tg) * 1e3], dtype=torch.float64, device=dev)
+        dist.all_reduce(gms, op=dist.ReduceOp.MAX)
+        gather = {"rows": int(allpos.shape[0]), "bytes": int(allpos.numel() * allpos.element_size()),
+                  "ms": round(float(gms.item()), 3), "collective": "all_gather (counts, padded payload), backend nccl=RCCL"}
+
     if rank == 0:
         launches = args.steps * world
         bytes_launch = bytes_per_expansion_model(expansions, depth_sum) / launches
@@ -323,6 +342,8 @@ def main():
             "extra": {"expansions": expansions, "leaves": leaves, "mean_depth": round(depth_sum / max(expansions, 1), 3),
                       "games_finished": finished, "search_ms_per_step": [round(x, 3) for x in kernel_ms]},
         }
+        if gather is not None:
+            out["extra"]["trajectory_allgather"] = gather
         # per-phase times (s_memtime stamps, one extra search with the stamped
         # kernel; shares applied to the unstamped launch time) and the tree-walk-only roofline
         # (select + expand-write + backup + publish; rollouts are integer VALU, not HBM).
