@@ -433,25 +433,25 @@ __device__ __forceinline__ void select_flush(const Tree &t, Fresh *fresh, Leaf *
             }
             if (k == (uint32_t)mi) ch = (uint32_t)leaf;
             if (node < f0) x0_dirty = true;  // X0 itself: written back when the flush is published
-            if (lane == 0) {
-                // Node(state, legal_moves) (mcts.cpp:23-34): all moves untried, no children
-                *(uint4 *)&fresh[leaf - f0] =
-                    make_uint4(untried_init((low_ >> 24) & 15u), low_,
-                               (uint32_t)node | ((uint32_t)mi << 16) | ((uint32_t)ldepth << 24), (uint32_t)lmask);
-                if (node >= f0) {  // the parent's copy in LDS
-                    fresh[node - f0].u = u;
-                    fresh[node - f0].ch[mi] = (uint16_t)leaf;
-                }
+            // Node(state, legal_moves) (mcts.cpp:23-34): all moves untried, no children.
+            // Uniform values to one address: every lane stores (no EXEC branches).
+            *(uint4 *)&fresh[leaf - f0] =
+                make_uint4(untried_init((low_ >> 24) & 15u), low_,
+                           (uint32_t)node | ((uint32_t)mi << 16) | ((uint32_t)ldepth << 24), (uint32_t)lmask);
+            if (node >= f0) {  // the parent's copy in LDS
+                fresh[node - f0].u = u;
+                fresh[node - f0].ch[mi] = (uint16_t)leaf;
             }
             cn.add(cn.expansions, 1);
             cn.add(cn.depth_sum, ldepth);
         }
         // the leaf's path: the walk's path plus the new node (the next walk resumes at `node`)
         const uint32_t lpath = (cnt && lane == (uint32_t)ldepth) ? (uint32_t)leaf : pathv;
-        if (lane == 0)
-            leaves[j] = Leaf{l0, l1, (uint32_t)leaf | ((uint32_t)ldepth << 16) | ((uint32_t)lturn << 24) | ((uint32_t)lmask << 25),
-                             0};
-        if (lane < (uint32_t)kMaxDepth) paths[j * kMaxDepth + lane] = (uint16_t)lpath;
+        leaves[j] = Leaf{l0, l1, (uint32_t)leaf | ((uint32_t)ldepth << 16) | ((uint32_t)lturn << 24) | ((uint32_t)lmask << 25),
+                         0};
+        // all 64 lanes store: lanes >= kMaxDepth spill into leaf j+1's path (written after
+        // this) or, for the flush's last leaf, into the scratch LDS that follows the paths
+        paths[j * kMaxDepth + lane] = (uint16_t)lpath;
         wave_mem_order();
         stamp.mark(3);
     }

@@ -228,7 +228,7 @@ __device__ void c4_rollouts(Leaf *L, int nb, Rng &rng, const uint32_t *s_order, 
                 }
             }
         }
-        if (lane == 0) L[j].val = val;
+        L[j].val = val;  // uniform: every lane stores
         cn.add(cn.plies, q);
     }
 }
