@@ -192,7 +192,8 @@ __device__ __forceinline__ uint32_t rng_below(Rng &r, uint32_t n) {
     for (;;) {
         if (r.off >= (uint32_t)kWin) rng_advance(r);
         const uint32_t v = r.wt >> sh;
-        const uint64_t bal = __ballot(lane >= r.off && v < n);
+        // one compare: words before `off` get bit 31 set (never < n)
+        const uint64_t bal = __ballot((v | ((lane - r.off) & 0x80000000u)) < n);
         if (bal) {
             const int f = __builtin_ctzll(bal);
             r.off = (uint32_t)f + 1;
@@ -415,10 +416,12 @@ __device__ __forceinline__ void select_flush(const Tree &t, Fresh *fresh, Leaf *
         const uint32_t cnt = untried_count(u);
         if (cnt) {  // expand (mcts.cpp:65-78): policy = random.choice(untried)
             const uint32_t r = rng_below(rng, cnt);
-            // the r-th untried move in bit order (lane b holds bit b of the untried mask)
+            // the r-th untried move in bit order: lane b (< 7) holding set bit b of the untried
+            // mask compares its rank; other lanes compare 0xFF (one compare per lane)
             const uint32_t um = u & 0x7Fu;
-            const int mi = __builtin_ctzll(
-                __ballot(lane < 7u && ((um >> (lane & 7u)) & 1u) && (uint32_t)__popc(um & ((1u << (lane & 7u)) - 1u)) == r));
+            const uint32_t b7 = lane & 7u;
+            const uint32_t rank = (lane < 7u && ((um >> b7) & 1u)) ? (uint32_t)__popc(um & ((1u << b7) - 1u)) : 0xFFu;
+            const int mi = __builtin_ctzll(__ballot(rank == r));
             u &= ~(1u << mi);
             const int col = (int)((ow >> (3 * mi)) & 7u);
             const uint64_t bit = drop_bit(b0 | b1, col);
