@@ -214,6 +214,8 @@ struct Leaf {
     uint64_t p0, p1;  // stones of 'X' / 'O'
     uint32_t meta;    // node | depth << 16 | turn << 24 | legal mask << 25
     int32_t val;      // rollout value from the leaf's side to move
+    uint32_t ow;      // d_order[legal mask]: the move-list order word (saves the rollout a lookup)
+    uint32_t pad;
 };
 
 // LDS copy of a node created in the current flush.  During selection the node lives only
@@ -414,6 +416,7 @@ __device__ __forceinline__ void select_flush(const Tree &t, Fresh *fresh, Leaf *
         int leaf = node, ldepth = depth, lturn = turn, lmask = cmask;
         uint64_t l0 = b0, l1 = b1;
         const uint32_t cnt = untried_count(u);
+        uint32_t low_ = ow;  // the leaf's move-list order word
         if (cnt) {  // expand (mcts.cpp:65-78): policy = random.choice(untried)
             const uint32_t r = rng_below(rng, cnt);
             // the r-th untried move in bit order: lane b (< 7) holding set bit b of the untried
@@ -429,7 +432,7 @@ __device__ __forceinline__ void select_flush(const Tree &t, Fresh *fresh, Leaf *
             lturn = turn ^ 1;
             leaf = nnodes++;
             ldepth = depth + 1;
-            uint32_t low_ = ow;  // the leaf's legal set is the node's unless the column filled
+            low_ = ow;  // the leaf's legal set is the node's unless the column filled
             if (bit & kTop) {
                 lmask &= ~(1 << col);
                 low_ = uni(s_order[lmask]);
@@ -451,7 +454,7 @@ __device__ __forceinline__ void select_flush(const Tree &t, Fresh *fresh, Leaf *
         // the leaf's path: the walk's path plus the new node (the next walk resumes at `node`)
         const uint32_t lpath = (cnt && lane == (uint32_t)ldepth) ? (uint32_t)leaf : pathv;
         leaves[j] = Leaf{l0, l1, (uint32_t)leaf | ((uint32_t)ldepth << 16) | ((uint32_t)lturn << 24) | ((uint32_t)lmask << 25),
-                         0};
+                         0, low_, 0};
         // all 64 lanes store: lanes >= kMaxDepth spill into leaf j+1's path (written after
         // this) or, for the flush's last leaf, into the scratch LDS that follows the paths
         paths[j * kMaxDepth + lane] = (uint16_t)lpath;

@@ -144,7 +144,7 @@ __device__ void c4_rollouts(Leaf *L, int nb, Rng &rng, const uint32_t *s_order, 
         } else if (room0 >= 0) {  // not check_draw
             int room = room0;
             int mask = (int)(lm >> 25);
-            uint32_t ow = uni(s_order[mask]);
+            uint32_t ow = uni(L[j].ow);
             uint32_t n = (ow >> 24) & 15u;
             uint32_t sh = (uint32_t)__clz(n);
             for (;;) {
@@ -530,6 +530,7 @@ __global__ __launch_bounds__(kBlock) void c4_rollout_debug_kernel(Arena a, int f
         s_leaf[0].p0 = s.stones[0];
         s_leaf[0].p1 = s.stones[1];
         s_leaf[0].meta = ((uint32_t)s.turn << 24) | ((uint32_t)legal_mask(s.stones[0] | s.stones[1]) << 25);
+        s_leaf[0].ow = s_order[legal_mask(s.stones[0] | s.stones[1])];
     }
     wave_mem_order();
     Counters cn;
@@ -562,6 +563,7 @@ __global__ __launch_bounds__(kBlock) void c4_rollout_seq_kernel(Arena a, int g, 
             s_leaf[lane].p0 = s.stones[0];
             s_leaf[lane].p1 = s.stones[1];
             s_leaf[lane].meta = ((uint32_t)s.turn << 24) | ((uint32_t)legal_mask(s.stones[0] | s.stones[1]) << 25);
+            s_leaf[lane].ow = s_order[legal_mask(s.stones[0] | s.stones[1])];
         }
         wave_mem_order();
         rng_fill(rng, rng.use() + kLookahead);
