@@ -428,7 +428,7 @@ __global__ __launch_bounds__(256) void value_head_kernel(int n, int hw, const _F
     if (lane == 0) values[i] = (double)tanhf(d + fcb);
 }
 
-int conv_impl() {  // ZC_CONV_IMPL=tile: 256-pixel tiles, one workgroup per CU; default: half tiles
+int conv_impl() {  // ZC_CONV_IMPL=tile: 256-pixel tiles for every layer; default: half tiles for 128 planes
     static const int v = [] {
         const char *e = getenv("ZC_CONV_IMPL");
         return e && !strcmp(e, "tile") ? 0 : 1;
@@ -439,7 +439,7 @@ int conv_impl() {  // ZC_CONV_IMPL=tile: 256-pixel tiles, one workgroup per CU; 
 template <int H, int W, int BPW, int BPH, int CIN>
 void launch_conv(int n, const void *in, const void *wt, const float *bias, const void *res, void *out, int relu,
                  hipStream_t s) {
-    if (conv_impl() == 1) {
+    if (conv_impl() == 1 && CIN >= 64) {  // the 32-plane stem runs faster on 256-pixel tiles
         const size_t lds = (size_t)(kHalfPix + 1 + kCout) * (CIN + 8) * sizeof(_Float16);
         hipLaunchKernelGGL((conv3x3_half_kernel<H, W, BPH, CIN>), dim3((n + BPH - 1) / BPH), dim3(256), lds, s, n,
                            (const _Float16 *)in, (const _Float16 *)wt, bias, (const _Float16 *)res, (_Float16 *)out,
