@@ -21,13 +21,31 @@
 namespace zc {
 namespace {
 
+// Where the previous simulation of the same flush stopped.  No backup happens inside a
+// flush, so every decision above that node is unchanged and the next walk from the root
+// would arrive there again: it resumes there (the C4 search's flush structure,
+// c4_device.h::select_flush).  Below it every child created in this flush has Na == 0
+// (+inf), so the resumed walk takes first-unvisited slots, as the full walk would.
+struct Resume {
+    int node = 0, depth = 0, nN = 0;
+    uint32_t pathv = 0;
+    bool valid = false;
+};
+
 // select + expand + record of ONE simulation (mcts.cpp:129-147).  Returns the leaf node;
 // its depth in `ldepth`; lane l of `pathv` holds the slot of the edge into level l.
 __device__ int simulate(const ChessParams &p, const CTree &t, CLds &L, ConstDouble *logtab, Rng &rng, int done,
-                        int &nnodes, int &slots, int &status, int &ldepth, uint32_t &pathv, Counters &cn) {
+                        int &nnodes, int &slots, int &status, int &ldepth, uint32_t &pathv, Counters &cn,
+                        Resume &rs) {
     const uint32_t lane = lane_id();
     int node = 0, depth = 0, nN = done;
     pathv = 0;
+    if (rs.valid) {
+        node = rs.node;
+        depth = rs.depth;
+        nN = rs.nN;
+        pathv = rs.pathv;
+    }
     for (;;) {  // select (mcts.cpp:47-63)
         const ChessNode *N = &t.nodes[node];
         const uint32_t base = uni(N->base);
@@ -79,6 +97,11 @@ __device__ int simulate(const ChessParams &p, const CTree &t, CLds &L, ConstDoub
     ChessNode *N = &t.nodes[node];
     const int nu = uni((int)N->nu);
     ldepth = depth;
+    rs.node = node;
+    rs.depth = depth;
+    rs.nN = nN;
+    rs.pathv = pathv;
+    rs.valid = true;
     if (nu == 0 || status) return node;
 
     // expand (mcts.cpp:65-78): the policy picks among the untried moves, in untried order
@@ -227,10 +250,11 @@ __device__ int chess_select_flush(const ChessParams &p, const CTree &t, CLds &L,
     uint32_t *paths = p.ca.paths + (size_t)g * p.max_batch * kChessPath;
     uint32_t *meta = p.ca.meta + (size_t)g * p.max_batch;
     int j = 0;
+    Resume rs;
     for (; j < nb && !status; ++j) {
         int d = 0;
         uint32_t pathv = 0;
-        const int leaf = simulate(p, t, L, logtab, rng, done, nnodes, slots, status, d, pathv, cn);
+        const int leaf = simulate(p, t, L, logtab, rng, done, nnodes, slots, status, d, pathv, cn, rs);
         if (lane < (uint32_t)kChessPath) paths[(size_t)j * kChessPath + lane] = pathv;
         if (lane == 0) meta[j] = (uint32_t)leaf | ((uint32_t)d << 16);
     }
