@@ -47,12 +47,13 @@ __device__ __forceinline__ uint32_t piece_value(uint32_t x) {
 }
 __device__ __forceinline__ bool inb(int r, int c) { return (unsigned)r < 8u && (unsigned)c < 8u; }
 
-// direction tables (chess_backend.cpp:17-34)
+// direction tables (chess_backend.cpp:17-34), compile-time constants: the loops over them
+// are unrolled, so offsets become immediates instead of constant-memory loads
 struct Dir {
-    int8_t dr, dc;
+    int dr, dc;
 };
-__constant__ Dir kKnight[8] = {{-2, -1}, {-2, 1}, {-1, -2}, {-1, 2}, {1, -2}, {1, 2}, {2, -1}, {2, 1}};
-__constant__ Dir kAll8[8] = {{-1, -1}, {-1, 1}, {1, -1}, {1, 1}, {-1, 0}, {1, 0}, {0, -1}, {0, 1}};
+constexpr Dir kKnight[8] = {{-2, -1}, {-2, 1}, {-1, -2}, {-1, 2}, {1, -2}, {1, 2}, {2, -1}, {2, 1}};
+constexpr Dir kAll8[8] = {{-1, -1}, {-1, 1}, {1, -1}, {1, 1}, {-1, 0}, {1, 0}, {0, -1}, {0, 1}};
 // bishops use kAll8[0..4), rooks kAll8[4..8), queens and kings kAll8[0..8)
 
 __device__ __forceinline__ uint32_t pack_move(int from, int to, uint32_t v) {
@@ -82,9 +83,10 @@ __device__ __forceinline__ void piece_moves(const uint8_t *b, int t, int s, uint
             }
         }
     } else if (up == 'N' || up == 'K') {
-        const Dir *D = up == 'N' ? kKnight : kAll8;
+        const bool kn = up == 'N';
+#pragma unroll
         for (int i = 0; i < 8; ++i) {
-            const int rr = r + D[i].dr, cc = c + D[i].dc;
+            const int rr = r + (kn ? kKnight[i].dr : kAll8[i].dr), cc = c + (kn ? kKnight[i].dc : kAll8[i].dc);
             if (!inb(rr, cc)) continue;
             const uint32_t x = b[rr * 8 + cc];
             if (empty_sq(x)) emit(s, rr * 8 + cc, 0u);
@@ -92,7 +94,9 @@ __device__ __forceinline__ void piece_moves(const uint8_t *b, int t, int s, uint
         }
     } else if (up == 'B' || up == 'R' || up == 'Q') {
         const int d0 = up == 'R' ? 4 : 0, d1 = up == 'B' ? 4 : 8;
-        for (int i = d0; i < d1; ++i) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            if (i < d0 || i >= d1) continue;
             const int dr = kAll8[i].dr, dc = kAll8[i].dc;
             int rr = r + dr, cc = c + dc;
             while (inb(rr, cc)) {
@@ -124,11 +128,13 @@ __device__ __forceinline__ bool attacked_after(const uint8_t *b, int t, int kr, 
     if (inb(pr, kc - 1) && at(pr, kc - 1) == pawn) return true;
     if (inb(pr, kc + 1) && at(pr, kc + 1) == pawn) return true;
     const uint32_t kn = t ? 'N' : 'n';
+#pragma unroll
     for (int i = 0; i < 8; ++i) {
         const int rr = kr + kKnight[i].dr, cc = kc + kKnight[i].dc;
         if (inb(rr, cc) && at(rr, cc) == kn) return true;
     }
     const uint32_t q = t ? 'Q' : 'q';
+#pragma unroll
     for (int i = 0; i < 8; ++i) {  // rook lines (kAll8[4..8)) first, then bishop lines: same answer
         const int dr = kAll8[i].dr, dc = kAll8[i].dc;
         const uint32_t p1 = i < 4 ? (t ? 'B' : 'b') : (t ? 'R' : 'r');
@@ -144,6 +150,7 @@ __device__ __forceinline__ bool attacked_after(const uint8_t *b, int t, int kr, 
         }
     }
     const uint32_t kk = t ? 'K' : 'k';
+#pragma unroll
     for (int i = 0; i < 8; ++i) {
         const int rr = kr + kAll8[i].dr, cc = kc + kAll8[i].dc;
         if (inb(rr, cc) && at(rr, cc) == kk) return true;
