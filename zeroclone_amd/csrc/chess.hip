@@ -25,7 +25,7 @@ __global__ __launch_bounds__(64) void chess_legal_kernel(int n, const zc_chess_s
     if (i >= n) return;
     load_board(S.board, states[i]);
     const int t = __builtin_amdgcn_readfirstlane(states[i].turn);
-    const int k = legal_moves(S.board, t, S.legal, S.pseudo);
+    const int k = legal_moves(S.board, t, S.legal, S.pseudo, S.region);
     for (int j = (int)lane(); j < k; j += 64) moves[(size_t)i * kMaxLegal + j] = S.legal[j];
     if (lane() == 0) counts[i] = k;
 }
@@ -40,7 +40,7 @@ __global__ __launch_bounds__(64) void chess_children_kernel(int n, const zc_ches
     const zc_chess_state st = states[i];
     load_board(S.board, st);
     const int t = __builtin_amdgcn_readfirstlane(st.turn);
-    const int k = legal_moves(S.board, t, S.legal, S.pseudo);
+    const int k = legal_moves(S.board, t, S.legal, S.pseudo, S.region);
     if (lane() == 0) counts[i] = k;
     for (int j = (int)lane(); j < k; j += 64) {
         zc_chess_state c = st;
@@ -67,7 +67,7 @@ __global__ __launch_bounds__(64) void chess_terminal_kernel(int n, const zc_ches
     const zc_chess_state st = states[i];
     load_board(S.board, st);
     const int t = __builtin_amdgcn_readfirstlane(st.turn);
-    const int k = legal_moves(S.board, t, S.legal, S.pseudo);
+    const int k = legal_moves(S.board, t, S.legal, S.pseudo, S.region);
     const uint64_t km = __ballot(S.board[lane()] == (t == 0 ? 'K' : 'k'));
     const int ks = km ? __builtin_ctzll(km) : -1;
     const bool check = attacked_after(S.board, t, ks >= 0 ? ks >> 3 : -1, ks >= 0 ? ks & 7 : -1, -1, -1, 0);

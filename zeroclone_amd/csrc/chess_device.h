@@ -28,6 +28,7 @@ namespace {
 
 constexpr int kMaxLegal = 256;   // the output capacity per position (real chess: <= 218)
 constexpr int kMaxPseudo = 512;  // pseudo-legal scratch per position
+constexpr int kRegion = 28;      // per-lane generation region (a queen has <= 27 moves)
 
 __device__ __forceinline__ uint32_t lane() { return __lane_id(); }
 
@@ -177,10 +178,11 @@ __device__ __forceinline__ uint64_t king_mask(const uint8_t *b, int side) {
 }
 
 // get_legal_moves for the board in LDS `b` (64 bytes) with side to move t.  Writes the
-// packed legal moves to out[0..n) (LDS or global), pseudo-legal scratch in LDS `ps`.
+// packed legal moves to out[0..n) (LDS or global); LDS scratch: pseudo-legal list `ps`
+// (kMaxPseudo) and per-lane generation regions `reg` (64 x kRegion).
 // Returns n (wave-uniform), or -1 when the position has more than kMaxPseudo pseudo-legal
 // or kMaxLegal legal moves (never in reachable chess).
-__device__ __forceinline__ int legal_moves(const uint8_t *b, int t, uint16_t *out, uint16_t *ps) {
+__device__ __forceinline__ int legal_moves(const uint8_t *b, int t, uint16_t *out, uint16_t *ps, uint16_t *reg) {
     const uint32_t s = lane();
     const uint32_t pc = b[s];
     // insufficient material (:188-198): no P/R/Q of either colour and at most one minor
@@ -189,13 +191,16 @@ __device__ __forceinline__ int legal_moves(const uint8_t *b, int t, uint16_t *ou
     const int minor = __popcll(__ballot(up == 'B' || up == 'N'));
     if (!heavy && minor <= 1) return 0;
     const bool mine = !empty_sq(pc) && ((t == 0) == is_white(pc));
+    // one generation pass into this lane's own region (a piece has at most 27 pseudo-legal
+    // moves), then each lane copies its run to its place in board-scan order
+    uint16_t *const own = reg + s * kRegion;
     uint32_t cnt = 0;
-    if (mine) piece_moves(b, t, (int)s, pc, [&](int, int, uint32_t) { ++cnt; });
+    if (mine) piece_moves(b, t, (int)s, pc, [&](int f, int to, uint32_t v) { own[cnt++] = (uint16_t)pack_move(f, to, v); });
     uint32_t total;
-    uint32_t off = wave_excl_sum(cnt, total);
+    const uint32_t off = wave_excl_sum(cnt, total);
     if (total > (uint32_t)kMaxPseudo) return -1;
-    if (mine)
-        piece_moves(b, t, (int)s, pc, [&](int f, int to, uint32_t v) { ps[off++] = (uint16_t)pack_move(f, to, v); });
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    for (uint32_t k = 0; k < cnt; ++k) ps[off + k] = own[k];
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     const uint64_t kings = king_mask(b, t);
     const uint32_t kch = t == 0 ? 'K' : 'k';
@@ -251,6 +256,7 @@ struct ChessScratch {
     uint8_t board[64];
     uint16_t legal[kMaxLegal];
     uint16_t pseudo[kMaxPseudo];
+    uint16_t region[64 * kRegion];
 };
 
 }  // namespace

@@ -63,7 +63,7 @@ __device__ void create_node(const CTree &t, CLds &L, int id, int parent, int pac
     L.s.board[lane] = L.st.board[lane];
     wave_sync_mem();
     const int turn = uni((int)L.st.turn);
-    int n = chessdev::legal_moves(L.s.board, turn, L.s.legal, L.s.pseudo);
+    int n = chessdev::legal_moves(L.s.board, turn, L.s.legal, L.s.pseudo, L.s.region);
     if (n < 0) {
         status = ZC_STATUS_CAPACITY;
         n = 0;
