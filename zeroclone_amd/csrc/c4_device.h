@@ -115,14 +115,18 @@ __device__ __forceinline__ uint32_t temper(uint32_t y) {
 // The game's stream lives in a ring of RAW MT words x[p] (absolute position p, slot
 // p % kRingWords).  The recurrence x[p] = x[p-227] ^ twist(x[p-624], x[p-623]) regenerates
 // it kChunk words at a time, all lanes in parallel (every input is >= 227 words older).
+// Three 64-word windows sit in registers: wt (tempered, the window holding the next word),
+// wn (tempered, the one after) and wx (raw, in flight from the ring), so a 64-word view
+// starting at ANY position of wt is two lane permutes away (rng_view).
 struct Rng {
     uint32_t *ring;
     uint32_t base;   // low 32 bits of the absolute position at the search's start (use0)
     int32_t wrel;    // window start - use0 (a multiple of 64 in absolute terms; may be < 0)
-    uint32_t off;    // next word to consume = window start + off, off in [0, 64]
+    uint32_t off;    // next word to consume = window start + off, off in [0, 128)
     int32_t grel;    // words generated so far - use0
     uint32_t wt;     // tempered x[window start + lane]
-    uint32_t wn;     // raw x[window start + 64 + lane], in flight until the window advances
+    uint32_t wn;     // tempered x[window start + 64 + lane]
+    uint32_t wx;     // raw x[window start + 128 + lane], in flight until the window advances
     __device__ __forceinline__ int32_t use() const { return wrel + (int32_t)off; }  // relative to use0
     __device__ __forceinline__ uint32_t slot(int32_t rel) const { return (base + (uint32_t)rel) & kRingMask; }
 };
@@ -164,17 +168,30 @@ __device__ __forceinline__ void rng_open(Rng &r, uint32_t *ring, uint64_t use0, 
     r.grel = (int32_t)(gen0 - use0);
     r.off = (uint32_t)use0 & (uint32_t)(kWin - 1);
     r.wrel = -(int32_t)r.off;
-    rng_fill(r, r.wrel + 2 * kWin);
+    rng_fill(r, r.wrel + 3 * kWin);
     r.wt = temper(r.ring[r.slot(r.wrel + (int32_t)lane_id())]);
-    r.wn = r.ring[r.slot(r.wrel + kWin + (int32_t)lane_id())];
+    r.wn = temper(r.ring[r.slot(r.wrel + kWin + (int32_t)lane_id())]);
+    r.wx = r.ring[r.slot(r.wrel + 2 * kWin + (int32_t)lane_id())];
 }
 
+// Move the windows on by 64 words (precondition: off >= 64).
 __device__ __forceinline__ void rng_advance(Rng &r) {
     r.wrel += kWin;
-    r.off = 0;
-    r.wt = temper(r.wn);
-    if (r.grel < r.wrel + 2 * kWin) rng_fill(r, r.wrel + 2 * kWin);
-    r.wn = r.ring[r.slot(r.wrel + kWin + (int32_t)lane_id())];
+    r.off -= (uint32_t)kWin;
+    r.wt = r.wn;
+    r.wn = temper(r.wx);
+    if (r.grel < r.wrel + 3 * kWin) rng_fill(r, r.wrel + 3 * kWin);
+    r.wx = r.ring[r.slot(r.wrel + 2 * kWin + (int32_t)lane_id())];
+}
+
+// The 64 tempered words from the next unconsumed one on: lane l = word off + l of the
+// window (precondition: off < 64).
+__device__ __forceinline__ uint32_t rng_view(const Rng &r) {
+    const uint32_t j = lane_id() + r.off;
+    const int idx = (int)((j & 63u) << 2);
+    const uint32_t a = (uint32_t)__builtin_amdgcn_ds_bpermute(idx, (int)r.wt);
+    const uint32_t b = (uint32_t)__builtin_amdgcn_ds_bpermute(idx, (int)r.wn);
+    return j < 64u ? a : b;
 }
 
 // rngpos after the search: {use0 + use(), use0 + grel}

@@ -102,14 +102,18 @@ __device__ __forceinline__ uint32_t row_prev(uint32_t x) {
 //   win -> -1 if the side to move at the end (the loser) is the leaf's side to move, else +1
 // check_win looks at the LAST mover only (c4_backend.py:27, tokens[1 - turn]).
 //
-// Plies are simulated a BLOCK at a time.  While the legal set is unchanged (no column has
-// filled), the draws are exactly the window words w with (w >> (32-k)) < n, in stream
-// order — so one ballot yields the moves of every ply the window covers.  Lane k (an
-// accepted word) is ply q_k = #accepted lanes below it; its column comes from the move
-// order, its row from the column height plus #earlier accepted lanes in the same column
-// (packed 4-bit per-column prefix sums).  The block ends at its first column fill or at the
-// board-full ply (both known without the win test), at its 31st ply, or at its last
-// accepted word.
+// Plies are simulated a BLOCK at a time over a 64-word view of the stream that starts at the
+// next unconsumed word (rng_view).  While the legal set is unchanged, the draws are exactly
+// the view words w with (w >> (32-k)) < n, in stream order — so one ballot yields the moves
+// of every ply the view covers.  Lane k (an accepted word) is ply q_k = #accepted lanes below
+// it; its column comes from the move order, its row from the column height plus #earlier
+// accepted lanes in the same column (packed 4-bit per-column prefix sums).
+//
+// A column fill changes the legal set (n, k and the CPython order).  The block's FIRST fill
+// is absorbed: the words after it are re-drawn under the new legal set (a second ballot and
+// prefix sum over the same view, the new order word prefetched for every possible column at
+// the block's start).  The block ends at its second fill, the board-full ply, its 31st ply
+// or its last accepted word.
 //
 // The win test runs on a COMPACTED copy of the block's plies: ply q goes (through 64 dwords
 // of LDS) to lane (q & 1)*16 + q/2 and to that lane + 32, so rows 0 and 2 hold the first
@@ -149,31 +153,58 @@ __device__ void c4_rollouts(Leaf *L, int nb, Rng &rng, const uint32_t *s_order, 
             uint32_t sh = (uint32_t)__clz(n);
             for (;;) {
                 if (rng.off >= (uint32_t)kWin) rng_advance(rng);
-                const uint32_t v = rng.wt >> sh;
-                // accepted words: v < n, at or after the next unconsumed word
-                const uint64_t A = __ballot((v | ((lane - rng.off) & 0x80000000u)) < n);
+                // order word of the legal set minus column `lane` (lanes 0..6), for a fill
+                const uint32_t owm = s_order[(uint32_t)mask & ~(1u << (lane & 7u))];
+                const uint32_t wv = rng_view(rng);  // lane l: word off + l
+                uint32_t v = wv >> sh;
+                uint64_t A = __ballot(v < n);  // accepted words
                 if (!A) {
-                    rng.off = kWin;
+                    rng.off += (uint32_t)kWin;
                     continue;
                 }
                 cn.add(cn.blocks, 1);
-                const uint32_t qk = mbcnt(A);                    // this lane's ply in the block
-                const uint32_t col = (ow >> (3 * (v & 7u))) & 7u;  // its column (if accepted)
+                const uint64_t occ = me | op;
+                const uint32_t cap_r = min((uint32_t)room, 30u);  // last ply index the board allows
+                uint32_t qk = mbcnt(A);                            // this lane's ply in the block
+                uint32_t col = (ow >> (3 * (v & 7u))) & 7u;        // its column (if accepted)
                 // earlier plies in the same column: 4-bit per-column counters, prefix-summed
                 // (a nibble can only overflow past 15 plies in one column, i.e. after that
-                // column filled — beyond the block's first event, so never read)
-                const uint32_t one = mask_sel0(A, 1u << (4 * col));
-                const uint32_t same = ((scan_add32(one) - one) >> (4 * col)) & 15u;
-                const uint32_t h0 = (uint32_t)__popcll(((me | op) >> (7 * col)) & 0x3Full);
-                const uint32_t row = h0 + same;  // exact up to the block's first fill
-                // the block's last ply before any win: its first column fill, the board-full
-                // ply, ply 30, or its last accepted word (so there always is one)
-                const uint32_t nacc = (uint32_t)__popc(in_vgpr((uint32_t)A)) + (uint32_t)__popc(in_vgpr((uint32_t)(A >> 32)));
-                const uint32_t cap = min(min((uint32_t)room, 30u), nacc - 1u);
-                const bool fills = row == 5u;
-                const uint64_t R5 = __ballot(fills);
-                const uint64_t E0 = __ballot(mask_sel0(A, (fills ? 63u : qk) + 1u) > cap);
-                const uint32_t l0 = (uint32_t)__builtin_ctzll(E0);
+                // column filled — beyond the block's end, so never read)
+                uint32_t one = mask_sel0(A, 1u << (4 * col));
+                uint32_t same = ((scan_add32(one) - one) >> (4 * col)) & 15u;
+                uint32_t row = (uint32_t)__popcll((occ >> (7 * col)) & 0x3Full) + same;
+                uint32_t nacc = (uint32_t)__popc(in_vgpr((uint32_t)A)) + (uint32_t)__popc(in_vgpr((uint32_t)(A >> 32)));
+                bool fills = row == 5u;
+                uint64_t E0 = __ballot(mask_sel0(A, (fills ? 63u : qk) + 1u) > min(cap_r, nacc - 1u));
+                uint32_t l0 = (uint32_t)__builtin_ctzll(E0);
+                // the first fill, with room for more plies: re-draw the words after it under
+                // the new legal set
+                uint32_t lf = 64u;  // lane of the absorbed fill (64: none)
+                uint32_t ow2 = ow, cf = 0;
+                const uint32_t q0 = (uint32_t)__builtin_amdgcn_readlane((int)qk, (int)l0);
+                const uint32_t f0 = (uint32_t)__builtin_amdgcn_readlane((int)fills, (int)l0);
+                if (f0 && q0 < cap_r) {
+                    lf = l0;
+                    cf = (uint32_t)__builtin_amdgcn_readlane((int)col, (int)lf);
+                    ow2 = (uint32_t)__builtin_amdgcn_readlane((int)owm, (int)cf);
+                    const uint32_t n2 = (ow2 >> 24) & 15u;
+                    const uint32_t v2 = wv >> __clz(n2);
+                    const uint64_t low = (2ull << lf) - 1ull;  // lanes 0..lf
+                    // one compare: lanes 0..lf get bit 31 set (never < n2)
+                    A = (A & low) | __ballot((v2 | ((lane - lf - 1u) & 0x80000000u)) < n2);
+                    v = mask_sel(low, v2, v);
+                    const uint32_t owl = mask_sel(low, ow2, ow);
+                    qk = mbcnt(A);
+                    col = (owl >> (3 * (v & 7u))) & 7u;
+                    one = mask_sel0(A, 1u << (4 * col));
+                    same = ((scan_add32(one) - one) >> (4 * col)) & 15u;
+                    row = (uint32_t)__popcll((occ >> (7 * col)) & 0x3Full) + same;
+                    nacc = (uint32_t)__popc(in_vgpr((uint32_t)A)) + (uint32_t)__popc(in_vgpr((uint32_t)(A >> 32)));
+                    fills = row == 5u && lane > lf;  // the absorbed fill no longer ends the block
+                    E0 = __ballot(mask_sel0(A, (fills ? 63u : qk) + 1u) > min(cap_r, nacc - 1u));
+                    l0 = (uint32_t)__builtin_ctzll(E0);
+                }
+                // the block's last ply before any win
                 const uint32_t last = (uint32_t)__builtin_amdgcn_readlane((int)qk, (int)l0);
                 const uint64_t K = __ballot(mask_sel(A, 255u, qk) <= last);  // lanes of plies 0..last
                 // compact plies 0..last by parity (and a copy 32 lanes up); other lanes
@@ -199,7 +230,7 @@ __device__ void c4_rollouts(Leaf *L, int nb, Rng &rng, const uint32_t *s_order, 
                 const uint64_t Ew = __ballot(mask_sel0(K, (W32 >> c) & 1u) != 0u);
                 const uint32_t endlane = min(ff1(Ew), l0);
                 const uint32_t endply = (uint32_t)__builtin_amdgcn_readlane((int)qk, (int)endlane);
-                rng.off = endlane + 1u;  // words through the block's last ply are consumed
+                rng.off += endlane + 1u;  // words through the block's last ply are consumed
                 // both sides' stones after ply endply: first mover through ply 2*(endply/2)
                 // (row 0, inclusive), second mover through the odd plies <= endply (row 1,
                 // exclusive: lane 16 + (endply+1)/2; zero at the row's start)
@@ -219,13 +250,17 @@ __device__ void c4_rollouts(Leaf *L, int nb, Rng &rng, const uint32_t *s_order, 
                     val = 0;
                     break;
                 }
-                if ((R5 >> endlane) & 1u) {
-                    // a column filled: the legal set (and its CPython order) changes
+                if (endlane >= lf) {  // the absorbed fill was played: its legal set from now on
+                    mask &= ~(1 << cf);
+                    ow = ow2;
+                }
+                if (__builtin_amdgcn_readlane((int)fills, (int)endlane)) {
+                    // the block ended at a column fill: the legal set (and its CPython order) changes
                     mask &= ~(1 << __builtin_amdgcn_readlane((int)col, (int)endlane));
                     ow = uni(s_order[mask]);
-                    n = (ow >> 24) & 15u;
-                    sh = (uint32_t)__clz(n);
                 }
+                n = (ow >> 24) & 15u;
+                sh = (uint32_t)__clz(n);
             }
         }
         L[j].val = val;  // uniform: every lane stores

@@ -41,7 +41,7 @@ constexpr int kChunk = 192;            // words per generation step (<= 227, mul
 constexpr int kBlock = 64;             // threads per workgroup: one wave = one game
 constexpr int kPhases = 8;             // diagnostic phase-stamp slots per game
 
-static_assert(kLookahead + kChunk + 624 + 128 < kRingWords, "ring must retain the current MT block");
+static_assert(kLookahead + kChunk + 624 + 192 < kRingWords, "ring must retain the current MT block");
 
 struct Arena {
     uint8_t *nodes = nullptr;     // [G][M][128 B]
