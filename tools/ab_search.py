@@ -1,0 +1,50 @@
+#!/usr/bin/env python3
+"""A/B timing of library variants on the C2 search (4096 games x 800 sims x bs 32).
+
+    python tools/ab_search.py libA.so libB.so ...   (paths relative to the repo root)
+
+Each round runs every variant in its own process (ZC_LIB=<path>), in turn, so that clock
+and thermal drift hit all of them alike; prints the median search time per variant."""
+import os
+import statistics
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+CHILD = r'''
+import sys, time, torch
+sys.path.insert(0, %r)
+import numpy as np
+from zeroclone_amd import _native
+G, S, B = %d, 800, 32
+eng = _native.NativeEngine(max_games=G, max_sims=S, max_batch=B)
+roots = np.zeros(G, _native.C4_STATE_DTYPE)
+ts = []
+for r in range(9):
+    eng.seed(0, list(range(r * G, (r + 1) * G)))
+    t = time.perf_counter()
+    eng.c4_search(roots, S, 1.4, B)
+    ts.append(time.perf_counter() - t)
+ts = sorted(ts[2:])
+print(ts[len(ts) // 2] * 1e3)
+'''
+
+
+def main():
+    libs = sys.argv[1:]
+    games = int(os.environ.get("AB_GAMES", "4096"))
+    res = {lib: [] for lib in libs}
+    for rnd in range(int(os.environ.get("AB_ROUNDS", "3"))):
+        for lib in libs:
+            env = dict(os.environ, ZC_LIB=os.path.join(ROOT, lib))
+            out = subprocess.run([sys.executable, "-c", CHILD % (ROOT, games)], env=env, check=True,
+                                 capture_output=True, text=True, timeout=300).stdout
+            res[lib].append(float(out.strip().splitlines()[-1]))
+            print(rnd, lib, res[lib][-1], flush=True)
+    for lib in libs:
+        print(f"{lib}: median {statistics.median(res[lib]):.3f} ms  all {res[lib]}")
+
+
+if __name__ == "__main__":
+    main()

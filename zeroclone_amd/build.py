@@ -12,7 +12,8 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
-LIB = os.path.join(HERE, "libzeroclone_amd.so")
+# ZC_LIB: load (and build) another copy of the library, e.g. a variant for an A/B timing run
+LIB = os.environ.get("ZC_LIB") or os.path.join(HERE, "libzeroclone_amd.so")
 SOURCES = ["engine.hip", "c4_search.hip", "c4_ext.hip", "chess.hip", "chess_search.hip", "chess_puct.hip", "net_conv.hip"]
 HEADERS = ["zc_internal.h", "c4_order_table.h", "c4_device.h", "chess_device.h", "chess_tree.h", "counter_rng.h", os.path.join("..", "..", "include", "zeroclone.h")]
 ARCH = os.environ.get("ZC_OFFLOAD_ARCH", "gfx950")
@@ -41,13 +42,14 @@ def build(force: bool = False, verbose: bool = False) -> str:
     if not force and not _stale():
         return LIB
     from concurrent.futures import ThreadPoolExecutor
-    objdir = os.path.join(HERE, "build_obj")
+    objdir = os.path.join(HERE, "build_obj" if LIB.endswith("libzeroclone_amd.so") else "build_obj_" + os.path.basename(LIB))
     os.makedirs(objdir, exist_ok=True)
     # -ffp-contract=off: the UCT arithmetic must round exactly like the reference's
     # (explicit fma only where GCC emitted one for mcts.cpp:44).
     def compile_one(src):
         obj = os.path.join(objdir, os.path.splitext(src)[0] + ".o")
-        cmd = [hipcc(), f"--offload-arch={ARCH}", *FLAGS, "-c", os.path.join(CSRC, src), "-o", obj]
+        cmd = [hipcc(), f"--offload-arch={ARCH}", *FLAGS, *os.environ.get("ZC_CFLAGS", "").split(), "-c",
+               os.path.join(CSRC, src), "-o", obj]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         subprocess.run(cmd, check=True)

@@ -30,6 +30,9 @@ __device__ __forceinline__ void load_tables(uint32_t *s_order) {
     for (int i = (int)threadIdx.x; i < 128; i += blockDim.x) s_order[i] = d_order[i];
 }
 constexpr int kWin = 64;                             // RNG window: one word per lane
+// LDS bytes after the leaves' paths: select_flush stores a path with all 64 lanes, so the
+// last leaf's lanes >= kMaxDepth land here
+constexpr int kPathSpill = 2 * (64 - kMaxDepth) + 24;
 
 // ------------------------------------------------------------------ wave helpers
 __device__ __forceinline__ uint32_t uni(uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); }
@@ -473,7 +476,7 @@ __device__ __forceinline__ void select_flush(const Tree &t, Fresh *fresh, Leaf *
         leaves[j] = Leaf{l0, l1, (uint32_t)leaf | ((uint32_t)ldepth << 16) | ((uint32_t)lturn << 24) | ((uint32_t)lmask << 25),
                          0, low_, 0};
         // all 64 lanes store: lanes >= kMaxDepth spill into leaf j+1's path (written after
-        // this) or, for the flush's last leaf, into the scratch LDS that follows the paths
+        // this) or, for the flush's last leaf, into the kPathSpill bytes that follow the paths
         paths[j * kMaxDepth + lane] = (uint16_t)lpath;
         wave_mem_order();
         stamp.mark(3);

@@ -58,9 +58,6 @@ __device__ __forceinline__ uint32_t scan_add32(uint32_t x) {
     return x;
 }
 
-// LDS words of the rollout's compaction scratch: 64 compacted plies + 96 for lanes not written
-constexpr int kPermWords = 160;
-
 // Inclusive prefix OR within each 16-lane row (DPP row_shr 1, 2, 4, 8): four independent
 // 16-lane scans per wave, of two values at once (the two halves of a bitboard), interleaved
 // so that each DPP read finds its operand written two instructions earlier.
@@ -111,9 +108,11 @@ __device__ __forceinline__ uint32_t row_prev(uint32_t x) {
 //
 // A column fill changes the legal set (n, k and the CPython order).  The block's FIRST fill
 // is absorbed: the words after it are re-drawn under the new legal set (a second ballot and
-// prefix sum over the same view, the new order word prefetched for every possible column at
-// the block's start).  The block ends at its second fill, the board-full ply, its 31st ply
-// or its last accepted word.
+// prefix sum over the same view; the order words after one or two fills come from a table
+// of every column pair read at the block's start).  The block ends at its second fill, the
+// board-full ply, its 31st ply or its last accepted word: ~1.29 blocks per rollout (2.12
+// with 64-aligned windows and no absorption).  Absorbing every fill (~1.03 blocks) measured
+// SLOWER: 4,841 vs 3,554 rollout cycles per simulation.
 //
 // The win test runs on a COMPACTED copy of the block's plies: ply q goes (through 64 dwords
 // of LDS) to lane (q & 1)*16 + q/2 and to that lane + 32, so rows 0 and 2 hold the first
@@ -125,17 +124,20 @@ __device__ __forceinline__ uint32_t row_prev(uint32_t x) {
 // Work is placed for the scalar unit's sake: the boards are uniform values kept in VGPRs,
 // lane conditions are single compares whose ballots are used as v_cndmask masks, and the
 // scalar unit only handles the masks, the block's end and the loop control.
-__device__ void c4_rollouts(Leaf *L, int nb, Rng &rng, const uint32_t *s_order, uint32_t *s_perm, Counters &cn) {
+__device__ void c4_rollouts(Leaf *L, int nb, Rng &rng, const uint32_t *s_order, Counters &cn) {
     const uint32_t lane = lane_id();
     const uint32_t lrow = lane >> 4;
     const uint32_t myply = 2u * (lane & 15u) + (lrow & 1u);  // ply of this lane in the compacted layout
     const bool first_row = (lrow & 1u) == 0;                  // rows 0, 2: the block's first mover
     const uint32_t d1 = lrow < 2 ? 1u : 6u, d2 = lrow < 2 ? 7u : 8u;
     const uint32_t hd = (0x08070601u >> (8u * (lane & 3u))) & 0xFFu;  // lanes 0..3: one direction each
+    // lane 7a + b (< 49): the columns {a, b} (a == b: one column) whose fills a block may see
+    const uint32_t pairbits = lane < 49u ? (1u << (lane / 7u)) | (1u << (lane % 7u)) : 0u;
     for (int j = 0; j < nb; ++j) {
         const uint32_t lm = uni(L[j].meta);
         const uint64_t x0 = in_vgpr(L[j].p0);
         const uint64_t x1 = in_vgpr(L[j].p1);
+        const uint32_t low0 = uni(L[j].ow);
         const bool tn = (lm >> 24) & 1u;
         uint64_t me = tn ? x1 : x0;  // side to move
         uint64_t op = tn ? x0 : x1;  // last mover
@@ -148,13 +150,13 @@ __device__ void c4_rollouts(Leaf *L, int nb, Rng &rng, const uint32_t *s_order, 
         } else if (room0 >= 0) {  // not check_draw
             int room = room0;
             int mask = (int)(lm >> 25);
-            uint32_t ow = uni(L[j].ow);
+            uint32_t ow = low0;
             uint32_t n = (ow >> 24) & 15u;
             uint32_t sh = (uint32_t)__clz(n);
             for (;;) {
                 if (rng.off >= (uint32_t)kWin) rng_advance(rng);
-                // order word of the legal set minus column `lane` (lanes 0..6), for a fill
-                const uint32_t owm = s_order[(uint32_t)mask & ~(1u << (lane & 7u))];
+                // order words of the legal set minus the columns of `pairbits`, for the fills
+                const uint32_t owp = s_order[(uint32_t)mask & ~pairbits];
                 const uint32_t wv = rng_view(rng);  // lane l: word off + l
                 uint32_t v = wv >> sh;
                 uint64_t A = __ballot(v < n);  // accepted words
@@ -186,7 +188,7 @@ __device__ void c4_rollouts(Leaf *L, int nb, Rng &rng, const uint32_t *s_order, 
                 if (f0 && q0 < cap_r) {
                     lf = l0;
                     cf = (uint32_t)__builtin_amdgcn_readlane((int)col, (int)lf);
-                    ow2 = (uint32_t)__builtin_amdgcn_readlane((int)owm, (int)cf);
+                    ow2 = (uint32_t)__builtin_amdgcn_readlane((int)owp, (int)(8u * cf));
                     const uint32_t n2 = (ow2 >> 24) & 15u;
                     const uint32_t v2 = wv >> __clz(n2);
                     const uint64_t low = (2ull << lf) - 1ull;  // lanes 0..lf
@@ -207,15 +209,13 @@ __device__ void c4_rollouts(Leaf *L, int nb, Rng &rng, const uint32_t *s_order, 
                 // the block's last ply before any win
                 const uint32_t last = (uint32_t)__builtin_amdgcn_readlane((int)qk, (int)l0);
                 const uint64_t K = __ballot(mask_sel(A, 255u, qk) <= last);  // lanes of plies 0..last
-                // compact plies 0..last by parity (and a copy 32 lanes up); other lanes
-                // write to a scratch area above
+                // compact plies 0..last by parity into lanes 0..31 (a forward lane permute;
+                // other lanes all go to lane 31, which no ply <= 30 uses), then copy them 32
+                // lanes up
                 const uint32_t c = (qk & 1u) * 16u + (qk >> 1);
-                const uint32_t t = mask_sel(K, 64u + lane, c);
                 const uint32_t b = 7u * col + row + 1u;
-                s_perm[t] = b;
-                s_perm[t + 32] = b;
-                wave_mem_order();
-                const uint32_t pb = s_perm[lane];
+                const uint32_t pl = (uint32_t)__builtin_amdgcn_ds_permute((int)(mask_sel(K, 31u, c) << 2), (int)b);
+                const uint32_t pb = __builtin_amdgcn_permlane32_swap(pl, pl, false, false)[0];
                 const uint64_t V = __ballot(myply <= last);  // lanes holding plies 0..last
                 const uint64_t bit = 1ull << (pb - 1u);
                 uint32_t blo = mask_sel0(V, (uint32_t)bit), bhi = mask_sel0(V, (uint32_t)(bit >> 32));
@@ -250,14 +250,15 @@ __device__ void c4_rollouts(Leaf *L, int nb, Rng &rng, const uint32_t *s_order, 
                     val = 0;
                     break;
                 }
-                if (endlane >= lf) {  // the absorbed fill was played: its legal set from now on
-                    mask &= ~(1 << cf);
-                    ow = ow2;
-                }
-                if (__builtin_amdgcn_readlane((int)fills, (int)endlane)) {
-                    // the block ended at a column fill: the legal set (and its CPython order) changes
-                    mask &= ~(1 << __builtin_amdgcn_readlane((int)col, (int)endlane));
-                    ow = uni(s_order[mask]);
+                // the legal set (and its CPython order) after the block's fills: the absorbed
+                // one if it was played, and the one the block ended at
+                const bool fa = endlane >= lf;
+                const bool fe = __builtin_amdgcn_readlane((int)fills, (int)endlane) != 0;
+                if (fa | fe) {
+                    const uint32_t ce = fe ? (uint32_t)__builtin_amdgcn_readlane((int)col, (int)endlane) : cf;
+                    const uint32_t ca = fa ? cf : ce;
+                    mask &= ~((1 << ca) | (1 << ce));
+                    ow = (uint32_t)__builtin_amdgcn_readlane((int)owp, (int)(7u * ca + ce));
                 }
                 n = (ow >> 24) & 15u;
                 sh = (uint32_t)__clz(n);
@@ -355,9 +356,9 @@ __global__ __launch_bounds__(kBlock) void c4_search_kernel(SearchParams p) {
     Fresh *const fresh = (Fresh *)(s_dyn + kTabBytes);
     Leaf *const leaves = (Leaf *)(s_dyn + kTabBytes + sizeof(Fresh) * (size_t)p.bs);
     uint16_t *const paths = (uint16_t *)(s_dyn + kTabBytes + (sizeof(Fresh) + sizeof(Leaf)) * (size_t)p.bs);
-    uint32_t *const s_perm = (uint32_t *)(s_dyn + kTabBytes +
-                                          (sizeof(Fresh) + sizeof(Leaf) + sizeof(uint16_t) * kMaxDepth) * (size_t)p.bs);
-    uint8_t *const s_sel = (uint8_t *)(s_perm + kPermWords);  // Philox mode only
+    uint8_t *const s_sel = (uint8_t *)(s_dyn + kTabBytes +
+                                       (sizeof(Fresh) + sizeof(Leaf) + sizeof(uint16_t) * kMaxDepth) * (size_t)p.bs +
+                                       kPathSpill);  // Philox mode only
     load_tables(s_order);
     if (PHILOX) load_sel(s_sel);
     __syncthreads();
@@ -425,7 +426,7 @@ __global__ __launch_bounds__(kBlock) void c4_search_kernel(SearchParams p) {
             c4_rollouts_philox(leaves, nb, s_sel, make_uint2((uint32_t)p.philox_seed, (uint32_t)(p.philox_seed >> 32)),
                                (uint32_t)done, tag, (uint32_t)g, cn);
         else
-            c4_rollouts(leaves, nb, rng, s_order, s_perm, cn);
+            c4_rollouts(leaves, nb, rng, s_order, cn);
         wave_mem_order();
         stamp.mark(4);
 
@@ -550,7 +551,6 @@ __global__ __launch_bounds__(kBlock) void c4_rollout_debug_kernel(Arena a, int f
                                                                   int64_t *out_words) {
     __shared__ Leaf s_leaf[1];
     __shared__ uint32_t s_order[128];
-    __shared__ uint32_t s_perm[kPermWords];
     load_tables(s_order);
     __syncthreads();
     const uint32_t lane = lane_id();
@@ -569,7 +569,7 @@ __global__ __launch_bounds__(kBlock) void c4_rollout_debug_kernel(Arena a, int f
     }
     wave_mem_order();
     Counters cn;
-    c4_rollouts(s_leaf, 1, rng, s_order, s_perm, cn);
+    c4_rollouts(s_leaf, 1, rng, s_order, cn);
     wave_mem_order();
     if (lane == 0) {
         out_value[gl] = s_leaf[0].val;
@@ -583,7 +583,6 @@ __global__ __launch_bounds__(kBlock) void c4_rollout_seq_kernel(Arena a, int g, 
                                                                 int32_t *out_value, int64_t *out_words) {
     __shared__ Leaf s_leaf[kBlock];
     __shared__ uint32_t s_order[128];
-    __shared__ uint32_t s_perm[kPermWords];
     load_tables(s_order);
     __syncthreads();
     const uint32_t lane = lane_id();
@@ -602,7 +601,7 @@ __global__ __launch_bounds__(kBlock) void c4_rollout_seq_kernel(Arena a, int g, 
         }
         wave_mem_order();
         rng_fill(rng, rng.use() + kLookahead);
-        c4_rollouts(s_leaf, cnt, rng, s_order, s_perm, cn);
+        c4_rollouts(s_leaf, cnt, rng, s_order, cn);
         wave_mem_order();
         if ((int)lane < cnt) out_value[base + lane] = s_leaf[lane].val;
         wave_mem_order();
@@ -643,7 +642,7 @@ __global__ void uct_debug_kernel(int n, const double *logn, const int32_t *na, c
 }  // namespace
 
 size_t c4_search_lds_bytes(int bs) {
-    return kTabBytes + (sizeof(Leaf) + sizeof(Fresh) + sizeof(uint16_t) * kMaxDepth) * (size_t)bs + kPermWords * sizeof(uint32_t);
+    return kTabBytes + (sizeof(Leaf) + sizeof(Fresh) + sizeof(uint16_t) * kMaxDepth) * (size_t)bs + kPathSpill;
 }
 
 void launch_c4_search(const SearchParams &p, hipStream_t s) {
