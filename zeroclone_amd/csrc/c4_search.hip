@@ -438,33 +438,41 @@ __global__ __launch_bounds__(kBlock) void c4_search_kernel(SearchParams p) {
         //   levels > d0 (fresh nodes): LDS atomics into the fresh node's in-edge counters,
         //     written to HBM with the fresh records below.
         // Node::N is not stored: it equals Na of the in-edge (root: leaves flushed so far).
+        // the prefix edges' counters are read first, so their HBM latency overlaps the LDS work
+        const bool pre = lane >= 1 && lane <= (uint32_t)d0;
+        const int par = __shfl((int)(fs.ppath & 0xFFFFu), (int)lane - 1);
+        const int act = (int)(fs.ppath >> 16);
+        int32_t na0 = 0, w0 = 0;
+        if (pre) {
+            na0 = t.na(par)[act];
+            w0 = t.w(par)[act];
+        }
         int S = 0;
         for (int base = 0; base < nb; base += 64) {
+            // lane = leaf: S, and the fresh edges (levels d0+1..d of the leaf's path), one level
+            // per step for all leaves at once
             const int jj = base + (int)lane;
-            int sv = 0;
+            int v = 0, d = -1, sv = 0;
             if (jj < nb) {
-                const int v = leaves[jj].val;
-                sv = ((leaves[jj].meta >> 16) & 1u) ? -v : v;
+                const uint32_t meta = leaves[jj].meta;
+                v = leaves[jj].val;
+                d = (int)((meta >> 16) & 0xFFu);
+                sv = (d & 1) ? -v : v;
             }
             S += __popcll(__ballot(sv > 0)) - __popcll(__ballot(sv < 0));
-        }
-        for (int j = 0; j < nb; ++j) {
-            const uint32_t meta = uni(leaves[j].meta);
-            const int d = (int)((meta >> 16) & 0xFFu);
-            const int v = uni(leaves[j].val);
-            if (lane > (uint32_t)d0 && lane <= (uint32_t)d) {
-                const int fi = (int)paths[j * kMaxDepth + lane] - f0;
-                const int vl = ((d - (int)lane) & 1) ? -v : v;
-                atomicAdd(&fresh[fi].na, 1);
-                atomicAdd(&fresh[fi].w, -vl);
+            for (int l = d0 + 1; __ballot(l <= d); ++l) {
+                if (l <= d) {
+                    const int fi = (int)paths[jj * kMaxDepth + l] - f0;
+                    const int vl = ((d - l) & 1) ? -v : v;
+                    atomicAdd(&fresh[fi].na, 1);
+                    atomicAdd(&fresh[fi].w, -vl);
+                }
             }
         }
-        if (lane >= 1 && lane <= (uint32_t)d0) {
-            const int par = __shfl((int)(fs.ppath & 0xFFFFu), (int)lane - 1);
-            const int act = (int)(fs.ppath >> 16);
+        if (pre) {
             const int dw = (lane & 1u) ? S : -S;  // Wa -= (-1)^l * S
-            const int32_t na1 = t.na(par)[act] + nb;
-            const int32_t w1 = t.w(par)[act] + dw;
+            const int32_t na1 = na0 + nb;
+            const int32_t w1 = w0 + dw;
             t.na(par)[act] = na1;
             t.w(par)[act] = w1;
             t.q(par)[act] = (double)w1 / (double)na1;  // Qa = Wa / Na
