@@ -112,10 +112,11 @@ __device__ __forceinline__ uint32_t row_prev(uint32_t x) {
 // of every column pair read at the block's start).  The block ends at its second fill, the
 // board-full ply, its 31st ply or its last accepted word: ~1.29 blocks per rollout (2.12
 // with 64-aligned windows and no absorption).  Absorbing every fill (~1.03 blocks) measured
-// SLOWER: 4,841 vs 3,554 rollout cycles per simulation.
+// SLOWER (4,841 vs 3,554 rollout cycles per simulation), as did a second absorbed fill
+// (+4.7 %) and an absorption computed branch-free in every block (+1 %).
 //
-// The win test runs on a COMPACTED copy of the block's plies: ply q goes (through 64 dwords
-// of LDS) to lane (q & 1)*16 + q/2 and to that lane + 32, so rows 0 and 2 hold the first
+// The win test runs on a COMPACTED copy of the block's plies: ply q goes (one forward lane
+// permute) to lane (q & 1)*16 + q/2 and to that lane + 32, so rows 0 and 2 hold the first
 // mover's plies in order, rows 1 and 3 the other side's.  One 16-lane prefix-OR scan per
 // row then gives every ply its mover's new stones, and the copy lets rows 0/1 test the
 // vertical and horizontal directions while rows 2/3 test the diagonals.  The first winning
