@@ -66,6 +66,39 @@ def test_rollouts_match_reference(eng, golden):
     assert [int(x) for x in words] == [c["consumed"] for c in cases]
 
 
+def test_sequential_rollouts_stress_block_logic(eng):
+    """Thousands of rollouts back to back on ONE stream (value.batch order), from positions of
+    every depth — many with full or nearly full columns, won and drawn boards included — so
+    that blocks cross stream windows and absorb column fills (one or two per block, ply-30
+    caps, board-full draws) in every combination.  Each value and the stream position after
+    the whole sequence must equal the oracle's."""
+    rng = random.Random(2024)
+    boards = []
+    while len(boards) < 3000:
+        b, t = "." * 42, 0
+        depth = rng.randint(0, 42)
+        lean = rng.sample(range(7), rng.randint(1, 7))  # columns the game prefers: fills come early
+        for _ in range(depth):
+            legal = [col for col in range(7) if b[col] == "."]
+            if not legal:
+                break
+            pref = [col for col in legal if col in lean]
+            col = rng.choice(pref if pref and rng.random() < 0.8 else legal)
+            b, t = oracle.play(b, t, col)
+            if oracle.check_win(b, t) and rng.random() < 0.7:
+                break
+        boards.append((b, t))
+    seed = 77
+    mt = oracle.MT(seed)
+    exp = []
+    for b, t in boards:
+        exp.append(oracle.lib().zco_rollout(b.encode(), t, ctypes.byref(mt.s)))
+    eng.seed(3, [seed])
+    got, words = eng.c4_rollouts(states([{"board": b, "turn": t} for b, t in boards]), game=3)
+    assert [int(x) for x in got] == exp
+    assert words == mt.drawn
+
+
 def test_get_move_matches_reference(eng, golden):
     cases = golden("c4_get_move.json")["cases"]
     groups = defaultdict(list)
