@@ -468,8 +468,6 @@ __device__ __forceinline__ void select_flush(const Tree &t, Fresh *fresh, Leaf *
                 fresh[node - f0].u = u;
                 fresh[node - f0].ch[mi] = (uint16_t)leaf;
             }
-            cn.add(cn.expansions, 1);
-            cn.add(cn.depth_sum, ldepth);
         }
         // the leaf's path: the walk's path plus the new node (the next walk resumes at `node`)
         const uint32_t lpath = (cnt && lane == (uint32_t)ldepth) ? (uint32_t)leaf : pathv;
@@ -484,6 +482,20 @@ __device__ __forceinline__ void select_flush(const Tree &t, Fresh *fresh, Leaf *
     if (node == x0node) {
         x_u = u;
         x_ch = ch;
+    }
+    // the flush's expansions = its fresh nodes; their depths summed lane-parallel (bit-sliced
+    // ballots) instead of per expansion on the chain
+    {
+        const int nf = nnodes - f0;
+        int dsum = 0;
+        for (int base = 0; base < nf; base += 64) {
+            const int i = base + (int)lane;
+            const uint32_t d = i < nf ? fresh[i].link >> 24 : 0u;
+#pragma unroll
+            for (int bit = 0; bit < 6; ++bit) dsum += __popcll(__ballot((d >> bit) & 1u)) << bit;
+        }
+        cn.add(cn.expansions, nf);
+        cn.add(cn.depth_sum, dsum);
     }
     fs.x0_dirty = x0_dirty;
     fs.x_u = x_u;
