@@ -295,7 +295,8 @@ int zc_chess_puct_end(zc_engine *eng, int32_t first_game, int32_t n_games, float
  *     weight [9][128][cin] fp16 (tap = ky*3+kx, then output channel, then input channel),
  *     bias [128] f32, residual NULL or [n][h][w][128] fp16, relu 0/1.  Shapes: (h, w) in
  *     {(8, 8), (6, 7)}, cin in {32, 128}; others are ZC_EINVAL.
- *   zc_net_planes_to_nhwc_async: state_to_tensor planes [n][cin][h*w] fp16 -> [n][h*w][cpad].
+ *   zc_net_planes_to_nhwc_async: state_to_tensor planes [n][cin][h*w] fp16 -> [n][h*w][cpad],
+ *     zero padded; cpad a multiple of 8 (16-byte rows), d_out 16-byte aligned.
  *   zc_net_value_head_async: mean over pixels -> dot(fc_w[128]) + fc_b -> tanh, as fp64
  *     values[n] (the input of zc_*_ext_backup).
  * Device pointers, enqueued on hip_stream (NULL = null stream); no engine needed. */

@@ -843,7 +843,9 @@ int zc_net_conv3x3_async(int32_t n, int32_t h, int32_t w, int32_t cin, const voi
 
 int zc_net_planes_to_nhwc_async(int32_t n, int32_t cin, int32_t hw, int32_t cpad, const void *d_planes, void *d_out,
                                 void *hip_stream) {
-    if (n < 0 || cin < 1 || hw < 1 || cpad < cin || (n && (!d_planes || !d_out))) return fail(ZC_EINVAL, "bad argument");
+    if (n < 0 || cin < 1 || hw < 1 || cpad < cin || (cpad & 7) || ((uintptr_t)d_out & 15) ||
+        (n && (!d_planes || !d_out)))
+        return fail(ZC_EINVAL, "bad argument");
     if (!n) return ZC_OK;
     zc::launch_net_planes_to_nhwc(n, cin, hw, cpad, d_planes, d_out, (hipStream_t)hip_stream);
     ZC_HIP(hipGetLastError());

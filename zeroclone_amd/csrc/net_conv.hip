@@ -405,8 +405,17 @@ __global__ void planes_to_nhwc_kernel(int n, int cin, int hw, int cpad, const _F
     const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (g >= (int64_t)n * hw) return;
     const int i = (int)(g / hw), p = (int)(g - (int64_t)i * hw);
-    _Float16 *o = out + g * cpad;
-    for (int c = 0; c < cpad; ++c) o[c] = c < cin ? planes[((size_t)i * cin + c) * hw + p] : (_Float16)0.0f;
+    const _Float16 *src = planes + (size_t)i * cin * hw + p;
+    h8 *o = (h8 *)(out + g * cpad);  // cpad is a multiple of 8: 16-byte stores
+    for (int c8 = 0; c8 < cpad / 8; ++c8) {
+        h8 v;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const int c = c8 * 8 + e;
+            v[e] = c < cin ? src[(size_t)c * hw] : (_Float16)0.0f;
+        }
+        o[c8] = v;
+    }
 }
 
 // head (network.py:37-42): global average pool -> Linear(128, 1) -> tanh, in fp32; one wave
