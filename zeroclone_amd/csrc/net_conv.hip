@@ -219,11 +219,14 @@ __global__ __launch_bounds__(256) void conv3x3_kernel(int nboards, const _Float1
 }
 
 // Half-tile form: 128-pixel tiles with ONE weight buffer, 70 KB of LDS, so two workgroups
-// share a CU and one's staging, barriers and epilogue run under the other's MFMAs.  Wave w
+// share a CU and one's staging, barriers and epilogue run under the other's MFMAs.  Its
+// epilogue goes through LDS so that the residual loads and output stores cover whole
+// 256-byte pixel rows (3-7 % per layer over per-fragment 16-byte pieces).  Wave w
 // owns output channels [64 (w & 1), +64) x pixels [64 (w >> 1), +64) (2 x 2 MFMA tiles).
 // Per tap: the next tap's weights are fetched into registers during the MFMAs, then
 // barrier -> store -> barrier.  Same accumulation order as conv3x3_kernel (bit-identical).
 constexpr int kHalfPix = 128;
+constexpr size_t kHalfEpiBytes = (size_t)kHalfPix * (kCout + 4) * sizeof(float);  // the epilogue's fp32 tile
 
 template <int H, int W, int BPW, int CIN>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void conv3x3_half_kernel(int nboards, const _Float16 *__restrict__ in,
@@ -353,51 +356,48 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         }
     }
 
-    h4 rv[2][2][4];
-    if (res) {
+    // epilogue through LDS: the fp32 tile is transposed to [pixel][cout] (rows padded by 4
+    // floats) so that bias, residual, ReLU and the fp16 store run on whole 256-byte output
+    // rows, 16 lanes per pixel — coalesced residual loads and stores instead of 16-byte
+    // pieces of 32 different rows per instruction.  Same fp32 operations in the same order.
+    constexpr int SL = kCout + 4;
+    // (the launch sizes the LDS for this tile too: kHalfEpiBytes)
+    float *const sacc = (float *)lds;
+    __syncthreads();  // every wave is done with the input tile and the weights
 #pragma unroll
-        for (int t = 0; t < 2; ++t) {
-            const int P = min(p0 + t * 32 + r, max(npix - 1, 0));
-            const size_t orow = ((size_t)b0 * HW + P) * kCout;
-#pragma unroll
-            for (int m = 0; m < 2; ++m)
-#pragma unroll
-                for (int g = 0; g < 4; ++g) rv[t][m][g] = *(const h4 *)(res + orow + (m0 + m) * 32 + 8 * g + 4 * hh);
-        }
-    }
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-        const int P = p0 + t * 32 + r;
-        const size_t orow = ((size_t)b0 * HW + P) * kCout;
+    for (int t = 0; t < 2; ++t)
 #pragma unroll
         for (int m = 0; m < 2; ++m)
 #pragma unroll
             for (int g = 0; g < 4; ++g) {
-                const int co = (m0 + m) * 32 + 8 * g + 4 * hh;
-                const float4 bb = *(const float4 *)(bias + co);
-                float v0 = acc[m][t][4 * g + 0] + bb.x, v1 = acc[m][t][4 * g + 1] + bb.y;
-                float v2 = acc[m][t][4 * g + 2] + bb.z, v3 = acc[m][t][4 * g + 3] + bb.w;
-                if (res) {
-                    v0 += (float)rv[t][m][g][0];
-                    v1 += (float)rv[t][m][g][1];
-                    v2 += (float)rv[t][m][g][2];
-                    v3 += (float)rv[t][m][g][3];
-                }
-                if (relu) {
-                    v0 = fmaxf(v0, 0.0f);
-                    v1 = fmaxf(v1, 0.0f);
-                    v2 = fmaxf(v2, 0.0f);
-                    v3 = fmaxf(v3, 0.0f);
-                }
-                h4 o;
-                o[0] = (_Float16)v0;
-                o[1] = (_Float16)v1;
-                o[2] = (_Float16)v2;
-                o[3] = (_Float16)v3;
-                if (P < npix) *(h4 *)(out + orow + co) = o;
+                const int P = p0 + t * 32 + r, co = (m0 + m) * 32 + 8 * g + 4 * hh;
+                *(float4 *)(sacc + P * SL + co) =
+                    make_float4(acc[m][t][4 * g + 0], acc[m][t][4 * g + 1], acc[m][t][4 * g + 2], acc[m][t][4 * g + 3]);
             }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < kHalfPix * (kCout / 8) / 256; ++q) {
+        const int i = tid + q * 256, P = i >> 4, c0 = (i & 15) * 8;
+        if (P < npix) {
+            const size_t o = ((size_t)b0 * HW + P) * kCout + c0;
+            h8 rv8;
+            if (res) rv8 = *(const h8 *)(res + o);
+            const float4 a0 = *(const float4 *)(sacc + P * SL + c0), a1 = *(const float4 *)(sacc + P * SL + c0 + 4);
+            const float4 b0v = *(const float4 *)(bias + c0), b1v = *(const float4 *)(bias + c0 + 4);
+            float v[8] = {a0.x + b0v.x, a0.y + b0v.y, a0.z + b0v.z, a0.w + b0v.w,
+                          a1.x + b1v.x, a1.y + b1v.y, a1.z + b1v.z, a1.w + b1v.w};
+            h8 ov;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                if (res) v[e] += (float)rv8[e];
+                if (relu) v[e] = fmaxf(v[e], 0.0f);
+                ov[e] = (_Float16)v[e];
+            }
+            *(h8 *)(out + o) = ov;
+        }
     }
 }
+
 
 // planes [n][cin][H*W] (state_to_tensor layout, fp16) -> NHWC [n][H*W][cpad], zero padded.
 __global__ void planes_to_nhwc_kernel(int n, int cin, int hw, int cpad, const _Float16 *__restrict__ planes,
@@ -449,7 +449,7 @@ template <int H, int W, int BPW, int BPH, int CIN>
 void launch_conv(int n, const void *in, const void *wt, const float *bias, const void *res, void *out, int relu,
                  hipStream_t s) {
     if (conv_impl() == 1 && CIN >= 64) {  // the 32-plane stem runs faster on 256-pixel tiles
-        const size_t lds = (size_t)(kHalfPix + 1 + kCout) * (CIN + 8) * sizeof(_Float16);
+        const size_t lds = std::max((size_t)(kHalfPix + 1 + kCout) * (CIN + 8) * sizeof(_Float16), kHalfEpiBytes);
         hipLaunchKernelGGL((conv3x3_half_kernel<H, W, BPH, CIN>), dim3((n + BPH - 1) / BPH), dim3(256), lds, s, n,
                            (const _Float16 *)in, (const _Float16 *)wt, bias, (const _Float16 *)res, (_Float16 *)out,
                            relu);
