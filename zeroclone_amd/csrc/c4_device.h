@@ -16,7 +16,8 @@ constexpr uint32_t kRingMask = kRingWords - 1;
 constexpr uint64_t kBottom = 0x0000040810204081ull;  // bit 7c: bottom cell of column c
 constexpr uint64_t kFull = kBottom * 0x3Full;        // the 42 playable cells
 constexpr uint64_t kTop = kBottom << 5;              // top playable cell of each column
-constexpr int kTabBytes = 128 * 4;  // LDS table: move-list order[128]
+// LDS tables: move-list order[128] u32, then sel[128][8] u8 (the r-th set bit of a 7-bit mask)
+constexpr int kTabBytes = 128 * 4 + 128 * 8;
 
 // Untried moves of a node (record +4 / Fresh.u): bit i (i < 7) set while move i of the
 // node's move list is untried; bits 28..31 = number of moves.  The reference keeps the
@@ -25,10 +26,26 @@ constexpr int kTabBytes = 128 * 4;  // LDS table: move-list order[128]
 __device__ __forceinline__ uint32_t untried_init(uint32_t n) { return ((1u << n) - 1u) | (n << 28); }
 __device__ __forceinline__ uint32_t untried_count(uint32_t u) { return (uint32_t)__popc(u & 0x7Fu); }
 
-// Fill the LDS table (whole workgroup): s_order = d_order.
+// Fill the LDS tables (whole workgroup): s_order = d_order; sel[m][r] = position of the r-th
+// set bit of m (7 when m has fewer), right after s_order.
 __device__ __forceinline__ void load_tables(uint32_t *s_order) {
     for (int i = (int)threadIdx.x; i < 128; i += blockDim.x) s_order[i] = d_order[i];
+    uint8_t *const s_sel = (uint8_t *)(s_order + 128);
+    for (int i = (int)threadIdx.x; i < 1024; i += blockDim.x) {
+        const uint32_t m = (uint32_t)i >> 3, r = (uint32_t)i & 7u;
+        uint32_t c = 0, pos = 7;
+        for (uint32_t b = 0; b < 7; ++b)
+            if ((m >> b) & 1u) {
+                if (c == r) {
+                    pos = b;
+                    break;
+                }
+                ++c;
+            }
+        s_sel[i] = (uint8_t)pos;
+    }
 }
+__device__ __forceinline__ const uint8_t *sel_table(const uint32_t *s_order) { return (const uint8_t *)(s_order + 128); }
 constexpr int kWin = 64;                             // RNG window: one word per lane
 // LDS bytes after the leaves' paths: select_flush stores a path with all 64 lanes, so the
 // last leaf's lanes >= kMaxDepth land here
@@ -218,6 +235,27 @@ __device__ __forceinline__ uint32_t rng_below(Rng &r, uint32_t n) {
             const int f = __builtin_ctzll(bal);
             r.off = (uint32_t)f + 1;
             return (uint32_t)__builtin_amdgcn_readlane((int)v, f);
+        }
+        r.off = kWin;
+    }
+}
+
+// random.choice(untried) of an expansion (policy_functions.py:12 with the untried list in
+// list order, mcts.cpp:67-72): rng_below(n) as above, but every lane also looks up row[v]
+// (row = sel[untried mask]: the v-th untried move) for its own candidate word, so the move
+// index of the accepted draw is a readlane of that lookup (n <= 7, so v < 8).
+__device__ __forceinline__ uint32_t rng_below_pick(Rng &r, uint32_t n, const uint8_t *row) {
+    const uint32_t sh = (uint32_t)__clz(n);
+    const uint32_t lane = lane_id();
+    for (;;) {
+        if (r.off >= (uint32_t)kWin) rng_advance(r);
+        const uint32_t v = r.wt >> sh;
+        const uint32_t pick = row[v & 7u];
+        const uint64_t bal = __ballot((v | ((lane - r.off) & 0x80000000u)) < n);
+        if (bal) {
+            const int f = __builtin_ctzll(bal);
+            r.off = (uint32_t)f + 1;
+            return (uint32_t)__builtin_amdgcn_readlane((int)pick, f);
         }
         r.off = kWin;
     }
@@ -438,13 +476,8 @@ __device__ __forceinline__ void select_flush(const Tree &t, Fresh *fresh, Leaf *
         const uint32_t cnt = untried_count(u);
         uint32_t low_ = ow;  // the leaf's move-list order word
         if (cnt) {  // expand (mcts.cpp:65-78): policy = random.choice(untried)
-            const uint32_t r = rng_below(rng, cnt);
-            // the r-th untried move in bit order: lane b (< 7) holding set bit b of the untried
-            // mask compares its rank; other lanes compare 0xFF (one compare per lane)
-            const uint32_t um = u & 0x7Fu;
-            const uint32_t b7 = lane & 7u;
-            const uint32_t rank = (lane < 7u && ((um >> b7) & 1u)) ? (uint32_t)__popc(um & ((1u << b7) - 1u)) : 0xFFu;
-            const int mi = __builtin_ctzll(__ballot(rank == r));
+            // the r-th untried move in bit order, r = random.choice's draw
+            const int mi = (int)rng_below_pick(rng, cnt, sel_table(s_order) + 8u * (u & 0x7Fu));
             u &= ~(1u << mi);
             const int col = (int)((ow >> (3 * mi)) & 7u);
             const uint64_t bit = drop_bit(b0 | b1, col);

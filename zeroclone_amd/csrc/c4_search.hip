@@ -327,23 +327,6 @@ __device__ void c4_rollouts_philox(Leaf *L, int nb, const uint8_t *s_sel, uint2 
     }
 }
 
-// s_sel[m*8 + r] = the r-th set bit of the 7-bit column mask m (Philox mode's move pick).
-__device__ __forceinline__ void load_sel(uint8_t *s_sel) {
-    for (int i = (int)threadIdx.x; i < 1024; i += blockDim.x) {
-        const uint32_t m = (uint32_t)i >> 3, r = (uint32_t)i & 7u;
-        uint32_t c = 0, pos = 7;
-        for (uint32_t b = 0; b < 7; ++b)
-            if ((m >> b) & 1u) {
-                if (c == r) {
-                    pos = b;
-                    break;
-                }
-                ++c;
-            }
-        s_sel[i] = (uint8_t)pos;
-    }
-}
-
 // ------------------------------------------------------------------ the search kernel
 // STAMP = diagnostic build: lane 0 adds s_memtime deltas per phase into p.a.phase[g][0..7] =
 // {rng generation at flush start, first walk of a flush, resumed walks, expansion + leaf
@@ -357,11 +340,8 @@ __global__ __launch_bounds__(kBlock) void c4_search_kernel(SearchParams p) {
     Fresh *const fresh = (Fresh *)(s_dyn + kTabBytes);
     Leaf *const leaves = (Leaf *)(s_dyn + kTabBytes + sizeof(Fresh) * (size_t)p.bs);
     uint16_t *const paths = (uint16_t *)(s_dyn + kTabBytes + (sizeof(Fresh) + sizeof(Leaf)) * (size_t)p.bs);
-    uint8_t *const s_sel = (uint8_t *)(s_dyn + kTabBytes +
-                                       (sizeof(Fresh) + sizeof(Leaf) + sizeof(uint16_t) * kMaxDepth) * (size_t)p.bs +
-                                       kPathSpill);  // Philox mode only
+    const uint8_t *const s_sel = sel_table(s_order);
     load_tables(s_order);
-    if (PHILOX) load_sel(s_sel);
     __syncthreads();
     // log(N) table read through the constant address space: uniform index -> scalar loads,
     // which do not sit in the vector-memory counter the walk and the RNG window wait on.
@@ -559,7 +539,7 @@ __global__ __launch_bounds__(kBlock) void c4_rollout_debug_kernel(Arena a, int f
                                                                   const zc_c4_state *states, int32_t *out_value,
                                                                   int64_t *out_words) {
     __shared__ Leaf s_leaf[1];
-    __shared__ uint32_t s_order[128];
+    __shared__ uint32_t s_order[kTabBytes / 4];  // order + select tables
     load_tables(s_order);
     __syncthreads();
     const uint32_t lane = lane_id();
@@ -591,7 +571,7 @@ __global__ __launch_bounds__(kBlock) void c4_rollout_debug_kernel(Arena a, int f
 __global__ __launch_bounds__(kBlock) void c4_rollout_seq_kernel(Arena a, int g, int n, const zc_c4_state *states,
                                                                 int32_t *out_value, int64_t *out_words) {
     __shared__ Leaf s_leaf[kBlock];
-    __shared__ uint32_t s_order[128];
+    __shared__ uint32_t s_order[kTabBytes / 4];  // order + select tables
     load_tables(s_order);
     __syncthreads();
     const uint32_t lane = lane_id();
@@ -655,7 +635,7 @@ size_t c4_search_lds_bytes(int bs) {
 }
 
 void launch_c4_search(const SearchParams &p, hipStream_t s) {
-    const size_t lds = c4_search_lds_bytes(p.bs) + (p.philox ? 1024 : 0);
+    const size_t lds = c4_search_lds_bytes(p.bs);
     const dim3 grid(p.n_games), block(kBlock);
     if (p.philox) {
         if (p.stamp)
