@@ -125,7 +125,23 @@ __device__ __forceinline__ uint32_t row_prev(uint32_t x) {
 // Work is placed for the scalar unit's sake: the boards are uniform values kept in VGPRs,
 // lane conditions are single compares whose ballots are used as v_cndmask masks, and the
 // scalar unit only handles the masks, the block's end and the loop control.
-__device__ void c4_rollouts(Leaf *L, int nb, Rng &rng, const uint32_t *s_order, Counters &cn) {
+#ifndef ZC_RSTAMP
+#define ZC_RSTAMP 0  // diagnostic build: 1..6 = accumulate one rollout region's cycles into *sub
+#endif
+// RMARK(k): region k ends here (s_memtime pinned by scheduling barriers; only when ZC_RSTAMP)
+#define RMARK(k)                                                    \
+    do {                                                            \
+        if (ZC_RSTAMP && sub) {                                     \
+            __builtin_amdgcn_sched_barrier(0);                      \
+            const uint64_t now_ = __builtin_amdgcn_s_memtime();     \
+            __builtin_amdgcn_sched_barrier(0);                      \
+            if (ZC_RSTAMP == (k)) *sub += now_ - t_;                \
+            t_ = now_;                                              \
+        }                                                           \
+    } while (0)
+__device__ void c4_rollouts(Leaf *L, int nb, Rng &rng, const uint32_t *s_order, Counters &cn,
+                            uint64_t *sub = nullptr) {
+    uint64_t t_ = ZC_RSTAMP && sub ? __builtin_amdgcn_s_memtime() : 0;
     const uint32_t lane = lane_id();
     const uint32_t lrow = lane >> 4;
     const uint32_t myply = 2u * (lane & 15u) + (lrow & 1u);  // ply of this lane in the compacted layout
@@ -135,6 +151,7 @@ __device__ void c4_rollouts(Leaf *L, int nb, Rng &rng, const uint32_t *s_order, 
     // lane 7a + b (< 49): the columns {a, b} (a == b: one column) whose fills a block may see
     const uint32_t pairbits = lane < 49u ? (1u << (lane / 7u)) | (1u << (lane % 7u)) : 0u;
     for (int j = 0; j < nb; ++j) {
+        RMARK(6);  // regions: 1 leaf setup, 2 view, 3 first segment, 4 absorbed fill, 5 win test, 6 block tail
         const uint32_t lm = uni(L[j].meta);
         const uint64_t x0 = in_vgpr(L[j].p0);
         const uint64_t x1 = in_vgpr(L[j].p1);
@@ -146,7 +163,9 @@ __device__ void c4_rollouts(Leaf *L, int nb, Rng &rng, const uint32_t *s_order, 
         int q = 0;  // plies played in this rollout
         const uint64_t hm = op & (op >> hd);
         const int room0 = 41 - (int)uni((uint32_t)__popcll(me | op));  // 41 - stones
-        if (__ballot(lane < 4u && (hm & (hm >> (2u * hd))) != 0)) {  // has_four(last mover)
+        const bool won = __ballot(lane < 4u && (hm & (hm >> (2u * hd))) != 0) != 0;
+        RMARK(1);
+        if (won) {  // has_four(last mover)
             val = -1;
         } else if (room0 >= 0) {  // not check_draw
             int room = room0;
@@ -154,10 +173,12 @@ __device__ void c4_rollouts(Leaf *L, int nb, Rng &rng, const uint32_t *s_order, 
             uint32_t ow = low0;
             uint32_t n = (ow >> 24) & 15u;
             uint32_t sh = (uint32_t)__clz(n);
+            // order words of the legal set minus the columns of `pairbits`, for the fills
+            // (read as soon as the legal set is known, well before a fill needs it)
+            uint32_t owp = s_order[(uint32_t)mask & ~pairbits];
             for (;;) {
+                RMARK(6);
                 if (rng.off >= (uint32_t)kWin) rng_advance(rng);
-                // order words of the legal set minus the columns of `pairbits`, for the fills
-                const uint32_t owp = s_order[(uint32_t)mask & ~pairbits];
                 const uint32_t wv = rng_view(rng);  // lane l: word off + l
                 uint32_t v = wv >> sh;
                 uint64_t A = __ballot(v < n);  // accepted words
@@ -166,6 +187,7 @@ __device__ void c4_rollouts(Leaf *L, int nb, Rng &rng, const uint32_t *s_order, 
                     continue;
                 }
                 cn.add(cn.blocks, 1);
+                RMARK(2);
                 const uint64_t occ = me | op;
                 const uint32_t cap_r = min((uint32_t)room, 30u);  // last ply index the board allows
                 uint32_t qk = mbcnt(A);                            // this lane's ply in the block
@@ -186,6 +208,7 @@ __device__ void c4_rollouts(Leaf *L, int nb, Rng &rng, const uint32_t *s_order, 
                 uint32_t ow2 = ow, cf = 0;
                 const uint32_t q0 = (uint32_t)__builtin_amdgcn_readlane((int)qk, (int)l0);
                 const uint32_t f0 = (uint32_t)__builtin_amdgcn_readlane((int)fills, (int)l0);
+                RMARK(3);
                 if (f0 && q0 < cap_r) {
                     lf = l0;
                     cf = (uint32_t)__builtin_amdgcn_readlane((int)col, (int)lf);
@@ -207,6 +230,7 @@ __device__ void c4_rollouts(Leaf *L, int nb, Rng &rng, const uint32_t *s_order, 
                     E0 = __ballot(mask_sel0(A, (fills ? 63u : qk) + 1u) > min(cap_r, nacc - 1u));
                     l0 = (uint32_t)__builtin_ctzll(E0);
                 }
+                RMARK(4);
                 // the block's last ply before any win
                 const uint32_t last = (uint32_t)__builtin_amdgcn_readlane((int)qk, (int)l0);
                 const uint64_t K = __ballot(mask_sel(A, 255u, qk) <= last);  // lanes of plies 0..last
@@ -243,6 +267,7 @@ __device__ void c4_rollouts(Leaf *L, int nb, Rng &rng, const uint32_t *s_order, 
                 op = odd ? b2 : a2;
                 q += (int)endply + 1;
                 room -= (int)endply + 1;
+                RMARK(5);
                 if (Ew) {  // the ply's mover completed four
                     val = (q & 1) ? 1 : -1;
                     break;
@@ -260,6 +285,7 @@ __device__ void c4_rollouts(Leaf *L, int nb, Rng &rng, const uint32_t *s_order, 
                     const uint32_t ca = fa ? cf : ce;
                     mask &= ~((1 << ca) | (1 << ce));
                     ow = (uint32_t)__builtin_amdgcn_readlane((int)owp, (int)(7u * ca + ce));
+                    owp = s_order[(uint32_t)mask & ~pairbits];
                 }
                 n = (ow >> 24) & 15u;
                 sh = (uint32_t)__clz(n);
@@ -407,7 +433,7 @@ __global__ __launch_bounds__(kBlock) void c4_search_kernel(SearchParams p) {
             c4_rollouts_philox(leaves, nb, s_sel, make_uint2((uint32_t)p.philox_seed, (uint32_t)(p.philox_seed >> 32)),
                                (uint32_t)done, tag, (uint32_t)g, cn);
         else
-            c4_rollouts(leaves, nb, rng, s_order, cn);
+            c4_rollouts(leaves, nb, rng, s_order, cn, STAMP ? &stamp.ph[7] : nullptr);
         wave_mem_order();
         stamp.mark(4);
 
