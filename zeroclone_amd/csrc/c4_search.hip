@@ -147,23 +147,37 @@ __device__ void c4_rollouts(Leaf *L, int nb, Rng &rng, const uint32_t *s_order, 
     const uint32_t myply = 2u * (lane & 15u) + (lrow & 1u);  // ply of this lane in the compacted layout
     const bool first_row = (lrow & 1u) == 0;                  // rows 0, 2: the block's first mover
     const uint32_t d1 = lrow < 2 ? 1u : 6u, d2 = lrow < 2 ? 7u : 8u;
-    const uint32_t hd = (0x08070601u >> (8u * (lane & 3u))) & 0xFFu;  // lanes 0..3: one direction each
     // lane 7a + b (< 49): the columns {a, b} (a == b: one column) whose fills a block may see
     const uint32_t pairbits = lane < 49u ? (1u << (lane / 7u)) | (1u << (lane % 7u)) : 0u;
+    // per leaf, lane-parallel (lane = leaf of a group of 64): side to move / last mover stones,
+    // has_four(last mover) and 41 - stones, read out by readlane when the leaf's turn comes
+    uint64_t me_v = 0, op_v = 0, won_m = 0;
+    uint32_t lm_v = 0, ow_v = 0;
+    int room_v = 0;
     for (int j = 0; j < nb; ++j) {
         RMARK(6);  // regions: 1 leaf setup, 2 view, 3 first segment, 4 absorbed fill, 5 win test, 6 block tail
-        const uint32_t lm = uni(L[j].meta);
-        const uint64_t x0 = in_vgpr(L[j].p0);
-        const uint64_t x1 = in_vgpr(L[j].p1);
-        const uint32_t low0 = uni(L[j].ow);
-        const bool tn = (lm >> 24) & 1u;
-        uint64_t me = tn ? x1 : x0;  // side to move
-        uint64_t op = tn ? x0 : x1;  // last mover
+        const int jl = j & 63;
+        if (jl == 0) {
+            const int jj = j + (int)lane;
+            if (jj < nb) {
+                lm_v = L[jj].meta;
+                ow_v = L[jj].ow;
+                const uint64_t x0 = L[jj].p0, x1 = L[jj].p1;
+                const bool tnv = (lm_v >> 24) & 1u;
+                me_v = tnv ? x1 : x0;
+                op_v = tnv ? x0 : x1;
+                room_v = 41 - __popcll(x0 | x1);
+            }
+            won_m = __ballot(jj < nb && has_four(op_v));
+        }
+        const uint32_t lm = (uint32_t)__builtin_amdgcn_readlane((int)lm_v, jl);
+        uint64_t me = in_vgpr(readlane64(me_v, jl));  // side to move
+        uint64_t op = in_vgpr(readlane64(op_v, jl));  // last mover
+        const uint32_t low0 = (uint32_t)__builtin_amdgcn_readlane((int)ow_v, jl);
+        const int room0 = __builtin_amdgcn_readlane(room_v, jl);
+        const bool won = (won_m >> jl) & 1u;
         int val = 0;
         int q = 0;  // plies played in this rollout
-        const uint64_t hm = op & (op >> hd);
-        const int room0 = 41 - (int)uni((uint32_t)__popcll(me | op));  // 41 - stones
-        const bool won = __ballot(lane < 4u && (hm & (hm >> (2u * hd))) != 0) != 0;
         RMARK(1);
         if (won) {  // has_four(last mover)
             val = -1;
