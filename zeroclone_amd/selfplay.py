@@ -121,6 +121,96 @@ class C4SelfPlay:
         self.eng.close()
 
 
+class ChessSelfPlay:
+    """Device-resident chess self-play: the chess form of `C4SelfPlay`.  G games live on one
+    GPU as zc_chess_state rows; one `step()` searches every game (Value('crude_chess_score')
+    in the search kernel, or a value network between the stepwise select and backup
+    kernels), plays the chosen moves (zc_chess_play_async) and tests the new positions
+    (zc_chess_terminal_async: check_win, stalemate, fifty-move rule) on the device, and
+    restarts finished games from the initial position.  The repetition half of check_draw
+    (chess_backend.cpp:416-441: both sides' move histories end in >= 3 repeats of a block of
+    >= 2 moves) needs the move histories, which the device rows do not carry: the host keeps
+    them (most recent move first, as the reference's deques) and applies that test after
+    every step.  Results follow Engine._evaluate (engine.py:148-153): check_win -> turn*2-1
+    of the position after the move, a draw -> 0.  Game slot g of rank r is global game r*G+g
+    with its own CPython MT19937 stream seeded seed + global id, as in C4SelfPlay."""
+
+    def __init__(self, games: int, sims: int, c: float = 1.4, batch_size: int = 32, seed: int = 0,
+                 rank: int = 0, device: int = 0, policy: int = _native.ZC_POLICY_IMMEDIATE_VALUE,
+                 freedom: float = 3.0, net=None, init_fen: str | None = None):
+        self.G, self.sims, self.c, self.bs = games, sims, c, batch_size
+        self.policy, self.freedom = int(policy), float(freedom)
+        self.dev = torch.device("cuda", device)
+        self.eng = _native.NativeEngine(max_games=games, max_sims=sims, max_batch=batch_size, device=device)
+        self.eng.chess_reserve()
+        self.first_id = rank * games
+        self.eng.seed(0, [seed + self.first_id + g for g in range(games)])
+        init = _native.chess_from_fen(init_fen) if init_fen else _native.chess_init()
+        self.init_row = torch.from_numpy(np.frombuffer(init.tobytes(), np.uint8).reshape(1, 72).copy()).to(self.dev)
+        self.init_turn = int(np.asarray(init["turn"]).reshape(-1)[0])
+        self.roots = self.init_row.repeat(games, 1).contiguous()
+        self.moves = torch.zeros(games, dtype=torch.int16, device=self.dev)
+        self.na = torch.zeros((games, _native.CHESS_MAX_MOVES), dtype=torch.int32, device=self.dev)
+        self.stats = torch.zeros((games, _native.STATS_FIELDS), dtype=torch.int64, device=self.dev)
+        self.flags = torch.zeros(games, dtype=torch.int32, device=self.dev)
+        self.vs = self.value_fn = None
+        if net is not None:
+            from .valued import ChessValuedSearch, NetValue
+            self.vs = ChessValuedSearch(self.eng, games, batch_size, leaves=False, policy=self.policy,
+                                        freedom=self.freedom)
+            self.value_fn = NetValue(net)
+        self._turn = [self.init_turn] * games
+        self._hist = [([], []) for _ in range(games)]   # (white, black), most recent first
+        self._moves = [[] for _ in range(games)]
+        self.finished = []   # (global game id, move list, result)
+
+    def step(self) -> np.ndarray:
+        """One move for every game; returns the per-game results (ONGOING = 2).  Finished
+        games restart from the initial position."""
+        from .engine.games.chess.chess_backend import has_repeated_prefix
+        s = torch.cuda.current_stream(self.dev).cuda_stream
+        if self.vs is None:
+            self.eng.chess_search_async(0, self.G, self.roots.data_ptr(), self.sims, self.c, self.bs, self.policy,
+                                        self.freedom, self.moves.data_ptr(), self.na.data_ptr(),
+                                        self.stats.data_ptr(), s)
+        else:
+            mv, _, st = self.vs.run(self.roots, self.sims, self.c, self.value_fn)
+            self.moves.copy_(mv)
+            self.stats.copy_(st)
+        self.eng.chess_play_async(self.G, self.roots.data_ptr(), self.moves.data_ptr(), self.roots.data_ptr(), s)
+        self.eng.chess_terminal_async(self.G, self.roots.data_ptr(), self.flags.data_ptr(), s)
+        mv = self.moves.cpu().numpy().view(np.uint16)
+        fl = self.flags.cpu().numpy()
+        if (self.stats[:, 5] == _native.ZC_STATUS_CAPACITY).any():
+            raise RuntimeError("chess search exceeded the tree's child-slot pool or depth limit")
+        res = np.full(self.G, ONGOING, np.int32)
+        done = []
+        draw_flags = _native.ZC_CHESS_STALEMATE | _native.ZC_CHESS_FIFTY
+        for g in range(self.G):
+            if mv[g] == 0xFFFF:
+                raise RuntimeError(f"game slot {g}: no legal move at a non-terminal root")
+            move = _native.unpack_chess_move(int(mv[g]))
+            self._hist[g][self._turn[g]].insert(0, move)   # play_move: the mover's deque, front
+            self._moves[g].append(move)
+            self._turn[g] ^= 1
+            if fl[g] & _native.ZC_CHESS_WIN:
+                res[g] = self._turn[g] * 2 - 1
+            elif fl[g] & draw_flags or (has_repeated_prefix(self._hist[g][0]) and has_repeated_prefix(self._hist[g][1])):
+                res[g] = 0
+            if res[g] != ONGOING:
+                self.finished.append((self.first_id + g, self._moves[g], int(res[g])))
+                self._moves[g] = []
+                self._hist[g] = ([], [])
+                self._turn[g] = self.init_turn
+                done.append(g)
+        if done:
+            self.roots[torch.tensor(done, dtype=torch.int64, device=self.dev)] = self.init_row
+        return res
+
+    def close(self):
+        self.eng.close()
+
+
 def gather_positions(local: torch.Tensor, group=None) -> torch.Tensor:
     """All-gather variable-length [n_r, 3] int64 position rows from every rank (rank order):
     an all_gather of the counts, then of payloads padded to the largest count."""
