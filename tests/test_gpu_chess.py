@@ -147,3 +147,62 @@ def test_backend_module_is_a_drop_in(golden):
     assert draws == exp and any(draws)
     t = cb.state_to_tensor(cb.create_init_state())
     assert t.shape == (17, 8, 8) and t[12].sum() == 64 and t[0, 6].sum() == 8
+
+
+def _random_positions(n_games=60, plies=90, seed=11):
+    """Positions along random games (oracle rules) from the reference tests' FENs, plus
+    boards no game reaches: random piece soup, missing or doubled kings, unknown characters."""
+    import oracle
+    rng = np.random.default_rng(seed)
+    fens = ["rnbqkbnr/pppppppp/8/8/8/8/PPPPPPPP/RNBQKBNR w KQkq - 0 1",
+            "r3k2r/p1ppqpb1/bn2pnp1/3PN3/1p2P3/2N2Q1p/PPPBBPPP/R3K2R w KQkq - 0 1",
+            "8/2p5/3p4/KP5r/1R3p1k/8/4P1P1/8 w - - 0 1",
+            "r3k2r/Pppp1ppp/1b3nbN/nP6/BBP1P3/q4N2/Pp1P2PP/R2Q1RK1 w kq - 0 1",
+            "rnbq1k1r/pp1Pbppp/2p5/8/2B5/8/PPP1NnPP/RNBQK2R w KQ - 1 8"]
+    out = []
+    for g in range(n_games):
+        s = oracle.chess_from_fen(fens[g % len(fens)])
+        for _ in range(plies):
+            out.append((bytes(s.board), s.turn, s.fifty, s.castle))
+            ms = oracle.chess_moves(s)
+            if not ms:
+                break
+            s = oracle.chess_play(s, ms[rng.integers(len(ms))])
+    alphabet = np.frombuffer(b"PNBRQKpnbrqk", np.uint8)
+    for i in range(400):
+        b = np.full(64, ord(" "), np.uint8)
+        k = rng.integers(2, 24)
+        sq = rng.choice(64, k, replace=False)
+        b[sq] = rng.choice(alphabet, k)
+        if i % 4 == 0:   # exactly one king each, as in play
+            b[(b == ord("K")) | (b == ord("k"))] = ord(" ")
+            ks = rng.choice(64, 2, replace=False)
+            b[ks[0]], b[ks[1]] = ord("K"), ord("k")
+        if i % 5 == 1:
+            b[rng.integers(64)] = rng.choice(np.frombuffer(b"X.z\x00#", np.uint8))
+        out.append((b.tobytes(), int(rng.integers(2)), int(rng.integers(60)), int(rng.integers(16))))
+    return out
+
+
+def test_random_positions_match_oracle(eng):
+    """Move lists and terminal flags on ~5,000 game positions and 400 irregular boards
+    (the bitboard view and the byte view of chess_device.h both exercised) vs the oracle."""
+    import oracle
+    from zeroclone_amd._native import CHESS_STATE_DTYPE, ZC_CHESS_FIFTY, ZC_CHESS_STALEMATE, ZC_CHESS_WIN
+    pos = _random_positions()
+    a = np.zeros(len(pos), CHESS_STATE_DTYPE)
+    for i, (b, t, f, c) in enumerate(pos):
+        a[i]["board"] = np.frombuffer(b, np.uint8)
+        a[i]["turn"], a[i]["fifty"], a[i]["castle"] = t, f, c
+    st = dev(a)
+    moves, counts = legal(eng, st)
+    flags = torch.zeros(len(pos), dtype=torch.int32, device="cuda")
+    eng.chess_terminal_async(len(pos), st.data_ptr(), flags.data_ptr())
+    f = flags.cpu().numpy()
+    for i, (b, t, fifty, c) in enumerate(pos):
+        s = oracle.chess_state(b.decode("latin-1"), t, fifty, c)
+        want = [list(m) for m in oracle.chess_moves(s)]
+        assert counts[i] == len(want), (i, b)
+        assert [decode(m) for m in moves[i, :counts[i]]] == want, (i, b)
+        assert bool(f[i] & ZC_CHESS_WIN) == oracle.chess_win(s), (i, b)
+        assert bool(f[i] & (ZC_CHESS_STALEMATE | ZC_CHESS_FIFTY)) == oracle.chess_draw(s), (i, b)

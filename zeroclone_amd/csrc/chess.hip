@@ -68,9 +68,7 @@ __global__ __launch_bounds__(64) void chess_terminal_kernel(int n, const zc_ches
     load_board(S.board, st);
     const int t = __builtin_amdgcn_readfirstlane(st.turn);
     const int k = legal_moves(S.board, t, S.legal, S.pseudo, S.region);
-    const uint64_t km = __ballot(S.board[lane()] == (t == 0 ? 'K' : 'k'));
-    const int ks = km ? __builtin_ctzll(km) : -1;
-    const bool check = attacked_after(S.board, t, ks >= 0 ? ks >> 3 : -1, ks >= 0 ? ks & 7 : -1, -1, -1, 0);
+    const bool check = in_check(S.board, t);
     if (lane() == 0) {
         int f = 0;
         if (k == 0 && check) f |= ZC_CHESS_WIN;

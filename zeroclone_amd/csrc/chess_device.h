@@ -61,26 +61,140 @@ __device__ __forceinline__ uint32_t pack_move(int from, int to, uint32_t v) {
     return (uint32_t)from | ((uint32_t)to << 6) | (v << 12);
 }
 
+// Two views of the board answer the generator's and the legality test's questions:
+//   ByteView: the reference's bytes in LDS, any character (unknown pieces, missing kings);
+//   BitView:  uniform 64-bit masks built by ballots, used when every square holds one of
+//             " PNBRQKpnbrqk" (or 0) and the mover has a king — every reachable position.
+// Probes then become bit tests in registers instead of dependent LDS reads, and the check
+// test is a handful of shifts and bit scans per ray instead of a walk square by square.
+// probe(s): -2 empty; -1 not capturable (own piece, enemy king, unknown white/black char);
+// otherwise the capture value fabs(piece_val) of the enemy piece on s.
+struct ByteView {
+    const uint8_t *b;
+    int t;
+    __device__ __forceinline__ int probe(int s) const {
+        const uint32_t x = b[s];
+        if (empty_sq(x)) return -2;
+        return (enemy(x, t) && upper(x) != 'K') ? (int)piece_value(x) : -1;
+    }
+    __device__ __forceinline__ uint32_t piece_at(int s) const { return b[s]; }
+    __device__ __forceinline__ bool attacked(int k, int from, int to, uint32_t pc) const;
+};
+
+constexpr uint64_t kFileA = 0x0101010101010101ull;
+constexpr uint64_t kNotA = ~kFileA, kNotH = ~(kFileA << 7);
+constexpr uint64_t kNotAB = ~(kFileA | (kFileA << 1)), kNotGH = ~((kFileA << 6) | (kFileA << 7));
+constexpr uint64_t kDiag = 0x8040201008040201ull;  // squares (i, i)
+constexpr uint64_t kAnti = 0x0102040810204080ull;  // squares (i, 7 - i)
+
+struct BitView {
+    uint64_t occ;              // non-empty squares
+    uint64_t cap;              // capturable: the enemy's pieces other than kings
+    uint64_t tP, tNB, tR;      // piece types (either colour), for capture values
+    uint64_t eP, eN, eBQ, eRQ, eK;  // the enemy's attackers of the mover's king
+    uint64_t kings;            // the mover's kings
+    int t;
+    __device__ __forceinline__ int probe(int s) const {
+        if (!((occ >> s) & 1ull)) return -2;
+        if (!((cap >> s) & 1ull)) return -1;
+        return ((tP >> s) & 1ull) ? 1 : ((tNB >> s) & 1ull) ? 3 : ((tR >> s) & 1ull) ? 5 : 9;
+    }
+    __device__ __forceinline__ uint32_t piece_at(int s) const {  // only "is it the mover's king" is asked
+        return ((kings >> s) & 1ull) ? (t == 0 ? 'K' : 'k') : 0u;
+    }
+    // king_attacked (:85-144) for the mover's king on square k (0..63) after the piece on
+    // `from` moved to `to` (-1, -1: the position as it stands): the moved piece is the
+    // mover's, so it only blocks; the enemy piece it captured, if any, no longer attacks.
+    __device__ __forceinline__ bool attacked(int k, int from, int to, uint32_t) const {
+        const uint64_t fb = from >= 0 ? (1ull << from) : 0ull, tb = to >= 0 ? (1ull << to) : 0ull;
+        const uint64_t keep = ~tb;
+        const uint64_t o = (occ & ~fb) | tb;
+        const uint64_t kb = 1ull << k;
+        const uint64_t pawns = t == 0 ? (((kb >> 9) & kNotH) | ((kb >> 7) & kNotA))
+                                      : (((kb << 7) & kNotH) | ((kb << 9) & kNotA));
+        const uint64_t knights = ((kb << 17) & kNotA) | ((kb << 15) & kNotH) | ((kb << 10) & kNotAB) |
+                                 ((kb << 6) & kNotGH) | ((kb >> 17) & kNotH) | ((kb >> 15) & kNotA) |
+                                 ((kb >> 10) & kNotGH) | ((kb >> 6) & kNotAB);
+        const uint64_t king = ((kb << 1) & kNotA) | ((kb >> 1) & kNotH) | (kb << 8) | (kb >> 8) |
+                              ((kb << 9) & kNotA) | ((kb << 7) & kNotH) | ((kb >> 7) & kNotA) | ((kb >> 9) & kNotH);
+        if (((pawns & eP) | (knights & eN) | (king & eK)) & keep) return true;
+        // sliders: the nearest occupied square of each ray must not be an enemy slider of
+        // the ray's kind (rook lines: rook or queen; diagonals: bishop or queen)
+        const int r = k >> 3, c = k & 7;
+        const uint64_t low = kb - 1ull, high = ~low & ~kb;
+        const uint64_t file = kFileA << c, rank = 0xFFull << (8 * r);
+        const int dd = r - c, da = r + c - 7;
+        const uint64_t diag = dd >= 0 ? kDiag << (8 * dd) : kDiag >> (-8 * dd);
+        const uint64_t anti = da >= 0 ? kAnti << (8 * da) : kAnti >> (-8 * da);
+        const uint64_t ao = eRQ & keep, ad = eBQ & keep;
+        auto lowest = [&](uint64_t ray, uint64_t a) {  // rays towards higher indices
+            const uint64_t bl = ray & o;
+            return (bl & (0ull - bl) & a) != 0ull;
+        };
+        auto highest = [&](uint64_t ray, uint64_t a) {  // rays towards lower indices
+            const uint64_t bl = ray & o;
+            return bl != 0ull && ((a >> (63 - __builtin_clzll(bl))) & 1ull);
+        };
+        return lowest(file & high, ao) || lowest(rank & high, ao) || highest(file & low, ao) ||
+               highest(rank & low, ao) || lowest(diag & high, ad) || lowest(anti & high, ad) ||
+               highest(diag & low, ad) || highest(anti & low, ad);
+    }
+};
+
+__device__ __forceinline__ bool known_piece(uint32_t x) {
+    switch (x) {
+        case 0: case ' ':
+        case 'P': case 'N': case 'B': case 'R': case 'Q': case 'K':
+        case 'p': case 'n': case 'b': case 'r': case 'q': case 'k': return true;
+        default: return false;
+    }
+}
+
+// The BitView of the board for side t to move, built from x = this lane's square.  Returns
+// false (view unusable) when some square holds another character or the mover has no king.
+__device__ __forceinline__ bool make_bitview(uint32_t x, int t, BitView &v) {
+    if (__ballot(!known_piece(x)) != 0ull) return false;
+    const uint32_t up = upper(x);
+    const bool filled = !empty_sq(x);
+    const uint64_t white = __ballot(filled && is_white(x)), black = __ballot(filled && !is_white(x));
+    const uint64_t en = t == 0 ? black : white, own = t == 0 ? white : black;
+    const uint64_t P = __ballot(up == 'P'), N = __ballot(up == 'N'), B = __ballot(up == 'B');
+    const uint64_t R = __ballot(up == 'R'), Q = __ballot(up == 'Q'), K = __ballot(up == 'K');
+    v.occ = white | black;
+    v.cap = en & ~K;
+    v.tP = P;
+    v.tNB = N | B;
+    v.tR = R;
+    v.eP = en & P;
+    v.eN = en & N;
+    v.eBQ = en & (B | Q);
+    v.eRQ = en & (R | Q);
+    v.eK = en & K;
+    v.kings = own & K;
+    v.t = t;
+    return v.kings != 0ull;
+}
+
 // Pseudo-legal moves of the piece `pc` on square s (row r, col c); F(from, to, value) is
 // called for each in the reference's order.  Returns nothing; the caller counts or stores.
-template <class F>
-__device__ __forceinline__ void piece_moves(const uint8_t *b, int t, int s, uint32_t pc, F &&emit) {
+template <class V, class F>
+__device__ __forceinline__ void piece_moves(const V &b, int s, uint32_t pc, F &&emit) {
     const int r = s >> 3, c = s & 7;
     const uint32_t up = upper(pc);
     if (up == 'P') {
         const int dir = pc == 'P' ? -1 : 1;
         const int nr = r + dir;
-        if (inb(nr, c) && empty_sq(b[nr * 8 + c])) {
+        if (inb(nr, c) && b.probe(nr * 8 + c) == -2) {
             emit(s, nr * 8 + c, 0u);
-            if (r == (pc == 'P' ? 6 : 1) && inb(nr + dir, c) && empty_sq(b[(nr + dir) * 8 + c]))
+            if (r == (pc == 'P' ? 6 : 1) && inb(nr + dir, c) && b.probe((nr + dir) * 8 + c) == -2)
                 emit(s, (nr + dir) * 8 + c, 0u);
         }
 #pragma unroll
         for (int k = 0; k < 2; ++k) {
             const int cc = c + (k ? 1 : -1);
             if (inb(nr, cc)) {
-                const uint32_t x = b[nr * 8 + cc];
-                if (enemy(x, t) && upper(x) != 'K') emit(s, nr * 8 + cc, piece_value(x));
+                const int x = b.probe(nr * 8 + cc);
+                if (x >= 0) emit(s, nr * 8 + cc, (uint32_t)x);
             }
         }
     } else if (up == 'N' || up == 'K') {
@@ -89,9 +203,9 @@ __device__ __forceinline__ void piece_moves(const uint8_t *b, int t, int s, uint
         for (int i = 0; i < 8; ++i) {
             const int rr = r + (kn ? kKnight[i].dr : kAll8[i].dr), cc = c + (kn ? kKnight[i].dc : kAll8[i].dc);
             if (!inb(rr, cc)) continue;
-            const uint32_t x = b[rr * 8 + cc];
-            if (empty_sq(x)) emit(s, rr * 8 + cc, 0u);
-            else if (enemy(x, t) && upper(x) != 'K') emit(s, rr * 8 + cc, piece_value(x));
+            const int x = b.probe(rr * 8 + cc);
+            if (x == -2) emit(s, rr * 8 + cc, 0u);
+            else if (x >= 0) emit(s, rr * 8 + cc, (uint32_t)x);
         }
     } else if (up == 'B' || up == 'R' || up == 'Q') {
         const int d0 = up == 'R' ? 4 : 0, d1 = up == 'B' ? 4 : 8;
@@ -101,11 +215,11 @@ __device__ __forceinline__ void piece_moves(const uint8_t *b, int t, int s, uint
             const int dr = kAll8[i].dr, dc = kAll8[i].dc;
             int rr = r + dr, cc = c + dc;
             while (inb(rr, cc)) {
-                const uint32_t x = b[rr * 8 + cc];
-                if (empty_sq(x)) {
+                const int x = b.probe(rr * 8 + cc);
+                if (x == -2) {
                     emit(s, rr * 8 + cc, 0u);
                 } else {
-                    if (enemy(x, t) && upper(x) != 'K') emit(s, rr * 8 + cc, piece_value(x));
+                    if (x >= 0) emit(s, rr * 8 + cc, (uint32_t)x);
                     break;
                 }
                 rr += dr;
@@ -159,6 +273,10 @@ __device__ __forceinline__ bool attacked_after(const uint8_t *b, int t, int kr, 
     return false;
 }
 
+__device__ __forceinline__ bool ByteView::attacked(int k, int from, int to, uint32_t pc) const {
+    return attacked_after(b, t, k >= 0 ? (k >> 3) : -1, k >= 0 ? (k & 7) : -1, from, to, pc);
+}
+
 // Exclusive prefix sum over the wave (DPP row scan + row broadcasts).
 __device__ __forceinline__ uint32_t wave_excl_sum(uint32_t x, uint32_t &total) {
     uint32_t v = x;
@@ -177,32 +295,22 @@ __device__ __forceinline__ uint64_t king_mask(const uint8_t *b, int side) {
     return __ballot(b[lane()] == (side == 0 ? 'K' : 'k'));
 }
 
-// get_legal_moves for the board in LDS `b` (64 bytes) with side to move t.  Writes the
-// packed legal moves to out[0..n) (LDS or global); LDS scratch: pseudo-legal list `ps`
-// (kMaxPseudo) and per-lane generation regions `reg` (64 x kRegion).
-// Returns n (wave-uniform), or -1 when the position has more than kMaxPseudo pseudo-legal
-// or kMaxLegal legal moves (never in reachable chess).
-__device__ __forceinline__ int legal_moves(const uint8_t *b, int t, uint16_t *out, uint16_t *ps, uint16_t *reg) {
+template <class V>
+__device__ __forceinline__ int legal_moves_view(const V &v, int t, uint32_t pc, uint64_t kings, uint16_t *out,
+                                                uint16_t *ps, uint16_t *reg) {
     const uint32_t s = lane();
-    const uint32_t pc = b[s];
-    // insufficient material (:188-198): no P/R/Q of either colour and at most one minor
-    const uint32_t up = upper(pc);
-    const uint64_t heavy = __ballot(up == 'P' || up == 'R' || up == 'Q');
-    const int minor = __popcll(__ballot(up == 'B' || up == 'N'));
-    if (!heavy && minor <= 1) return 0;
     const bool mine = !empty_sq(pc) && ((t == 0) == is_white(pc));
     // one generation pass into this lane's own region (a piece has at most 27 pseudo-legal
     // moves), then each lane copies its run to its place in board-scan order
     uint16_t *const own = reg + s * kRegion;
     uint32_t cnt = 0;
-    if (mine) piece_moves(b, t, (int)s, pc, [&](int f, int to, uint32_t v) { own[cnt++] = (uint16_t)pack_move(f, to, v); });
+    if (mine) piece_moves(v, (int)s, pc, [&](int f, int to, uint32_t val) { own[cnt++] = (uint16_t)pack_move(f, to, val); });
     uint32_t total;
     const uint32_t off = wave_excl_sum(cnt, total);
     if (total > (uint32_t)kMaxPseudo) return -1;
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     for (uint32_t k = 0; k < cnt; ++k) ps[off + k] = own[k];
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    const uint64_t kings = king_mask(b, t);
     const uint32_t kch = t == 0 ? 'K' : 'k';
     int n = 0;
     for (uint32_t base = 0; base < total; base += 64) {
@@ -212,12 +320,11 @@ __device__ __forceinline__ int legal_moves(const uint8_t *b, int t, uint16_t *ou
         if (i < total) {
             m = ps[i];
             const int from = (int)(m & 63u), to = (int)((m >> 6) & 63u);
-            const uint32_t mp = b[from];
+            const uint32_t mp = v.piece_at(from);
             // find_king on the board after the move: first square holding the mover's king
             const uint64_t km = (kings & ~(1ull << from)) | (mp == kch ? (1ull << to) : 0ull);
             const int k = km ? __builtin_ctzll(km) : -1;
-            const int kr = k >= 0 ? (k >> 3) : -1, kc = k >= 0 ? (k & 7) : -1;
-            legal = !attacked_after(b, t, kr, kc, from, to, mp);
+            legal = !v.attacked(k, from, to, mp);
         }
         const uint64_t L = __ballot(legal);
         const int rank = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(L >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)L, 0u));
@@ -226,6 +333,34 @@ __device__ __forceinline__ int legal_moves(const uint8_t *b, int t, uint16_t *ou
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     return n > kMaxLegal ? -1 : n;
+}
+
+// get_legal_moves for the board in LDS `b` (64 bytes) with side to move t.  Writes the
+// packed legal moves to out[0..n) (LDS or global); LDS scratch: pseudo-legal list `ps`
+// (kMaxPseudo) and per-lane generation regions `reg` (64 x kRegion).
+// Returns n (wave-uniform), or -1 when the position has more than kMaxPseudo pseudo-legal
+// or kMaxLegal legal moves (never in reachable chess).
+__device__ __forceinline__ int legal_moves(const uint8_t *b, int t, uint16_t *out, uint16_t *ps, uint16_t *reg) {
+    const uint32_t pc = b[lane()];
+    // insufficient material (:188-198): no P/R/Q of either colour and at most one minor
+    const uint32_t up = upper(pc);
+    const uint64_t heavy = __ballot(up == 'P' || up == 'R' || up == 'Q');
+    const int minor = __popcll(__ballot(up == 'B' || up == 'N'));
+    if (!heavy && minor <= 1) return 0;
+    BitView bv;
+    if (make_bitview(pc, t, bv)) return legal_moves_view(bv, t, pc, bv.kings, out, ps, reg);
+    return legal_moves_view(ByteView{b, t}, t, pc, king_mask(b, t), out, ps, reg);
+}
+
+// king_attacked for side t's king (the first one; absent -> the reference's (-1,-1) probes)
+// on the board b as it stands: the check test of check_win and of the crude score.
+__device__ __forceinline__ bool in_check(const uint8_t *b, int t) {
+    const uint32_t x = b[lane()];
+    BitView bv;
+    if (make_bitview(x, t, bv)) return bv.attacked(__builtin_ctzll(bv.kings), -1, -1, 0);
+    const uint64_t km = king_mask(b, t);
+    const int ks = km ? __builtin_ctzll(km) : -1;
+    return attacked_after(b, t, ks >= 0 ? ks >> 3 : -1, ks >= 0 ? ks & 7 : -1, -1, -1, 0);
 }
 
 // play_move (:364-400) without the history deques (those stay with the host State).

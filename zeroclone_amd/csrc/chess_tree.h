@@ -69,10 +69,7 @@ __device__ void create_node(const CTree &t, CLds &L, int id, int parent, int pac
         n = 0;
     }
     const int32_t mat = wave_sum(piece_material(L.s.board[lane]));
-    const uint64_t km = __ballot(L.s.board[lane] == (turn == 0 ? 'K' : 'k'));
-    const int ks = km ? __builtin_ctzll(km) : -1;
-    const bool check = chessdev::attacked_after(L.s.board, turn, ks >= 0 ? ks >> 3 : -1, ks >= 0 ? ks & 7 : -1, -1,
-                                                -1, 0);
+    const bool check = chessdev::in_check(L.s.board, turn);
     const int base = slots;
     if ((int64_t)base + n > t.S) {
         status = ZC_STATUS_CAPACITY;
