@@ -67,8 +67,8 @@ __global__ __launch_bounds__(64) void chess_terminal_kernel(int n, const zc_ches
     const zc_chess_state st = states[i];
     load_board(S.board, st);
     const int t = __builtin_amdgcn_readfirstlane(st.turn);
-    const int k = legal_moves(S.board, t, S.legal, S.pseudo, S.region);
-    const bool check = in_check(S.board, t);
+    bool check;
+    const int k = legal_moves_check(S.board, t, S.legal, S.pseudo, S.region, check);
     if (lane() == 0) {
         int f = 0;
         if (k == 0 && check) f |= ZC_CHESS_WIN;

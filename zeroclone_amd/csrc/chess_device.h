@@ -352,15 +352,36 @@ __device__ __forceinline__ int legal_moves(const uint8_t *b, int t, uint16_t *ou
     return legal_moves_view(ByteView{b, t}, t, pc, king_mask(b, t), out, ps, reg);
 }
 
-// king_attacked for side t's king (the first one; absent -> the reference's (-1,-1) probes)
-// on the board b as it stands: the check test of check_win and of the crude score.
-__device__ __forceinline__ bool in_check(const uint8_t *b, int t) {
-    const uint32_t x = b[lane()];
+// get_legal_moves and king_attacked of the side to move (check_win, crude_chess_score) on
+// one board view.
+__device__ __forceinline__ int legal_moves_check(const uint8_t *b, int t, uint16_t *out, uint16_t *ps, uint16_t *reg,
+                                                 bool &check) {
+    const uint32_t pc = b[lane()];
     BitView bv;
-    if (make_bitview(x, t, bv)) return bv.attacked(__builtin_ctzll(bv.kings), -1, -1, 0);
-    const uint64_t km = king_mask(b, t);
-    const int ks = km ? __builtin_ctzll(km) : -1;
-    return attacked_after(b, t, ks >= 0 ? ks >> 3 : -1, ks >= 0 ? ks & 7 : -1, -1, -1, 0);
+    const bool fast = make_bitview(pc, t, bv);
+    uint64_t kings;
+    if (fast) {
+        kings = bv.kings;
+        check = bv.attacked(__builtin_ctzll(kings), -1, -1, 0);
+    } else {
+        kings = king_mask(b, t);
+        const int ks = kings ? __builtin_ctzll(kings) : -1;
+        check = attacked_after(b, t, ks >= 0 ? ks >> 3 : -1, ks >= 0 ? ks & 7 : -1, -1, -1, 0);
+    }
+    const uint32_t up = upper(pc);
+    const uint64_t heavy = __ballot(up == 'P' || up == 'R' || up == 'Q');
+    const int minor = __popcll(__ballot(up == 'B' || up == 'N'));
+    if (!heavy && minor <= 1) return 0;  // insufficient material (:188-198)
+    return fast ? legal_moves_view(bv, t, pc, kings, out, ps, reg)
+                : legal_moves_view(ByteView{b, t}, t, pc, kings, out, ps, reg);
+}
+
+// Sum of piece values, white positive (crude_chess_score's material), by ballots.
+__device__ __forceinline__ int material(uint32_t x) {
+    auto n = [&](uint32_t w, uint32_t bl) {
+        return __popcll(__ballot(x == w)) - __popcll(__ballot(x == bl));
+    };
+    return n('P', 'p') + 3 * (n('N', 'n') + n('B', 'b')) + 5 * n('R', 'r') + 9 * n('Q', 'q');
 }
 
 // play_move (:364-400) without the history deques (those stay with the host State).

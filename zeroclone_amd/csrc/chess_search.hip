@@ -59,16 +59,19 @@ __device__ int simulate(const ChessParams &p, const CTree &t, CLds &L, ConstDoub
         int first_unv = 0x7FFFFFFF;
         double bv = -INFINITY;
         int bi = 0x7FFFFFFF;
+        int chv = 0xFFFF, nav = 0;  // this lane's slot of the last pass (nm <= 64: the only one)
         for (int b = 0; b < nm; b += 64) {
             const int j = b + (int)lane;
             bool valid = false;
             int32_t na = 0;
             double w = 0.0;
             if (j < nm) {
-                valid = t.ch[base + j] != 0xFFFF;
+                chv = t.ch[base + j];
+                valid = chv != 0xFFFF;
                 na = t.na[base + j];
                 w = t.w[base + j];
             }
+            nav = na;
             const uint64_t unv = __ballot(valid && na == 0);
             if (unv && first_unv == 0x7FFFFFFF) first_unv = b + __builtin_ctzll(unv);
             if (valid && na > 0) {
@@ -88,8 +91,14 @@ __device__ int simulate(const ChessParams &p, const CTree &t, CLds &L, ConstDoub
             if (bi == 0x7FFFFFFF) break;  // no child at all (cannot happen with nu == 0, nm > 0)
             best = uni(bi);
         }
-        const int nxt = uni((int)t.ch[base + best]);
-        nN = uni(t.na[base + best]);
+        int nxt;
+        if (nm <= 64) {  // the chosen slot is still in a lane's registers
+            nxt = __builtin_amdgcn_readlane(chv, best);
+            nN = __builtin_amdgcn_readlane(nav, best);
+        } else {
+            nxt = uni((int)t.ch[base + best]);
+            nN = uni(t.na[base + best]);
+        }
         ++depth;
         if (lane == (uint32_t)depth) pathv = base + (uint32_t)best;
         node = nxt;
@@ -104,45 +113,71 @@ __device__ int simulate(const ChessParams &p, const CTree &t, CLds &L, ConstDoub
     rs.valid = true;
     if (nu == 0 || status) return node;
 
-    // expand (mcts.cpp:65-78): the policy picks among the untried moves, in untried order
+    // expand (mcts.cpp:65-78): the policy picks among the untried moves, in untried order.
+    // The node's position is fetched now, under the policy's memory traffic.
+    const uint32_t stw = lane < 18 ? ((const uint32_t *)&N->st)[lane] : 0u;
     const uint32_t base = uni(N->base);
-    int local;
-    if (p.policy == 1) {
-        // Policy('immediate_value') (policy_functions.py:14-17): random.choice over the
-        // untried moves whose capture value >= max - policy_freedom
-        int best = -1;
-        for (int b = 0; b < nu; b += 64) {
-            const int i = b + (int)lane;
-            int v = -1;
-            if (i < nu) v = (int)(t.mv[base + t.ut[base + i]] >> 12);
+    int local, midx;
+    uint32_t m;
+    if (nu <= 64) {
+        // untried entry and move of lane i, read once: the policy, the erase and the chosen
+        // move all come out of these registers
+        const int utv = lane < (uint32_t)nu ? (int)t.ut[base + lane] : 0;
+        const uint32_t mvv = lane < (uint32_t)nu ? (uint32_t)t.mv[base + utv] : 0u;
+        if (p.policy == 1) {
+            // Policy('immediate_value') (policy_functions.py:14-17): random.choice over the
+            // untried moves whose capture value >= max - policy_freedom
+            int v = lane < (uint32_t)nu ? (int)(mvv >> 12) : -1;
             for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o));
-            best = max(best, v);
+            const double thr = (double)v - p.freedom;
+            const uint64_t cm = __ballot(lane < (uint32_t)nu && (double)(mvv >> 12) >= thr);
+            const uint32_t r = rng_below(rng, (uint32_t)__popcll(cm));
+            const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(cm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)cm, 0u));
+            local = __builtin_ctzll(__ballot(((cm >> lane) & 1ull) && rank == r));
+        } else {
+            local = (int)rng_below(rng, (uint32_t)nu);  // Policy('random'): random.choice(untried)
         }
-        const double thr = (double)best - p.freedom;
-        auto cand = [&](int i) { return (double)(t.mv[base + t.ut[base + i]] >> 12) >= thr; };
-        uint32_t k = 0;
-        for (int b = 0; b < nu; b += 64) {
-            const int i = b + (int)lane;
-            k += (uint32_t)__popcll(__ballot(i < nu && cand(i)));
-        }
-        const uint32_t r = rng_below(rng, k);
-        local = nth_true(nu, r, cand);
+        midx = __builtin_amdgcn_readlane(utv, local);
+        m = (uint32_t)__builtin_amdgcn_readlane((int)mvv, local);
+        // untried.erase(begin + local): entry i takes entry i + 1
+        const int nxt = __shfl(utv, (int)lane + 1);
+        if ((int)lane >= local && (int)lane < nu - 1) t.ut[base + lane] = (uint8_t)nxt;
     } else {
-        local = (int)rng_below(rng, (uint32_t)nu);  // Policy('random'): random.choice(untried)
-    }
-    const int midx = uni((int)t.ut[base + local]);
-    // untried.erase(begin + local): shift the tail down, 64 entries per pass (each pass
-    // reads entries the previous pass has not overwritten)
-    for (int b = local; b < nu - 1; b += 64) {
-        const int i = b + (int)lane;
-        uint8_t v = 0;
-        if (i < nu - 1) v = t.ut[base + i + 1];
-        wave_sync_mem();
-        if (i < nu - 1) t.ut[base + i] = v;
+        if (p.policy == 1) {
+            int best = -1;
+            for (int b = 0; b < nu; b += 64) {
+                const int i = b + (int)lane;
+                int v = -1;
+                if (i < nu) v = (int)(t.mv[base + t.ut[base + i]] >> 12);
+                for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o));
+                best = max(best, v);
+            }
+            const double thr = (double)best - p.freedom;
+            auto cand = [&](int i) { return (double)(t.mv[base + t.ut[base + i]] >> 12) >= thr; };
+            uint32_t k = 0;
+            for (int b = 0; b < nu; b += 64) {
+                const int i = b + (int)lane;
+                k += (uint32_t)__popcll(__ballot(i < nu && cand(i)));
+            }
+            const uint32_t r = rng_below(rng, k);
+            local = nth_true(nu, r, cand);
+        } else {
+            local = (int)rng_below(rng, (uint32_t)nu);
+        }
+        midx = uni((int)t.ut[base + local]);
+        // untried.erase(begin + local): shift the tail down, 64 entries per pass (each pass
+        // reads entries the previous pass has not overwritten)
+        for (int b = local; b < nu - 1; b += 64) {
+            const int i = b + (int)lane;
+            uint8_t v = 0;
+            if (i < nu - 1) v = t.ut[base + i + 1];
+            wave_sync_mem();
+            if (i < nu - 1) t.ut[base + i] = v;
+        }
+        m = uni((uint32_t)t.mv[base + midx]);
     }
     if (lane == 0) N->nu = (uint16_t)(nu - 1);
-    const uint32_t m = uni((uint32_t)t.mv[base + midx]);
-    if (lane < 18) ((uint32_t *)&L.st)[lane] = ((const uint32_t *)&N->st)[lane];
+    if (lane < 18) ((uint32_t *)&L.st)[lane] = stw;
     wave_sync_mem();
     if (lane == 0) chessdev::apply_move(L.st, m);
     wave_sync_mem();

@@ -37,39 +37,21 @@ struct CLds {
 
 __device__ __forceinline__ void wave_sync_mem() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); }
 
-__device__ __forceinline__ int32_t piece_material(uint32_t x) {
-    switch (x) {
-        case 'P': return 1;
-        case 'N': case 'B': return 3;
-        case 'R': return 5;
-        case 'Q': return 9;
-        case 'p': return -1;
-        case 'n': case 'b': return -3;
-        case 'r': return -5;
-        case 'q': return -9;
-        default: return 0;
-    }
-}
-
-__device__ __forceinline__ int32_t wave_sum(int32_t x) {
-    for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
-    return x;
-}
-
 // Node(state, get_legal_moves(state), parent, idx) (mcts.cpp:23-34) for the position in
 // L.st: moves in the reference order into fresh slots, all untried, no children.
 __device__ void create_node(const CTree &t, CLds &L, int id, int parent, int pact, int depth, int &slots, int &status) {
     const uint32_t lane = lane_id();
-    L.s.board[lane] = L.st.board[lane];
+    const uint32_t sq = L.st.board[lane];
+    L.s.board[lane] = (uint8_t)sq;
     wave_sync_mem();
     const int turn = uni((int)L.st.turn);
-    int n = chessdev::legal_moves(L.s.board, turn, L.s.legal, L.s.pseudo, L.s.region);
+    bool check;
+    int n = chessdev::legal_moves_check(L.s.board, turn, L.s.legal, L.s.pseudo, L.s.region, check);
     if (n < 0) {
         status = ZC_STATUS_CAPACITY;
         n = 0;
     }
-    const int32_t mat = wave_sum(piece_material(L.s.board[lane]));
-    const bool check = chessdev::in_check(L.s.board, turn);
+    const int32_t mat = chessdev::material(sq);
     const int base = slots;
     if ((int64_t)base + n > t.S) {
         status = ZC_STATUS_CAPACITY;
