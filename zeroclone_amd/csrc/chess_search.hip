@@ -26,10 +26,17 @@ namespace {
 // would arrive there again: it resumes there (the C4 search's flush structure,
 // c4_device.h::select_flush).  Below it every child created in this flush has Na == 0
 // (+inf), so the resumed walk takes first-unvisited slots, as the full walk would.
+// While that node still has untried moves (and at most 64), the next walk stops there again
+// and expands it: its untried list, moves and position stay in registers (`cached`), so
+// the simulation reads nothing of it from memory.
 struct Resume {
     int node = 0, depth = 0, nN = 0;
     uint32_t pathv = 0;
     bool valid = false;
+    bool cached = false;
+    int nu = 0, utv = 0;        // untried count; lane i: untried entry i
+    uint32_t base = 0, mvv = 0;  // first slot; lane i: the move of untried entry i
+    uint32_t stw = 0;            // lanes 0..17: the node's position (zc_chess_state words)
 };
 
 // select + expand + record of ONE simulation (mcts.cpp:129-147).  Returns the leaf node;
@@ -46,7 +53,7 @@ __device__ int simulate(const ChessParams &p, const CTree &t, CLds &L, ConstDoub
         nN = rs.nN;
         pathv = rs.pathv;
     }
-    for (;;) {  // select (mcts.cpp:47-63)
+    for (; !rs.cached;) {  // select (mcts.cpp:47-63)
         const ChessNode *N = &t.nodes[node];
         const uint32_t base = uni(N->base);
         const int nm = uni((int)N->nmoves), nu = uni((int)N->nu);
@@ -104,26 +111,35 @@ __device__ int simulate(const ChessParams &p, const CTree &t, CLds &L, ConstDoub
         node = nxt;
     }
     ChessNode *N = &t.nodes[node];
-    const int nu = uni((int)N->nu);
+    const bool hit = rs.cached;
+    const int nu = hit ? rs.nu : uni((int)N->nu);
     ldepth = depth;
     rs.node = node;
     rs.depth = depth;
     rs.nN = nN;
     rs.pathv = pathv;
     rs.valid = true;
+    rs.cached = false;
     if (nu == 0 || status) return node;
 
     // expand (mcts.cpp:65-78): the policy picks among the untried moves, in untried order.
     // The node's position is fetched now, under the policy's memory traffic.
-    const uint32_t stw = lane < 18 ? ((const uint32_t *)&N->st)[lane] : 0u;
-    const uint32_t base = uni(N->base);
+    const uint32_t stw = hit ? rs.stw : (lane < 18 ? ((const uint32_t *)&N->st)[lane] : 0u);
+    const uint32_t base = hit ? rs.base : uni(N->base);
     int local, midx;
     uint32_t m;
     if (nu <= 64) {
         // untried entry and move of lane i, read once: the policy, the erase and the chosen
         // move all come out of these registers
-        const int utv = lane < (uint32_t)nu ? (int)t.ut[base + lane] : 0;
-        const uint32_t mvv = lane < (uint32_t)nu ? (uint32_t)t.mv[base + utv] : 0u;
+        int utv;
+        uint32_t mvv;
+        if (hit) {
+            utv = rs.utv;
+            mvv = rs.mvv;
+        } else {
+            utv = lane < (uint32_t)nu ? (int)t.ut[base + lane] : 0;
+            mvv = lane < (uint32_t)nu ? (uint32_t)t.mv[base + utv] : 0u;
+        }
         if (p.policy == 1) {
             // Policy('immediate_value') (policy_functions.py:14-17): random.choice over the
             // untried moves whose capture value >= max - policy_freedom
@@ -141,7 +157,15 @@ __device__ int simulate(const ChessParams &p, const CTree &t, CLds &L, ConstDoub
         m = (uint32_t)__builtin_amdgcn_readlane((int)mvv, local);
         // untried.erase(begin + local): entry i takes entry i + 1
         const int nxt = __shfl(utv, (int)lane + 1);
-        if ((int)lane >= local && (int)lane < nu - 1) t.ut[base + lane] = (uint8_t)nxt;
+        const uint32_t nmv = (uint32_t)__shfl((int)mvv, (int)lane + 1);
+        const bool moved = (int)lane >= local;
+        if (moved && (int)lane < nu - 1) t.ut[base + lane] = (uint8_t)nxt;
+        rs.cached = nu > 1;  // the next walk stops here again
+        rs.nu = nu - 1;
+        rs.utv = moved ? nxt : utv;
+        rs.mvv = moved ? nmv : mvv;
+        rs.base = base;
+        rs.stw = stw;
     } else {
         if (p.policy == 1) {
             int best = -1;
