@@ -295,6 +295,12 @@ int zc_chess_puct_end(zc_engine *eng, int32_t first_game, int32_t n_games, float
  *     weight [9][128][cin] fp16 (tap = ky*3+kx, then output channel, then input channel),
  *     bias [128] f32, residual NULL or [n][h][w][128] fp16, relu 0/1.  Shapes: (h, w) in
  *     {(8, 8), (6, 7)}, cin in {32, 128}; others are ZC_EINVAL.
+ *   zc_net_conv3x3_pack_async: the same weights repacked for the streamed-weight kernel:
+ *     packed[((tap*(cin/16) + kc)*4 + mb)*512 + lane*8 + e] =
+ *     weight[tap][mb*32 + lane%32][kc*16 + 8*(lane/32) + e] (one contiguous 1-KB MFMA operand
+ *     fragment per (tap, kc, mb)); same size as weight.  Pack once per weight set.
+ *   zc_net_conv3x3_packed_async: zc_net_conv3x3_async on packed weights; bit-identical
+ *     output, faster (every wave streams its own weight fragments from L2; no LDS staging).
  *   zc_net_planes_to_nhwc_async: state_to_tensor planes [n][cin][h*w] fp16 -> [n][h*w][cpad],
  *     zero padded; cpad a multiple of 8 (16-byte rows), d_out 16-byte aligned.
  *   zc_net_value_head_async: mean over pixels -> dot(fc_w[128]) + fc_b -> tanh, as fp64
@@ -302,6 +308,10 @@ int zc_chess_puct_end(zc_engine *eng, int32_t first_game, int32_t n_games, float
  * Device pointers, enqueued on hip_stream (NULL = null stream); no engine needed. */
 int zc_net_conv3x3_async(int32_t n_boards, int32_t h, int32_t w, int32_t cin, const void *d_in, const void *d_weight,
                          const float *d_bias, const void *d_residual, void *d_out, int32_t relu, void *hip_stream);
+int zc_net_conv3x3_pack_async(int32_t cin, const void *d_weight, void *d_packed, void *hip_stream);
+int zc_net_conv3x3_packed_async(int32_t n_boards, int32_t h, int32_t w, int32_t cin, const void *d_in,
+                                const void *d_packed_weight, const float *d_bias, const void *d_residual, void *d_out,
+                                int32_t relu, void *hip_stream);
 int zc_net_planes_to_nhwc_async(int32_t n, int32_t cin, int32_t hw, int32_t cpad, const void *d_planes, void *d_out,
                                 void *hip_stream);
 int zc_net_value_head_async(int32_t n, int32_t hw, const void *d_act, const float *d_fc_w, float fc_b, double *d_values,

@@ -57,3 +57,36 @@ def test_single_conv_layer_exactness():
         ref = torch.nn.functional.conv2d(x.permute(0, 3, 1, 2).float().cpu(), wt, bias.cpu(), padding=1)
         ref = torch.relu(ref + res.permute(0, 3, 1, 2).float().cpu()).permute(0, 2, 3, 1)
         assert torch.equal(out.float().cpu(), ref), (h, w, cin)
+        # the packed, streamed-weight form on the same layer
+        wp = torch.empty_like(wk)
+        _native.check(L.zc_net_conv3x3_pack_async(cin, wk.data_ptr(), wp.data_ptr(), None))
+        out2 = torch.empty_like(out)
+        _native.check(L.zc_net_conv3x3_packed_async(n, h, w, cin, x.data_ptr(), wp.data_ptr(), bias.data_ptr(),
+                                                    res.data_ptr(), out2.data_ptr(), 1, None))
+        torch.cuda.synchronize()
+        assert torch.equal(out2.float().cpu(), ref), ("packed", h, w, cin)
+
+
+def test_packed_conv_is_bit_identical_to_the_staged_form():
+    """Random fp16 data, ragged board counts, with and without residual / ReLU: the packed
+    streamed-weight kernel accumulates in the staged kernels' order, so outputs agree bitwise."""
+    from zeroclone_amd import _native
+    L = _native.lib()
+    g = torch.Generator(device="cuda").manual_seed(7)
+    for (h, w, cin, n) in [(8, 8, 128, 1001), (6, 7, 128, 777), (8, 8, 32, 3), (6, 7, 32, 130)]:
+        x = torch.randn(n, h, w, cin, device="cuda", generator=g).half()
+        wk = (torch.randn(9, 128, cin, device="cuda", generator=g) * 0.05).half()
+        bias = torch.randn(128, device="cuda", generator=g) * 0.1
+        res = torch.randn(n, h, w, 128, device="cuda", generator=g).half()
+        wp = torch.empty_like(wk)
+        _native.check(L.zc_net_conv3x3_pack_async(cin, wk.data_ptr(), wp.data_ptr(), None))
+        for use_res, relu in ((False, 1), (True, 1), (True, 0)):
+            a = torch.empty((n, h, w, 128), dtype=torch.float16, device="cuda")
+            b = torch.empty_like(a)
+            rp = res.data_ptr() if use_res else None
+            _native.check(L.zc_net_conv3x3_async(n, h, w, cin, x.data_ptr(), wk.data_ptr(), bias.data_ptr(), rp,
+                                                 a.data_ptr(), relu, None))
+            _native.check(L.zc_net_conv3x3_packed_async(n, h, w, cin, x.data_ptr(), wp.data_ptr(), bias.data_ptr(), rp,
+                                                        b.data_ptr(), relu, None))
+            torch.cuda.synchronize()
+            assert torch.equal(a.view(torch.int16), b.view(torch.int16)), (h, w, cin, n, use_res, relu)

@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
-"""A/B of the conv3x3 implementations (ZC_CONV_IMPL = tile / half / w8; argv picks them):
+"""A/B of the conv3x3 implementations (ZC_CONV_IMPL = tile / half; stream2 / stream3 = the packed-weight
+form at 2 / 3 waves per SIMD; argv picks them):
 bit-identical outputs and per-layer time.  Runs each impl in a child process."""
 import json
 import os
@@ -22,9 +23,17 @@ for (h, w, n) in [(8, 8, 32768), (6, 7, 131072), (8, 8, 1000), (6, 7, 777)]:
         res = torch.randn(n, h, w, 128, device="cuda", generator=g).half()
         o = torch.empty(n, h, w, 128, device="cuda", dtype=torch.float16)
         fl = 2.0 * n * h * w * 128 * 9 * cin
+        packed = os.environ.get("ZC_AB_PACKED") == "1"
+        if packed:
+            wp = torch.empty_like(wt)
+            _native.check(L.zc_net_conv3x3_pack_async(cin, wt.data_ptr(), wp.data_ptr(), None))
         for use_res in (False, True):
-            f = lambda: _native.check(L.zc_net_conv3x3_async(n, h, w, cin, x.data_ptr(), wt.data_ptr(), bias.data_ptr(),
-                                                             res.data_ptr() if use_res else None, o.data_ptr(), 1, None))
+            if packed:
+                f = lambda: _native.check(L.zc_net_conv3x3_packed_async(n, h, w, cin, x.data_ptr(), wp.data_ptr(), bias.data_ptr(),
+                                                                        res.data_ptr() if use_res else None, o.data_ptr(), 1, None))
+            else:
+                f = lambda: _native.check(L.zc_net_conv3x3_async(n, h, w, cin, x.data_ptr(), wt.data_ptr(), bias.data_ptr(),
+                                                                 res.data_ptr() if use_res else None, o.data_ptr(), 1, None))
             f(); torch.cuda.synchronize()
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             a.record()
@@ -39,14 +48,17 @@ print(json.dumps(out))
 IMPLS = sys.argv[1:] or ["tile", "half"]
 res = {}
 for impl in IMPLS:
-    env = dict(os.environ, ZC_CONV_IMPL=impl)
+    if impl.startswith("stream"):  # packed weights: stream2 / stream3 = waves per SIMD
+        env = dict(os.environ, ZC_AB_PACKED="1", ZC_CONV_WPE=impl[-1])
+    else:
+        env = dict(os.environ, ZC_CONV_IMPL=impl)
     r = subprocess.run([sys.executable, "-c", CHILD, HERE], env=env, capture_output=True, text=True, timeout=600)
     if r.returncode:
         print(r.stderr[-3000:])
         sys.exit(r.returncode)
     res[impl] = json.loads(r.stdout.strip().splitlines()[-1])
 base = IMPLS[0]
-same = all(res[i][k]["hash"] == res[base][k]["hash"] for i in IMPLS for k in res[base])
+same = {i: all(res[i][k]["hash"] == res[base][k]["hash"] for k in res[base]) for i in IMPLS}
 for k in res[base]:
     print(f"{k:30s}" + " | ".join(f"{i} {res[i][k]['ms']:7.4f} ms {res[i][k]['tflops']:6.1f} TF" for i in IMPLS))
 print("bit-identical:", same)

@@ -841,6 +841,28 @@ int zc_net_conv3x3_async(int32_t n, int32_t h, int32_t w, int32_t cin, const voi
     return ZC_OK;
 }
 
+int zc_net_conv3x3_pack_async(int32_t cin, const void *d_weight, void *d_packed, void *hip_stream) {
+    if (!d_weight || !d_packed || ((uintptr_t)d_weight & 15) || ((uintptr_t)d_packed & 15))
+        return fail(ZC_EINVAL, "bad argument");
+    if (!zc::launch_net_pack_conv_weight(cin, d_weight, d_packed, (hipStream_t)hip_stream))
+        return fail(ZC_EINVAL, "conv3x3 pack: cin %d not supported", cin);
+    ZC_HIP(hipGetLastError());
+    return ZC_OK;
+}
+
+int zc_net_conv3x3_packed_async(int32_t n, int32_t h, int32_t w, int32_t cin, const void *d_in, const void *d_packed,
+                                const float *d_bias, const void *d_residual, void *d_out, int32_t relu,
+                                void *hip_stream) {
+    if (n < 0 || (n && (!d_in || !d_packed || !d_bias || !d_out)) || ((uintptr_t)d_packed & 15))
+        return fail(ZC_EINVAL, "bad argument");
+    if (!n) return ZC_OK;
+    if (!zc::launch_net_conv3x3_packed(n, h, w, cin, d_in, d_packed, d_bias, d_residual, d_out, relu ? 1 : 0,
+                                       (hipStream_t)hip_stream))
+        return fail(ZC_EINVAL, "conv3x3 shape (h %d, w %d, cin %d) not supported", h, w, cin);
+    ZC_HIP(hipGetLastError());
+    return ZC_OK;
+}
+
 int zc_net_planes_to_nhwc_async(int32_t n, int32_t cin, int32_t hw, int32_t cpad, const void *d_planes, void *d_out,
                                 void *hip_stream) {
     if (n < 0 || cin < 1 || hw < 1 || cpad < cin || (cpad & 7) || ((uintptr_t)d_out & 15) ||

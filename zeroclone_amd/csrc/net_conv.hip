@@ -399,6 +399,168 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 }
 
 
+// Streamed-weight form (zc_net_conv3x3_packed_async): wave w owns output channels
+// [32 w, +32) x all 128 pixels of the tile (4 MFMA tiles).  The weights are pre-packed so
+// that every A fragment (32 channels x 16 k of one tap) is one contiguous 1-KB piece, 16 B
+// per lane in MFMA operand order (pack_conv_weight_kernel); each wave streams its own
+// fragments from L2 straight into registers one tap ahead, so the LDS holds only the input
+// tile and the main loop has no barrier and no weight restaging.  WPE = waves per SIMD:
+// at 3 the fp32 epilogue tile goes through LDS in two 64-pixel halves, so three
+// workgroups fit a CU.  Same accumulation order as the other forms (bit-identical).
+template <int H, int W, int BPH, int CIN, int WPE>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE))) void conv3x3_stream_kernel(
+    int nboards, const _Float16 *__restrict__ in, const _Float16 *__restrict__ wp, const float *__restrict__ bias,
+    const _Float16 *__restrict__ res, _Float16 *__restrict__ out, int relu) {
+    constexpr int HW = H * W;
+    constexpr int PIX = BPH * HW;
+    static_assert(PIX <= kHalfPix, "tile too large");
+    constexpr int LD = CIN + 8;
+    constexpr int C8 = CIN / 8;
+    constexpr int KC = CIN / 16;
+    constexpr int NI = kHalfPix * C8 / 256;
+    extern __shared__ __attribute__((aligned(16))) _Float16 lds[];
+    _Float16 *const sin = lds;  // [kHalfPix + 1][LD]; the last row is zero
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int b0 = blockIdx.x * BPH;
+    const int npix = min(BPH, nboards - b0) * HW;
+    const h8 zero = {0, 0, 0, 0, 0, 0, 0, 0};
+    const int r = lane & 31, hh = lane >> 5;
+    // fragment (tap, kc) of this wave: wp + ((tap * KC + kc) * 4 + wave) * 512 + lane * 8
+    const _Float16 *const wa = wp + (size_t)wave * 512 + lane * 8;
+    h8 a[KC];
+#pragma unroll
+    for (int kc = 0; kc < KC; ++kc) a[kc] = *(const h8 *)(wa + (size_t)kc * 2048);
+    {
+        h8 v[NI];
+        const _Float16 *src = in + (size_t)b0 * HW * CIN;
+#pragma unroll
+        for (int q = 0; q < NI; ++q) {
+            const int i = tid + q * 256, row = i / C8, c8 = i - row * C8;
+            const h8 t = *(const h8 *)(src + min(row, npix - 1) * CIN + c8 * 8);
+            v[q] = row < npix ? t : zero;
+        }
+#pragma unroll
+        for (int q = 0; q < NI; ++q) {
+            const int i = tid + q * 256, row = i / C8, c8 = i - row * C8;
+            *(h8 *)(sin + row * LD + c8 * 8) = v[q];
+        }
+        if (tid < C8) *(h8 *)(sin + kHalfPix * LD + tid * 8) = zero;  // the off-board row
+    }
+    int pb[4], py[4], px[4];
+    bool pv[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        const int P = t * 32 + r;
+        pv[t] = P < npix;
+        pb[t] = P / HW;
+        const int rem = P - pb[t] * HW;
+        py[t] = rem / W;
+        px[t] = rem - py[t] * W;
+    }
+    f16x acc[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int k = 0; k < 16; ++k) acc[t][k] = 0.0f;
+    __syncthreads();  // the input tile is in LDS
+
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) {
+        h8 an[KC];
+        if (tap + 1 < 9) {
+#pragma unroll
+            for (int kc = 0; kc < KC; ++kc) an[kc] = *(const h8 *)(wa + (size_t)((tap + 1) * KC + kc) * 2048);
+        }
+        const int dy = tap / 3 - 1, dx = tap % 3 - 1;
+        const _Float16 *xb[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const int sy = py[t] + dy, sx = px[t] + dx;
+            const bool sv = pv[t] && (unsigned)sy < (unsigned)H && (unsigned)sx < (unsigned)W;
+            xb[t] = sin + (sv ? pb[t] * HW + sy * W + sx : kHalfPix) * LD + hh * 8;
+        }
+        h8 x[4], xn[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) x[t] = *(const h8 *)(xb[t]);
+#pragma unroll
+        for (int kc = 0; kc < KC; ++kc) {
+            if (kc + 1 < KC) {
+#pragma unroll
+                for (int t = 0; t < 4; ++t) xn[t] = *(const h8 *)(xb[t] + (kc + 1) * 16);
+            }
+#pragma unroll
+            for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[kc], x[t], acc[t], 0, 0, 0);
+            if (kc + 1 < KC) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // 1 MFMA
+                    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // 1 DS read
+                }
+#pragma unroll
+                for (int t = 0; t < 4; ++t) x[t] = xn[t];
+            }
+        }
+        if (tap + 1 < 9) {
+#pragma unroll
+            for (int kc = 0; kc < KC; ++kc) a[kc] = an[kc];
+        }
+    }
+
+    // epilogue through LDS (as in the half form): fp32 [pixel][cout] rows, then bias,
+    // residual, ReLU and the fp16 store on whole 256-byte output rows; NP pixels per pass
+    constexpr int SL = kCout + 4;
+    constexpr int NP = WPE >= 3 ? 64 : 128;
+    float *const sacc = (float *)lds;
+#pragma unroll
+    for (int h0 = 0; h0 < kHalfPix; h0 += NP) {
+        __syncthreads();  // the input tile / the previous pass is no longer read
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            if (t * 32 < h0 || t * 32 >= h0 + NP) continue;
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const int P = t * 32 + r - h0, co = wave * 32 + 8 * g + 4 * hh;
+                *(float4 *)(sacc + P * SL + co) =
+                    make_float4(acc[t][4 * g + 0], acc[t][4 * g + 1], acc[t][4 * g + 2], acc[t][4 * g + 3]);
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < NP * (kCout / 8) / 256; ++q) {
+            const int i = tid + q * 256, Pl = i >> 4, c0 = (i & 15) * 8, P = h0 + Pl;
+            if (P < npix) {
+                const size_t o = ((size_t)b0 * HW + P) * kCout + c0;
+                h8 rv8;
+                if (res) rv8 = *(const h8 *)(res + o);
+                const float4 a0 = *(const float4 *)(sacc + Pl * SL + c0), a1 = *(const float4 *)(sacc + Pl * SL + c0 + 4);
+                const float4 b0v = *(const float4 *)(bias + c0), b1v = *(const float4 *)(bias + c0 + 4);
+                float v[8] = {a0.x + b0v.x, a0.y + b0v.y, a0.z + b0v.z, a0.w + b0v.w,
+                              a1.x + b1v.x, a1.y + b1v.y, a1.z + b1v.z, a1.w + b1v.w};
+                h8 ov;
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                    if (res) v[e] += (float)rv8[e];
+                    if (relu) v[e] = fmaxf(v[e], 0.0f);
+                    ov[e] = (_Float16)v[e];
+                }
+                *(h8 *)(out + o) = ov;
+            }
+        }
+    }
+}
+
+// [9][kCout][cin] -> the stream form's fragments: packed[((tap * KC + kc) * 4 + mb) * 512 +
+// lane * 8 + e] = w[tap][mb * 32 + lane % 32][kc * 16 + 8 * (lane / 32) + e].
+__global__ void pack_conv_weight_kernel(int cin, const _Float16 *__restrict__ w, _Float16 *__restrict__ packed) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;  // one 8-half piece
+    const int KC = cin / 16;
+    if (i >= 9 * KC * 4 * 64) return;
+    const int lane = i & 63, mb = (i >> 6) & 3, kc = (i >> 8) % KC, tap = (i >> 8) / KC;
+    const int row = mb * 32 + (lane & 31), k0 = kc * 16 + 8 * (lane >> 5);
+    *(h8 *)(packed + (size_t)i * 8) = *(const h8 *)(w + ((size_t)tap * kCout + row) * cin + k0);
+}
+
 // planes [n][cin][H*W] (state_to_tensor layout, fp16) -> NHWC [n][H*W][cpad], zero padded.
 __global__ void planes_to_nhwc_kernel(int n, int cin, int hw, int cpad, const _Float16 *__restrict__ planes,
                                       _Float16 *__restrict__ out) {
@@ -445,6 +607,28 @@ int conv_impl() {  // ZC_CONV_IMPL=tile: 256-pixel tiles for every layer; defaul
     return v;
 }
 
+int stream_wpe() {  // ZC_CONV_WPE=2: the packed form at two workgroups per CU (default 3)
+    static const int v = [] {
+        const char *e = getenv("ZC_CONV_WPE");
+        return e && !strcmp(e, "2") ? 2 : 3;
+    }();
+    return v;
+}
+
+template <int H, int W, int BPH, int CIN>
+void launch_stream(int n, const void *in, const void *wp, const float *bias, const void *res, void *out, int relu,
+                   hipStream_t s) {
+    const size_t tile = (size_t)(kHalfPix + 1) * (CIN + 8) * sizeof(_Float16);
+    if (stream_wpe() == 2)
+        hipLaunchKernelGGL((conv3x3_stream_kernel<H, W, BPH, CIN, 2>), dim3((n + BPH - 1) / BPH), dim3(256),
+                           std::max(tile, kHalfEpiBytes), s, n, (const _Float16 *)in, (const _Float16 *)wp, bias,
+                           (const _Float16 *)res, (_Float16 *)out, relu);
+    else
+        hipLaunchKernelGGL((conv3x3_stream_kernel<H, W, BPH, CIN, 3>), dim3((n + BPH - 1) / BPH), dim3(256),
+                           std::max(tile, kHalfEpiBytes / 2), s, n, (const _Float16 *)in, (const _Float16 *)wp, bias,
+                           (const _Float16 *)res, (_Float16 *)out, relu);
+}
+
 template <int H, int W, int BPW, int BPH, int CIN>
 void launch_conv(int n, const void *in, const void *wt, const float *bias, const void *res, void *out, int relu,
                  hipStream_t s) {
@@ -470,6 +654,24 @@ bool launch_net_conv3x3(int n, int h, int w, int cin, const void *in, const void
     else if (h == 6 && w == 7 && cin == 128) launch_conv<6, 7, 6, 3, 128>(n, in, wt, bias, res, out, relu, s);
     else if (h == 6 && w == 7 && cin == 32) launch_conv<6, 7, 6, 3, 32>(n, in, wt, bias, res, out, relu, s);
     else return false;
+    return true;
+}
+
+bool launch_net_conv3x3_packed(int n, int h, int w, int cin, const void *in, const void *wp, const float *bias,
+                               const void *res, void *out, int relu, hipStream_t s) {
+    if (h == 8 && w == 8 && cin == 128) launch_stream<8, 8, 2, 128>(n, in, wp, bias, res, out, relu, s);
+    else if (h == 8 && w == 8 && cin == 32) launch_stream<8, 8, 2, 32>(n, in, wp, bias, res, out, relu, s);
+    else if (h == 6 && w == 7 && cin == 128) launch_stream<6, 7, 3, 128>(n, in, wp, bias, res, out, relu, s);
+    else if (h == 6 && w == 7 && cin == 32) launch_stream<6, 7, 3, 32>(n, in, wp, bias, res, out, relu, s);
+    else return false;
+    return true;
+}
+
+bool launch_net_pack_conv_weight(int cin, const void *w, void *packed, hipStream_t s) {
+    if (cin != 32 && cin != 128) return false;
+    const int n = 9 * (cin / 16) * 4 * 64;
+    hipLaunchKernelGGL(pack_conv_weight_kernel, dim3((n + 255) / 256), dim3(256), 0, s, cin, (const _Float16 *)w,
+                       (_Float16 *)packed);
     return true;
 }
 

@@ -187,6 +187,9 @@ void launch_chess_planes(int n, const zc_chess_state *s, void *planes, int f16, 
 
 bool launch_net_conv3x3(int n, int h, int w, int cin, const void *in, const void *wt, const float *bias,
                         const void *res, void *out, int relu, hipStream_t s);
+bool launch_net_conv3x3_packed(int n, int h, int w, int cin, const void *in, const void *wp, const float *bias,
+                               const void *res, void *out, int relu, hipStream_t s);
+bool launch_net_pack_conv_weight(int cin, const void *w, void *packed, hipStream_t s);
 void launch_net_planes_to_nhwc(int n, int cin, int hw, int cpad, const void *planes, void *out, hipStream_t s);
 void launch_net_value_head(int n, int hw, const void *act, const float *fcw, float fcb, double *values, hipStream_t s);
 

@@ -121,7 +121,8 @@ def for_inference(net: ValueNetwork, device, dtype=torch.float16, backend: str =
 
 class MfmaValueNetwork:
     """The folded ValueNetwork on this package's own MFMA kernels (csrc/net_conv.hip):
-    NHWC fp16 activations, implicit-GEMM conv3x3 on v_mfma_f32_32x32x16_f16 with the
+    NHWC fp16 activations, implicit-GEMM conv3x3 on v_mfma_f32_32x32x16_f16 (the packed,
+    streamed-weight form: zc_net_conv3x3_packed_async) with the
     bias / residual / ReLU epilogue fused, and the pooled tanh head writing fp64 values.
     Call with state_to_tensor planes [n, in_planes, H, W] fp16 (as the stepwise search
     exports them); returns fp64 values [n].  Buffers are cached per batch size, so a call
@@ -143,6 +144,15 @@ class MfmaValueNetwork:
             wp[:, : wt.shape[1]] = wt
             self.w.append(wp.permute(2, 3, 0, 1).reshape(9, 128, cin).contiguous().to(self.dev, torch.float16))
             self.b.append(conv.bias.detach().float().contiguous().to(self.dev))
+        # the streamed-weight kernel's operand order (zc_net_conv3x3_pack_async), packed once
+        from . import _native
+        self.wp = []
+        for wt in self.w:
+            wp = torch.empty_like(wt)
+            _native.check(_native.lib().zc_net_conv3x3_pack_async(wt.shape[2], wt.data_ptr(), wp.data_ptr(),
+                                                                  ctypes_stream(self.dev)))
+            self.wp.append(wp)
+        torch.cuda.current_stream(self.dev).synchronize()
         self.fcw = f.fc.weight.detach().float().reshape(-1).contiguous().to(self.dev)
         self.fcb = float(f.fc.bias.detach().float().item())
         self._bufs = {}
@@ -171,9 +181,9 @@ class MfmaValueNetwork:
         _native.check(L.zc_net_planes_to_nhwc_async(n, c, hw, self.cpad, planes.data_ptr(), x0.data_ptr(), s))
 
         def conv(i, src, dst, res):
-            _native.check(L.zc_net_conv3x3_async(n, h, w, src.shape[2], src.data_ptr(), self.w[i].data_ptr(),
-                                                 self.b[i].data_ptr(), res.data_ptr() if res is not None else None,
-                                                 dst.data_ptr(), 1, s))
+            _native.check(L.zc_net_conv3x3_packed_async(n, h, w, src.shape[2], src.data_ptr(), self.wp[i].data_ptr(),
+                                                        self.b[i].data_ptr(), res.data_ptr() if res is not None else None,
+                                                        dst.data_ptr(), 1, s))
         conv(0, x0, a, None)
         for k in range((len(self.w) - 1) // 2):
             conv(1 + 2 * k, a, t, None)
