@@ -419,7 +419,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
     constexpr int KC = CIN / 16;
     constexpr int NI = kHalfPix * C8 / 256;
     extern __shared__ __attribute__((aligned(16))) _Float16 lds[];
-    _Float16 *const sin = lds;  // [kHalfPix + 1][LD]; the last row is zero
+    // [kHalfPix + 16][LD]: the tile, then 16 zero rows.  An off-board pixel reads the zero
+    // row in the bank class of the row it would have read, so the 16 lanes of a read group
+    // stay on 16 different bank quads (one shared zero row cost a 2-way conflict at edges).
+    _Float16 *const sin = lds;
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int b0 = blockIdx.x * BPH;
@@ -445,7 +448,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
             const int i = tid + q * 256, row = i / C8, c8 = i - row * C8;
             *(h8 *)(sin + row * LD + c8 * 8) = v[q];
         }
-        if (tid < C8) *(h8 *)(sin + kHalfPix * LD + tid * 8) = zero;  // the off-board row
+        for (int z = tid; z < 16 * C8; z += 256) *(h8 *)(sin + (kHalfPix + z / C8) * LD + (z % C8) * 8) = zero;
     }
     int pb[4], py[4], px[4];
     bool pv[4];
@@ -467,43 +470,37 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
 
 #pragma unroll
     for (int tap = 0; tap < 9; ++tap) {
-        h8 an[KC];
-        if (tap + 1 < 9) {
-#pragma unroll
-            for (int kc = 0; kc < KC; ++kc) an[kc] = *(const h8 *)(wa + (size_t)((tap + 1) * KC + kc) * 2048);
-        }
         const int dy = tap / 3 - 1, dx = tap % 3 - 1;
         const _Float16 *xb[4];
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
             const int sy = py[t] + dy, sx = px[t] + dx;
             const bool sv = pv[t] && (unsigned)sy < (unsigned)H && (unsigned)sx < (unsigned)W;
-            xb[t] = sin + (sv ? pb[t] * HW + sy * W + sx : kHalfPix) * LD + hh * 8;
+            const int row = pb[t] * HW + sy * W + sx;
+            xb[t] = sin + (sv ? row : kHalfPix + (row & 15)) * LD + hh * 8;
         }
         h8 x[4], xn[4];
 #pragma unroll
         for (int t = 0; t < 4; ++t) x[t] = *(const h8 *)(xb[t]);
 #pragma unroll
         for (int kc = 0; kc < KC; ++kc) {
+            // the next k-step's four fragment reads go out before this step's MFMAs, pinned
+            // there, so they land under the MFMAs (left alone, the compiler pairs every read
+            // with its consumer and waits on it)
             if (kc + 1 < KC) {
 #pragma unroll
                 for (int t = 0; t < 4; ++t) xn[t] = *(const h8 *)(xb[t] + (kc + 1) * 16);
             }
+            __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
             for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[kc], x[t], acc[t], 0, 0, 0);
+            __builtin_amdgcn_sched_barrier(0);
+            // a ring: this fragment's register now fetches the same k-step of the next tap
+            if (tap + 1 < 9) a[kc] = *(const h8 *)(wa + (size_t)((tap + 1) * KC + kc) * 2048);
             if (kc + 1 < KC) {
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // 1 MFMA
-                    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // 1 DS read
-                }
 #pragma unroll
                 for (int t = 0; t < 4; ++t) x[t] = xn[t];
             }
-        }
-        if (tap + 1 < 9) {
-#pragma unroll
-            for (int kc = 0; kc < KC; ++kc) a[kc] = an[kc];
         }
     }
 
@@ -618,7 +615,7 @@ int stream_wpe() {  // ZC_CONV_WPE=2: the packed form at two workgroups per CU (
 template <int H, int W, int BPH, int CIN>
 void launch_stream(int n, const void *in, const void *wp, const float *bias, const void *res, void *out, int relu,
                    hipStream_t s) {
-    const size_t tile = (size_t)(kHalfPix + 1) * (CIN + 8) * sizeof(_Float16);
+    const size_t tile = (size_t)(kHalfPix + 16) * (CIN + 8) * sizeof(_Float16);
     if (stream_wpe() == 2)
         hipLaunchKernelGGL((conv3x3_stream_kernel<H, W, BPH, CIN, 2>), dim3((n + BPH - 1) / BPH), dim3(256),
                            std::max(tile, kHalfEpiBytes), s, n, (const _Float16 *)in, (const _Float16 *)wp, bias,
