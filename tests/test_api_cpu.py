@@ -73,3 +73,19 @@ def test_unsupported_plugins_fail_loudly():
         __name__ = "chess_backend"
     with pytest.raises(NotImplementedError):
         mcts.get_move(c4.create_init_state(), v, Policy("random"), Other(), 10)
+
+
+def test_schedule_hyperparams_follows_train_py():
+    """scripts/train.py:173-188 at the cycles where each cap or floor takes over."""
+    from zeroclone_amd.selfplay import schedule_hyperparams
+    s0 = schedule_hyperparams(0)
+    assert s0 == {"games": 500, "simulations": 100, "c_puct": 2.5, "lr": 3e-4}
+    s3 = schedule_hyperparams(3)
+    assert s3["games"] == 2000 and s3["simulations"] == 172 and abs(s3["c_puct"] - 2.5 * 0.97 ** 3) < 1e-15
+    s10 = schedule_hyperparams(10)
+    assert s10["simulations"] == 619 and abs(s10["lr"] - 3e-4 * 0.95 ** 10) < 1e-18
+    s30 = schedule_hyperparams(30)
+    assert s30["simulations"] == 800 and s30["c_puct"] == 1.25
+    assert schedule_hyperparams(200)["lr"] == 1e-5
+    assert schedule_hyperparams(1, games_cap=700, sims_cap=110)["games"] == 700
+    assert schedule_hyperparams(1, games_cap=700, sims_cap=110)["simulations"] == 110

@@ -96,3 +96,15 @@ def test_selfplay_matches_oracle_games_with_refill():
             checked += 1
     assert checked >= G   # every slot finished at least one game on average
     sp.close()
+
+
+def test_simulate_games_quota():
+    """train.py:simulate_games on the device pool: exactly `total` results, each a game the
+    pool recorded, in completion order."""
+    from zeroclone_amd.selfplay import simulate_games
+    sp = C4SelfPlay(16, 40, seed=3)
+    res = simulate_games(sp, 24, max_steps=200)
+    assert len(res) == 24 and set(res) <= {-1, 0, 1}
+    assert [f[2] for f in sp.finished[:24]] == res
+    assert simulate_games(sp, 0) == []
+    sp.close()

@@ -211,6 +211,38 @@ class ChessSelfPlay:
         self.eng.close()
 
 
+def simulate_games(pool, total_games: int, max_steps: int | None = None) -> list[int]:
+    """scripts/train.py:simulate_games (:151-170) on a device pool (C4SelfPlay or
+    ChessSelfPlay): step every game until `total_games` games have finished; returns their
+    results in completion order (slot order within a step), while their trajectories are in
+    `pool.finished`.  The reference starts min(total, threads) games and adds one per finished
+    game while fewer than `total_games` have started; the pool keeps every slot playing, so
+    games still running when the quota is met are surplus and not counted."""
+    if total_games < 0:
+        raise ValueError("total_games must be >= 0")
+    out: list[int] = []
+    steps = 0
+    while len(out) < total_games:
+        if max_steps is not None and steps >= max_steps:
+            raise RuntimeError(f"{len(out)} of {total_games} games finished in {max_steps} steps")
+        r = pool.step()
+        r = r.cpu().numpy() if torch.is_tensor(r) else np.asarray(r)
+        out.extend(int(v) for v in r[r != ONGOING])
+        steps += 1
+    return out[:total_games]
+
+
+def schedule_hyperparams(cycle: int, *, games_cap: int = 2000, sims_cap: int = 800, init_lr: float = 3e-4,
+                         lr_decay: float = 0.95, lr_floor: float = 1e-5) -> dict:
+    """scripts/train.py:schedule_hyperparams (:173-188): the self-play games, simulations per
+    move and exploration constant of training cycle `cycle`, and its learning rate."""
+    games = min(games_cap, 500 * (cycle + 1))
+    sims = int(min(100 * (1.2 ** cycle), sims_cap))
+    c_val = max(1.25, 2.5 * (0.97 ** cycle))
+    lr = max(init_lr * (lr_decay ** cycle), lr_floor)
+    return {"games": games, "simulations": sims, "c_puct": c_val, "lr": lr}
+
+
 def gather_positions(local: torch.Tensor, group=None) -> torch.Tensor:
     """All-gather variable-length [n_r, 3] int64 position rows from every rank (rank order):
     an all_gather of the counts, then of payloads padded to the largest count."""
