@@ -226,6 +226,13 @@ int zc_chess_play_async(zc_engine *eng, int32_t n, const zc_chess_state *d_in, c
 /* ZC_CHESS_* flags per position (check_win; check_draw without the repetition test). */
 int zc_chess_terminal_async(zc_engine *eng, int32_t n, const zc_chess_state *d_states, int32_t *d_flags,
                             void *hip_stream);
+/* has_repeated_prefix (chess_backend.cpp:148-180, pattern >= 2 moves, >= 3 repeats) of both
+ * sides' move histories: d_hist [n][2][cap] uint16 packed moves, each side's in play order
+ * (oldest first; the test reads them most recent first, as the reference's deques),
+ * d_len [n][2] moves per side (<= cap); d_out[n] = white's answer | black's << 1 — the
+ * repetition draw of check_draw is both bits.  cap in [1, 4096]; no engine needed. */
+int zc_chess_repetition_async(int32_t n, int32_t cap, const uint16_t *d_hist, const int32_t *d_len, int32_t *d_out,
+                              void *hip_stream);
 /* state_to_tensor: [n][17][8][8], planes_dtype ZC_F32 / ZC_F16. */
 int zc_chess_planes_async(zc_engine *eng, int32_t n, const zc_chess_state *d_states, void *d_planes,
                           int32_t planes_dtype, void *hip_stream);

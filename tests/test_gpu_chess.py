@@ -206,3 +206,48 @@ def test_random_positions_match_oracle(eng):
         assert [decode(m) for m in moves[i, :counts[i]]] == want, (i, b)
         assert bool(f[i] & ZC_CHESS_WIN) == oracle.chess_win(s), (i, b)
         assert bool(f[i] & (ZC_CHESS_STALEMATE | ZC_CHESS_FIFTY)) == oracle.chess_draw(s), (i, b)
+
+
+def _rep_sequences(rng, count, cap):
+    """Move histories (play order) rich in repeats: random over tiny alphabets, a block
+    repeated 1-4 times at the recent end, runs of one value, short ones."""
+    out = []
+    for i in range(count):
+        kind = i % 4
+        n = int(rng.integers(0, cap + 1)) if kind < 3 else int(rng.integers(0, 24))
+        if kind == 0:
+            s = rng.integers(0, 3, n)
+        elif kind == 1:
+            p, r = int(rng.integers(1, 9)), int(rng.integers(1, 5))
+            s = np.concatenate([rng.integers(0, 4, n), np.tile(rng.integers(0, 4, p), r)])[-n:] if n else np.zeros(0)
+        elif kind == 2:
+            s = np.concatenate([rng.integers(0, 2, n), np.full(int(rng.integers(0, 12)), 7)])[-n:] if n else np.zeros(0)
+        else:
+            s = rng.integers(0, 2, n)
+        out.append(np.asarray(s, np.uint16))
+    return out
+
+
+def test_repetition_matches_has_repeated_prefix():
+    """zc_chess_repetition_async against chess_backend.has_repeated_prefix (the KMP of
+    chess_backend.cpp:148-180) on 1,200 histories per side, most recent move first."""
+    from zeroclone_amd import _native
+    from zeroclone_amd.engine.games.chess.chess_backend import has_repeated_prefix
+    rng = np.random.default_rng(5)
+    cap, G = 300, 1200
+    seqs = _rep_sequences(rng, 2 * G, cap)
+    hist = np.zeros((G, 2, cap), np.uint16)
+    ln = np.zeros((G, 2), np.int32)
+    for k, s in enumerate(seqs):
+        hist[k // 2, k % 2, :len(s)] = s
+        ln[k // 2, k % 2] = len(s)
+    h, l = torch.from_numpy(hist.view(np.int16)).cuda(), torch.from_numpy(ln).cuda()
+    out = torch.zeros(G, dtype=torch.int32, device="cuda")
+    _native.check(_native.lib().zc_chess_repetition_async(G, cap, h.data_ptr(), l.data_ptr(), out.data_ptr(), None))
+    got = out.cpu().numpy()
+    hits = 0
+    for k, s in enumerate(seqs):
+        want = has_repeated_prefix([int(x) for x in s[::-1]])
+        hits += want
+        assert bool((got[k // 2] >> (k % 2)) & 1) == want, (k, s.tolist())
+    assert hits > 100   # the cases exercise both answers

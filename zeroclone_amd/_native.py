@@ -99,6 +99,8 @@ SIGNATURES = [
                                                ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     ("zc_chess_play_async", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p,
                                            ctypes.c_void_p, ctypes.c_void_p]),
+    ("zc_chess_repetition_async", ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p,
+                                                 ctypes.c_void_p, ctypes.c_void_p]),
     ("zc_chess_terminal_async", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p,
                                                ctypes.c_void_p]),
     ("zc_chess_planes_async", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p,

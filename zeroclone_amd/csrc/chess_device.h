@@ -28,7 +28,8 @@ namespace {
 
 constexpr int kMaxLegal = 256;   // the output capacity per position (real chess: <= 218)
 constexpr int kMaxPseudo = 512;  // pseudo-legal scratch per position
-constexpr int kRegion = 28;      // per-lane generation region (a queen has <= 27 moves)
+constexpr int kMaxHistory = 4096;  // moves per side the repetition test takes
+constexpr int kRegion = 28;     // per-lane generation region (a queen has <= 27 moves)
 
 __device__ __forceinline__ uint32_t lane() { return __lane_id(); }
 

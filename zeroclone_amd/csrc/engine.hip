@@ -533,6 +533,16 @@ int zc_chess_terminal_async(zc_engine *eng, int32_t n, const zc_chess_state *d_s
     return ZC_OK;
 }
 
+int zc_chess_repetition_async(int32_t n, int32_t cap, const uint16_t *d_hist, const int32_t *d_len, int32_t *d_out,
+                              void *hip_stream) {
+    if (n < 0 || (n && (!d_hist || !d_len || !d_out))) return fail(ZC_EINVAL, "bad argument");
+    if (!n) return ZC_OK;
+    if (!zc::launch_chess_repetition(n, cap, d_hist, d_len, d_out, (hipStream_t)hip_stream))
+        return fail(ZC_EINVAL, "history capacity %d outside [1, 4096]", cap);
+    ZC_HIP(hipGetLastError());
+    return ZC_OK;
+}
+
 int zc_chess_planes_async(zc_engine *eng, int32_t n, const zc_chess_state *d_states, void *d_planes,
                           int32_t planes_dtype, void *hip_stream) {
     if (planes_dtype != ZC_F32 && planes_dtype != ZC_F16) return fail(ZC_EINVAL, "planes_dtype must be ZC_F32 or ZC_F16");

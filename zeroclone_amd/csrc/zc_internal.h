@@ -184,6 +184,7 @@ void launch_chess_children(int n, const zc_chess_state *s, zc_chess_state *child
 void launch_chess_play(int n, const zc_chess_state *in, const uint16_t *moves, zc_chess_state *out, hipStream_t st);
 void launch_chess_terminal(int n, const zc_chess_state *s, int32_t *flags, hipStream_t st);
 void launch_chess_planes(int n, const zc_chess_state *s, void *planes, int f16, hipStream_t st);
+bool launch_chess_repetition(int n, int cap, const uint16_t *hist, const int32_t *len, int32_t *out, hipStream_t st);
 
 bool launch_net_conv3x3(int n, int h, int w, int cin, const void *in, const void *wt, const float *bias,
                         const void *res, void *out, int relu, hipStream_t s);
