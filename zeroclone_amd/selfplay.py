@@ -129,9 +129,8 @@ class ChessSelfPlay:
     (zc_chess_terminal_async: check_win, stalemate, fifty-move rule) on the device, and
     restarts finished games from the initial position.  The repetition half of check_draw
     (chess_backend.cpp:416-441: both sides' move histories end in >= 3 repeats of a block of
-    >= 2 moves) needs the move histories, which the device rows do not carry: the host keeps
-    them (most recent move first, as the reference's deques) and applies that test after
-    every step.  Results follow Engine._evaluate (engine.py:148-153): check_win -> turn*2-1
+    >= 2 moves) runs on the device too: each side's moves are appended to a per-game history
+    on the GPU and zc_chess_repetition_async tests both after every step.  Results follow Engine._evaluate (engine.py:148-153): check_win -> turn*2-1
     of the position after the move, a draw -> 0.  Game slot g of rank r is global game r*G+g
     with its own CPython MT19937 stream seeded seed + global id, as in C4SelfPlay."""
 
@@ -159,15 +158,19 @@ class ChessSelfPlay:
             self.vs = ChessValuedSearch(self.eng, games, batch_size, leaves=False, policy=self.policy,
                                         freedom=self.freedom)
             self.value_fn = NetValue(net)
+        self.hist_cap = 1024  # moves per side; a longer game raises
+        self.hist = torch.zeros((games, 2, self.hist_cap), dtype=torch.int16, device=self.dev)
+        self.hlen = torch.zeros((games, 2), dtype=torch.int32, device=self.dev)
+        self.turn = torch.full((games,), self.init_turn, dtype=torch.int64, device=self.dev)
+        self.rep = torch.zeros(games, dtype=torch.int32, device=self.dev)
+        self._slots = torch.arange(games, device=self.dev)
         self._turn = [self.init_turn] * games
-        self._hist = [([], []) for _ in range(games)]   # (white, black), most recent first
         self._moves = [[] for _ in range(games)]
         self.finished = []   # (global game id, move list, result)
 
     def step(self) -> np.ndarray:
         """One move for every game; returns the per-game results (ONGOING = 2).  Finished
         games restart from the initial position."""
-        from .engine.games.chess.chess_backend import has_repeated_prefix
         s = torch.cuda.current_stream(self.dev).cuda_stream
         if self.vs is None:
             self.eng.chess_search_async(0, self.G, self.roots.data_ptr(), self.sims, self.c, self.bs, self.policy,
@@ -179,8 +182,18 @@ class ChessSelfPlay:
             self.stats.copy_(st)
         self.eng.chess_play_async(self.G, self.roots.data_ptr(), self.moves.data_ptr(), self.roots.data_ptr(), s)
         self.eng.chess_terminal_async(self.G, self.roots.data_ptr(), self.flags.data_ptr(), s)
+        # play_move's history push (the mover's deque), then both sides' repetition test
+        at = self.hlen[self._slots, self.turn].clamp(max=self.hist_cap - 1).long()
+        self.hist[self._slots, self.turn, at] = self.moves
+        self.hlen[self._slots, self.turn] += 1
+        self.turn ^= 1
+        _native.check(_native.lib().zc_chess_repetition_async(self.G, self.hist_cap, self.hist.data_ptr(),
+                                                              self.hlen.data_ptr(), self.rep.data_ptr(), s))
         mv = self.moves.cpu().numpy().view(np.uint16)
         fl = self.flags.cpu().numpy()
+        rep = self.rep.cpu().numpy()
+        if int(self.hlen.max().item()) > self.hist_cap:
+            raise RuntimeError(f"a game exceeded {self.hist_cap} moves per side")
         if (self.stats[:, 5] == _native.ZC_STATUS_CAPACITY).any():
             raise RuntimeError("chess search exceeded the tree's child-slot pool or depth limit")
         res = np.full(self.G, ONGOING, np.int32)
@@ -189,22 +202,22 @@ class ChessSelfPlay:
         for g in range(self.G):
             if mv[g] == 0xFFFF:
                 raise RuntimeError(f"game slot {g}: no legal move at a non-terminal root")
-            move = _native.unpack_chess_move(int(mv[g]))
-            self._hist[g][self._turn[g]].insert(0, move)   # play_move: the mover's deque, front
-            self._moves[g].append(move)
+            self._moves[g].append(_native.unpack_chess_move(int(mv[g])))
             self._turn[g] ^= 1
             if fl[g] & _native.ZC_CHESS_WIN:
                 res[g] = self._turn[g] * 2 - 1
-            elif fl[g] & draw_flags or (has_repeated_prefix(self._hist[g][0]) and has_repeated_prefix(self._hist[g][1])):
+            elif fl[g] & draw_flags or rep[g] == 3:
                 res[g] = 0
             if res[g] != ONGOING:
                 self.finished.append((self.first_id + g, self._moves[g], int(res[g])))
                 self._moves[g] = []
-                self._hist[g] = ([], [])
                 self._turn[g] = self.init_turn
                 done.append(g)
         if done:
-            self.roots[torch.tensor(done, dtype=torch.int64, device=self.dev)] = self.init_row
+            d = torch.tensor(done, dtype=torch.int64, device=self.dev)
+            self.roots[d] = self.init_row
+            self.hlen[d] = 0
+            self.turn[d] = self.init_turn
         return res
 
     def close(self):
