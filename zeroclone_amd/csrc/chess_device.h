@@ -71,6 +71,7 @@ __device__ __forceinline__ uint32_t pack_move(int from, int to, uint32_t v) {
 // probe(s): -2 empty; -1 not capturable (own piece, enemy king, unknown white/black char);
 // otherwise the capture value fabs(piece_val) of the enemy piece on s.
 struct ByteView {
+    static constexpr bool kCheapProbe = false;  // probes are LDS reads
     const uint8_t *b;
     int t;
     __device__ __forceinline__ int probe(int s) const {
@@ -89,6 +90,7 @@ constexpr uint64_t kDiag = 0x8040201008040201ull;  // squares (i, i)
 constexpr uint64_t kAnti = 0x0102040810204080ull;  // squares (i, 7 - i)
 
 struct BitView {
+    static constexpr bool kCheapProbe = true;  // generation from masks (bit_piece_moves)
     uint64_t occ;              // non-empty squares
     uint64_t cap;              // capturable: the enemy's pieces other than kings
     uint64_t tP, tNB, tR;      // piece types (either colour), for capture values
@@ -141,6 +143,90 @@ struct BitView {
                highest(diag & low, ad) || highest(anti & low, ad);
     }
 };
+
+// Pseudo-legal moves of the piece `pc` on square s from the BitView's masks, in the
+// reference's order (piece_moves below is the square-by-square statement of it): target
+// sets come from shifts and masked bit scans, then each set is emitted in its order — a
+// knight's eight offsets (-17 ... +17) are in index order, a king's are tested one by one
+// in kAll8 order, and a slider's rays run away from s (descending indices for the
+// directions that lower the index, ascending for the others).
+template <class F>
+__device__ __forceinline__ void bit_piece_moves(const BitView &v, int s, uint32_t pc, F &&emit) {
+    const int r = s >> 3, c = s & 7;
+    const uint32_t up = upper(pc);
+    const uint64_t empty = ~v.occ, ok = ~v.occ | v.cap;
+    auto val = [&](int to) -> uint32_t {
+        if (!((v.cap >> to) & 1ull)) return 0u;
+        return ((v.tP >> to) & 1ull) ? 1u : ((v.tNB >> to) & 1ull) ? 3u : ((v.tR >> to) & 1ull) ? 5u : 9u;
+    };
+    auto asc = [&](uint64_t T) {
+        while (T) {
+            const int to = __builtin_ctzll(T);
+            T &= T - 1ull;
+            emit(s, to, val(to));
+        }
+    };
+    auto desc = [&](uint64_t T) {
+        while (T) {
+            const int to = 63 - __builtin_clzll(T);
+            T &= ~(1ull << to);
+            emit(s, to, val(to));
+        }
+    };
+    const uint64_t kb = 1ull << s;
+    if (up == 'P') {
+        const bool white = pc == 'P';
+        const int nr = r + (white ? -1 : 1);
+        if ((unsigned)nr < 8u) {
+            const int t1 = nr * 8 + c;
+            if ((empty >> t1) & 1ull) {
+                emit(s, t1, 0u);
+                const int t2 = t1 + (white ? -8 : 8);
+                if (r == (white ? 6 : 1) && ((empty >> t2) & 1ull)) emit(s, t2, 0u);
+            }
+            if (c > 0 && ((v.cap >> (t1 - 1)) & 1ull)) emit(s, t1 - 1, val(t1 - 1));
+            if (c < 7 && ((v.cap >> (t1 + 1)) & 1ull)) emit(s, t1 + 1, val(t1 + 1));
+        }
+    } else if (up == 'N') {
+        asc(ok & (((kb << 17) & kNotA) | ((kb << 15) & kNotH) | ((kb << 10) & kNotAB) | ((kb << 6) & kNotGH) |
+                  ((kb >> 17) & kNotH) | ((kb >> 15) & kNotA) | ((kb >> 10) & kNotGH) | ((kb >> 6) & kNotAB)));
+    } else if (up == 'K') {
+        const uint64_t T = ok & (((kb << 1) & kNotA) | ((kb >> 1) & kNotH) | (kb << 8) | (kb >> 8) |
+                                 ((kb << 9) & kNotA) | ((kb << 7) & kNotH) | ((kb >> 7) & kNotA) | ((kb >> 9) & kNotH));
+        constexpr int off[8] = {-9, -7, 7, 9, -8, 8, -1, 1};  // kAll8 order
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int to = s + off[i];
+            if ((unsigned)to < 64u && ((T >> to) & 1ull)) emit(s, to, val(to));
+        }
+    } else if (up == 'B' || up == 'R' || up == 'Q') {
+        const uint64_t low = kb - 1ull, high = ~low & ~kb;
+        const uint64_t file = kFileA << c, rank = 0xFFull << (8 * r);
+        const int dd = r - c, da = r + c - 7;
+        const uint64_t diag = dd >= 0 ? kDiag << (8 * dd) : kDiag >> (-8 * dd);
+        const uint64_t anti = da >= 0 ? kAnti << (8 * da) : kAnti >> (-8 * da);
+        auto up_ray = [&](uint64_t ray) {  // towards higher indices: through the nearest blocker
+            const uint64_t bl = ray & v.occ, first = bl & (0ull - bl);
+            asc(ok & (first ? ray & ((first << 1) - 1ull) : ray));
+        };
+        auto down_ray = [&](uint64_t ray) {  // towards lower indices
+            const uint64_t bl = ray & v.occ;
+            desc(ok & (bl ? ray & ~((1ull << (63 - __builtin_clzll(bl))) - 1ull) : ray));
+        };
+        if (up != 'R') {  // kAll8[0..4): (-1,-1) (-1,1) (1,-1) (1,1)
+            down_ray(diag & low);
+            down_ray(anti & low);
+            up_ray(anti & high);
+            up_ray(diag & high);
+        }
+        if (up != 'B') {  // kAll8[4..8): (-1,0) (1,0) (0,-1) (0,1)
+            down_ray(file & low);
+            up_ray(file & high);
+            down_ray(rank & low);
+            up_ray(rank & high);
+        }
+    }
+}
 
 __device__ __forceinline__ bool known_piece(uint32_t x) {
     switch (x) {
@@ -305,7 +391,11 @@ __device__ __forceinline__ int legal_moves_view(const V &v, int t, uint32_t pc, 
     // moves), then each lane copies its run to its place in board-scan order
     uint16_t *const own = reg + s * kRegion;
     uint32_t cnt = 0;
-    if (mine) piece_moves(v, (int)s, pc, [&](int f, int to, uint32_t val) { own[cnt++] = (uint16_t)pack_move(f, to, val); });
+    auto put = [&](int f, int to, uint32_t val) { own[cnt++] = (uint16_t)pack_move(f, to, val); };
+    if (mine) {
+        if constexpr (V::kCheapProbe) bit_piece_moves(v, (int)s, pc, put);
+        else piece_moves(v, (int)s, pc, put);
+    }
     uint32_t total;
     const uint32_t off = wave_excl_sum(cnt, total);
     if (total > (uint32_t)kMaxPseudo) return -1;
