@@ -578,21 +578,32 @@ __global__ void planes_to_nhwc_kernel(int n, int cin, int hw, int cpad, const _F
 }
 
 // head (network.py:37-42): global average pool -> Linear(128, 1) -> tanh, in fp32; one wave
-// per position, lane l owns channels 2l and 2l+1.  Writes the fp64 value the backup takes.
+// per position.  Lane l reads 16-byte pieces (channels 8 (l & 15) .. +8) of pixels l / 16,
+// +4, +8, ..., so every load instruction covers four whole 256-byte pixel rows; the four
+// pixel groups are then summed across lanes.  Writes the fp64 value the backup takes.
 __global__ __launch_bounds__(256) void value_head_kernel(int n, int hw, const _Float16 *__restrict__ act,
                                                          const float *__restrict__ fcw, float fcb,
                                                          double *__restrict__ values) {
     const int i = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
     const int lane = threadIdx.x & 63;
     if (i >= n) return;
-    const _Float16 *a = act + (size_t)i * hw * kCout + 2 * lane;
-    float s0 = 0.0f, s1 = 0.0f;
-    for (int p = 0; p < hw; ++p) {
-        s0 += (float)a[(size_t)p * kCout];
-        s1 += (float)a[(size_t)p * kCout + 1];
+    const int c0 = (lane & 15) * 8;
+    const _Float16 *a = act + (size_t)i * hw * kCout + c0;
+    float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int p = lane >> 4; p < hw; p += 4) {
+        const h8 v = *(const h8 *)(a + (size_t)p * kCout);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) s[e] += (float)v[e];
     }
-    float d = (s0 * fcw[2 * lane] + s1 * fcw[2 * lane + 1]) / (float)hw;
-    for (int o = 32; o > 0; o >>= 1) d += __shfl_xor(d, o);
+    float d = 0.f;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        float t = s[e] + __shfl_xor(s[e], 16);
+        t += __shfl_xor(t, 32);
+        d += t * fcw[c0 + e];
+    }
+    d /= (float)hw;
+    for (int o = 8; o > 0; o >>= 1) d += __shfl_xor(d, o);
     if (lane == 0) values[i] = (double)tanhf(d + fcb);
 }
 
