@@ -5,19 +5,29 @@ Workload (BASELINE.json configs[1] = SURVEY.md §8(d) C2; with --gpus N it is C3
 4096 concurrent Connect4 self-play games per GPU, 800 simulations per move, leaf batch 32,
 c = 1.4, the reference's random_rollout value and random expansion policy, exact-RNG mode
 (every game's CPython MT19937 stream consumed in the reference's order).  One STEP = one
-move for every game: the whole search (select/expand/rollout/backup x 800) on the GPU,
-then Engine.play_move + _evaluate on the device, finished games restarting from the
-opening (scripts/train.py:151-170 refill).  Games are sharded across ranks by global game
-id (seed = base + id) — no collective on the data path, so "scaling" is "weak".
+move for every game: the whole search (select/expand/rollout/backup x 800) on the GPU, then
+Engine.play_move + _evaluate, trajectory recording (positions appended, finished games
+labelled as Engine.get_dataset and pooled) and the refill of finished games
+(scripts/train.py:151-170), all on the device (selfplay.C4SelfPlay).  Before the warm-up
+the pool is run until every game slot has finished a game and started another, so the
+timed steps see games of mixed ages (steady-state self-play), not the lockstep opening.
 
-value = expansions created on all ranks in the K timed steps / max over ranks of the
-wall time of those K steps (barrier + device sync on both sides).
+Games are sharded across ranks by global game id (seed = base + id) — no collective on the
+data path ("scaling": "weak").  `--gpus N` without torchrun spawns N fresh processes (one
+per GPU; the parent never touches the GPU); under torchrun WORLD_SIZE must equal --gpus.
+After the timed steps the positions of the games finished on every rank are all-gathered
+into the replay buffer (RCCL over xGMI) — C3's one exchange, timed beside the metric.
+
+value = expansions created on all ranks in the K timed steps / max over ranks of the wall
+time of those K steps (barrier + device sync on both sides).
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import platform
+import socket
 import sys
 import time
 
@@ -38,11 +48,30 @@ def bytes_per_expansion_model(expansions: int, depth_sum: int) -> int:
     return 152 * depth_sum + 96 * expansions
 
 
+def host_cpus() -> dict:
+    """What the CPU baseline ran on: the threads used (the process's CPU share: the
+    scheduler affinity, capped by OMP_NUM_THREADS where the box sets it), nproc, the model."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    model = platform.processor() or ""
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"threads": max(1, min(aff, omp) if omp else aff), "nproc": os.cpu_count(), "affinity": aff,
+            "cpu_model": model}
+
+
 def cpu_baseline(sims: int, bs: int, c: float, budget_s: float = 15.0):
-    """The oracle port (oracle/c4_oracle.c, bit-exact to the reference), timed on host cores."""
+    """The oracle port (oracle/c4_oracle.c, bit-exact to the reference's get_move on the
+    committed fixtures), one game per pthread task across the host's CPU share."""
     import oracle
-    threads = max(1, min(16, os.cpu_count() or 1))
-    # calibrate on a small sample, then size the timed sample to ~budget_s
+    hc = host_cpus()
+    threads = hc["threads"]
     n0 = threads
     t = time.perf_counter()
     oracle.get_move_batch(["." * 42] * n0, [0] * n0, list(range(n0)), sims, c, bs, threads=threads)
@@ -50,11 +79,41 @@ def cpu_baseline(sims: int, bs: int, c: float, budget_s: float = 15.0):
     n = int(max(threads, min(65536, rate0 * budget_s / sims)))
     n = max(threads, (n // threads) * threads)
     t = time.perf_counter()
-    _, _, _ = oracle.get_move_batch(["." * 42] * n, [0] * n, list(range(1000, 1000 + n)), sims, c, bs, threads=threads)
+    oracle.get_move_batch(["." * 42] * n, [0] * n, list(range(1000, 1000 + n)), sims, c, bs, threads=threads)
     dt = time.perf_counter() - t
     return {"value": round(n * sims / dt, 1), "unit": "expansions/s", "cores": threads, "kind": "port",
+            "nproc": hc["nproc"], "cpu_model": hc["cpu_model"],
+            "port": "oracle/c4_oracle.c: C restatement pinned bit-exact to the reference's own get_move outputs "
+                    "(tests/golden/c4_get_move.json, 150 cases incl. 800 sims) and rollouts",
             "sample": f"{n} games x 1 move x {sims} sims from the opening (expansions = sims there), "
-                      f"batch {bs}, {threads} pthreads, oracle/c4_oracle.c, {dt:.1f}s"}
+                      f"batch {bs}, {threads} pthreads, {dt:.1f}s"}
+
+
+def cpu_baseline_chess(sims: int = 400, bs: int = 32, c: float = 1.4, budget_s: float = 10.0):
+    """Same-run CPU baseline of the chess crude mode (configs/crude_chess.yaml, C4 shape):
+    the oracle's chess get_move (oracle/chess_oracle.c, bit-exact to the reference's on the
+    26 committed get_move goldens), one opening search per task on a thread pool (ctypes
+    releases the GIL)."""
+    from concurrent.futures import ThreadPoolExecutor
+    import oracle
+    threads = host_cpus()["threads"]
+    root = oracle.chess_init()
+
+    def one(seed):
+        mt = oracle.MT(seed)
+        oracle.chess_get_move(root, mt, sims, c, bs, policy="immediate_value", freedom=3.0)
+
+    with ThreadPoolExecutor(threads) as ex:
+        t = time.perf_counter()
+        list(ex.map(one, range(threads)))
+        rate0 = threads / max(time.perf_counter() - t, 1e-6)
+        n = max(threads, int(rate0 * budget_s) // threads * threads)
+        t = time.perf_counter()
+        list(ex.map(one, range(100, 100 + n)))
+        dt = time.perf_counter() - t
+    return {"value": round(n * sims / dt, 1), "unit": "expansions/s", "cores": threads, "kind": "port",
+            "sample": f"{n} chess openings x {sims} sims, crude_chess_score, immediate_value(3), {threads} threads, "
+                      f"{dt:.1f}s (expansions ~= sims from the opening)"}
 
 
 MFMA_F16_PEAK_TFLOPS = 2500.0  # MI355X dense fp16 MFMA peak, ~2.5 PF (MI355X_MICROARCH.md; no sparsity)
@@ -174,147 +233,149 @@ def puct_mode(steps: int, dev) -> dict:
             "net_tflops_lower": round(fl / dt / 1e12, 1), "mfma_frac_lower": round(fl / dt / 1e12 / MFMA_F16_PEAK_TFLOPS, 4)}
 
 
-def philox_mode(eng, step, evs, acc, args, G: int, dev) -> dict:
+def philox_mode(sp, args) -> dict:
     """C2(ii): the same self-play steps with ZC_ROLLOUT_PHILOX (leaf-parallel rollouts on
     per-leaf Philox-seeded streams; statistical parity, tests/test_gpu_philox.py)."""
-    eng.c4_rollout_mode("philox", args.seed + 0xC2)
+    sp.eng.c4_rollout_mode("philox", args.seed + 0xC2)
     try:
-        step()
-        torch.cuda.synchronize(dev)
-        acc.zero_()
-        t0 = time.perf_counter()
-        for k in range(args.steps):
-            step(evs[k])
-        torch.cuda.synchronize(dev)
-        dt = time.perf_counter() - t0
+        r = run_steps(sp, args.steps, warmup=1)
     finally:
-        eng.c4_rollout_mode("exact")
-    kernel_ms = [a.elapsed_time(b) for a, b in evs]
-    expansions = int(acc[0].item())
-    return {"value": round(expansions / dt, 1), "unit": "expansions/s", "ms_per_step": round(dt / args.steps * 1e3, 3),
-            "search_ms_per_step": [round(x, 3) for x in kernel_ms], "expansions": expansions,
-            "config": f"C2(ii) {G} games x {args.sims} sims, batch {args.batch}: Philox rollout mode"}
+        sp.eng.c4_rollout_mode("exact")
+    return {"value": round(r["expansions"] / r["dt"], 1), "unit": "expansions/s",
+            "ms_per_step": round(r["dt"] / args.steps * 1e3, 3),
+            "search_ms_per_step": [round(x, 3) for x in r["kernel_ms"]], "expansions": r["expansions"],
+            "config": f"C2(ii) {sp.G} games x {args.sims} sims, batch {args.batch}: Philox rollout mode"}
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--games", type=int, default=4096, help="games per GPU")
-    ap.add_argument("--sims", type=int, default=800)
-    ap.add_argument("--batch", type=int, default=32)
-    ap.add_argument("--c", type=float, default=1.4)
-    ap.add_argument("--seed", type=int, default=0)
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--net-steps", type=int, default=1,
-                    help="moves of the C2(iii) value-network mode reported under extra (0 = skip; N=1 only)")
-    ap.add_argument("--traffic-bytes", type=float, default=None,
-                    help="per-launch HBM bytes of the search kernel from a separate rocprofv3 --pmc pass")
-    args = ap.parse_args()
+# ---------------------------------------------------------------------------------------------
+def burn_in(sp, max_steps: int = 200, check_every: int = 8) -> int:
+    """Step the pool until every slot has finished a game and started another (game numbers
+    >= G everywhere): the timed window then sees games of mixed ages.  Returns the steps."""
+    steps = 0
+    while steps < max_steps:
+        for _ in range(check_every):
+            sp.step()
+        steps += check_every
+        if int(sp.traj.slot[:, 1].min().item()) >= sp.G:
+            break
+    sp.take()   # the burn-in's games are not the timed window's
+    return steps
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
 
-    G, S, B = args.games, args.sims, args.batch
-    eng = _native.NativeEngine(max_games=G, max_sims=S, max_batch=B, device=local)
-    first_id = rank * G
-    eng.seed(0, [args.seed + first_id + g for g in range(G)])
+def run_steps(sp, steps: int, warmup: int, world: int = 1) -> dict:
+    """W untimed steps, then K timed steps bracketed by barrier + device sync; HIP events
+    around every search launch on the launch stream."""
+    dev = sp.dev
+    stream = torch.cuda.current_stream(dev)
+    acc = torch.zeros(4, dtype=torch.int64, device=dev)   # expansions, depth_sum, finished, leaves
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(max(steps, 1))]
 
-    roots = torch.zeros((G, 3), dtype=torch.int64, device=dev)   # zc_c4_state: stones[2], turn|reserved
-    moves = torch.zeros(G, dtype=torch.int32, device=dev)
-    na = torch.zeros((G, 7), dtype=torch.int32, device=dev)
-    stats = torch.zeros((G, _native.STATS_FIELDS), dtype=torch.int64, device=dev)   # zc_game_stats
-    results = torch.zeros(G, dtype=torch.int32, device=dev)
-    acc = torch.zeros(4, dtype=torch.int64, device=dev)          # expansions, depth_sum, finished, leaves
+    def one(ev):   # warm-up and timed steps run the same code (first use of a torch op loads its kernel)
+        ev[0].record(stream)
+        r = sp.step_search()
+        ev[1].record(stream)
+        sp.step_finish()
+        tally(r)
 
-    torch_stream = torch.cuda.Stream(dev)   # every launch of the step, and the timing events, on it
-    torch.cuda.set_stream(torch_stream)
+    def tally(r):
+        acc[0] += sp.stats[:, 0].sum()
+        acc[1] += sp.stats[:, 1].sum()
+        acc[2] += ((r != _native.ZC_C4_ONGOING) & (r != _native.ZC_SLOT_IDLE)).sum()
+        acc[3] += sp.stats[:, 2].sum()
 
-    def step(ev=None):
-        stream = torch_stream.cuda_stream
-        if ev is not None:
-            ev[0].record()
-        eng.c4_search_async(roots.data_ptr(), G, S, args.c, B, moves.data_ptr(), na.data_ptr(),
-                            stats.data_ptr(), stream=stream)
-        if ev is not None:
-            ev[1].record()
-        eng.c4_play_async(roots.data_ptr(), G, moves.data_ptr(), results.data_ptr(), reset=True, stream=stream)
-        acc[0] += stats[:, 0].sum()
-        acc[1] += stats[:, 1].sum()
-        acc[2] += (results != _native.ZC_C4_ONGOING).sum()
-        acc[3] += stats[:, 2].sum()
-
-    for _ in range(args.warmup):
-        step()
+    tally(sp.results)   # load the tally's torch kernels even when warmup == 0 (no step is run)
+    for _ in range(warmup):
+        one(evs[0])
     torch.cuda.synchronize(dev)
     acc.zero_()
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for k in range(args.steps):
-        step(evs[k])
+    for k in range(steps):
+        one(evs[k])
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
-
-    bad = int((stats[:, 5] != 0).sum().item())
-    if bad:
-        raise RuntimeError(f"{bad} games reported a nonzero search status")
+    if int((sp.stats[:, 5] != 0).sum().item()):
+        raise RuntimeError("a game reported a nonzero search status")
     kernel_ms = [a.elapsed_time(b) for a, b in evs]
-    tot = acc.clone()
-    dtt = torch.tensor([dt], dtype=torch.float64, device=dev)
-    kms = torch.tensor([sum(kernel_ms)], dtype=torch.float64, device=dev)
-    if world > 1:
+    tot = [int(x) for x in acc.tolist()]
+    return {"dt": dt, "kernel_ms": kernel_ms, "expansions": tot[0], "depth_sum": tot[1], "finished": tot[2],
+            "leaves": tot[3]}
+
+
+def reduce_over_ranks(counts, dt: float, kernel_ms_sum: float, device) -> tuple[list[int], float, float]:
+    """Whole-job aggregation: counters summed over ranks, wall time and kernel time the max
+    over ranks (a no-op at world size 1)."""
+    tot = torch.tensor(list(counts), dtype=torch.int64, device=device)
+    t = torch.tensor([dt, kernel_ms_sum], dtype=torch.float64, device=device)
+    if dist.is_initialized() and dist.get_world_size() > 1:
         dist.all_reduce(tot, op=dist.ReduceOp.SUM)
-        dist.all_reduce(dtt, op=dist.ReduceOp.MAX)
-        dist.all_reduce(kms, op=dist.ReduceOp.MAX)
-    expansions, depth_sum, finished, leaves = (int(x) for x in tot.tolist())
-    dt_max = float(dtt.item())
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return [int(x) for x in tot.tolist()], float(t[0].item()), float(t[1].item())
 
-    traffic, traffic_src = args.traffic_bytes, "--traffic-bytes" if args.traffic_bytes else None
-    if traffic is None:  # the committed PMC summary of this kernel (tools/summarize_profile.py)
-        import glob
-        prof = sorted(glob.glob(os.path.join(HERE, "profiles", "r*_c4_search_summary.json")))
-        if prof:
-            with open(prof[-1]) as fh:
-                hbm = json.load(fh).get("hbm")
-            if hbm:
-                traffic = hbm["bytes_per_launch"]
-                traffic_src = os.path.relpath(prof[-1], HERE)
 
-    # C3's one exchange (SURVEY §8(e)): the all-gather of finished trajectories into the
-    # replay buffer — here a payload of the right shape, this rank's K steps x G positions
-    # (24-B zc_c4_state rows), through selfplay.gather_positions (RCCL over xGMI).  Off the
-    # expansions/s clock, reported beside it.
-    gather = None
+def rank_ranges(world: int, games: int) -> list[list[int]]:
+    """Global game ids [first, last] of each rank (rank r owns r*G .. r*G+G-1)."""
+    return [[r * games, r * games + games - 1] for r in range(world)]
+
+
+def gather_trajectories(sp, world: int) -> dict:
+    """C3's one collective: this rank's finished games' positions (the device
+    pool, labels packed with the rows) all-gathered over ranks into the replay buffer."""
+    from zeroclone_amd.selfplay import gather_positions
+    local = sp.take_positions()
+    out = {"local_rows": int(local.shape[0])}
+    if world == 1:
+        return out
+    gather_positions(local)  # warm the communicator
+    dist.barrier()
+    torch.cuda.synchronize(sp.dev)
+    tg = time.perf_counter()
+    allpos = gather_positions(local)
+    torch.cuda.synchronize(sp.dev)
+    gms = torch.tensor([(time.perf_counter() - tg) * 1e3], dtype=torch.float64, device=sp.dev)
+    dist.all_reduce(gms, op=dist.ReduceOp.MAX)
+    out.update({"rows": int(allpos.shape[0]), "bytes": int(allpos.numel() * allpos.element_size()),
+                "ms": round(float(gms.item()), 3),
+                "collective": "all_gather (counts, padded payload) of finished games' 24-B positions, nccl=RCCL"})
+    return out
+
+
+def traffic_from_profiles():
+    """Per-launch HBM bytes of the search kernel from the newest committed PMC summary."""
+    import glob
+    prof = sorted(glob.glob(os.path.join(HERE, "profiles", "r*_c4_search_summary.json")))
+    if prof:
+        with open(prof[-1]) as fh:
+            hbm = json.load(fh).get("hbm")
+        if hbm:
+            return hbm["bytes_per_launch"], os.path.relpath(prof[-1], HERE)
+    return None, None
+
+
+def run_rank(args, rank: int, world: int, local: int):
     if world > 1:
-        from zeroclone_amd.selfplay import gather_positions
-        local = roots.repeat(args.steps, 1)
-        gather_positions(local)  # warm the communicator
-        dist.barrier()
-        torch.cuda.synchronize(dev)
-        tg = time.perf_counter()
-        allpos = gather_positions(local)
-        torch.cuda.synchronize(dev)
-        gms = torch.tensor([(time.perf_counter() - tg) * 1e3], dtype=torch.float64, device=dev)
-        dist.all_reduce(gms, op=dist.ReduceOp.MAX)
-        gather = {"rows": int(allpos.shape[0]), "bytes": int(allpos.numel() * allpos.element_size()),
-                  "ms": round(float(gms.item()), 3), "collective": "all_gather (counts, padded payload), backend nccl=RCCL"}
-
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    from zeroclone_amd.selfplay import C4SelfPlay
+    G, S, B = args.games, args.sims, args.batch
+    torch.cuda.set_stream(torch.cuda.Stream(dev))   # every launch and the timing events on one stream
+    sp = C4SelfPlay(G, S, c=args.c, batch_size=B, seed=args.seed, rank=rank, device=local, record=True)
+    burn = burn_in(sp) if args.burn_in else 0
+    r = run_steps(sp, args.steps, args.warmup, world)
+    gather = gather_trajectories(sp, world)
+    counts, dt_max, kms = reduce_over_ranks([r["expansions"], r["depth_sum"], r["finished"], r["leaves"]], r["dt"],
+                                            sum(r["kernel_ms"]), dev)
+    expansions, depth_sum, finished, leaves = counts
     if rank == 0:
+        traffic, traffic_src = (args.traffic_bytes, "--traffic-bytes") if args.traffic_bytes else traffic_from_profiles()
         launches = args.steps * world
         bytes_launch = bytes_per_expansion_model(expansions, depth_sum) / launches
-        avg_kernel_s = float(kms.item()) / 1e3 / args.steps
+        avg_kernel_s = kms / 1e3 / args.steps
         achieved = bytes_launch / avg_kernel_s / 1e9
         out = {
             "metric": METRIC,
@@ -330,52 +391,139 @@ def main():
             "dtype": "f64",
             "data": "synthetic: self-play from the empty board, per-game CPython MT19937 seeds base+game_id",
             "config": {"workload": f"C2/C3 Connect4 self-play, {G} games/GPU, {S} sims/move, batch {B}, "
-                                   f"c {args.c}, random_rollout exact-RNG mode",
+                                   f"c {args.c}, random_rollout exact-RNG mode, steady state (mixed game ages)",
                        "games_per_gpu": G, "global_games": G * world, "sims": S, "batch_size": B,
+                       "world_size": world, "rank_games": rank_ranges(world, G), "burn_in_steps": burn,
                        "parallelism": f"games sharded over {world} GPU(s), 1 process/GPU"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 5),
                          "traffic": traffic, "traffic_source": traffic_src,
                          "kernel": "c4_search_kernel", "avg_launch_ms": round(avg_kernel_s * 1e3, 3),
                          "bytes_per_launch_model": round(bytes_launch),
-                         "model": "SURVEY §8(d): 152*d+96 B per expansion, d counted in-kernel"},
+                         "model": "SURVEY §8(d): 152*d+96 B per expansion, d counted in-kernel",
+                         "limiter": "the per-game serial dependency chain (instruction issue/latency), not HBM: "
+                                    "see extra.issue and DESIGN §4"},
             "extra": {"expansions": expansions, "leaves": leaves, "mean_depth": round(depth_sum / max(expansions, 1), 3),
-                      "games_finished": finished, "search_ms_per_step": [round(x, 3) for x in kernel_ms]},
+                      "games_finished": finished, "search_ms_per_step": [round(x, 3) for x in r["kernel_ms"]],
+                      "trajectory_allgather": gather},
         }
-        if gather is not None:
-            out["extra"]["trajectory_allgather"] = gather
-        # per-phase times (s_memtime stamps, one extra search with the stamped
-        # kernel; shares applied to the unstamped launch time) and the tree-walk-only roofline
-        # (select + expand-write + backup + publish; rollouts are integer VALU, not HBM).
+        if args.issue_json:
+            with open(args.issue_json) as fh:
+                out["extra"]["issue"] = json.load(fh)
         if world == 1:
-            eng.phase_cycles(True)
-            eng.c4_search_async(roots.data_ptr(), G, S, args.c, B, moves.data_ptr(), na.data_ptr(), stats.data_ptr(),
-                                stream=torch_stream.cuda_stream)
-            torch.cuda.synchronize(dev)
-            ph = eng.phase_cycles(False)
-            tot_c = max(sum(ph.values()), 1)
-            share = {k: v / tot_c for k, v in ph.items() if k != "sub"}
-            walk = sum(share[k] for k in ("rng", "walk_first", "walk_resumed", "expand", "backup", "publish"))
-            out["extra"]["phases"] = {
-                "share": {k: round(v, 4) for k, v in share.items()},
-                "ms_per_launch": {k: round(v * avg_kernel_s * 1e3, 3) for k, v in share.items()},
-                "walk_roofline": {"t_walk_ms": round(walk * avg_kernel_s * 1e3, 3),
-                                  "achieved": round(bytes_launch / (walk * avg_kernel_s) / 1e9, 2),
-                                  "frac": round(bytes_launch / (walk * avg_kernel_s) / 1e9 / HBM_PEAK_GBS, 5),
-                                  "note": "SURVEY §8(d) roofline definition: model bytes / tree-walk time only"}}
+            out["extra"]["phases"] = phases(sp, args, bytes_launch, avg_kernel_s)
         if world == 1 and args.net_steps > 0:
-            out["extra"]["c2_philox"] = philox_mode(eng, step, evs, acc, args, G, dev)
+            out["extra"]["c2_philox"] = philox_mode(sp, args)
+            out["extra"]["record_overhead"] = record_overhead(sp, args)
+            sp.close()
+            sp = None
             out["extra"]["c2_value_net"] = net_mode(G, S, B, args.c, args.net_steps, dev)
             out["extra"]["c4_chess"] = chess_modes(args.net_steps, dev)
             out["extra"]["c5_chess_puct"] = puct_mode(args.net_steps, dev)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(S, B, args.c)
+            if args.net_steps > 0:
+                out["extra"]["c4_chess"]["crude"]["cpu_baseline"] = cpu_baseline_chess()
         else:
             out["cpu_baseline"] = None
         print(json.dumps(out), flush=True)
-    eng.close()
+    if sp is not None:
+        sp.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def phases(sp, args, bytes_launch: float, avg_kernel_s: float) -> dict:
+    """SURVEY §8(d) per-phase times: s_memtime stamps from one extra search with the stamped
+    kernel build, shares applied to the unstamped launch time; and the tree-walk-only
+    roofline (select + expand-write + backup + publish; rollouts are integer VALU, not HBM)."""
+    sp.eng.phase_cycles(True)
+    sp.step()
+    torch.cuda.synchronize(sp.dev)
+    ph = sp.eng.phase_cycles(False)
+    tot_c = max(sum(ph.values()), 1)
+    share = {k: v / tot_c for k, v in ph.items() if k != "sub"}
+    walk = sum(share[k] for k in ("rng", "walk_first", "walk_resumed", "expand", "backup", "publish"))
+    return {"share": {k: round(v, 4) for k, v in share.items()},
+            "ms_per_launch": {k: round(v * avg_kernel_s * 1e3, 3) for k, v in share.items()},
+            "walk_roofline": {"t_walk_ms": round(walk * avg_kernel_s * 1e3, 3),
+                              "achieved": round(bytes_launch / (walk * avg_kernel_s) / 1e9, 2),
+                              "frac": round(bytes_launch / (walk * avg_kernel_s) / 1e9 / HBM_PEAK_GBS, 5),
+                              "note": "SURVEY §8(d) roofline definition: model bytes / tree-walk time only "
+                                      "(phase shares from the stamped build: modelled, not a separate clock)"}}
+
+
+def record_overhead(sp, args) -> dict:
+    """Trajectory recording's cost: the same steps with and without zc_traj_record_async."""
+    sp.record = False
+    try:
+        off = run_steps(sp, args.steps, warmup=1)
+    finally:
+        sp.record = True
+        sp.start()
+    on = run_steps(sp, args.steps, warmup=1)
+    return {"ms_per_step_recorded": round(on["dt"] / args.steps * 1e3, 3),
+            "ms_per_step_unrecorded": round(off["dt"] / args.steps * 1e3, 3),
+            "ratio": round(on["dt"] / max(off["dt"], 1e-9), 4)}
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _spawned(rank: int, args, world: int, port: int):
+    os.environ.update({"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "RANK": str(rank),
+                       "LOCAL_RANK": str(rank), "WORLD_SIZE": str(world)})
+    run_rank(args, rank, world, rank)
+
+
+def parse_args(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--games", type=int, default=4096, help="games per GPU")
+    ap.add_argument("--sims", type=int, default=800)
+    ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--c", type=float, default=1.4)
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--no-burn-in", dest="burn_in", action="store_false",
+                    help="time from the lockstep opening instead of steady-state self-play")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--net-steps", type=int, default=1,
+                    help="moves of the network / chess modes reported under extra (0 = skip; N=1 only)")
+    ap.add_argument("--traffic-bytes", type=float, default=None,
+                    help="per-launch HBM bytes of the search kernel from a separate rocprofv3 --pmc pass")
+    ap.add_argument("--issue-json", default=os.path.join(HERE, "profiles", "r02_c4_search_issue.json"),
+                    help="SQ-counter issue summary of the search kernel (tools/summarize_profile.py)")
+    a = ap.parse_args(argv)
+    if a.issue_json and not os.path.exists(a.issue_json):
+        a.issue_json = None
+    return a
+
+
+def main():
+    args = parse_args()
+    if "WORLD_SIZE" in os.environ:   # launched by torchrun: one rank per process already
+        world = int(os.environ["WORLD_SIZE"])
+        if world != args.gpus:
+            raise SystemExit(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}")
+        run_rank(args, int(os.environ.get("RANK", "0")), world, int(os.environ.get("LOCAL_RANK", "0")))
+        return
+    if args.gpus < 1:
+        raise SystemExit("--gpus must be >= 1")
+    if args.gpus == 1:
+        run_rank(args, 0, 1, 0)
+        return
+    visible = torch.cuda.device_count()   # counts devices without initialising HIP in this process
+    if args.gpus > visible:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but only {visible} GPU(s) visible")
+    import torch.multiprocessing as mp
+    mp.spawn(_spawned, args=(args, args.gpus, _free_port()), nprocs=args.gpus, join=True)
 
 
 if __name__ == "__main__":

@@ -311,7 +311,8 @@ int zc_chess_puct_end(zc_engine *eng, int32_t first_game, int32_t n_games, float
  *   zc_net_planes_to_nhwc_async: state_to_tensor planes [n][cin][h*w] fp16 -> [n][h*w][cpad],
  *     zero padded; cpad a multiple of 8 (16-byte rows), d_out 16-byte aligned.
  *   zc_net_value_head_async: mean over pixels -> dot(fc_w[128]) + fc_b -> tanh, as fp64
- *     values[n] (the input of zc_*_ext_backup).
+ *     values[n] (the input of zc_*_ext_backup).  d_act = [n][hw][128] fp16 (exactly 128
+ *     channels), 16-byte aligned (ZC_EINVAL otherwise).
  * Device pointers, enqueued on hip_stream (NULL = null stream); no engine needed. */
 int zc_net_conv3x3_async(int32_t n_boards, int32_t h, int32_t w, int32_t cin, const void *d_in, const void *d_weight,
                          const float *d_bias, const void *d_residual, void *d_out, int32_t relu, void *hip_stream);
@@ -323,6 +324,57 @@ int zc_net_planes_to_nhwc_async(int32_t n, int32_t cin, int32_t hw, int32_t cpad
                                 void *hip_stream);
 int zc_net_value_head_async(int32_t n, int32_t hw, const void *d_act, const float *d_fc_w, float fc_b, double *d_values,
                             void *hip_stream);
+
+/* ---- self-play trajectories on the device ---------------------------
+ * Replaces the host half of self-play data collection: Engine.play_move's history append
+ * (engine/engine.py:98-108), Engine.get_dataset's labels (:60-89: factor 0 for a draw else
+ * -1, alternating, the game's list reversed) and scripts/train.py:simulate_games's refill
+ * and quota (:151-170: a slot starts a new game only while fewer than `quota` games have
+ * started).  The caller owns every buffer (device memory):
+ *   d_hist     [n][max_len] rows    the slot's current game, opening first
+ *   d_hmoves   [n][max_len] int16   move played from each of those positions
+ *   d_slot     [n][4] int32         {positions so far, game number (-1 = idle), scratch x2}
+ *   d_pool     [pool_cap] rows      finished games' positions, game after game (pool_cap < 2^31)
+ *   d_labels   [pool_cap] int32     get_dataset label of each pooled position
+ *   d_pool_moves [pool_cap] int16   move played from it (-1 at the game's last position)
+ *   d_games    [games_cap][4] int64 {game number, slot << 32 | (result + 1), first pooled
+ *                                    position, positions}
+ *   d_ctl      [8] int64            ZC_TRAJ_* counters below
+ *   d_init     one row              the opening (create_init_state)
+ * Rows are opaque records of row_bytes (a multiple of 8): a zc_c4_state is 24 bytes, a
+ * zc_chess_state 72.  Games land in the pool in completion order (atomics); the game
+ * records give each game's place. */
+typedef struct zc_traj_buffers {
+    int32_t row_bytes, max_len;
+    int64_t pool_cap;
+    int32_t games_cap, reserved;
+    void *d_hist;
+    int16_t *d_hmoves;
+    int32_t *d_slot;
+    void *d_pool;
+    int32_t *d_labels;
+    int16_t *d_pool_moves;
+    int64_t *d_games;
+    int64_t *d_ctl;
+    const void *d_init;
+} zc_traj_buffers;
+#define ZC_TRAJ_POSITIONS 0  /* pool positions reserved                                */
+#define ZC_TRAJ_GAMES 1      /* game records reserved                                  */
+#define ZC_TRAJ_NEXT 2       /* game number the next refill takes                      */
+#define ZC_TRAJ_QUOTA 3      /* games to start in total (simulate_games' total_games)  */
+#define ZC_TRAJ_FINISHED 4   /* games finished                                         */
+#define ZC_TRAJ_OVERFLOW 5   /* bit 0: pool full (games dropped); bit 1: a game longer than max_len */
+#define ZC_SLOT_IDLE 3       /* result of an idle slot                                 */
+/* After a move was played on every slot (d_states = positions after the move, d_moves =
+ * the moves, int16: Connect4 column / packed chess move): append each position to its
+ * slot's game; a finished game is copied to the pool and its slot restarts from d_init (the
+ * position in d_states is reset too) or goes idle.  Results: Connect4 passes
+ * d_results from zc_c4_play_async (reset = 0) and d_flags = d_rep = NULL; chess passes
+ * d_flags from zc_chess_terminal_async and d_rep from zc_chess_repetition_async (NULL = no
+ * repetition test) and d_results is written (Engine._evaluate).  Idle slots get
+ * ZC_SLOT_IDLE.  No engine needed; enqueued on hip_stream. */
+int zc_traj_record_async(int32_t n, const zc_traj_buffers *buf, void *d_states, const int16_t *d_moves,
+                         int32_t *d_results, const int32_t *d_flags, const int32_t *d_rep, void *hip_stream);
 
 /* ---- self-test hooks (used by the parity tests) -------------------------------------
  * UCT score exactly as the search kernel computes it (mcts.cpp:41-45), evaluated ON THE

@@ -78,6 +78,41 @@ def test_planes_match_state_to_tensor():
     assert np.array_equal(planes(np.array(rows, dtype=np.int64)), np.stack(tens))
 
 
+def _reference_update_replay(store, states_new, values_new, frac_old=0.30):
+    """scripts/train.py:_update_replay (:27-50), restated (the module-level lists are `store`)."""
+    if not store[0]:
+        store[0].append(states_new)
+        store[1].append(values_new)
+        return states_new, values_new
+    old_states, old_values = np.concatenate(store[0], axis=0), np.concatenate(store[1], axis=0)
+    k = int(frac_old * len(old_states))
+    if k > 0:
+        idx = np.random.choice(len(old_states), k, replace=False)
+        ss, sv = old_states[idx], old_values[idx]
+    else:
+        ss, sv = old_states[:0], old_values[:0]
+    store[0].append(states_new)
+    store[1].append(values_new)
+    return np.concatenate([ss, states_new], axis=0), np.concatenate([sv, values_new], axis=0)
+
+
+def test_replay_buffer_global_numpy_stream_matches_train_py():
+    """Default ReplayBuffer draws with numpy's global generator, as train.py does: after the
+    same np.random.seed, the same training sets — for numpy arrays and torch tensors."""
+    rng = np.random.default_rng(1)
+    batches = [(rng.integers(0, 1 << 40, (n, 3)), rng.integers(-1, 2, n).astype(np.float32)) for n in (40, 17, 33, 8)]
+    store = ([], [])
+    np.random.seed(123)
+    want = [_reference_update_replay(store, s, v) for s, v in batches]
+    for conv in (lambda x: x, torch.from_numpy):
+        rb = ReplayBuffer()
+        np.random.seed(123)
+        for (s, v), (ws, wv) in zip(batches, want):
+            gs, gv = rb.update(conv(s), conv(v))
+            gs, gv = (gs.numpy(), gv.numpy()) if torch.is_tensor(gs) else (gs, gv)
+            assert np.array_equal(gs, ws) and np.array_equal(gv, wv)
+
+
 def test_replay_buffer_semantics():
     rb = ReplayBuffer(seed=0)
     s1, v1 = np.arange(10)[:, None], np.arange(10)
@@ -87,3 +122,45 @@ def test_replay_buffer_semantics():
     a, b = rb.update(s2, v2)
     assert len(a) == 3 + 5 and np.array_equal(a[-5:], s2)
     assert len(set(a[:3, 0].tolist())) == 3 and all(x < 10 for x in a[:3, 0])
+
+
+def _bench_worker(rank, world, port, out):
+    import bench
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    # rank r ran (10 + r) expansions ... in (1 + r) s; kernels 2r ms
+    counts, dt, kms = bench.reduce_over_ranks([10 + rank, 20 + rank, rank, 5], 1.0 + rank, 2.0 * rank, "cpu")
+    out[rank] = (counts, dt, kms)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_bench_aggregation_gloo_world2():
+    """bench.py's whole-job reduction: counters summed over ranks, wall and kernel time the
+    max over ranks — the value the driver's N-GPU line reports."""
+    world, port = 2, _free_port()
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_bench_worker, args=(world, port, out), nprocs=world, join=True)
+    for r in range(world):
+        assert out[r] == ([21, 41, 1, 10], 2.0, 2.0)
+
+
+def test_bench_rank_ranges_and_launcher_errors():
+    import subprocess
+    import sys
+
+    import bench
+    assert bench.rank_ranges(2, 4096) == [[0, 4095], [4096, 8191]]
+    assert bench.rank_ranges(8, 4096)[7] == [7 * 4096, 8 * 4096 - 1]
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    # more GPUs than visible: a clear error before any GPU work (no GPU in this container)
+    p = subprocess.run([sys.executable, "bench.py", "--gpus", "2"], cwd=repo, env=env, capture_output=True, text=True,
+                       timeout=300)
+    assert p.returncode != 0 and "GPU(s) visible" in p.stderr
+    # under torchrun the world size must match --gpus
+    p = subprocess.run([sys.executable, "bench.py", "--gpus", "4"], cwd=repo, env={**env, "WORLD_SIZE": "2"},
+                       capture_output=True, text=True, timeout=300)
+    assert p.returncode != 0 and "WORLD_SIZE=2 but --gpus 4" in p.stderr

@@ -44,6 +44,18 @@ class EngineConfig(ctypes.Structure):
                 ("max_batch", ctypes.c_int32)]
 
 
+class TrajBuffers(ctypes.Structure):
+    """zc_traj_buffers (include/zeroclone.h): device pointers of a self-play trajectory pool."""
+    _fields_ = [("row_bytes", ctypes.c_int32), ("max_len", ctypes.c_int32), ("pool_cap", ctypes.c_int64),
+                ("games_cap", ctypes.c_int32), ("reserved", ctypes.c_int32), ("d_hist", ctypes.c_void_p),
+                ("d_hmoves", ctypes.c_void_p), ("d_slot", ctypes.c_void_p), ("d_pool", ctypes.c_void_p),
+                ("d_labels", ctypes.c_void_p), ("d_pool_moves", ctypes.c_void_p), ("d_games", ctypes.c_void_p),
+                ("d_ctl", ctypes.c_void_p), ("d_init", ctypes.c_void_p)]
+
+
+ZC_TRAJ_POSITIONS, ZC_TRAJ_GAMES, ZC_TRAJ_NEXT, ZC_TRAJ_QUOTA, ZC_TRAJ_FINISHED, ZC_TRAJ_OVERFLOW = range(6)
+ZC_SLOT_IDLE = 3
+
 C4_STATE_DTYPE = np.dtype([("stones", "<u8", (2,)), ("turn", "<i4"), ("reserved", "<i4")])
 STATS_DTYPE = np.dtype([("expansions", "<i8"), ("depth_sum", "<i8"), ("leaves", "<i8"),
                         ("rollout_plies", "<i8"), ("rng_words", "<i8"), ("status", "<i8"),
@@ -143,6 +155,8 @@ SIGNATURES = [
                                                    ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     ("zc_net_value_head_async", ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p,
                                                ctypes.c_float, ctypes.c_void_p, ctypes.c_void_p]),
+    ("zc_traj_record_async", ctypes.c_int, [ctypes.c_int32, P(TrajBuffers), ctypes.c_void_p, ctypes.c_void_p,
+                                            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     ("zc_chess_from_fen", ctypes.c_int, [ctypes.c_char_p, ctypes.c_void_p]),
     ("zc_chess_init", ctypes.c_int, [ctypes.c_void_p]),
     ("zc_c4_from_rows", ctypes.c_int, [ctypes.c_char_p, ctypes.c_int32, P(C4State)]),

@@ -543,6 +543,25 @@ int zc_chess_repetition_async(int32_t n, int32_t cap, const uint16_t *d_hist, co
     return ZC_OK;
 }
 
+int zc_traj_record_async(int32_t n, const zc_traj_buffers *buf, void *d_states, const int16_t *d_moves,
+                         int32_t *d_results, const int32_t *d_flags, const int32_t *d_rep, void *hip_stream) {
+    if (n < 0 || !buf) return fail(ZC_EINVAL, "bad argument");
+    const zc_traj_buffers &b = *buf;
+    if (b.row_bytes < 8 || (b.row_bytes & 7) || b.max_len < 2 || b.pool_cap < 0 || b.pool_cap > INT32_MAX ||
+        b.games_cap < 0)
+        return fail(ZC_EINVAL, "bad trajectory buffer shape (row_bytes %d, max_len %d)", b.row_bytes, b.max_len);
+    if (!b.d_hist || !b.d_hmoves || !b.d_slot || !b.d_pool || !b.d_labels || !b.d_pool_moves || !b.d_games ||
+        !b.d_ctl || !b.d_init)
+        return fail(ZC_EINVAL, "null trajectory buffer");
+    if (((uintptr_t)b.d_hist | (uintptr_t)b.d_pool | (uintptr_t)b.d_init | (uintptr_t)d_states) & 7)
+        return fail(ZC_EINVAL, "rows must be 8-byte aligned");
+    if (n && (!d_states || !d_moves || !d_results)) return fail(ZC_EINVAL, "bad argument");
+    if (!n) return ZC_OK;
+    zc::launch_traj_record(n, b, d_states, d_moves, d_results, d_flags, d_rep, (hipStream_t)hip_stream);
+    ZC_HIP(hipGetLastError());
+    return ZC_OK;
+}
+
 int zc_chess_planes_async(zc_engine *eng, int32_t n, const zc_chess_state *d_states, void *d_planes,
                           int32_t planes_dtype, void *hip_stream) {
     if (planes_dtype != ZC_F32 && planes_dtype != ZC_F16) return fail(ZC_EINVAL, "planes_dtype must be ZC_F32 or ZC_F16");
@@ -887,6 +906,8 @@ int zc_net_planes_to_nhwc_async(int32_t n, int32_t cin, int32_t hw, int32_t cpad
 int zc_net_value_head_async(int32_t n, int32_t hw, const void *d_act, const float *d_fc_w, float fc_b,
                             double *d_values, void *hip_stream) {
     if (n < 0 || hw < 1 || (n && (!d_act || !d_fc_w || !d_values))) return fail(ZC_EINVAL, "bad argument");
+    // the head reads whole 256-byte pixel rows (128 fp16 channels) in 16-byte pieces
+    if ((uintptr_t)d_act & 15) return fail(ZC_EINVAL, "d_act must be 16-byte aligned (128-channel fp16 NHWC rows)");
     if (!n) return ZC_OK;
     zc::launch_net_value_head(n, hw, d_act, d_fc_w, fc_b, d_values, (hipStream_t)hip_stream);
     ZC_HIP(hipGetLastError());

@@ -205,6 +205,10 @@ void launch_c4_rollout_debug(const Arena &a, int M, int first_game, int n, const
 void launch_c4_rollout_seq(const Arena &a, int game, int n, const zc_c4_state *states, int32_t *out_value,
                            int64_t *out_words, hipStream_t s);
 void launch_c4_play(int n, zc_c4_state *states, const int32_t *moves, int32_t *results, int reset, hipStream_t s);
+enum : int { kTrajPositions = ZC_TRAJ_POSITIONS, kTrajGames = ZC_TRAJ_GAMES, kTrajNext = ZC_TRAJ_NEXT,
+             kTrajQuota = ZC_TRAJ_QUOTA, kTrajFinished = ZC_TRAJ_FINISHED, kTrajOverflow = ZC_TRAJ_OVERFLOW };
+void launch_traj_record(int n, const zc_traj_buffers &b, void *states, const int16_t *moves, int32_t *results,
+                        const int32_t *flags, const int32_t *rep, hipStream_t s);
 void launch_uct_debug(int n, const double *logn, const int32_t *na, const double *q, double c, double *out,
                       hipStream_t s);
 

@@ -11,8 +11,9 @@ select and backup kernels.  Called directly, `Value` behaves as the reference's:
 * `crude_chess_score` (:48-55): 1000 if check_win(state), else (turn*-2+1) * material.
 * `network_latest` / `network_at_path` (:61-130): the reference's ValueNetwork template
   (zeroclone_amd.nets) for `model_type` (chess_value: 17 planes; connect4: 2 planes), in fp16
-  on the GPU; weights from `path` / models/<model_type>/latest.pth when present (state_dict,
-  loaded with weights_only=True), else the random init, as the reference.
+  on the GPU; weights from `path` / <models_dir>/<model_type>/latest.pth when present (the
+  reference's whole-module pickle or a state_dict, loaded with weights_only=True through the
+  reference's allowlist mapped onto this package's classes), else the random init.
 """
 from __future__ import annotations
 
@@ -75,14 +76,10 @@ class Value:
     # ---------------------------------------------------------------- network modes
     def _init_network(self):
         import torch
-        from ..nets import ValueNetwork, for_inference
+        from ..nets import for_inference
         mt = self.init_args.get("model_type", "chess_value")
-        net = ValueNetwork(in_planes=MODEL_PLANES.get(mt, 17))
-        path = self.init_args.get("path") if self.name == "network_at_path" else \
-            os.path.join("models", mt, "latest.pth")
-        if path and os.path.exists(path):
-            sd = torch.load(path, map_location="cpu", weights_only=True)
-            net.load_state_dict(sd.state_dict() if hasattr(sd, "state_dict") else sd)
+        path = self.init_args.get("path") if self.name == "network_at_path" else latest_path(mt, self.init_args)
+        net = load_value_network(path, mt)
         self.zc_model = for_inference(net.eval(), "cuda", torch.float16)
         self.batch_size = self.init_args.get("batch_size", 1)
 
@@ -97,6 +94,56 @@ class Value:
 
     network_latest = _network
     network_at_path = _network
+
+
+def models_dir(init_args=None) -> str:
+    """Where `network_latest` looks for <model_type>/latest.pth.  The reference resolves it
+    next to its models package (models/core.py:10-13); here: the `models_dir` value arg, else
+    $ZC_MODELS_DIR, else zeroclone_amd/models (the package's own models directory)."""
+    d = (init_args or {}).get("models_dir") or os.environ.get("ZC_MODELS_DIR")
+    return d or os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "models")
+
+
+def latest_path(model_type: str, init_args=None) -> str:
+    return os.path.join(models_dir(init_args), model_type, "latest.pth")
+
+
+def _reference_safe_globals():
+    """The allowlist the reference registers before loading (models/chess_value/network.py:
+    add_safe_globals), with the reference's own classes mapped by qualified name to this
+    package's mirror classes: a checkpoint written by scripts/train.py:143 (torch.save of the
+    whole module) then loads with weights_only=True — nothing in the file is executed."""
+    import torch.nn as nn
+    from .. import nets
+    ref = "models.{}.network"
+    out = [nn.Conv2d, nn.BatchNorm2d, nn.ReLU, nn.AdaptiveAvgPool2d, nn.Linear, nn.Tanh, nn.Sequential, nn.Flatten,
+           nets.ValueNetwork, nets.ResidualBlock]
+    for mt in MODEL_PLANES:
+        out += [(nets.ValueNetwork, ref.format(mt) + ".ValueNetwork"),
+                (nets.ResidualBlock, ref.format(mt) + ".ResidualBlock")]
+    return out
+
+
+def load_value_network(path, model_type: str = "chess_value"):
+    """value_functions.py:init_network_latest / init_network_at_path (:101-130): the model at
+    `path` when it exists, else a random-init ValueNetwork.  Accepts both a whole pickled
+    module (the reference's format) and a plain state_dict; always weights_only=True.
+    Returns an fp32 CPU `nets.ValueNetwork` whose width and depth are the checkpoint's."""
+    import torch
+    from ..nets import ValueNetwork
+    planes = MODEL_PLANES.get(model_type, 17)
+    if not path or not os.path.exists(path):
+        return ValueNetwork(in_planes=planes)
+    with torch.serialization.safe_globals(_reference_safe_globals()):
+        obj = torch.load(path, map_location="cpu", weights_only=True)
+    sd = obj.state_dict() if isinstance(obj, torch.nn.Module) else obj
+    if not isinstance(sd, dict) or "stem.0.weight" not in sd:
+        raise ValueError(f"{path}: not a ValueNetwork checkpoint (no stem.0.weight)")
+    channels, in_planes = int(sd["stem.0.weight"].shape[0]), int(sd["stem.0.weight"].shape[1])
+    blocks = len({k.split(".")[1] for k in sd if k.startswith("res.")})
+    net = ValueNetwork(channels, blocks, in_planes=in_planes)
+    net.load_state_dict(sd)
+    return net
 
 
 def _looks_like_c4(backend, states):

@@ -1,21 +1,26 @@
-"""Device-resident Connect4 self-play and the multi-GPU trajectory exchange.
+"""Device-resident self-play, its trajectories, and the multi-GPU trajectory exchange.
 
-`C4SelfPlay` is the batched form of scripts/train.py:simulate_games (:151-170) +
-Engine.play_mcts_parallel (engine/engine.py:131-138): G games live on one GPU as bitboards;
-one `step()` searches every game (zc_c4_search_async), plays the chosen moves and
-evaluates them (zc_c4_play_async, Engine.play_move/_evaluate), and restarts finished games
-from the opening — the refill the reference does with add_game.  Game slot g of rank r is
-global game r*G + g and draws from its own CPython MT19937 stream seeded seed + global id,
-so per-game results do not depend on the number of GPUs.
+`C4SelfPlay` / `ChessSelfPlay` are the batched form of scripts/train.py:simulate_games
+(:151-170) + Engine.play_mcts_parallel (engine/engine.py:131-138): G games live on one GPU;
+one `step()` searches every game, plays the chosen moves and evaluates them
+(Engine.play_move/_evaluate) on the device.  Game slot g of rank r is global slot r*G + g
+and draws from its own CPython MT19937 stream seeded seed + global slot id, so per-game
+results do not depend on the number of GPUs.
 
-Finished games are labelled exactly as Engine.get_dataset (engine.py:60-89) labels them and
-kept as compact positions (zc_c4_state rows: stones X, stones O, turn | label << 32).
-`gather_positions` all-gathers every rank's finished positions (counts first, then a padded
+Trajectories never leave the device while games are played (`Trajectories`,
+zc_traj_record_async): every position is appended to its slot's game in HBM; a finished game
+is labelled exactly as Engine.get_dataset (engine.py:60-89) labels it and copied to a
+device pool, and its slot restarts from the opening (or goes idle once simulate_games'
+quota of games has started).  `take()` returns the pool's games in start order as device
+tensors; `gather_positions` all-gathers every rank's positions (counts first, then a padded
 payload) over torch.distributed — RCCL over xGMI on the GPUs, gloo on CPU — the one
-collective of the scale-out path.  `ReplayBuffer` is
-scripts/train.py:_update_replay (:27-50).
+collective of the scale-out path; `ReplayBuffer` is
+scripts/train.py:_update_replay (:27-50) over device tensors.
 """
 from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
 
 import numpy as np
 import torch
@@ -23,6 +28,8 @@ import torch
 from . import _native
 
 ONGOING = _native.ZC_C4_ONGOING
+IDLE = _native.ZC_SLOT_IDLE
+_UNLIMITED = 1 << 62
 
 
 def dataset_labels(n_states: int, result: int) -> np.ndarray:
@@ -54,93 +61,220 @@ def planes(positions: np.ndarray) -> np.ndarray:
     return out
 
 
+@dataclass
+class TrajBatch:
+    """Finished games taken from a `Trajectories` pool, in start order (device tensors).
+
+    rows   [n, row_bytes // 8] int64  positions (zc_c4_state / zc_chess_state records)
+    labels [n] int32                  Engine.get_dataset label of each position
+    moves  [n] int16                  move played from it (-1 at a game's last position)
+    games  [k, 5] int64               game number, slot, result, first row, positions
+    """
+    rows: torch.Tensor
+    labels: torch.Tensor
+    moves: torch.Tensor
+    games: torch.Tensor
+
+    def results(self) -> list[int]:
+        return [int(r) for r in self.games[:, 2].cpu().tolist()]
+
+
+class Trajectories:
+    """Per-slot game histories and the pool of finished games, all in HBM (zc_traj_record_async).
+
+    `max_len` positions per game (Connect4: 43), room for `games_cap` finished games and
+    `pool_cap` positions until the next `take()`."""
+
+    def __init__(self, n_slots: int, init_row: torch.Tensor, max_len: int, games_cap: int, pool_cap: int,
+                 device: torch.device):
+        init = init_row.reshape(-1).contiguous().view(torch.uint8)
+        if init.numel() % 8:
+            raise ValueError("row size must be a multiple of 8 bytes")
+        self.n, self.W, self.max_len, self.dev = n_slots, init.numel() // 8, max_len, device
+        self.init = init.view(torch.int64).to(device).clone()
+        self.hist = torch.zeros((n_slots, max_len, self.W), dtype=torch.int64, device=device)
+        self.hmoves = torch.zeros((n_slots, max_len), dtype=torch.int16, device=device)
+        self.slot = torch.zeros((n_slots, 4), dtype=torch.int32, device=device)
+        self.ctl = torch.zeros(8, dtype=torch.int64, device=device)
+        self._alloc_pool(games_cap, pool_cap)
+        self.start(None)
+
+    def _alloc_pool(self, games_cap: int, pool_cap: int):
+        self.games_cap, self.pool_cap = int(games_cap), int(pool_cap)
+        self.pool = torch.zeros((self.pool_cap, self.W), dtype=torch.int64, device=self.dev)
+        self.labels = torch.zeros(self.pool_cap, dtype=torch.int32, device=self.dev)
+        self.pool_moves = torch.zeros(self.pool_cap, dtype=torch.int16, device=self.dev)
+        self.games = torch.zeros((self.games_cap, 4), dtype=torch.int64, device=self.dev)
+        b = _native.TrajBuffers()
+        b.row_bytes, b.max_len, b.pool_cap, b.games_cap = 8 * self.W, self.max_len, self.pool_cap, self.games_cap
+        for f, t in (("d_hist", self.hist), ("d_hmoves", self.hmoves), ("d_slot", self.slot), ("d_pool", self.pool),
+                     ("d_labels", self.labels), ("d_pool_moves", self.pool_moves), ("d_games", self.games),
+                     ("d_ctl", self.ctl), ("d_init", self.init)):
+            setattr(b, f, t.data_ptr())
+        self._buf = b
+
+    def start(self, quota: int | None, games_cap: int | None = None):
+        """Slot g plays game g (g < quota) or idles; the pool is emptied.  quota None = no
+        limit (every finished game's slot starts another)."""
+        q = _UNLIMITED if quota is None else int(quota)
+        if games_cap is not None and games_cap > self.games_cap:
+            self._alloc_pool(games_cap, games_cap * self.max_len)
+        ids = torch.arange(self.n, dtype=torch.int32, device=self.dev)
+        self.slot.zero_()
+        self.slot[:, 0] = 1
+        self.slot[:, 1] = torch.where(ids < min(q, self.n), ids, torch.full_like(ids, -1))
+        self.hist[:, 0] = self.init
+        self.ctl.zero_()
+        self.ctl[_native.ZC_TRAJ_NEXT] = min(q, self.n)
+        self.ctl[_native.ZC_TRAJ_QUOTA] = q
+
+    def record(self, d_states: int, moves: torch.Tensor, results: torch.Tensor, flags: torch.Tensor | None = None,
+               rep: torch.Tensor | None = None, stream: int = 0):
+        _native.check(_native.lib().zc_traj_record_async(
+            self.n, ctypes.byref(self._buf), ctypes.c_void_p(d_states), ctypes.c_void_p(moves.data_ptr()),
+            ctypes.c_void_p(results.data_ptr()), ctypes.c_void_p(flags.data_ptr() if flags is not None else None),
+            ctypes.c_void_p(rep.data_ptr() if rep is not None else None), ctypes.c_void_p(stream or None)))
+
+    def finished(self) -> int:
+        """Games finished since start() (one device read)."""
+        return int(self.ctl[_native.ZC_TRAJ_FINISHED].item())
+
+    def take(self) -> TrajBatch:
+        """The pooled games, sorted by game number (start order), as device tensors; the pool
+        is emptied (slots keep their games in progress)."""
+        ctl = self.ctl.cpu().tolist()
+        if ctl[_native.ZC_TRAJ_OVERFLOW]:
+            raise RuntimeError("trajectory pool overflow: " + ("pool full (take() more often or raise games_cap) "
+                                                               if ctl[_native.ZC_TRAJ_OVERFLOW] & 1 else "")
+                               + ("a game longer than max_len" if ctl[_native.ZC_TRAJ_OVERFLOW] & 2 else ""))
+        k, n = int(ctl[_native.ZC_TRAJ_GAMES]), int(ctl[_native.ZC_TRAJ_POSITIONS])
+        g = self.games[:k]
+        order = torch.argsort(g[:, 0])
+        g = g[order]
+        lens = g[:, 3]
+        starts = torch.cumsum(lens, 0) - lens
+        idx = torch.repeat_interleave(g[:, 2] - starts, lens, output_size=n) + torch.arange(n, device=self.dev)
+        games = torch.stack([g[:, 0], g[:, 1] >> 32, (g[:, 1] & 0xFFFFFFFF) - 1, starts, lens], dim=1)
+        out = TrajBatch(self.pool[idx].clone(), self.labels[idx].clone(), self.pool_moves[idx].clone(), games)
+        self.ctl[_native.ZC_TRAJ_POSITIONS] = 0
+        self.ctl[_native.ZC_TRAJ_GAMES] = 0
+        return out
+
+
 class C4SelfPlay:
+    """Connect4 self-play pool on one GPU: search (zc_c4_search_async) + play/evaluate
+    (zc_c4_play_async) + trajectory recording (zc_traj_record_async), all stream-ordered,
+    no host synchronisation per step."""
+
+    MAX_LEN = 43   # the opening + at most 42 moves
+
     def __init__(self, games: int, sims: int, c: float = 1.4, batch_size: int = 32, seed: int = 0,
-                 rank: int = 0, device: int = 0, record: bool = True):
+                 rank: int = 0, device: int = 0, record: bool = True, games_cap: int | None = None):
         self.G, self.sims, self.c, self.bs = games, sims, c, batch_size
-        self.dev = torch.device("cuda", device)
-        self.eng = _native.NativeEngine(max_games=games, max_sims=sims, max_batch=batch_size, device=device)
+        self.dev = torch.device("cuda", device) if isinstance(device, int) else torch.device(device)
+        self.eng = _native.NativeEngine(max_games=games, max_sims=sims, max_batch=batch_size,
+                                        device=self.dev.index or 0)
         self.first_id = rank * games
         self.eng.seed(0, [seed + self.first_id + g for g in range(games)])
         self.roots = torch.zeros((games, 3), dtype=torch.int64, device=self.dev)
         self.moves = torch.zeros(games, dtype=torch.int32, device=self.dev)
+        self.moves16 = torch.zeros(games, dtype=torch.int16, device=self.dev)
         self.na = torch.zeros((games, 7), dtype=torch.int32, device=self.dev)
         self.stats = torch.zeros((games, _native.STATS_FIELDS), dtype=torch.int64, device=self.dev)
         self.results = torch.zeros(games, dtype=torch.int32, device=self.dev)
         self.record = record
-        # current game of every slot: positions so far (host copies, appended per step)
-        self._hist = [[] for _ in range(games)]
-        self.finished = []   # (global game id, move list, result, positions[n,3])
-        self._moves = [[] for _ in range(games)]
+        self.traj = None
+        if record:
+            cap = games_cap or max(8 * games, 1024)
+            self.traj = Trajectories(games, torch.zeros(24, dtype=torch.uint8), self.MAX_LEN, cap,
+                                     cap * self.MAX_LEN, self.dev)
 
-    def step(self) -> torch.Tensor:
-        """One move for every game (on torch's current stream); returns the per-game results
-        tensor (ONGOING = 2).  Finished games restart from the opening."""
-        s = torch.cuda.current_stream(self.dev).cuda_stream
-        before = self.roots.clone() if self.record else None
+    def start(self, quota: int | None = None):
+        """Every slot back to the opening; with a quota, slots beyond it idle and finished
+        slots start new games only while fewer than `quota` have started."""
+        self.roots.zero_()
+        if self.traj is not None:
+            self.traj.start(quota, games_cap=quota)
+
+    def step(self, stream: int | None = None) -> torch.Tensor:
+        """One move for every game (on torch's current stream unless given); returns the
+        per-game results tensor (ONGOING = 2, IDLE = 3).  Finished games restart from the
+        opening."""
+        self.step_search(stream)
+        return self.step_finish(stream)
+
+    def step_search(self, stream: int | None = None) -> torch.Tensor:
+        """The search half of a step (zc_c4_search_async); returns the results tensor the
+        finish half will fill."""
+        s = stream if stream is not None else torch.cuda.current_stream(self.dev).cuda_stream
         self.eng.c4_search_async(self.roots.data_ptr(), self.G, self.sims, self.c, self.bs, self.moves.data_ptr(),
                                  self.na.data_ptr(), self.stats.data_ptr(), stream=s)
-        self.eng.c4_play_async(self.roots.data_ptr(), self.G, self.moves.data_ptr(), self.results.data_ptr(),
-                               reset=False, stream=s)
-        if self.record:
-            self._collect(before)
-        else:
-            self._refill()
         return self.results
 
-    def _refill(self):
-        done = self.results != ONGOING
-        self.roots[done] = 0
+    def step_finish(self, stream: int | None = None) -> torch.Tensor:
+        """Play + evaluate the searched moves, record the positions, refill finished games."""
+        s = stream if stream is not None else torch.cuda.current_stream(self.dev).cuda_stream
+        self.eng.c4_play_async(self.roots.data_ptr(), self.G, self.moves.data_ptr(), self.results.data_ptr(),
+                               reset=not self.record, stream=s)
+        if self.record:
+            self.moves16.copy_(self.moves)
+            self.traj.record(self.roots.data_ptr(), self.moves16, self.results, stream=s)
+        return self.results
 
-    def _collect(self, before: torch.Tensor):
-        pre = before.cpu().numpy()
-        post = self.roots.cpu().numpy()
-        res = self.results.cpu().numpy()
-        mv = self.moves.cpu().numpy()
-        for g in range(self.G):
-            if not self._hist[g]:
-                self._hist[g].append(pre[g].copy())
-            self._moves[g].append(int(mv[g]))
-            self._hist[g].append(post[g].copy())
-            if res[g] != ONGOING:
-                pos = np.stack(self._hist[g]).astype(np.int64)
-                lab = dataset_labels(len(pos), int(res[g]))
-                pos[:, 2] = (pos[:, 2] & 1) | (lab.astype(np.int64) << 32)
-                self.finished.append((self.first_id + g, self._moves[g], int(res[g]), pos))
-                self._hist[g], self._moves[g] = [], []
-        self._refill()
+    def take(self) -> TrajBatch:
+        return self.traj.take()
 
-    def take_positions(self):
-        """Positions of the games finished since the last call: [n, 3] int64 rows with the
-        Engine.get_dataset label in the high half of column 2."""
-        rows = [f[3] for f in self.finished]
-        self.finished = []
-        return np.concatenate(rows) if rows else np.zeros((0, 3), np.int64)
+    def take_positions(self) -> torch.Tensor:
+        """Positions of the games finished since the last take, in start order: [n, 3] int64
+        device rows (stones X, stones O, turn | Engine.get_dataset label << 32)."""
+        b = self.take()
+        rows = b.rows.clone()
+        rows[:, 2] = (rows[:, 2] & 1) | (b.labels.to(torch.int64) << 32)
+        return rows
+
+    def finished_games(self, batch: TrajBatch | None = None):
+        """Host view of taken games (tests / inspection): (global slot id, moves, result,
+        positions [n, 3] with labels) per game, in start order."""
+        b = batch if batch is not None else self.take()
+        return _host_games(b, self.first_id, lambda m: int(m))
 
     def close(self):
         self.eng.close()
+
+
+def _host_games(b: TrajBatch, first_id: int, move_fn):
+    rows, labels, moves = b.rows.cpu().numpy(), b.labels.cpu().numpy(), b.moves.cpu().numpy()
+    out = []
+    for gno, slot, res, off, n in b.games.cpu().numpy().tolist():
+        pos = rows[off:off + n].copy()
+        if pos.shape[1] == 3:
+            pos[:, 2] = (pos[:, 2] & 1) | (labels[off:off + n].astype(np.int64) << 32)
+        out.append((first_id + slot, [move_fn(m) for m in moves[off:off + n - 1]], res, pos))
+    return out
 
 
 class ChessSelfPlay:
     """Device-resident chess self-play: the chess form of `C4SelfPlay`.  G games live on one
     GPU as zc_chess_state rows; one `step()` searches every game (Value('crude_chess_score')
     in the search kernel, or a value network between the stepwise select and backup
-    kernels), plays the chosen moves (zc_chess_play_async) and tests the new positions
-    (zc_chess_terminal_async: check_win, stalemate, fifty-move rule) on the device, and
-    restarts finished games from the initial position.  The repetition half of check_draw
-    (chess_backend.cpp:416-441: both sides' move histories end in >= 3 repeats of a block of
-    >= 2 moves) runs on the device too: each side's moves are appended to a per-game history
-    on the GPU and zc_chess_repetition_async tests both after every step.  Results follow Engine._evaluate (engine.py:148-153): check_win -> turn*2-1
-    of the position after the move, a draw -> 0.  Game slot g of rank r is global game r*G+g
-    with its own CPython MT19937 stream seeded seed + global id, as in C4SelfPlay."""
+    kernels), plays the chosen moves (zc_chess_play_async), tests the new positions
+    (zc_chess_terminal_async: check_win, stalemate, fifty-move rule) and both sides' move
+    histories (zc_chess_repetition_async: the repetition half of check_draw,
+    chess_backend.cpp:416-441) on the device, and records the games (zc_traj_record_async:
+    results by Engine._evaluate, engine.py:148-153; finished games restart from the initial
+    position).  Nothing is read back per step; errors (a game longer than the history
+    capacity, a search out of tree capacity, no move at a live root) are collected on the
+    device and raised by `check()` / `take()`."""
 
     def __init__(self, games: int, sims: int, c: float = 1.4, batch_size: int = 32, seed: int = 0,
                  rank: int = 0, device: int = 0, policy: int = _native.ZC_POLICY_IMMEDIATE_VALUE,
-                 freedom: float = 3.0, net=None, init_fen: str | None = None):
+                 freedom: float = 3.0, net=None, init_fen: str | None = None, games_cap: int | None = None,
+                 hist_cap: int = 1024):
         self.G, self.sims, self.c, self.bs = games, sims, c, batch_size
         self.policy, self.freedom = int(policy), float(freedom)
-        self.dev = torch.device("cuda", device)
-        self.eng = _native.NativeEngine(max_games=games, max_sims=sims, max_batch=batch_size, device=device)
+        self.dev = torch.device("cuda", device) if isinstance(device, int) else torch.device(device)
+        self.eng = _native.NativeEngine(max_games=games, max_sims=sims, max_batch=batch_size,
+                                        device=self.dev.index or 0)
         self.eng.chess_reserve()
         self.first_id = rank * games
         self.eng.seed(0, [seed + self.first_id + g for g in range(games)])
@@ -152,26 +286,34 @@ class ChessSelfPlay:
         self.na = torch.zeros((games, _native.CHESS_MAX_MOVES), dtype=torch.int32, device=self.dev)
         self.stats = torch.zeros((games, _native.STATS_FIELDS), dtype=torch.int64, device=self.dev)
         self.flags = torch.zeros(games, dtype=torch.int32, device=self.dev)
+        self.results = torch.zeros(games, dtype=torch.int32, device=self.dev)
         self.vs = self.value_fn = None
         if net is not None:
             from .valued import ChessValuedSearch, NetValue
             self.vs = ChessValuedSearch(self.eng, games, batch_size, leaves=False, policy=self.policy,
                                         freedom=self.freedom)
             self.value_fn = NetValue(net)
-        self.hist_cap = 1024  # moves per side; a longer game raises
+        self.hist_cap = hist_cap  # moves per side
         self.hist = torch.zeros((games, 2, self.hist_cap), dtype=torch.int16, device=self.dev)
         self.hlen = torch.zeros((games, 2), dtype=torch.int32, device=self.dev)
         self.turn = torch.full((games,), self.init_turn, dtype=torch.int64, device=self.dev)
         self.rep = torch.zeros(games, dtype=torch.int32, device=self.dev)
+        self.err = torch.zeros(3, dtype=torch.int32, device=self.dev)
         self._slots = torch.arange(games, device=self.dev)
-        self._turn = [self.init_turn] * games
-        self._moves = [[] for _ in range(games)]
-        self.finished = []   # (global game id, move list, result)
+        max_len = 2 * self.hist_cap + 1
+        cap = games_cap or max(8 * games, 1024)
+        self.traj = Trajectories(games, self.init_row[0], max_len, cap, cap * 160, self.dev)
 
-    def step(self) -> np.ndarray:
-        """One move for every game; returns the per-game results (ONGOING = 2).  Finished
-        games restart from the initial position."""
-        s = torch.cuda.current_stream(self.dev).cuda_stream
+    def start(self, quota: int | None = None):
+        self.roots.copy_(self.init_row.expand_as(self.roots))
+        self.hlen.zero_()
+        self.turn.fill_(self.init_turn)
+        self.traj.start(quota, games_cap=quota)
+
+    def step(self, stream: int | None = None) -> torch.Tensor:
+        """One move for every game; returns the per-game results tensor (ONGOING = 2,
+        IDLE = 3).  Finished games restart from the initial position."""
+        s = stream if stream is not None else torch.cuda.current_stream(self.dev).cuda_stream
         if self.vs is None:
             self.eng.chess_search_async(0, self.G, self.roots.data_ptr(), self.sims, self.c, self.bs, self.policy,
                                         self.freedom, self.moves.data_ptr(), self.na.data_ptr(),
@@ -189,60 +331,57 @@ class ChessSelfPlay:
         self.turn ^= 1
         _native.check(_native.lib().zc_chess_repetition_async(self.G, self.hist_cap, self.hist.data_ptr(),
                                                               self.hlen.data_ptr(), self.rep.data_ptr(), s))
-        mv = self.moves.cpu().numpy().view(np.uint16)
-        fl = self.flags.cpu().numpy()
-        rep = self.rep.cpu().numpy()
-        if int(self.hlen.max().item()) > self.hist_cap:
+        self.err[0] |= (self.hlen > self.hist_cap).any().to(torch.int32)
+        self.err[1] |= (self.stats[:, 5] == _native.ZC_STATUS_CAPACITY).any().to(torch.int32)
+        self.err[2] |= (self.moves == -1).any().to(torch.int32)
+        self.traj.record(self.roots.data_ptr(), self.moves, self.results, flags=self.flags, rep=self.rep, stream=s)
+        live = (self.results == ONGOING)
+        self.hlen *= live.to(torch.int32)[:, None]
+        self.turn = torch.where(live, self.turn, torch.full_like(self.turn, self.init_turn))
+        return self.results
+
+    def check(self):
+        e = self.err.cpu().tolist()
+        if e[0]:
             raise RuntimeError(f"a game exceeded {self.hist_cap} moves per side")
-        if (self.stats[:, 5] == _native.ZC_STATUS_CAPACITY).any():
+        if e[1]:
             raise RuntimeError("chess search exceeded the tree's child-slot pool or depth limit")
-        res = np.full(self.G, ONGOING, np.int32)
-        done = []
-        draw_flags = _native.ZC_CHESS_STALEMATE | _native.ZC_CHESS_FIFTY
-        for g in range(self.G):
-            if mv[g] == 0xFFFF:
-                raise RuntimeError(f"game slot {g}: no legal move at a non-terminal root")
-            self._moves[g].append(_native.unpack_chess_move(int(mv[g])))
-            self._turn[g] ^= 1
-            if fl[g] & _native.ZC_CHESS_WIN:
-                res[g] = self._turn[g] * 2 - 1
-            elif fl[g] & draw_flags or rep[g] == 3:
-                res[g] = 0
-            if res[g] != ONGOING:
-                self.finished.append((self.first_id + g, self._moves[g], int(res[g])))
-                self._moves[g] = []
-                self._turn[g] = self.init_turn
-                done.append(g)
-        if done:
-            d = torch.tensor(done, dtype=torch.int64, device=self.dev)
-            self.roots[d] = self.init_row
-            self.hlen[d] = 0
-            self.turn[d] = self.init_turn
-        return res
+        if e[2]:
+            raise RuntimeError("no legal move at a non-terminal root")
+
+    def take(self) -> TrajBatch:
+        self.check()
+        return self.traj.take()
+
+    def finished_games(self, batch: TrajBatch | None = None):
+        """(global slot id, moves ((fr, fc, tr, tc), value), result, rows [n, 9] int64) per
+        game, in start order (host copies)."""
+        b = batch if batch is not None else self.take()
+        return _host_games(b, self.first_id, lambda m: _native.unpack_chess_move(int(m) & 0xFFFF))
 
     def close(self):
         self.eng.close()
 
 
-def simulate_games(pool, total_games: int, max_steps: int | None = None) -> list[int]:
+def simulate_games(pool, total_games: int, max_steps: int | None = None, check_every: int = 4) -> list[int]:
     """scripts/train.py:simulate_games (:151-170) on a device pool (C4SelfPlay or
-    ChessSelfPlay): step every game until `total_games` games have finished; returns their
-    results in completion order (slot order within a step), while their trajectories are in
-    `pool.finished`.  The reference starts min(total, threads) games and adds one per finished
-    game while fewer than `total_games` have started; the pool keeps every slot playing, so
-    games still running when the quota is met are surplus and not counted."""
+    ChessSelfPlay): games 0..min(total, G)-1 start in slots 0.., a finished game's slot starts
+    the next game while fewer than `total_games` have started, and every started game is
+    played to its end.  Returns the results by game number (start order), as the
+    reference's `final` list; the games' trajectories stay in the pool (`pool.take()`)."""
     if total_games < 0:
         raise ValueError("total_games must be >= 0")
-    out: list[int] = []
+    pool.start(total_games)
     steps = 0
-    while len(out) < total_games:
+    while total_games and (steps % check_every or pool.traj.finished() < total_games):
         if max_steps is not None and steps >= max_steps:
-            raise RuntimeError(f"{len(out)} of {total_games} games finished in {max_steps} steps")
-        r = pool.step()
-        r = r.cpu().numpy() if torch.is_tensor(r) else np.asarray(r)
-        out.extend(int(v) for v in r[r != ONGOING])
+            raise RuntimeError(f"{pool.traj.finished()} of {total_games} games finished in {max_steps} steps")
+        pool.step()
         steps += 1
-    return out[:total_games]
+    pool.last_batch = pool.take()
+    res = pool.last_batch.results()
+    assert len(res) == total_games, (len(res), total_games)
+    return res
 
 
 def schedule_hyperparams(cycle: int, *, games_cap: int = 2000, sims_cap: int = 800, init_lr: float = 3e-4,
@@ -257,8 +396,9 @@ def schedule_hyperparams(cycle: int, *, games_cap: int = 2000, sims_cap: int = 8
 
 
 def gather_positions(local: torch.Tensor, group=None) -> torch.Tensor:
-    """All-gather variable-length [n_r, 3] int64 position rows from every rank (rank order):
-    an all_gather of the counts, then of payloads padded to the largest count."""
+    """All-gather variable-length [n_r, ...] position rows from every rank (rank order; e.g.
+    [n, 3] int64 Connect4 rows with labels, or chess rows): an all_gather of the counts,
+    then of payloads padded to the largest count."""
     import torch.distributed as dist
     world = dist.get_world_size(group)
     n = torch.tensor([local.shape[0]], dtype=torch.int64, device=local.device)
@@ -266,7 +406,7 @@ def gather_positions(local: torch.Tensor, group=None) -> torch.Tensor:
     dist.all_gather(counts, n, group=group)
     counts = [int(c.item()) for c in counts]
     m = max(counts) if counts else 0
-    pad = torch.zeros((m, 3), dtype=torch.int64, device=local.device)
+    pad = torch.zeros((m,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
     pad[: local.shape[0]] = local
     bufs = [torch.zeros_like(pad) for _ in range(world)]
     dist.all_gather(bufs, pad, group=group)
@@ -274,27 +414,39 @@ def gather_positions(local: torch.Tensor, group=None) -> torch.Tensor:
 
 
 class ReplayBuffer:
-    """scripts/train.py:_update_replay (:27-50): the training set of a cycle = all new data +
-    a uniform sample (without replacement) of 30 % of everything seen before."""
+    """scripts/train.py:_update_replay (:27-50): the training set of a cycle = a uniform
+    sample (without replacement) of 30 % of everything seen before, then all new data.
+
+    Works on numpy arrays or device tensors (the pooled positions stay on the GPU: the old
+    data is concatenated and indexed on the device).  The sample indices come from numpy's
+    GLOBAL generator, `np.random.choice(len(old), k, replace=False)`, exactly the
+    reference's call — so after the same `np.random.seed` the same rows are drawn; pass
+    `seed` for a private generator instead."""
 
     def __init__(self, frac_old: float = 0.30, seed: int | None = None):
         self.frac_old = frac_old
         self.states, self.values = [], []
-        self.rng = np.random.default_rng(seed)
+        self.rng = np.random.default_rng(seed) if seed is not None else None
 
-    def update(self, states_new: np.ndarray, values_new: np.ndarray):
+    @staticmethod
+    def _cat(xs):
+        return torch.cat(xs, dim=0) if torch.is_tensor(xs[0]) else np.concatenate(xs, axis=0)
+
+    def update(self, states_new, values_new):
         if not self.states:
             self.states.append(states_new)
             self.values.append(values_new)
             return states_new, values_new
-        old_s = np.concatenate(self.states, axis=0)
-        old_v = np.concatenate(self.values, axis=0)
+        old_s, old_v = self._cat(self.states), self._cat(self.values)
         k = int(self.frac_old * len(old_s))
         if k > 0:
-            idx = self.rng.choice(len(old_s), k, replace=False)
+            idx = (self.rng.choice(len(old_s), k, replace=False) if self.rng is not None
+                   else np.random.choice(len(old_s), k, replace=False))
+            if torch.is_tensor(old_s):
+                idx = torch.from_numpy(idx).to(old_s.device)
             ss, sv = old_s[idx], old_v[idx]
         else:
             ss, sv = old_s[:0], old_v[:0]
         self.states.append(states_new)
         self.values.append(values_new)
-        return np.concatenate([ss, states_new], axis=0), np.concatenate([sv, values_new], axis=0)
+        return self._cat([ss, states_new]), self._cat([sv, values_new])
