@@ -386,6 +386,15 @@ int zc_debug_uct(zc_engine *eng, int32_t n, const double *logn, const int32_t *n
 int zc_debug_c4_rollout(zc_engine *eng, int32_t first_game, int32_t n, const zc_c4_state *states,
                         int32_t *out_value, int64_t *out_words);
 
+/* A chess tree after a search (PUCT or UCT), copied to host buffers for the parity tests:
+ * out_nodes = raw 96-byte node records (position, first slot, #moves, #untried, parent,
+ * parent slot index, depth, material, in-check, evaluated), then per child slot the packed
+ * move, prior, Na, Wa and child node (0xFFFF = none); out_counts = {nodes, slots used}.
+ * Synchronises the device. */
+int zc_debug_chess_tree(zc_engine *eng, int32_t game, int32_t max_nodes, int32_t max_slots, void *out_nodes,
+                        uint16_t *out_mv, float *out_prior, int32_t *out_na, double *out_w, uint16_t *out_child,
+                        int32_t *out_counts);
+
 /* Diagnostic phase stamps: returns (into out8, may be NULL) the shader-cycle sums since the
  * previous call, over all games, of {RNG generation, first walk of each flush, resumed
  * walks, expansion + leaf bookkeeping, rollouts, backup, publish, 0}, resets them, and switches

@@ -63,6 +63,11 @@ STATS_DTYPE = np.dtype([("expansions", "<i8"), ("depth_sum", "<i8"), ("leaves", 
 CHESS_STATE_DTYPE = np.dtype([("board", "u1", (64,)), ("turn", "u1"), ("fifty", "u1"), ("castle", "u1"),
                               ("reserved", "u1", (5,))])
 CHESS_MAX_MOVES = 256
+# ChessNode (zc_internal.h): the device tree's node record, as zc_debug_chess_tree copies it
+CHESS_NODE_DTYPE = np.dtype([("st", "u1", (72,)), ("base", "<u4"), ("nmoves", "<u2"), ("nu", "<u2"),
+                             ("parent", "<u2"), ("pact", "<u2"), ("depth", "<u2"), ("material", "<i2"),
+                             ("check", "u1"), ("evaluated", "u1"), ("pad", "u1", (6,))])
+assert CHESS_NODE_DTYPE.itemsize == 96
 ZC_CHESS_WIN, ZC_CHESS_STALEMATE, ZC_CHESS_FIFTY, ZC_CHESS_OVERFLOW = 1, 2, 4, 8
 ZC_POLICY_RANDOM, ZC_POLICY_IMMEDIATE_VALUE = 0, 1
 ZC_STATUS_CAPACITY = 4
@@ -164,6 +169,9 @@ SIGNATURES = [
     ("zc_c4_legal_order", ctypes.c_int, [ctypes.c_int32, P(ctypes.c_int32)]),
     ("zc_debug_uct", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p,
                                     ctypes.c_void_p, ctypes.c_double, ctypes.c_void_p]),
+    ("zc_debug_chess_tree", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                           ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                           ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     ("zc_debug_phase_cycles", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, P(ctypes.c_int64)]),
     ("zc_debug_c4_rollout", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p,
                                            ctypes.c_void_p, ctypes.c_void_p]),
@@ -373,6 +381,20 @@ class NativeEngine:
         check(lib().zc_chess_children_async(self._h, n, ctypes.c_void_p(d_states), ctypes.c_void_p(d_children),
                                             ctypes.c_void_p(d_moves or None), ctypes.c_void_p(d_counts),
                                             ctypes.c_void_p(stream or None)))
+
+    def debug_chess_tree(self, game: int, max_nodes: int = 1 << 16, max_slots: int = 1 << 22) -> dict:
+        """Game `game`'s chess tree after a search (test hook): node records and slot arrays."""
+        nodes = np.zeros(max_nodes, CHESS_NODE_DTYPE)
+        mv = np.zeros(max_slots, np.uint16)
+        pr = np.zeros(max_slots, np.float32)
+        na = np.zeros(max_slots, np.int32)
+        w = np.zeros(max_slots, np.float64)
+        ch = np.zeros(max_slots, np.uint16)
+        cnt = np.zeros(2, np.int32)
+        check(lib().zc_debug_chess_tree(self._h, int(game), max_nodes, max_slots, _ptr(nodes), _ptr(mv), _ptr(pr),
+                                        _ptr(na), _ptr(w), _ptr(ch), _ptr(cnt)))
+        n, s = int(cnt[0]), int(cnt[1])
+        return {"nodes": nodes[:n], "mv": mv[:s], "prior": pr[:s], "na": na[:s], "w": w[:s], "child": ch[:s]}
 
     def chess_play_async(self, n: int, d_in: int, d_moves: int, d_out: int, stream: int = 0):
         check(lib().zc_chess_play_async(self._h, n, ctypes.c_void_p(d_in), ctypes.c_void_p(d_moves),

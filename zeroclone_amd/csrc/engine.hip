@@ -858,6 +858,34 @@ int zc_chess_puct_end(zc_engine *eng, int32_t first, int32_t n, float temperatur
     return ZC_OK;
 }
 
+int zc_debug_chess_tree(zc_engine *eng, int32_t game, int32_t max_nodes, int32_t max_slots, void *out_nodes,
+                        uint16_t *out_mv, float *out_prior, int32_t *out_na, double *out_w, uint16_t *out_child,
+                        int32_t *out_counts) {
+    if (!eng || !out_nodes || !out_mv || !out_prior || !out_na || !out_w || !out_child || !out_counts)
+        return fail(ZC_EINVAL, "null argument");
+    if (int r = check_games(eng, game, 1)) return r;
+    std::lock_guard<std::mutex> lk(eng->mu);
+    ZC_HIP(hipSetDevice(eng->cfg.device));
+    const zc::ChessArena &c = eng->ca;
+    if (!c.nodes) return fail(ZC_EINVAL, "no chess tree (no chess search has run)");
+    ZC_HIP(hipStreamSynchronize(nullptr));
+    ZC_HIP(hipDeviceSynchronize());
+    int32_t ctl[2];  // per-game control words 0, 1: nodes, slots used
+    ZC_HIP(hipMemcpy(ctl, c.ctl + (size_t)game * zc::kCtlWords, sizeof ctl, hipMemcpyDeviceToHost));
+    if (ctl[0] > max_nodes || ctl[1] > max_slots)
+        return fail(ZC_ECAPACITY, "tree has %d nodes / %d slots (buffers: %d / %d)", ctl[0], ctl[1], max_nodes, max_slots);
+    const size_t no = (size_t)game * eng->M, so = (size_t)game * (size_t)c.S;
+    ZC_HIP(hipMemcpy(out_nodes, c.nodes + no, (size_t)ctl[0] * sizeof(zc::ChessNode), hipMemcpyDeviceToHost));
+    ZC_HIP(hipMemcpy(out_mv, c.mv + so, (size_t)ctl[1] * sizeof(uint16_t), hipMemcpyDeviceToHost));
+    ZC_HIP(hipMemcpy(out_prior, c.prior + so, (size_t)ctl[1] * sizeof(float), hipMemcpyDeviceToHost));
+    ZC_HIP(hipMemcpy(out_na, c.na + so, (size_t)ctl[1] * sizeof(int32_t), hipMemcpyDeviceToHost));
+    ZC_HIP(hipMemcpy(out_w, c.w + so, (size_t)ctl[1] * sizeof(double), hipMemcpyDeviceToHost));
+    ZC_HIP(hipMemcpy(out_child, c.ch + so, (size_t)ctl[1] * sizeof(uint16_t), hipMemcpyDeviceToHost));
+    out_counts[0] = ctl[0];
+    out_counts[1] = ctl[1];
+    return ZC_OK;
+}
+
 // ---------------------------------------------------------------- value-network layers
 int zc_net_conv3x3_async(int32_t n, int32_t h, int32_t w, int32_t cin, const void *d_in, const void *d_weight,
                          const float *d_bias, const void *d_residual, void *d_out, int32_t relu, void *hip_stream) {
