@@ -233,6 +233,35 @@ def puct_mode(steps: int, dev) -> dict:
             "net_tflops_lower": round(fl / dt / 1e12, 1), "mfma_frac_lower": round(fl / dt / 1e12 / MFMA_F16_PEAK_TFLOPS, 4)}
 
 
+def c4_puct_mode(games: int, sims: int, bs: int, steps: int, dev) -> dict:
+    """C2 with the PUCT extension (SURVEY §8 a21 on the target game): 4096 games x 800 sims,
+    policy (7 column logits) + value ResNet 128x8 random init fp16 on the MFMA tower,
+    Dirichlet root noise, temperature 1, one move per HIP graph."""
+    from zeroclone_amd.nets import MfmaPolicyValueNetwork, PolicyValueNetwork, flops_per_position
+    from zeroclone_amd.valued import C4PuctSearch
+    eng = _native.NativeEngine(max_games=games, max_sims=sims, max_batch=bs, device=dev.index)
+    roots = torch.zeros((games, 3), dtype=torch.int64, device=dev)
+    torch.manual_seed(0)
+    net = MfmaPolicyValueNetwork(PolicyValueNetwork(in_planes=2, board=(6, 7), n_logits=7).eval(), dev)
+    ps = C4PuctSearch(eng, games, bs, seed=1, leaves=False)
+    g = ps.capture(roots, sims, lambda leaves, planes, counts: net(planes), temperature=1.0)
+    g.replay()
+    torch.cuda.synchronize(dev)
+    t = time.perf_counter()
+    exp = 0
+    for _ in range(steps):
+        g.replay()
+        exp += int(ps.stats[:, 0].sum().item())
+    dt = time.perf_counter() - t
+    nfl = _native.check(_native.lib().zc_chess_puct_flushes(sims, bs))
+    fl = flops_per_position(128, 8, 2, 6, 7) * games * bs * nfl * steps
+    eng.close()
+    return {"value": round(exp / dt, 1), "unit": "expansions/s", "ms_per_move": round(dt / steps * 1e3, 1),
+            "config": f"C2 + PUCT: {games} games x {sims} sims, c_puct 1.5, Dirichlet(0.3, 0.25), policy (7 logits) + "
+                      "value ResNet 128x8 random init fp16 (MFMA tower), temperature 1",
+            "net_tflops_lower": round(fl / dt / 1e12, 1), "mfma_frac_lower": round(fl / dt / 1e12 / MFMA_F16_PEAK_TFLOPS, 4)}
+
+
 def philox_mode(sp, args) -> dict:
     """C2(ii): the same self-play steps with ZC_ROLLOUT_PHILOX (leaf-parallel rollouts on
     per-leaf Philox-seeded streams; statistical parity, tests/test_gpu_philox.py)."""
@@ -418,6 +447,7 @@ def run_rank(args, rank: int, world: int, local: int):
             sp.close()
             sp = None
             out["extra"]["c2_value_net"] = net_mode(G, S, B, args.c, args.net_steps, dev)
+            out["extra"]["c2_puct"] = c4_puct_mode(G, S, B, args.net_steps, dev)
             out["extra"]["c4_chess"] = chess_modes(args.net_steps, dev)
             out["extra"]["c5_chess_puct"] = puct_mode(args.net_steps, dev)
         if world == 1 and not args.no_cpu_baseline:

@@ -295,6 +295,28 @@ int zc_chess_puct_backup(zc_engine *eng, int32_t first_game, int32_t n_games, in
 int zc_chess_puct_end(zc_engine *eng, int32_t first_game, int32_t n_games, float temperature, uint16_t *d_out_move,
                       int32_t *d_out_root_na, float *d_out_root_prior, zc_game_stats *d_out_stats, void *hip_stream);
 
+/* ---- Connect4 PUCT search (AlphaZero-style; no reference counterpart) -----
+ * The chess PUCT search's rules (above) on the Connect4 rules of c4_backend.py: moves in
+ * CPython set order, a node is terminal when the last mover has four (value -1 for the side
+ * to move) or the board is full (value 0).  Flush count as zc_chess_puct_flushes.  select
+ * exports the leaves (zc_c4_state) and their state_to_tensor planes [2][6][7]; backup takes
+ * per leaf slot the value for the side to move and 7 column logits (logits_dtype ZC_F32 /
+ * ZC_F16); end writes the move (a column), root visits and, optionally, root priors after
+ * noise, per column [n][7]. */
+int zc_c4_puct_begin(zc_engine *eng, int32_t first_game, int32_t n_games, const zc_c4_state *d_roots, int32_t sims,
+                     double c_puct, int32_t batch_size, float dirichlet_alpha, float dirichlet_eps, uint64_t seed,
+                     void *hip_stream);
+int zc_c4_puct_select(zc_engine *eng, int32_t first_game, int32_t n_games, int32_t flush, zc_c4_state *d_leaves,
+                      void *d_planes, int32_t planes_dtype, int32_t *d_counts, void *hip_stream);
+int zc_c4_puct_backup(zc_engine *eng, int32_t first_game, int32_t n_games, int32_t flush, const double *d_values,
+                      const void *d_logits, int32_t logits_dtype, void *hip_stream);
+int zc_c4_puct_end(zc_engine *eng, int32_t first_game, int32_t n_games, float temperature, int32_t *d_out_move,
+                   int32_t *d_out_root_na, float *d_out_root_prior, zc_game_stats *d_out_stats, void *hip_stream);
+/* Test hook: game `game`'s Connect4 PUCT tree as raw 192-byte node records (stones X/O, move
+ * order word, turn, #moves, evaluated, won, parent, parent slot, depth, children[8], N[8],
+ * P[8] float, W[8] double); *out_count = nodes.  Synchronises the device. */
+int zc_debug_c4_puct_tree(zc_engine *eng, int32_t game, int32_t max_nodes, void *out_nodes, int32_t *out_count);
+
 /* ---- Value-network layers on the matrix cores (models/chess_value/network.py:24-45) -----
  * The residual tower of ValueNetwork with BatchNorm folded into the convolutions, NHWC fp16
  * activations ([n][h][w][c], a pixel's channels contiguous), 128 output channels.

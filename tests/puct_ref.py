@@ -1,5 +1,5 @@
-"""A plain-Python restatement of the PUCT search of zeroclone_amd/csrc/chess_puct.hip, for
-the parity tests (test infrastructure; the rules come from the oracle).  The search has no
+"""A plain-Python restatement of the PUCT searches of zeroclone_amd/csrc/chess_puct.hip and
+c4_puct.hip, for the parity tests (test infrastructure; the rules come from the oracle).  The search has no
 reference counterpart, so this file is its specification in executable
 form: same arithmetic order in fp64, same tie-breaking, same flush / virtual-loss protocol.
 """
@@ -8,10 +8,38 @@ import math
 import oracle
 
 
+class ChessRules:
+    """chess_puct.hip: the reference's chess rules (oracle restatement of chess_backend.cpp)."""
+    moves = staticmethod(oracle.chess_moves)
+    play = staticmethod(oracle.chess_play)
+    win = staticmethod(oracle.chess_win)
+
+
+class C4Rules:
+    """c4_puct.hip: Connect4 (c4_backend.py) on state = (42-char board, side to move): moves
+    are the legal columns in CPython set order, none once the last mover has four or the
+    board is full; win = the last mover has four."""
+
+    @staticmethod
+    def moves(s):
+        b, t = s
+        if oracle.check_win(b, t) or oracle.check_draw(b):
+            return []
+        return oracle.set_order(sum(1 << col for col in range(7) if b[col] == "."))
+
+    @staticmethod
+    def play(s, col):
+        return oracle.play(s[0], s[1], col)
+
+    @staticmethod
+    def win(s):
+        return oracle.check_win(s[0], s[1])
+
+
 class Node:
-    def __init__(self, state):
+    def __init__(self, state, rules=ChessRules):
         self.s = state
-        self.moves = oracle.chess_moves(state)
+        self.moves = rules.moves(state)
         n = len(self.moves)
         self.N = [0] * n
         self.W = [0.0] * n
@@ -20,10 +48,10 @@ class Node:
         self.evaluated = False
 
 
-def search(state, sims, bs, c, value_fn, prior_fn):
-    """value_fn(zcc_state) -> value for the side to move; prior_fn(node) -> priors (list,
+def search(state, sims, bs, c, value_fn, prior_fn, rules=ChessRules):
+    """value_fn(state) -> value for the side to move; prior_fn(node) -> priors (list,
     float) for the node's moves.  Returns (root moves, root visits, chosen index)."""
-    root = Node(state)
+    root = Node(state, rules)
     flushes = 1 + (sims - 1 + bs - 1) // bs
     for f in range(flushes):
         nb = 1 if f == 0 else max(0, min(bs, sims - 1 - (f - 1) * bs))
@@ -45,14 +73,14 @@ def search(state, sims, bs, c, value_fn, prior_fn):
                 node.W[best] -= 1.0
                 path.append((node, best))
                 if node.child[best] is None:
-                    node.child[best] = Node(oracle.chess_play(node.s, node.moves[best]))
+                    node.child[best] = Node(rules.play(node.s, node.moves[best]), rules)
                     node = node.child[best]
                     break
                 node = node.child[best]
             leaves.append((node, path))
         for node, path in leaves:
             if len(node.moves) == 0:
-                v = -1.0 if oracle.chess_win(node.s) else 0.0
+                v = -1.0 if rules.win(node.s) else 0.0
             else:
                 v = value_fn(node.s)
                 if not node.evaluated:

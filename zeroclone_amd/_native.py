@@ -68,6 +68,12 @@ CHESS_NODE_DTYPE = np.dtype([("st", "u1", (72,)), ("base", "<u4"), ("nmoves", "<
                              ("parent", "<u2"), ("pact", "<u2"), ("depth", "<u2"), ("material", "<i2"),
                              ("check", "u1"), ("evaluated", "u1"), ("pad", "u1", (6,))])
 assert CHESS_NODE_DTYPE.itemsize == 96
+# C4PNode (zc_internal.h): the Connect4 PUCT tree's node record
+C4_PNODE_DTYPE = np.dtype([("s0", "<u8"), ("s1", "<u8"), ("order", "<u4"), ("turn", "u1"), ("nmoves", "u1"),
+                           ("evaluated", "u1"), ("won", "u1"), ("parent", "<u2"), ("pact", "u1"), ("depth", "u1"),
+                           ("pad0", "<u4"), ("child", "<u2", (8,)), ("na", "<i4", (8,)), ("pr", "<f4", (8,)),
+                           ("w", "<f8", (8,)), ("pad1", "u1", (16,))])
+assert C4_PNODE_DTYPE.itemsize == 192
 ZC_CHESS_WIN, ZC_CHESS_STALEMATE, ZC_CHESS_FIFTY, ZC_CHESS_OVERFLOW = 1, 2, 4, 8
 ZC_POLICY_RANDOM, ZC_POLICY_IMMEDIATE_VALUE = 0, 1
 ZC_STATUS_CAPACITY = 4
@@ -149,6 +155,19 @@ SIGNATURES = [
     ("zc_chess_puct_end", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_float,
                                          ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                          ctypes.c_void_p]),
+    ("zc_c4_puct_begin", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p,
+                                        ctypes.c_int32, ctypes.c_double, ctypes.c_int32, ctypes.c_float,
+                                        ctypes.c_float, ctypes.c_uint64, ctypes.c_void_p]),
+    ("zc_c4_puct_select", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p,
+                                         ctypes.c_void_p]),
+    ("zc_c4_puct_backup", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p]),
+    ("zc_c4_puct_end", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_float,
+                                      ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                      ctypes.c_void_p]),
+    ("zc_debug_c4_puct_tree", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p,
+                                             ctypes.c_void_p]),
     ("zc_net_conv3x3_async", ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
                                             ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                             ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p]),
@@ -458,6 +477,34 @@ class NativeEngine:
         check(lib().zc_chess_puct_end(self._h, first_game, n, float(temperature), ctypes.c_void_p(d_move),
                                       ctypes.c_void_p(d_na), ctypes.c_void_p(d_prior or None),
                                       ctypes.c_void_p(d_stats), ctypes.c_void_p(stream or None)))
+
+    # ---- Connect4 PUCT search (device pointers as ints)
+    def c4_puct_begin(self, first_game, n, d_roots, sims, c_puct, batch_size, alpha, eps, seed, stream=0):
+        check(lib().zc_c4_puct_begin(self._h, first_game, n, ctypes.c_void_p(d_roots), int(sims), float(c_puct),
+                                     int(batch_size), float(alpha), float(eps), int(seed) & (2**64 - 1),
+                                     ctypes.c_void_p(stream or None)))
+
+    def c4_puct_select(self, first_game, n, flush, d_leaves=0, d_planes=0, planes_f16=True, d_counts=0, stream=0):
+        check(lib().zc_c4_puct_select(self._h, first_game, n, int(flush), ctypes.c_void_p(d_leaves or None),
+                                      ctypes.c_void_p(d_planes or None), ZC_F16 if planes_f16 else ZC_F32,
+                                      ctypes.c_void_p(d_counts or None), ctypes.c_void_p(stream or None)))
+
+    def c4_puct_backup(self, first_game, n, flush, d_values, d_logits, logits_f16=False, stream=0):
+        check(lib().zc_c4_puct_backup(self._h, first_game, n, int(flush), ctypes.c_void_p(d_values),
+                                      ctypes.c_void_p(d_logits), ZC_F16 if logits_f16 else ZC_F32,
+                                      ctypes.c_void_p(stream or None)))
+
+    def c4_puct_end(self, first_game, n, temperature, d_move, d_na, d_prior, d_stats, stream=0):
+        check(lib().zc_c4_puct_end(self._h, first_game, n, float(temperature), ctypes.c_void_p(d_move),
+                                   ctypes.c_void_p(d_na), ctypes.c_void_p(d_prior or None),
+                                   ctypes.c_void_p(d_stats), ctypes.c_void_p(stream or None)))
+
+    def debug_c4_puct_tree(self, game: int, max_nodes: int = 1 << 16) -> np.ndarray:
+        """Game `game`'s Connect4 PUCT tree (test hook): node records (C4_PNODE_DTYPE)."""
+        out = np.zeros(max_nodes, C4_PNODE_DTYPE)
+        cnt = np.zeros(1, np.int32)
+        check(lib().zc_debug_c4_puct_tree(self._h, int(game), max_nodes, _ptr(out), _ptr(cnt)))
+        return out[:int(cnt[0])]
 
     def c4_rollouts(self, states: np.ndarray, game: int = 0):
         """Sequential rollouts of `states` on one game's stream: (values[n], words consumed)."""

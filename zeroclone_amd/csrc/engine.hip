@@ -233,6 +233,9 @@ int zc_engine_destroy(zc_engine *eng) {
         (void)hipStreamSynchronize(eng->stream);
         free_arena(eng->a);
         free_chess(eng->ca);
+        void *c4p[] = {eng->c4p_nodes, eng->c4p_ctl, eng->c4p_paths, eng->c4p_meta};
+        for (void *q : c4p)
+            if (q) (void)hipFree(q);
         (void)hipStreamDestroy(eng->stream);
     }
     delete eng;
@@ -855,6 +858,157 @@ int zc_chess_puct_end(zc_engine *eng, int32_t first, int32_t n, float temperatur
     p.out_stats = d_stats;
     zc::launch_chess_puct_end(p, (hipStream_t)hip_stream);
     ZC_HIP(hipGetLastError());
+    return ZC_OK;
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------- Connect4 PUCT search
+namespace {
+int ensure_c4p(zc_engine *e) {
+    if (e->c4p_nodes) return ZC_OK;
+    const size_t G = (size_t)e->cfg.max_games, M = (size_t)e->M;
+    int rc = dalloc(e, &e->c4p_nodes, G * M);
+    if (!rc) rc = dalloc(e, &e->c4p_ctl, G * zc::kCtlWords);
+    if (!rc) rc = dalloc(e, &e->c4p_paths, G * (size_t)e->cfg.max_batch * zc::kMaxDepth);
+    if (!rc) rc = dalloc(e, &e->c4p_meta, G * (size_t)e->cfg.max_batch);
+    if (!rc && hipMemset(e->c4p_ctl, 0, G * zc::kCtlWords * sizeof(int32_t)) != hipSuccess)
+        rc = fail(ZC_EHIP, "memset failed");
+    if (rc) {
+        void *q[] = {e->c4p_nodes, e->c4p_ctl, e->c4p_paths, e->c4p_meta};
+        for (void *x : q)
+            if (x) (void)hipFree(x);
+        e->c4p_nodes = nullptr;
+        e->c4p_ctl = nullptr;
+        e->c4p_paths = e->c4p_meta = nullptr;
+    }
+    return rc;
+}
+zc::C4PuctParams c4p_params(zc_engine *e, int32_t first, int32_t n) {
+    zc::C4PuctParams p{};
+    p.first_game = first;
+    p.n_games = n;
+    p.sims = e->qx_sims;
+    p.bs = e->qx_bs;
+    p.M = e->M;
+    p.max_batch = e->cfg.max_batch;
+    p.c = e->qx_c;
+    p.nodes = e->c4p_nodes;
+    p.ctl = e->c4p_ctl;
+    p.paths = e->c4p_paths;
+    p.meta = e->c4p_meta;
+    p.dir_alpha = e->qx_alpha;
+    p.dir_eps = e->qx_eps;
+    p.seed = e->qx_seed;
+    return p;
+}
+int check_qx(zc_engine *e, int32_t first, int32_t n, int32_t flush, bool need_flush) {
+    if (!e->qx_active) return fail(ZC_EINVAL, "no Connect4 PUCT search in progress (call zc_c4_puct_begin first)");
+    if (first < e->qx_first || n < 0 || (int64_t)first + n > (int64_t)e->qx_first + e->qx_n)
+        return fail(ZC_EINVAL, "games [%d, %d) outside the PUCT search's range", first, first + n);
+    const int nflush = 1 + (e->qx_sims - 1 + e->qx_bs - 1) / e->qx_bs;
+    if (need_flush && (flush < 0 || flush >= nflush)) return fail(ZC_EINVAL, "flush %d outside [0, %d)", flush, nflush);
+    return ZC_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int zc_c4_puct_begin(zc_engine *eng, int32_t first, int32_t n, const zc_c4_state *d_roots, int32_t sims,
+                     double c_puct, int32_t bs, float alpha, float eps, uint64_t seed, void *hip_stream) {
+    if (!eng || (n && !d_roots)) return fail(ZC_EINVAL, "null argument");
+    if (int r = check_search(eng, first, n, sims, c_puct, bs)) return r;
+    if (sims < 2) return fail(ZC_EINVAL, "PUCT search needs sims >= 2 (flush 0 evaluates the root)");
+    if (!(alpha > 0.0f) || !(eps >= 0.0f && eps <= 1.0f)) return fail(ZC_EINVAL, "need alpha > 0 and 0 <= eps <= 1");
+    std::lock_guard<std::mutex> lk(eng->mu);
+    ZC_HIP(hipSetDevice(eng->cfg.device));
+    if (int r = ensure_c4p(eng)) return r;
+    eng->qx_first = first;
+    eng->qx_n = n;
+    eng->qx_sims = sims;
+    eng->qx_bs = bs;
+    eng->qx_c = c_puct;
+    eng->qx_alpha = alpha;
+    eng->qx_eps = eps;
+    eng->qx_seed = seed;
+    eng->qx_active = true;
+    if (!n) return ZC_OK;
+    zc::C4PuctParams p = c4p_params(eng, first, n);
+    p.roots = d_roots;
+    zc::launch_c4_puct_begin(p, (hipStream_t)hip_stream);
+    ZC_HIP(hipGetLastError());
+    return ZC_OK;
+}
+
+int zc_c4_puct_select(zc_engine *eng, int32_t first, int32_t n, int32_t flush, zc_c4_state *d_leaves, void *d_planes,
+                      int32_t planes_dtype, int32_t *d_counts, void *hip_stream) {
+    if (!eng) return fail(ZC_EINVAL, "null argument");
+    if (planes_dtype != ZC_F32 && planes_dtype != ZC_F16) return fail(ZC_EINVAL, "planes_dtype must be ZC_F32 or ZC_F16");
+    std::lock_guard<std::mutex> lk(eng->mu);
+    if (int r = check_qx(eng, first, n, flush, true)) return r;
+    if (!n) return ZC_OK;
+    ZC_HIP(hipSetDevice(eng->cfg.device));
+    zc::C4PuctParams p = c4p_params(eng, first, n);
+    p.flush = flush;
+    p.leaves = d_leaves;
+    p.planes = d_planes;
+    p.planes_f16 = planes_dtype == ZC_F16;
+    p.counts = d_counts;
+    zc::launch_c4_puct_select(p, (hipStream_t)hip_stream);
+    ZC_HIP(hipGetLastError());
+    return ZC_OK;
+}
+
+int zc_c4_puct_backup(zc_engine *eng, int32_t first, int32_t n, int32_t flush, const double *d_values,
+                      const void *d_logits, int32_t logits_dtype, void *hip_stream) {
+    if (!eng || (n && (!d_values || !d_logits))) return fail(ZC_EINVAL, "null argument");
+    if (logits_dtype != ZC_F32 && logits_dtype != ZC_F16) return fail(ZC_EINVAL, "logits_dtype must be ZC_F32 or ZC_F16");
+    std::lock_guard<std::mutex> lk(eng->mu);
+    if (int r = check_qx(eng, first, n, flush, true)) return r;
+    if (!n) return ZC_OK;
+    ZC_HIP(hipSetDevice(eng->cfg.device));
+    zc::C4PuctParams p = c4p_params(eng, first, n);
+    p.flush = flush;
+    p.values = d_values;
+    p.logits = d_logits;
+    p.logits_f16 = logits_dtype == ZC_F16;
+    zc::launch_c4_puct_backup(p, (hipStream_t)hip_stream);
+    ZC_HIP(hipGetLastError());
+    return ZC_OK;
+}
+
+int zc_c4_puct_end(zc_engine *eng, int32_t first, int32_t n, float temperature, int32_t *d_move, int32_t *d_na,
+                   float *d_prior, zc_game_stats *d_stats, void *hip_stream) {
+    if (!eng || (n && (!d_move || !d_na || !d_stats))) return fail(ZC_EINVAL, "null argument");
+    if (!(temperature >= 0.0f)) return fail(ZC_EINVAL, "temperature must be >= 0");
+    std::lock_guard<std::mutex> lk(eng->mu);
+    if (int r = check_qx(eng, first, n, 0, false)) return r;
+    if (!n) return ZC_OK;
+    ZC_HIP(hipSetDevice(eng->cfg.device));
+    zc::C4PuctParams p = c4p_params(eng, first, n);
+    p.temperature = temperature;
+    p.out_move = d_move;
+    p.out_na = d_na;
+    p.out_prior = d_prior;
+    p.out_stats = d_stats;
+    zc::launch_c4_puct_end(p, (hipStream_t)hip_stream);
+    ZC_HIP(hipGetLastError());
+    return ZC_OK;
+}
+
+int zc_debug_c4_puct_tree(zc_engine *eng, int32_t game, int32_t max_nodes, void *out_nodes, int32_t *out_count) {
+    if (!eng || !out_nodes || !out_count) return fail(ZC_EINVAL, "null argument");
+    if (int r = check_games(eng, game, 1)) return r;
+    std::lock_guard<std::mutex> lk(eng->mu);
+    ZC_HIP(hipSetDevice(eng->cfg.device));
+    if (!eng->c4p_nodes) return fail(ZC_EINVAL, "no Connect4 PUCT tree (no PUCT search has run)");
+    ZC_HIP(hipDeviceSynchronize());
+    int32_t nn = 0;
+    ZC_HIP(hipMemcpy(&nn, eng->c4p_ctl + (size_t)game * zc::kCtlWords, sizeof nn, hipMemcpyDeviceToHost));
+    if (nn > max_nodes) return fail(ZC_ECAPACITY, "tree has %d nodes (buffer: %d)", nn, max_nodes);
+    ZC_HIP(hipMemcpy(out_nodes, eng->c4p_nodes + (size_t)game * eng->M, (size_t)nn * sizeof(zc::C4PNode),
+                     hipMemcpyDeviceToHost));
+    *out_count = nn;
     return ZC_OK;
 }
 

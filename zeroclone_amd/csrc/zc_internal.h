@@ -167,6 +167,54 @@ struct ChessParams {
     float *out_prior;           // end (optional): root priors after noise [n][ZC_CHESS_MAX_MOVES]
 };
 
+// ---------------------------------------------------------------- Connect4 PUCT search
+// (c4_puct.hip; SURVEY §8 a21 on the target game).  One 192-byte record per node, slot k of
+// the node's move list (CPython set order) at index k of every per-slot array.
+struct C4PNode {
+    uint64_t s0, s1;      // stones of 'X' / 'O'
+    uint32_t order;       // packed 3-bit move-list columns | #moves << 24 (d_order of the legal mask)
+    uint8_t turn;         // side to move
+    uint8_t nmoves;       // moves searched from here: 0 at a terminal position
+    uint8_t evaluated;    // the network's priors are in pr[]
+    uint8_t won;          // the last mover has four (check_win)
+    uint16_t parent;
+    uint8_t pact, depth;
+    uint32_t pad0;
+    uint16_t child[8];    // 0xFFFF = none
+    int32_t na[8];        // N (virtual losses included while a flush is pending)
+    float pr[8];          // P
+    double w[8];          // W (fp64)
+    uint8_t pad1[16];
+};
+
+struct C4PuctParams {
+    int first_game, n_games, sims, bs, M, max_batch, flush;
+    double c;                 // c_puct
+    C4PNode *nodes;           // [G][M]
+    int32_t *ctl;             // [G][kCtlWords]
+    uint32_t *paths;          // [G][max_batch][kMaxDepth] edge into level l: node | slot << 16
+    uint32_t *meta;           // [G][max_batch] leaf node | depth << 16
+    const zc_c4_state *roots;
+    zc_c4_state *leaves;
+    void *planes;
+    int planes_f16;
+    int32_t *counts;
+    const double *values;
+    const void *logits;       // backup: [n*bs][7] column logits
+    int logits_f16;
+    float dir_alpha, dir_eps;
+    uint64_t seed;
+    float temperature;
+    int32_t *out_move;        // column
+    int32_t *out_na;          // [n][7] visits per column
+    float *out_prior;         // [n][7] root priors per column (optional)
+    zc_game_stats *out_stats;
+};
+void launch_c4_puct_begin(const C4PuctParams &p, hipStream_t s);
+void launch_c4_puct_select(const C4PuctParams &p, hipStream_t s);
+void launch_c4_puct_backup(const C4PuctParams &p, hipStream_t s);
+void launch_c4_puct_end(const C4PuctParams &p, hipStream_t s);
+
 void launch_chess_search(const ChessParams &p, hipStream_t s);     // crude_chess_score, whole move
 void launch_chess_ext_begin(const ChessParams &p, hipStream_t s);
 void launch_chess_ext_select(const ChessParams &p, hipStream_t s);
@@ -224,6 +272,15 @@ struct zc_engine {
     int rollout_mode = 0;        // ZC_ROLLOUT_EXACT / ZC_ROLLOUT_PHILOX
     uint64_t rollout_seed = 0;
     zc::ChessArena ca;  // allocated on the first chess search
+    // the Connect4 PUCT tree (allocated on the first zc_c4_puct_begin) and its search in progress
+    zc::C4PNode *c4p_nodes = nullptr;
+    int32_t *c4p_ctl = nullptr;
+    uint32_t *c4p_paths = nullptr, *c4p_meta = nullptr;
+    int qx_first = 0, qx_n = 0, qx_sims = 0, qx_bs = 0;
+    double qx_c = 0;
+    float qx_alpha = 0, qx_eps = 0;
+    uint64_t qx_seed = 0;
+    bool qx_active = false;
     // the chess PUCT search in progress
     int px_first = 0, px_n = 0, px_sims = 0, px_bs = 0;
     double px_c = 0;

@@ -237,3 +237,56 @@ class ChessPuctSearch:
         with torch.cuda.graph(g):
             self.enqueue(roots, sims, net_fn, temperature, first_game)
         return g
+
+
+class C4PuctSearch:
+    """AlphaZero-style PUCT search for Connect4 (zc_c4_puct_*, SURVEY §8 a21 on the target
+    game): the chess PUCT search's selection, virtual loss, Dirichlet root noise and
+    temperature on the Connect4 rules.
+
+    net_fn(leaves, planes, counts) -> (values fp64 [n*bs], logits [n*bs, 7] fp32/fp16, one per
+    column) — e.g. `lambda l, p, c: net(p)` with nets.MfmaPolicyValueNetwork over
+    PolicyValueNetwork(in_planes=2, board=(6, 7), n_logits=7)."""
+
+    def __init__(self, eng: "_native.NativeEngine", n_games: int, batch_size: int = 32, c_puct: float = 1.5,
+                 dirichlet_alpha: float = 0.3, dirichlet_eps: float = 0.25, seed: int = 0,
+                 planes_dtype: torch.dtype = torch.float16, leaves: bool = True):
+        if batch_size > eng.max_batch:
+            raise ValueError(f"batch_size {batch_size} > engine max_batch {eng.max_batch}")
+        self.eng, self.n, self.bs = eng, n_games, batch_size
+        self.c, self.alpha, self.eps, self.seed = c_puct, dirichlet_alpha, dirichlet_eps, seed
+        self.dev = torch.device("cuda", eng.device)
+        L = n_games * batch_size
+        self.leaves = torch.zeros((L, 3), dtype=torch.int64, device=self.dev) if leaves else None
+        self.planes = torch.zeros((L, 2, 6, 7), dtype=planes_dtype, device=self.dev)
+        self.counts = torch.zeros(n_games, dtype=torch.int32, device=self.dev)
+        self.values = torch.zeros(L, dtype=torch.float64, device=self.dev)
+        self.move = torch.zeros(n_games, dtype=torch.int32, device=self.dev)
+        self.na = torch.zeros((n_games, 7), dtype=torch.int32, device=self.dev)
+        self.prior = torch.zeros((n_games, 7), dtype=torch.float32, device=self.dev)
+        self.stats = torch.zeros((n_games, _native.STATS_FIELDS), dtype=torch.int64, device=self.dev)
+        # the tree arena exists before any graph capture
+        z = torch.zeros((1, 3), dtype=torch.int64, device=self.dev)
+        eng.c4_puct_begin(0, 0, z.data_ptr(), 2, c_puct, batch_size, dirichlet_alpha, dirichlet_eps, seed)
+
+    def enqueue(self, roots: torch.Tensor, sims: int, net_fn, temperature: float = 0.0, first_game: int = 0):
+        e, n = self.eng, self.n
+        p = lambda t: t.data_ptr() if t is not None else 0  # noqa: E731
+        nfl = _native.check(_native.lib().zc_chess_puct_flushes(int(sims), int(self.bs)))
+        e.c4_puct_begin(first_game, n, roots.data_ptr(), sims, self.c, self.bs, self.alpha, self.eps, self.seed,
+                        _stream(self.dev))
+        for f in range(nfl):
+            e.c4_puct_select(first_game, n, f, p(self.leaves), p(self.planes), self.planes.dtype == torch.float16,
+                             self.counts.data_ptr(), _stream(self.dev))
+            v, logits = net_fn(self.leaves, self.planes, self.counts)
+            if v is not self.values:
+                self.values.copy_(v.reshape(-1))
+            logits = logits.contiguous()
+            e.c4_puct_backup(first_game, n, f, self.values.data_ptr(), logits.data_ptr(),
+                             logits.dtype == torch.float16, _stream(self.dev))
+        e.c4_puct_end(first_game, n, temperature, self.move.data_ptr(), self.na.data_ptr(), self.prior.data_ptr(),
+                      self.stats.data_ptr(), _stream(self.dev))
+        return self.move, self.na, self.stats
+
+    run = ChessPuctSearch.run
+    capture = ChessPuctSearch.capture
