@@ -4,7 +4,9 @@
     python tools/ab_search.py libA.so libB.so ...   (paths relative to the repo root)
 
 Each round runs every variant in its own process (ZC_LIB=<path>), in turn, so that clock
-and thermal drift hit all of them alike; prints the median search time per variant."""
+and thermal drift hit all of them alike; prints the median search time per variant.
+AB_ROOTS=mixed searches from mid-game roots (random depths 0..27, the steady-state mix of
+self-play) instead of the empty board."""
 import os
 import statistics
 import subprocess
@@ -20,6 +22,30 @@ from zeroclone_amd import _native
 G, S, B = %d, 800, 32
 eng = _native.NativeEngine(max_games=G, max_sims=S, max_batch=B)
 roots = np.zeros(G, _native.C4_STATE_DTYPE)
+if %r == "mixed":
+    rs = np.random.default_rng(1234)
+    def has4(b):
+        for sh in (1, 7, 6, 8):
+            m = b & (b >> sh)
+            if m & (m >> (2 * sh)):
+                return True
+        return False
+    for i in range(G):
+        while True:
+            st, turn, ok = [0, 0], 0, True
+            for _ in range(int(rs.integers(0, 28))):
+                occ = st[0] | st[1]
+                cols = [c for c in range(7) if not (occ >> (7 * c + 5)) & 1]
+                c = int(rs.choice(cols))
+                st[turn] |= (occ + (1 << (7 * c))) & (0x3F << (7 * c))
+                if has4(st[turn]):
+                    ok = False
+                    break
+                turn ^= 1
+            if ok:
+                break
+        roots[i]["stones"] = st
+        roots[i]["turn"] = turn
 ts = []
 for r in range(9):
     eng.seed(0, list(range(r * G, (r + 1) * G)))
@@ -38,7 +64,8 @@ def main():
     for rnd in range(int(os.environ.get("AB_ROUNDS", "3"))):
         for lib in libs:
             env = dict(os.environ, ZC_LIB=os.path.join(ROOT, lib))
-            out = subprocess.run([sys.executable, "-c", CHILD % (ROOT, games)], env=env, check=True,
+            out = subprocess.run([sys.executable, "-c", CHILD % (ROOT, games, os.environ.get("AB_ROOTS", "empty"))],
+                                 env=env, check=True,
                                  capture_output=True, text=True, timeout=300).stdout
             res[lib].append(float(out.strip().splitlines()[-1]))
             print(rnd, lib, res[lib][-1], flush=True)

@@ -206,7 +206,8 @@ __device__ __forceinline__ void rng_advance(Rng &r) {
 
 // The 64 tempered words from the next unconsumed one on: lane l = word off + l of the
 // window (precondition: off < 64).
-__device__ __forceinline__ uint32_t rng_view(const Rng &r) {
+template <class R>
+__device__ __forceinline__ uint32_t rng_view(const R &r) {
     const uint32_t j = lane_id() + r.off;
     const int idx = (int)((j & 63u) << 2);
     const uint32_t a = (uint32_t)__builtin_amdgcn_ds_bpermute(idx, (int)r.wt);
@@ -220,10 +221,133 @@ __device__ __forceinline__ void rng_close(const Rng &r, uint64_t use0, uint64_t 
     rngpos[1] = use0 + (uint64_t)(int64_t)r.grel;
 }
 
+// ------------------------------------------------------------------ the stream in LDS
+// The fused search (c4_search_kernel) keeps its game's stream in a 1024-word LDS ring
+// instead of the HBM ring: the recurrence runs one 64-word step per window advance, lane l
+// generating x[W + 128 + l] (W = the new window start) from inputs read one advance earlier
+// (x[p-624], x[p-623], x[p-227] are all older than W + 128 - 163, so they are known a whole
+// window ahead), and the new raw word is the new `wx` itself — no HBM traffic and no
+// memory wait on the chain.  Invariant: words [W - 832, W + 192) are in the ring.
+// The HBM ring is the hand-over format to every other kernel and to zc_rng_get_state: the
+// kernel loads its game's last 1024 words at the start and, at the end, writes back the
+// words [min(U & ~63, block start, G' - 624), G') (U = next word, block = the 624-word block
+// holding word U-1, G' = words generated, at least that block's end) — what rng_open,
+// zc_rng_get_state and the recurrence read.
+constexpr int kLRingWords = 1024;
+constexpr uint32_t kLRingMask = kLRingWords - 1;
+constexpr int kLRingBytes = kLRingWords * 4;
+
+struct LRng {
+    uint32_t *lds;   // this wave's ring: raw x[p] at slot p % 1024
+    uint32_t base;   // low 32 bits of the absolute position at the search's start (use0)
+    int32_t wrel;    // window start - use0
+    uint32_t off;    // next word to consume = window start + off, off in [0, 128)
+    int32_t hrel;    // words [.., use0 + hrel) were in the ring at the start (hrel >= 192 - off)
+    uint32_t wt;     // tempered x[W + lane]
+    uint32_t wn;     // tempered x[W + 64 + lane]
+    uint32_t wx;     // raw x[W + 128 + lane]
+    uint32_t ia, ib, im;  // raw x[p-624], x[p-623], x[p-227] for p = W + 192 + lane (the next step)
+    __device__ __forceinline__ int32_t use() const { return wrel + (int32_t)off; }
+    __device__ __forceinline__ uint32_t slot(int32_t rel) const { return (base + (uint32_t)rel) & kLRingMask; }
+};
+
+__device__ __forceinline__ uint32_t mt_twist(uint32_t a, uint32_t b, uint32_t m) {
+    const uint32_t y = (a & 0x80000000u) | (b & 0x7fffffffu);
+    return m ^ (y >> 1) ^ ((b & 1u) ? 0x9908b0dfu : 0u);
+}
+
+__device__ __forceinline__ void lrng_prefetch(LRng &r) {
+    const int32_t p = r.wrel + 192 + (int32_t)lane_id();
+    r.ia = r.lds[r.slot(p - 624)];
+    r.ib = r.lds[r.slot(p - 623)];
+    r.im = r.lds[r.slot(p - 227)];
+}
+
+// Generate absolute words [g, end) in the ring, 64 at a time (every input is >= 227 older).
+__device__ __forceinline__ void lrng_generate_abs(uint32_t *lds, uint64_t g, uint64_t end) {
+    const uint32_t lane = lane_id();
+    for (; g < end; g += 64) {
+        const uint32_t p = (uint32_t)g + lane;
+        const uint32_t a = lds[(p - 624) & kLRingMask], b = lds[(p - 623) & kLRingMask],
+                       m = lds[(p - 227) & kLRingMask];
+        if (g + lane < end) lds[p & kLRingMask] = mt_twist(a, b, m);
+        wave_mem_order();
+    }
+}
+
+// use0 / gen0: absolute positions (words consumed / generated) from the game's rngpos.
+// Words already generated (and the seeded block 0..623, which no recurrence produces) are
+// kept: an advance inside them re-reads the ring instead of generating (hrel).
+__device__ __forceinline__ void lrng_open(LRng &r, uint32_t *lds, const uint32_t *ring, uint64_t use0, uint64_t gen0) {
+    const uint32_t lane = lane_id();
+    r.lds = lds;
+    r.base = (uint32_t)use0;
+    r.off = (uint32_t)use0 & (uint32_t)(kWin - 1);
+    r.wrel = -(int32_t)r.off;
+    const uint64_t w0 = use0 - r.off, target = w0 + 192;
+    // the ring can take every word up to gen0 when gen0 - w0 <= 960 (always after this
+    // kernel's own close: <= 879); an HBM kernel's lookahead may go further, and then its
+    // ring is valid throughout, so the words past the first window are generated again
+    const uint64_t g = gen0 <= w0 + 960 ? gen0 : (target < 624 ? 624 : target);
+    for (uint32_t i = lane; i < (uint32_t)kLRingWords; i += 64) {
+        const uint32_t p = (uint32_t)g - (uint32_t)kLRingWords + i;
+        lds[p & kLRingMask] = ring[p & kRingMask];
+    }
+    wave_mem_order();
+    lrng_generate_abs(lds, g, target);
+    r.hrel = (int32_t)(g - use0);
+    r.wt = temper(lds[r.slot(r.wrel + (int32_t)lane)]);
+    r.wn = temper(lds[r.slot(r.wrel + kWin + (int32_t)lane)]);
+    r.wx = lds[r.slot(r.wrel + 2 * kWin + (int32_t)lane)];
+    lrng_prefetch(r);
+}
+
+// Move the windows on by 64 words (precondition: off >= 64); one recurrence step.
+__device__ __forceinline__ void rng_advance(LRng &r) {
+    r.wrel += kWin;
+    r.off -= (uint32_t)kWin;
+    r.wt = r.wn;
+    r.wn = temper(r.wx);
+    const int32_t p = r.wrel + 128 + (int32_t)lane_id();
+    uint32_t x = mt_twist(r.ia, r.ib, r.im);
+    if (r.wrel + 128 < r.hrel) {  // only inside the seeded block: words already in the ring
+        const uint32_t old = r.lds[r.slot(p)];
+        x = p < r.hrel ? old : x;
+    }
+    r.lds[r.slot(p)] = x;
+    r.wx = x;
+    lrng_prefetch(r);
+}
+
+// Write the stream back to the game's HBM ring and rngpos (see above).
+__device__ __forceinline__ void lrng_close(const LRng &r, uint32_t *ring, uint64_t use0, uint64_t *rngpos) {
+    const uint32_t lane = lane_id();
+    const uint64_t U = use0 + (uint64_t)(int64_t)r.use();
+    uint64_t G = use0 + (uint64_t)(int64_t)max(r.wrel + 192, r.hrel);
+    const uint64_t blk = U ? (U - 1) / 624 : 0;
+    const uint64_t bend = (blk + 1) * 624;
+    wave_mem_order();
+    if (G < bend) {
+        lrng_generate_abs(r.lds, G, bend);
+        G = bend;
+    }
+    // what rng_open reads (the window of U), what zc_rng_get_state reads (U-1's block) and
+    // what the recurrence reads next (the last 624 words); at most 815 words
+    const uint64_t wu = U & ~(uint64_t)(kWin - 1);
+    uint64_t start = wu < blk * 624 ? wu : blk * 624;
+    start = start < G - 624 ? start : G - 624;
+    for (uint64_t q = start + lane; q < G; q += 64) ring[(uint32_t)q & kRingMask] = r.lds[(uint32_t)q & kLRingMask];
+    if (lane == 0) {
+        rngpos[0] = U;
+        rngpos[1] = G;
+    }
+}
+
 // random._randbelow_with_getrandbits(n), 1 <= n < 2**31: k = n.bit_length(); draw
 // getrandbits(k) = word >> (32-k) until < n.  All window words are tested at once; the
 // first accepted one (in stream order) is the draw, and everything before it is consumed.
-__device__ __forceinline__ uint32_t rng_below(Rng &r, uint32_t n) {
+template <class R>
+__device__ __forceinline__ uint32_t rng_below(R &r, uint32_t n) {
     const uint32_t sh = (uint32_t)__clz(n);
     const uint32_t lane = lane_id();
     for (;;) {
@@ -244,7 +368,8 @@ __device__ __forceinline__ uint32_t rng_below(Rng &r, uint32_t n) {
 // list order, mcts.cpp:67-72): rng_below(n) as above, but every lane also looks up row[v]
 // (row = sel[untried mask]: the v-th untried move) for its own candidate word, so the move
 // index of the accepted draw is a readlane of that lookup (n <= 7, so v < 8).
-__device__ __forceinline__ uint32_t rng_below_pick(Rng &r, uint32_t n, const uint8_t *row) {
+template <class R>
+__device__ __forceinline__ uint32_t rng_below_pick(R &r, uint32_t n, const uint8_t *row) {
     const uint32_t sh = (uint32_t)__clz(n);
     const uint32_t lane = lane_id();
     for (;;) {
@@ -379,10 +504,10 @@ struct FlushSel {
 // QW = false: the record's +64 slots hold Q (rollout mode, W in the side array);
 // QW = true:  they hold W in fp64 and Q = W / Na is formed here — the same IEEE quotient
 //             mcts.cpp:95 stores, so the UCT inputs are bit-identical.
-template <bool QW, bool STAMP>
+template <bool QW, bool STAMP, class RNG>
 __device__ __forceinline__ void select_flush(const Tree &t, Fresh *fresh, Leaf *leaves, uint16_t *paths,
                                              const uint32_t *s_order, ConstDouble *logtab,
-                                             Rng &rng, Counters &cn, Stamp<STAMP> &stamp, int &nnodes, int &status,
+                                             RNG &rng, Counters &cn, Stamp<STAMP> &stamp, int &nnodes, int &status,
                                              uint64_t rp0, uint64_t rp1, int rturn, int done, int nb, double c,
                                              FlushSel &fs) {
     const uint32_t lane = lane_id();
@@ -446,70 +571,136 @@ __device__ __forceinline__ void select_flush(const Tree &t, Fresh *fresh, Leaf *
     fs.ppath = pathv;
     stamp.mark(1);
 
-    for (int j = 0; j < nb; ++j) {
-        // resume at `node` (fully described by u, ow, ch, cmask in registers)
-        for (;;) {
-            if (untried_count(u)) break;  // untried moves: expand here
+    // The rest of the flush, a node at a time.  Below X0 the walks take the lowest slot
+    // holding a fresh child and a node is left only once it has no untried move, so the
+    // flush visits a chain of nodes X0 = N0, N1, ... and at each one expands m = min(#untried,
+    // leaves left) moves in a row: m random.choice draws over m, m-1, ... remaining moves
+    // (count-sequence known in advance), then the next node is N's child in its lowest slot.
+    // The draws are a scalar chain over ONE 64-word view (the accepted word of each draw is
+    // the first word after the previous one with (w >> (32-k)) < n); the children and their
+    // leaves are then built lane-parallel (lane i = the i-th draw), and the walk into the next
+    // node reads the child from those lanes — no LDS round trip, no per-leaf scalar work.
+    // ul: the node's untried list (move indices in list order, 3 bits each; random.choice's
+    // r-th element, erased in place as mcts.cpp:67-72 does).
+    constexpr uint32_t kIdentList = 0x1AC688u;  // 0, 1, ..., 6
+    uint32_t ul = 0;
+    {
+        uint32_t c = 0;
+        for (uint32_t bb = 0; bb < 7; ++bb)
+            if ((u >> bb) & 1u) ul |= bb << (3 * c++);
+    }
+    int bulk0 = 0;          // first node id of the last bulk (the children of `node`)
+    uint32_t inv = 0;       // slot s of `node` expanded by draw i of that bulk: (8 | i) << 4s
+    uint32_t c_low = 0, c_lmask = 0;  // lane i: child i's order word / legal mask
+    int j = 0;
+    while (j < nb) {
+        const uint32_t cnt = untried_count(u);
+        if (cnt == 0) {
             const uint64_t fm = __ballot(k < (u >> 28) && ch != 0xFFFF && (int)ch >= f0) & 0xFFull;
-            if (!fm) break;  // no child at all: terminal, re-queued as its own leaf
+            if (!fm) {  // no child at all: terminal, every remaining leaf of the flush is this node
+                const uint32_t meta = (uint32_t)node | ((uint32_t)depth << 16) | ((uint32_t)turn << 24) |
+                                      ((uint32_t)cmask << 25);
+                for (int i = (int)lane; j + i < nb; i += 64) leaves[j + i] = Leaf{b0, b1, meta, 0, ow, 0};
+                for (; j < nb; ++j) paths[j * kMaxDepth + lane] = (uint16_t)pathv;
+                wave_mem_order();
+                break;
+            }
             const int s = __builtin_ctzll(fm);
-            const int child = __builtin_amdgcn_readlane((int)ch, s);
+            const int child = bulk0 + (int)((inv >> (4 * s)) & 7u);
             if (node == x0node) {  // leaving X0 for good (walks never go back up)
                 x_u = u;
                 x_ch = ch;
             }
+            const int i = (int)((inv >> (4 * s)) & 7u);
             const uint64_t bit = drop_bit(b0 | b1, (int)((ow >> (3 * s)) & 7u));
             if (turn) b1 |= bit; else b0 |= bit;
             turn ^= 1;
             ++depth;
             if (lane == (uint32_t)depth) pathv = (uint32_t)child | ((uint32_t)s << 16);
             node = child;
-            const uint4 fh = *(const uint4 *)&fresh[child - f0];  // u, ow, link, lmask
-            u = uni(fh.x);
-            ow = uni(fh.y);
-            cmask = uni((int)fh.w);
-            ch = fresh[child - f0].ch[k];
+            ow = (uint32_t)__builtin_amdgcn_readlane((int)c_low, i);
+            cmask = __builtin_amdgcn_readlane((int)c_lmask, i);
+            u = untried_init((ow >> 24) & 15u);
+            ul = kIdentList;
+            ch = 0xFFFF;
+            stamp.mark(2);
+            continue;
         }
-        stamp.mark(2);
-        int leaf = node, ldepth = depth, lturn = turn, lmask = cmask;
-        uint64_t l0 = b0, l1 = b1;
-        const uint32_t cnt = untried_count(u);
-        uint32_t low_ = ow;  // the leaf's move-list order word
-        if (cnt) {  // expand (mcts.cpp:65-78): policy = random.choice(untried)
-            // the r-th untried move in bit order, r = random.choice's draw
-            const int mi = (int)rng_below_pick(rng, cnt, sel_table(s_order) + 8u * (u & 0x7Fu));
-            u &= ~(1u << mi);
+        // ---- m draws (random.choice over cnt, cnt-1, ... untried moves)
+        const int m = min((int)cnt, nb - j);
+        uint32_t picks = 0, ucl = 0;
+        inv = 0;
+        {
+            int done = 0;
+            uint32_t n = cnt;
+            for (;;) {  // one 64-word view per pass
+                if (rng.off >= (uint32_t)kWin) rng_advance(rng);
+                const uint32_t w = rng_view(rng);  // lane l: word off + l
+                uint64_t gt = ~0ull;               // lanes after the last accepted word
+                int f = -1;
+                for (; done < m; ++done, --n) {
+                    const uint32_t sh = (uint32_t)__clz(n);
+                    const uint64_t A = __ballot((w >> sh) < n) & gt;
+                    if (!A) break;
+                    f = __builtin_ctzll(A);
+                    gt = (uint64_t)0 - (2ull << f);
+                    // the r-th untried move (r = the draw), erased from the list
+                    const uint32_t r = (uint32_t)__builtin_amdgcn_readlane((int)w, f) >> sh;
+                    const uint32_t mi = (ul >> (3 * r)) & 7u;
+                    const uint32_t lowm = (1u << (3 * r)) - 1u;
+                    ul = (ul & lowm) | ((ul >> 3) & ~lowm);
+                    picks |= mi << (3 * done);
+                    inv |= (8u | (uint32_t)done) << (4 * mi);
+                    ucl |= 1u << mi;
+                }
+                if (done < m) {  // the view ran out: all of it is consumed
+                    rng.off += (uint32_t)kWin;
+                    continue;
+                }
+                rng.off += (uint32_t)f + 1u;
+                break;
+            }
+        }
+        u &= ~ucl;
+        // ---- the m children and their leaves, lane i = draw i
+        {
+            const uint32_t li = lane & 7u;
+            const uint32_t mi = (picks >> (3 * li)) & 7u;
             const int col = (int)((ow >> (3 * mi)) & 7u);
             const uint64_t bit = drop_bit(b0 | b1, col);
-            if (turn) l1 |= bit; else l0 |= bit;
-            lturn = turn ^ 1;
-            leaf = nnodes++;
-            ldepth = depth + 1;
-            low_ = ow;  // the leaf's legal set is the node's unless the column filled
-            if (bit & kTop) {
-                lmask &= ~(1 << col);
-                low_ = uni(s_order[lmask]);
+            const bool filled = (bit & kTop) != 0;
+            c_lmask = (uint32_t)cmask & ~(filled ? (1u << col) : 0u);
+            c_low = ow;
+            if ((int)lane < m && filled) c_low = s_order[c_lmask];
+            const int ldepth = depth + 1;
+            const uint32_t leaf = (uint32_t)nnodes + lane;
+            if ((int)lane < m) {
+                *(uint4 *)&fresh[leaf - (uint32_t)f0] =
+                    make_uint4(untried_init((c_low >> 24) & 15u), c_low,
+                               (uint32_t)node | (mi << 16) | ((uint32_t)ldepth << 24), c_lmask);
+                const uint64_t l0 = turn ? b0 : (b0 | bit), l1 = turn ? (b1 | bit) : b1;
+                leaves[j + (int)lane] = Leaf{l0, l1,
+                                             leaf | ((uint32_t)ldepth << 16) | ((uint32_t)(turn ^ 1) << 24) | (c_lmask << 25),
+                                             0, c_low, 0};
             }
-            if (k == (uint32_t)mi) ch = (uint32_t)leaf;
-            if (node < f0) x0_dirty = true;  // X0 itself: written back when the flush is published
-            // Node(state, legal_moves) (mcts.cpp:23-34): all moves untried, no children.
-            // Uniform values to one address: every lane stores (no EXEC branches).
-            *(uint4 *)&fresh[leaf - f0] =
-                make_uint4(untried_init((low_ >> 24) & 15u), low_,
-                           (uint32_t)node | ((uint32_t)mi << 16) | ((uint32_t)ldepth << 24), (uint32_t)lmask);
-            if (node >= f0) {  // the parent's copy in LDS
-                fresh[node - f0].u = u;
-                fresh[node - f0].ch[mi] = (uint16_t)leaf;
+            // leaf j+i's path: the walk's path plus the new node (all 64 lanes store: lanes
+            // >= kMaxDepth spill into the next leaf's path, written after this, or the spill bytes)
+            for (int i = 0; i < m; ++i)
+                paths[(j + i) * kMaxDepth + lane] = (uint16_t)(lane == (uint32_t)ldepth ? (uint32_t)(nnodes + i) : pathv);
+            // the node's new children
+            const uint32_t pk = (inv >> (4 * k)) & 15u;
+            if (pk & 8u) ch = (uint32_t)nnodes + (pk & 7u);
+            if (node >= f0) {  // the node's copy in LDS
+                if (lane == 0) fresh[node - f0].u = u;
+                if (lane < 8 && (pk & 8u)) fresh[node - f0].ch[k] = (uint16_t)ch;
+            } else {
+                x0_dirty = true;  // X0 itself: written back when the flush is published
             }
+            wave_mem_order();
         }
-        // the leaf's path: the walk's path plus the new node (the next walk resumes at `node`)
-        const uint32_t lpath = (cnt && lane == (uint32_t)ldepth) ? (uint32_t)leaf : pathv;
-        leaves[j] = Leaf{l0, l1, (uint32_t)leaf | ((uint32_t)ldepth << 16) | ((uint32_t)lturn << 24) | ((uint32_t)lmask << 25),
-                         0, low_, 0};
-        // all 64 lanes store: lanes >= kMaxDepth spill into leaf j+1's path (written after
-        // this) or, for the flush's last leaf, into the kPathSpill bytes that follow the paths
-        paths[j * kMaxDepth + lane] = (uint16_t)lpath;
-        wave_mem_order();
+        bulk0 = nnodes;
+        nnodes += m;
+        j += m;
         stamp.mark(3);
     }
     if (node == x0node) {

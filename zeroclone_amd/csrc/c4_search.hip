@@ -139,7 +139,8 @@ __device__ __forceinline__ uint32_t row_prev(uint32_t x) {
             t_ = now_;                                              \
         }                                                           \
     } while (0)
-__device__ void c4_rollouts(Leaf *L, int nb, Rng &rng, const uint32_t *s_order, Counters &cn,
+template <class R>
+__device__ void c4_rollouts(Leaf *L, int nb, R &rng, const uint32_t *s_order, Counters &cn,
                             uint64_t *sub = nullptr) {
     uint64_t t_ = ZC_RSTAMP && sub ? __builtin_amdgcn_s_memtime() : 0;
     const uint32_t lane = lane_id();
@@ -368,28 +369,38 @@ __device__ void c4_rollouts_philox(Leaf *L, int nb, const uint8_t *s_sel, uint2 
 }
 
 // ------------------------------------------------------------------ the search kernel
+constexpr int kSearchWaves = 4;  // games (waves) per workgroup
+__host__ __device__ constexpr size_t c4_search_wave_lds(int bs) {
+    return ((size_t)kLRingBytes + (sizeof(Leaf) + sizeof(Fresh) + sizeof(uint16_t) * kMaxDepth) * (size_t)bs +
+            kPathSpill + 15) & ~(size_t)15;
+}
+
 // STAMP = diagnostic build: lane 0 adds s_memtime deltas per phase into p.a.phase[g][0..7] =
 // {rng generation at flush start, first walk of a flush, resumed walks, expansion + leaf
 //  bookkeeping, rollouts, backup, publish, -}.
 template <bool STAMP, bool PHILOX>
-__global__ __launch_bounds__(kBlock) void c4_search_kernel(SearchParams p) {
+__global__ __launch_bounds__(kSearchWaves * kBlock) void c4_search_kernel(SearchParams p) {
     extern __shared__ __attribute__((aligned(16))) uint8_t s_dyn[];
-    // LDS: order[128] u32, fresh[bs] (48 B), leaves[bs] (24 B),
+    // LDS: order[128] u32 + sel[128][8] (the workgroup's tables), then per wave (game):
+    //      MT ring (1024 raw words), fresh[bs] (48 B), leaves[bs] (24 B),
     //      paths[bs][kMaxDepth] (u16 node ids)
     uint32_t *const s_order = (uint32_t *)s_dyn;
-    Fresh *const fresh = (Fresh *)(s_dyn + kTabBytes);
-    Leaf *const leaves = (Leaf *)(s_dyn + kTabBytes + sizeof(Fresh) * (size_t)p.bs);
-    uint16_t *const paths = (uint16_t *)(s_dyn + kTabBytes + (sizeof(Fresh) + sizeof(Leaf)) * (size_t)p.bs);
+    const uint32_t wave = threadIdx.x >> 6;
+    uint8_t *const s_wave = s_dyn + kTabBytes + (size_t)wave * c4_search_wave_lds(p.bs);
+    uint32_t *const s_ring = (uint32_t *)s_wave;
+    Fresh *const fresh = (Fresh *)(s_wave + kLRingBytes);
+    Leaf *const leaves = (Leaf *)(s_wave + kLRingBytes + sizeof(Fresh) * (size_t)p.bs);
+    uint16_t *const paths = (uint16_t *)(s_wave + kLRingBytes + (sizeof(Fresh) + sizeof(Leaf)) * (size_t)p.bs);
     const uint8_t *const s_sel = sel_table(s_order);
     load_tables(s_order);
     __syncthreads();
     // log(N) table read through the constant address space: uniform index -> scalar loads,
-    // which do not sit in the vector-memory counter the walk and the RNG window wait on.
+    // which do not sit in the vector-memory counter the walk waits on.
     ConstDouble *logtab = (ConstDouble *)p.a.logtab;
 
     const uint32_t lane = lane_id();
     const uint32_t k = lane & 7u;
-    const int gl = blockIdx.x;  // game within this call (one wave per game)
+    const int gl = (int)(blockIdx.x * (blockDim.x >> 6) + wave);  // game within this call (one wave per game)
     if (gl >= p.n_games) return;
     const int g = p.game_ids ? uni(p.game_ids[gl]) : p.first_game + gl;
 
@@ -412,9 +423,10 @@ __global__ __launch_bounds__(kBlock) void c4_search_kernel(SearchParams p) {
     const Arena &a = p.a;
     const Tree t{a.nodes + (size_t)g * p.M * kRecBytes, a.W + (size_t)g * p.M * kSlots};
 
-    Rng rng;
-    rng_open(rng, a.ring + (size_t)g * kRingWords, uni64(a.rngpos[2 * (size_t)g]), uni64(a.rngpos[2 * (size_t)g + 1]));
-    const uint32_t tag = uni((uint32_t)a.rngpos[2 * (size_t)g]);  // Philox mode: stream per move
+    LRng rng;
+    const uint64_t use0 = uni64(a.rngpos[2 * (size_t)g]);
+    lrng_open(rng, s_ring, a.ring + (size_t)g * kRingWords, use0, uni64(a.rngpos[2 * (size_t)g + 1]));
+    const uint32_t tag = uni((uint32_t)use0);  // Philox mode: stream per move
     Counters cn;
     int status = 0;
 
@@ -428,7 +440,6 @@ __global__ __launch_bounds__(kBlock) void c4_search_kernel(SearchParams p) {
     Stamp<STAMP> stamp;
     for (int done = 0; done < p.sims;) {
         const int nb = min(p.bs, p.sims - done);
-        rng_fill(rng, rng.use() + kLookahead);
         stamp.mark(0);
 
         // ---- selection + expansion of nb leaves (mcts.cpp:129-147) -------------------------
@@ -570,8 +581,8 @@ __global__ __launch_bounds__(kBlock) void c4_search_kernel(SearchParams p) {
         st.rollout_blocks = cn.blocks;
         st.rng_words = rng.use();
         p.out_stats[gl] = st;
-        rng_close(rng, a.rngpos[2 * (size_t)g], a.rngpos + 2 * (size_t)g);
     }
+    lrng_close(rng, a.ring + (size_t)g * kRingWords, use0, a.rngpos + 2 * (size_t)g);
 }
 
 // ------------------------------------------------------------------ small kernels
@@ -670,13 +681,21 @@ __global__ void uct_debug_kernel(int n, const double *logn, const int32_t *na, c
 
 }  // namespace
 
-size_t c4_search_lds_bytes(int bs) {
-    return kTabBytes + (sizeof(Leaf) + sizeof(Fresh) + sizeof(uint16_t) * kMaxDepth) * (size_t)bs + kPathSpill;
+// Games per workgroup: up to kSearchWaves share the tables (4 x ~9.3 KB + 1.5 KB at bs 32, so
+// four workgroups = 16 waves per CU fit the CU's 160 KB of LDS); fewer when a large batch
+// would not fit one workgroup (sharing only lowers the LDS per game).
+static int c4_search_wpg(int bs) {
+    int w = kSearchWaves;
+    while (w > 1 && kTabBytes + (size_t)w * c4_search_wave_lds(bs) > (size_t)(160 * 1024)) w >>= 1;
+    return w;
 }
 
+size_t c4_search_lds_bytes(int bs) { return kTabBytes + (size_t)c4_search_wpg(bs) * c4_search_wave_lds(bs); }
+
 void launch_c4_search(const SearchParams &p, hipStream_t s) {
+    const int wpg = c4_search_wpg(p.bs);
     const size_t lds = c4_search_lds_bytes(p.bs);
-    const dim3 grid(p.n_games), block(kBlock);
+    const dim3 grid((p.n_games + wpg - 1) / wpg), block(wpg * kBlock);
     if (p.philox) {
         if (p.stamp)
             hipLaunchKernelGGL((c4_search_kernel<true, true>), grid, block, lds, s, p);
