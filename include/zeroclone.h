@@ -181,6 +181,34 @@ int zc_c4_ext_backup(zc_engine *eng, int32_t first_game, int32_t n_games, int32_
 int zc_c4_ext_end(zc_engine *eng, int32_t first_game, int32_t n_games, int32_t *d_out_move, int32_t *d_out_root_na,
                   zc_game_stats *d_out_stats, void *hip_stream);
 
+/* ---- Connect4 stepwise search with a HOST policy (any Python callable) ---------------
+ * The §8(b) fallback for a Policy that is neither Policy('random') nor
+ * Policy('immediate_value'): mcts.cpp's expand (:65-78) calls policy(untried_moves) once
+ * per expansion, so inside a zc_c4_ext_begin .. end search each simulation of flush f is
+ *
+ *   zc_c4_hp_walk(eng, game, f, j, d_node)      select (mcts.cpp:47-63) from the root over
+ *                                                the device tree -> the node, its position and
+ *                                                its untried moves (columns, list order)
+ *   k = index of policy(untried) in untried      (caller, e.g. Python)
+ *   zc_c4_hp_expand(eng, game, f, j, k, d_leaf) expand (mcts.cpp:65-78) with the k-th untried
+ *                                                move (ignored when the node has none), leaf j
+ *                                                of the pending flush -> d_leaf
+ *
+ * for j = 0 .. leaves of the flush - 1, then zc_c4_ext_backup(eng, game, 1, f, values) as
+ * usual.  The engine's RNG stream is not used (the caller's policy and value own theirs).
+ * One game per call; every call only enqueues on hip_stream. */
+typedef struct zc_c4_hp_node {
+    zc_c4_state state;   /* position of the node the walk stopped at */
+    int32_t node;        /* its id in the game's tree */
+    int32_t n_untried;   /* untried moves (0: no legal move, the node itself becomes the leaf) */
+    int32_t depth;       /* plies below the root */
+    int32_t untried[7];  /* columns of the untried moves, in the node's move-list order */
+} zc_c4_hp_node;
+int zc_c4_hp_walk(zc_engine *eng, int32_t game, int32_t flush, int32_t leaf, zc_c4_hp_node *d_node,
+                  void *hip_stream);
+int zc_c4_hp_expand(zc_engine *eng, int32_t game, int32_t flush, int32_t leaf, int32_t untried_index,
+                    zc_c4_state *d_leaf, void *hip_stream);
+
 /* ---- Connect4 rules on the host (engine/games/connect4/c4_backend.py) --------------- */
 /* rows: 42 chars, row 0 = top, 'X', 'O', anything else = empty. */
 int zc_c4_from_rows(const char *rows42, int32_t turn, zc_c4_state *out);

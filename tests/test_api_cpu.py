@@ -64,7 +64,7 @@ def test_unsupported_plugins_fail_loudly():
     with pytest.raises(NotImplementedError):
         Value("mystery_value")
     v = Value("random_rollout")
-    with pytest.raises(NotImplementedError):
+    with pytest.raises(AttributeError):   # as the reference's Policy.__call__ getattr fails
         mcts.get_move(c4.create_init_state(), v, Policy("mystery_policy"), c4, 10)
     with pytest.raises(NotImplementedError):   # chess value on a Connect4 game
         mcts.get_move(c4.create_init_state(), Value("crude_chess_score"), Policy("random"), c4, 10)

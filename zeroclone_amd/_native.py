@@ -57,6 +57,9 @@ ZC_TRAJ_POSITIONS, ZC_TRAJ_GAMES, ZC_TRAJ_NEXT, ZC_TRAJ_QUOTA, ZC_TRAJ_FINISHED,
 ZC_SLOT_IDLE = 3
 
 C4_STATE_DTYPE = np.dtype([("stones", "<u8", (2,)), ("turn", "<i4"), ("reserved", "<i4")])
+# zc_c4_hp_node: the host-policy walk's end (include/zeroclone.h)
+C4_HP_NODE_DTYPE = np.dtype([("state", C4_STATE_DTYPE), ("node", "<i4"), ("n_untried", "<i4"), ("depth", "<i4"),
+                             ("untried", "<i4", (7,))])
 STATS_DTYPE = np.dtype([("expansions", "<i8"), ("depth_sum", "<i8"), ("leaves", "<i8"),
                         ("rollout_plies", "<i8"), ("rng_words", "<i8"), ("status", "<i8"),
                         ("rollout_blocks", "<i8"), ("reserved", "<i8")])
@@ -112,6 +115,10 @@ SIGNATURES = [
                                         ctypes.c_void_p]),
     ("zc_c4_ext_backup", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
                                         ctypes.c_void_p, ctypes.c_void_p]),
+    ("zc_c4_hp_walk", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p,
+                                     ctypes.c_void_p]),
+    ("zc_c4_hp_expand", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                       ctypes.c_void_p, ctypes.c_void_p]),
     ("zc_c4_ext_end", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p,
                                      ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     ("zc_c4_rollouts", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p,
@@ -385,6 +392,14 @@ class NativeEngine:
     def c4_ext_backup(self, first_game: int, n: int, flush: int, d_values: int, stream: int = 0) -> None:
         check(lib().zc_c4_ext_backup(self._h, first_game, n, int(flush), ctypes.c_void_p(d_values),
                                      ctypes.c_void_p(stream or None)))
+
+    def c4_hp_walk(self, game: int, flush: int, leaf: int, d_node: int, stream: int = 0) -> None:
+        check(lib().zc_c4_hp_walk(self._h, game, int(flush), int(leaf), ctypes.c_void_p(d_node),
+                                  ctypes.c_void_p(stream or None)))
+
+    def c4_hp_expand(self, game: int, flush: int, leaf: int, index: int, d_leaf: int = 0, stream: int = 0) -> None:
+        check(lib().zc_c4_hp_expand(self._h, game, int(flush), int(leaf), int(index), ctypes.c_void_p(d_leaf or None),
+                                    ctypes.c_void_p(stream or None)))
 
     def c4_ext_end(self, first_game: int, n: int, d_move: int, d_na: int, d_stats: int, stream: int = 0) -> None:
         check(lib().zc_c4_ext_end(self._h, first_game, n, ctypes.c_void_p(d_move), ctypes.c_void_p(d_na),

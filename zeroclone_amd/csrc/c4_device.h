@@ -488,36 +488,22 @@ struct FlushSel {
     uint32_t x_u, x_ch;  // X0's untried word / child slot `lane & 7` as last seen
 };
 
-// select + expand of the nb leaves of one flush (mcts.cpp:129-147), shared by the fused
-// rollout search and the stepwise search.
-//
-// No backup happens inside a flush, so (1) the UCT path from the root to the node X0 where
-// the flush's first walk stops is shared by every leaf of the flush (each walk resumes where
-// the previous one expanded, always at or below X0), and (2) every node below X0 is created
-// in this flush ("fresh": id >= f0, Na = W = 0 on every edge).  The reference's walk from a
-// node without untried moves takes the first child with the largest UCT; an unvisited child
-// scores +inf, so below X0 that is simply the lowest slot holding a fresh child — no
-// arithmetic, no HBM.  Fresh nodes live in LDS (`fresh`) until the caller publishes them.
-// Leaf j goes to leaves[j] (board, node, depth, turn, legal mask) and its path (node ids of
-// levels 0..depth) to paths[j][*].
-//
+// The walk from the root over HBM records (select, mcts.cpp:47-63): the UCT child (first
+// maximum, +inf for an unvisited edge) until a node with untried moves or without children.
 // QW = false: the record's +64 slots hold Q (rollout mode, W in the side array);
 // QW = true:  they hold W in fp64 and Q = W / Na is formed here — the same IEEE quotient
 //             mcts.cpp:95 stores, so the UCT inputs are bit-identical.
-template <bool QW, bool STAMP, class RNG>
-__device__ __forceinline__ void select_flush(const Tree &t, Fresh *fresh, Leaf *leaves, uint16_t *paths,
-                                             const uint32_t *s_order, ConstDouble *logtab,
-                                             RNG &rng, Counters &cn, Stamp<STAMP> &stamp, int &nnodes, int &status,
-                                             uint64_t rp0, uint64_t rp1, int rturn, int done, int nb, double c,
-                                             FlushSel &fs) {
+struct WalkEnd {
+    int node, depth, turn;
+    uint64_t b0, b1;     // the node's position
+    uint32_t pathv;      // lane l (l <= depth): level l of the path = node | slot << 16
+    uint32_t u, ow, ch;  // the node's record (ch: slot lane & 7)
+};
+template <bool QW>
+__device__ __forceinline__ WalkEnd walk_hbm(const Tree &t, ConstDouble *logtab, uint64_t rp0, uint64_t rp1,
+                                            int rturn, int done, double c, int &status) {
     const uint32_t lane = lane_id();
-    const uint32_t k = lane & 7u;  // child slot handled by this lane (lanes 8.. mirror 0..7)
-    const int f0 = nnodes;
-    for (int i = (int)lane; i < nb; i += 64) {  // fresh slots: no children, zero in-edge counters
-        fresh[i].na = 0;
-        fresh[i].w = 0;
-        *(uint4 *)fresh[i].ch = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
-    }
+    const uint32_t k = lane & 7u;
     int node = 0, depth = 0, turn = rturn, nN = done;  // nN = N(node) = Na of its in-edge
     uint64_t b0 = rp0, b1 = rp1;
     uint32_t pathv = (lane == 0) ? 0x00FF0000u : 0u;
@@ -561,6 +547,39 @@ __device__ __forceinline__ void select_flush(const Tree &t, Fresh *fresh, Leaf *
         ++depth;
         if (lane == (uint32_t)depth) pathv = (uint32_t)node | ((uint32_t)best << 16);
     }
+    return WalkEnd{node, depth, turn, b0, b1, pathv, u, ow, ch};
+}
+
+// select + expand of the nb leaves of one flush (mcts.cpp:129-147), shared by the fused
+// rollout search and the stepwise search.
+//
+// No backup happens inside a flush, so (1) the UCT path from the root to the node X0 where
+// the flush's first walk stops is shared by every leaf of the flush (each walk resumes where
+// the previous one expanded, always at or below X0), and (2) every node below X0 is created
+// in this flush ("fresh": id >= f0, Na = W = 0 on every edge).  The reference's walk from a
+// node without untried moves takes the first child with the largest UCT; an unvisited child
+// scores +inf, so below X0 that is simply the lowest slot holding a fresh child — no
+// arithmetic, no HBM.  Fresh nodes live in LDS (`fresh`) until the caller publishes them.
+// Leaf j goes to leaves[j] (board, node, depth, turn, legal mask) and its path (node ids of
+// levels 0..depth) to paths[j][*].  QW: as walk_hbm.
+template <bool QW, bool STAMP, class RNG>
+__device__ __forceinline__ void select_flush(const Tree &t, Fresh *fresh, Leaf *leaves, uint16_t *paths,
+                                             const uint32_t *s_order, ConstDouble *logtab,
+                                             RNG &rng, Counters &cn, Stamp<STAMP> &stamp, int &nnodes, int &status,
+                                             uint64_t rp0, uint64_t rp1, int rturn, int done, int nb, double c,
+                                             FlushSel &fs) {
+    const uint32_t lane = lane_id();
+    const uint32_t k = lane & 7u;  // child slot handled by this lane (lanes 8.. mirror 0..7)
+    const int f0 = nnodes;
+    for (int i = (int)lane; i < nb; i += 64) {  // fresh slots: no children, zero in-edge counters
+        fresh[i].na = 0;
+        fresh[i].w = 0;
+        *(uint4 *)fresh[i].ch = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
+    }
+    WalkEnd we = walk_hbm<QW>(t, logtab, rp0, rp1, rturn, done, c, status);
+    int node = we.node, depth = we.depth, turn = we.turn;
+    uint64_t b0 = we.b0, b1 = we.b1;
+    uint32_t pathv = we.pathv, u = we.u, ow = we.ow, ch = we.ch;
     int cmask = legal_mask(b0 | b1);  // legal columns of the current node
     const int x0node = node;
     bool x0_dirty = false;

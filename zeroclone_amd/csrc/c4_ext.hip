@@ -18,6 +18,10 @@
 namespace zc {
 namespace {
 
+__device__ __forceinline__ uint32_t mbcnt_lo(uint64_t m) {  // set bits of m in lanes below this one
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
 __device__ __forceinline__ Tree ext_tree(const ExtParams &p, int g) {
     return Tree{p.a.nodes + (size_t)g * p.M * kRecBytes, p.a.W + (size_t)g * p.M * kSlots};
 }
@@ -261,7 +265,132 @@ __global__ __launch_bounds__(kBlock) void c4_ext_end_kernel(ExtParams p) {
     }
 }
 
+// ---- host-policy search (zc_c4_hp_*, the §8(b) fallback for any policy callable) --------
+// One game, one simulation at a time: walk (select over the HBM tree, fresh children of the
+// pending flush included — their edges have Na = 0, so UCT takes them first exactly as in
+// mcts.cpp:41-45), the caller's policy picks among the untried moves, expand.  The pending
+// flush is kept in the stepwise search's format (ctl F0 / D0 / path, ext_paths, ext_meta),
+// so zc_c4_ext_backup applies it.
+__global__ __launch_bounds__(kBlock) void c4_hp_walk_kernel(ExtParams p) {
+    const uint32_t lane = lane_id();
+    const int g = p.first_game;
+    const Arena &a = p.a;
+    int32_t *ctl = a.ext_ctl + (size_t)g * kCtlWords;
+    int status = uni(ctl[kCtlStatus]);
+    zc_c4_hp_node *out = p.hp_node;
+    if (status) {
+        if (lane == 0) {
+            out->node = -1;
+            out->n_untried = 0;
+            out->depth = 0;
+        }
+        return;
+    }
+    const Tree t = ext_tree(p, g);
+    const zc_c4_state root = a.ext_roots[g];
+    const WalkEnd we = walk_hbm<true>(t, (ConstDouble *)a.logtab, uni64(root.stones[0]), uni64(root.stones[1]),
+                                      uni(root.turn), p.flush * p.bs, p.c, status);
+    const size_t lbase = (size_t)g * p.max_batch;
+    if (lane <= (uint32_t)we.depth) a.ext_paths[(lbase + p.hp_leaf) * kMaxDepth + lane] = (uint16_t)we.pathv;
+    if (p.hp_leaf == 0) {  // the flush's X0: its prefix path is every leaf's (backup)
+        if (lane <= (uint32_t)we.depth) ctl[kCtlPath + lane] = (int32_t)we.pathv;
+        if (lane == 0) {
+            ctl[kCtlD0] = we.depth;
+            ctl[kCtlF0] = ctl[kCtlNodes];
+        }
+    }
+    const uint32_t cnt = status ? 0u : untried_count(we.u);
+    // the untried moves' columns in list order: bit l of the untried word is move l
+    const bool in = lane < 7 && ((we.u >> lane) & 1u);
+    const uint32_t rank = mbcnt_lo(__ballot(in));
+    if (in) out->untried[rank] = (int32_t)((we.ow >> (3 * lane)) & 7u);
+    if (lane < 7 && lane >= cnt) out->untried[lane] = -1;
+    if (lane == 0) {
+        out->state.stones[0] = we.b0;
+        out->state.stones[1] = we.b1;
+        out->state.turn = we.turn;
+        out->state.reserved = 0;
+        out->node = we.node;
+        out->n_untried = (int32_t)cnt;
+        out->depth = we.depth;
+        ctl[kCtlHpNode] = we.node;
+        ctl[kCtlHpNode + 1] = we.depth | (we.turn << 8);
+        ctl[kCtlHpNode + 2] = (int32_t)(uint32_t)we.b0;
+        ctl[kCtlHpNode + 3] = (int32_t)(uint32_t)(we.b0 >> 32);
+        ctl[kCtlHpNode + 4] = (int32_t)(uint32_t)we.b1;
+        ctl[kCtlHpNode + 5] = (int32_t)(uint32_t)(we.b1 >> 32);
+        ctl[kCtlStatus] = status;
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void c4_hp_expand_kernel(ExtParams p) {
+    const uint32_t lane = lane_id();
+    const int g = p.first_game;
+    const Arena &a = p.a;
+    int32_t *ctl = a.ext_ctl + (size_t)g * kCtlWords;
+    if (uni(ctl[kCtlStatus])) return;
+    const Tree t = ext_tree(p, g);
+    const int node = uni(ctl[kCtlHpNode]);
+    const int dt = uni(ctl[kCtlHpNode + 1]);
+    const int depth = dt & 0xFF, turn = (dt >> 8) & 1;
+    const uint64_t b0 = (uint64_t)(uint32_t)uni(ctl[kCtlHpNode + 2]) | ((uint64_t)(uint32_t)uni(ctl[kCtlHpNode + 3]) << 32);
+    const uint64_t b1 = (uint64_t)(uint32_t)uni(ctl[kCtlHpNode + 4]) | ((uint64_t)(uint32_t)uni(ctl[kCtlHpNode + 5]) << 32);
+    const uint32_t u = uni(t.hdr(node)[1]);
+    const uint32_t ow = uni(t.hdr(node)[3]);
+    const uint32_t cnt = untried_count(u);
+    int nnodes = uni(ctl[kCtlNodes]);
+    int leaf = node, ldepth = depth, lturn = turn;
+    uint64_t l0 = b0, l1 = b1;
+    if (cnt) {
+        if (p.hp_index < 0 || p.hp_index >= (int)cnt) {
+            if (lane == 0) ctl[kCtlStatus] = ZC_STATUS_INTERNAL;
+            return;
+        }
+        // expand (mcts.cpp:65-78): the hp_index-th untried move in list order
+        const bool in = lane < 7 && ((u >> lane) & 1u);
+        const uint32_t rank = mbcnt_lo(__ballot(in));
+        const int mi = __builtin_ctzll(__ballot(in && rank == (uint32_t)p.hp_index));
+        const int col = (int)((ow >> (3 * mi)) & 7u);
+        const uint64_t bit = drop_bit(b0 | b1, col);
+        if (turn) l1 |= bit; else l0 |= bit;
+        lturn = turn ^ 1;
+        ldepth = depth + 1;
+        leaf = nnodes++;
+        node_init(t, leaf, node, mi, ldepth, uni(d_order[legal_mask(l0 | l1)]));
+        if (lane == 0) {
+            t.hdr(node)[1] = u & ~(1u << mi);
+            t.child(node)[mi] = (uint16_t)leaf;
+            a.ext_paths[((size_t)g * p.max_batch + p.hp_leaf) * kMaxDepth + ldepth] = (uint16_t)leaf;
+            ctl[kCtlExp] += 1;
+            ctl[kCtlDepth] += ldepth;
+        }
+    }
+    if (lane == 0) {
+        const uint32_t lmask = (uint32_t)legal_mask(l0 | l1);
+        a.ext_meta[(size_t)g * p.max_batch + p.hp_leaf] =
+            (uint32_t)leaf | ((uint32_t)ldepth << 16) | ((uint32_t)lturn << 24) | (lmask << 25);
+        if (p.leaves) {
+            zc_c4_state s;
+            s.stones[0] = l0;
+            s.stones[1] = l1;
+            s.turn = lturn;
+            s.reserved = 0;
+            p.leaves[0] = s;
+        }
+        ctl[kCtlNodes] = nnodes;
+        ctl[kCtlNb] = p.hp_leaf + 1;
+    }
+}
+
 }  // namespace
+
+void launch_c4_hp_walk(const ExtParams &p, hipStream_t s) {
+    hipLaunchKernelGGL(c4_hp_walk_kernel, dim3(1), dim3(kBlock), 0, s, p);
+}
+
+void launch_c4_hp_expand(const ExtParams &p, hipStream_t s) {
+    hipLaunchKernelGGL(c4_hp_expand_kernel, dim3(1), dim3(kBlock), 0, s, p);
+}
 
 void launch_c4_ext_begin(const ExtParams &p, hipStream_t s) {
     hipLaunchKernelGGL(c4_ext_begin_kernel, dim3(p.n_games), dim3(kBlock), 0, s, p);

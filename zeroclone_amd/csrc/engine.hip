@@ -1,6 +1,7 @@
 // engine.hip — host side of the C-ABI (include/zeroclone.h): engine arena in HBM, per-game
 // CPython-compatible random streams, argument checking, and the synchronous / stream-
 // ordered search entry points.
+#include <algorithm>
 #include <math.h>
 #include <stdarg.h>
 #include <stdio.h>
@@ -493,6 +494,44 @@ int zc_c4_ext_end(zc_engine *eng, int32_t first, int32_t n, int32_t *d_move, int
     p.out_na = d_na;
     p.out_stats = d_stats;
     zc::launch_c4_ext_end(p, (hipStream_t)hip_stream);
+    ZC_HIP(hipGetLastError());
+    return ZC_OK;
+}
+
+int zc_c4_hp_walk(zc_engine *eng, int32_t game, int32_t flush, int32_t leaf, zc_c4_hp_node *d_node,
+                  void *hip_stream) {
+    if (!eng || !d_node) return fail(ZC_EINVAL, "null argument");
+    std::lock_guard<std::mutex> lk(eng->mu);
+    if (int r = check_ext_range(eng, game, 1)) return r;
+    if (int r = check_flush(eng, flush)) return r;
+    const int nb = std::min(eng->ext_bs, eng->ext_sims - flush * eng->ext_bs);
+    if (leaf < 0 || leaf >= nb) return fail(ZC_EINVAL, "leaf %d outside flush %d's [0, %d)", leaf, flush, nb);
+    ZC_HIP(hipSetDevice(eng->cfg.device));
+    zc::ExtParams p = ext_params(eng, game, 1);
+    p.flush = flush;
+    p.hp_leaf = leaf;
+    p.hp_node = d_node;
+    zc::launch_c4_hp_walk(p, (hipStream_t)hip_stream);
+    ZC_HIP(hipGetLastError());
+    return ZC_OK;
+}
+
+int zc_c4_hp_expand(zc_engine *eng, int32_t game, int32_t flush, int32_t leaf, int32_t untried_index,
+                    zc_c4_state *d_leaf, void *hip_stream) {
+    if (!eng) return fail(ZC_EINVAL, "null argument");
+    std::lock_guard<std::mutex> lk(eng->mu);
+    if (int r = check_ext_range(eng, game, 1)) return r;
+    if (int r = check_flush(eng, flush)) return r;
+    const int nb = std::min(eng->ext_bs, eng->ext_sims - flush * eng->ext_bs);
+    if (leaf < 0 || leaf >= nb) return fail(ZC_EINVAL, "leaf %d outside flush %d's [0, %d)", leaf, flush, nb);
+    if (untried_index < -1 || untried_index > 6) return fail(ZC_EINVAL, "untried index %d outside [-1, 7)", untried_index);
+    ZC_HIP(hipSetDevice(eng->cfg.device));
+    zc::ExtParams p = ext_params(eng, game, 1);
+    p.flush = flush;
+    p.hp_leaf = leaf;
+    p.hp_index = untried_index;
+    p.leaves = d_leaf;
+    zc::launch_c4_hp_expand(p, (hipStream_t)hip_stream);
     ZC_HIP(hipGetLastError());
     return ZC_OK;
 }

@@ -73,6 +73,8 @@ enum : int {
     kCtlExp = 6,     // expansions so far
     kCtlDepth = 7,   // sum of expansion depths
     kCtlUse0 = 8,    // (2 words) RNG position at begin
+    kCtlHpNode = 10, // host-policy search, the last walk's end: node, depth | turn << 8 (word 11),
+                     // position s0 lo/hi, s1 lo/hi (words 12..15)
     kCtlPath = 16,   // [kMaxDepth] root..X0: node | slot << 16
     kCtlWords = 64,
 };
@@ -103,6 +105,9 @@ struct ExtParams {
     const double *values;      // backup
     int32_t *out_move, *out_na;
     zc_game_stats *out_stats;  // end
+    // host-policy stepwise search (zc_c4_hp_*): leaf index in the flush, untried index, node out
+    int hp_leaf, hp_index;
+    zc_c4_hp_node *hp_node;
 };
 
 // ---------------------------------------------------------------- chess tree search
@@ -247,6 +252,8 @@ void launch_c4_ext_begin(const ExtParams &p, hipStream_t s);
 void launch_c4_ext_select(const ExtParams &p, hipStream_t s);
 void launch_c4_ext_backup(const ExtParams &p, hipStream_t s);
 void launch_c4_ext_end(const ExtParams &p, hipStream_t s);
+void launch_c4_hp_walk(const ExtParams &p, hipStream_t s);
+void launch_c4_hp_expand(const ExtParams &p, hipStream_t s);
 void launch_c4_search(const SearchParams &p, hipStream_t s);
 void launch_c4_rollout_debug(const Arena &a, int M, int first_game, int n, const zc_c4_state *states,
                              int32_t *out_value, int64_t *out_words, hipStream_t s);

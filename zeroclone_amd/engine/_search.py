@@ -10,6 +10,10 @@ Policy('random') and Policy('immediate_value', policy_freedom=f) run on the devi
 chess; Connect4 moves carry no capture value, so for Connect4 immediate_value picks among
 all untried moves exactly like random (policy_functions.py:14-17 with all values 0) and both
 map to the same device policy.
+
+Any other policy callable (SURVEY §8(b)'s fallback) runs the Connect4 search in host-policy
+mode: the tree stays on the device and every expansion calls policy(untried_moves) on the
+host, where mcts.cpp:65-78 calls it (zc_c4_hp_walk / zc_c4_hp_expand, `c4_host_policy_moves`).
 """
 from __future__ import annotations
 
@@ -35,13 +39,28 @@ def game_of(backend, state) -> str:
     raise NotImplementedError(f"backend {name!r}: only Connect4 and chess run on the MI355X search path")
 
 
+HOST_POLICY = -1   # any other callable: called on the host at each expansion
+
+
 def policy_of(policy):
+    from .policy_functions import Policy
     name = getattr(policy, "name", None) or "random"
-    if name == "random":
+    ours = isinstance(policy, Policy) and type(policy).random is Policy.random and \
+        type(policy).immediate_value is Policy.immediate_value
+    # the reference's own Policy objects (engine/policy_functions.py) are accepted as well
+    theirs = type(policy).__name__ == "Policy" and type(policy).__module__.endswith("policy_functions") and \
+        not isinstance(policy, Policy)
+    builtin = ours or theirs
+    if builtin and name == "random":
         return _native.ZC_POLICY_RANDOM, 0.0
-    if name == "immediate_value":
+    if builtin and name == "immediate_value":
         return _native.ZC_POLICY_IMMEDIATE_VALUE, float(getattr(policy, "args", {}).get("policy_freedom", 0))
-    raise NotImplementedError(f"policy {name!r}: only Policy('random') and Policy('immediate_value') run on the GPU")
+    if isinstance(policy, Policy) and not callable(getattr(policy, name, None)):
+        # the reference fails at the first expansion (policy_functions.py:7 getattr)
+        raise AttributeError(f"'{type(policy).__name__}' object has no attribute {name!r}")
+    if callable(policy):
+        return HOST_POLICY, 0.0
+    raise TypeError("a policy must be callable as policy(untried_moves) (policy_functions.py:6-8)")
 
 
 def value_kind(value) -> str:
@@ -67,6 +86,8 @@ def chess_moves(eng, ids, states, sims, c, bs, value, policy, backend):
     ((fr, fc, tr, tc), capture_value), None for a game with no legal move."""
     import torch
     pol, freedom = policy_of(policy)
+    if pol == HOST_POLICY:
+        raise NotImplementedError("a host policy callable runs on the Connect4 search only")
     kind = value_kind(value)
     n = len(ids)
     dev = torch.device("cuda", eng.device)
@@ -133,3 +154,52 @@ def c4_moves(eng, ids, roots, sims, c, bs, value, backend):
     if st[:, 5].any():
         raise ValueError(f"invalid root for the search (status {int(st[:, 5].max())})")
     return [(int(m), 0) for m in mv.cpu().numpy()]
+
+
+def c4_host_policy_moves(eng, ids, roots, sims, c, bs, value, policy, backend):
+    """The §8(b) fallback: mcts.get_move with an arbitrary policy callable.  Per game, per
+    simulation: zc_c4_hp_walk selects (mcts.cpp:47-63) on the device tree, the policy picks
+    among the untried moves on the host exactly as mcts.cpp:67-70 calls it (the untried moves
+    as a list in the node's order; the action's list.index), zc_c4_hp_expand expands; each
+    flush's leaves go to value.batch (mcts.cpp:116) and zc_c4_ext_backup.  Python's `random`
+    is used only by the policy and the value themselves, in the reference's order."""
+    import torch
+    from .games.connect4 import c4_backend as zb
+    dev = torch.device("cuda", eng.device)
+    stream = torch.cuda.current_stream(dev)
+    s = stream.cuda_stream
+    node = torch.zeros(_native.C4_HP_NODE_DTYPE.itemsize, dtype=torch.uint8, device=dev)
+    leaf = torch.zeros(3, dtype=torch.int64, device=dev)
+    vals = torch.zeros(bs, dtype=torch.float64, device=dev)
+    mv = torch.zeros(1, dtype=torch.int32, device=dev)
+    na = torch.zeros((1, 7), dtype=torch.int32, device=dev)
+    st = torch.zeros((1, _native.STATS_FIELDS), dtype=torch.int64, device=dev)
+    out = []
+    for gi, root in zip(ids, roots):
+        r = torch.from_numpy(np.asarray([root], _native.C4_STATE_DTYPE).view(np.int64).reshape(1, 3).copy()).to(dev)
+        eng.c4_ext_begin(int(gi), 1, r.data_ptr(), sims, c, bs, s)
+        for f in range((sims + bs - 1) // bs):
+            nb = min(bs, sims - f * bs)
+            states = []
+            for j in range(nb):
+                eng.c4_hp_walk(int(gi), f, j, node.data_ptr(), s)
+                nd = node.cpu().numpy().view(_native.C4_HP_NODE_DTYPE)[0]
+                if int(nd["node"]) < 0:
+                    raise ValueError("invalid root for the search (bad state or no legal move)")
+                k = -1
+                n_un = int(nd["n_untried"])
+                if n_un:
+                    moves = [(int(col), 0) for col in nd["untried"][:n_un]]
+                    k = moves.index(policy(moves))
+                eng.c4_hp_expand(int(gi), f, j, k, leaf.data_ptr(), s)
+                row = leaf.cpu().numpy().view(np.uint64)
+                states.append(zb.from_zc(int(row[0]), int(row[1]), int(row[2]) & 1))
+            v = [float(x) for x in value.batch(states, backend=backend)]
+            vals[:nb].copy_(torch.tensor(v, dtype=torch.float64))
+            eng.c4_ext_backup(int(gi), 1, f, vals.data_ptr(), s)
+        eng.c4_ext_end(int(gi), 1, mv.data_ptr(), na.data_ptr(), st.data_ptr(), s)
+        stream.synchronize()
+        if int(st[0, 5].item()):
+            raise RuntimeError(f"host-policy search failed (status {int(st[0, 5].item())})")
+        out.append((int(mv[0].item()), 0))
+    return out

@@ -160,7 +160,7 @@ class Engine:
         game = None
         for v in {id(v): v for v in self.values}.values():
             game = _plugin_check(self.states[idxs[0]], v, self.policy, self.backend)
-        if self.rng_mode == "global":
+        if self.rng_mode == "global" or _search.policy_of(self.policy)[0] == _search.HOST_POLICY:
             return {i: get_move(self.states[i], self.values[self.states[i].turn], self.policy, self.backend,
                                 simulations, c, batch_size) for i in idxs}
         need = max(idxs) + 1

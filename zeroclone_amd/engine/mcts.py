@@ -10,7 +10,9 @@ stream is handed back advanced by exactly what the reference would have consumed
 reference's state.  The GIL is released during device calls (ctypes).
 
 Supported plugins: the Connect4 and chess backends (this package's, or the reference's —
-states with the same fields), Policy('random') / Policy('immediate_value'), and any value
+states with the same fields), Policy('random') / Policy('immediate_value') on the device, any
+other policy callable for Connect4 (called on the host at each expansion, the tree still on
+the device: _search.c4_host_policy_moves), and any value
 object: Value('random_rollout') (Connect4) and Value('crude_chess_score') (chess) run inside
 the search kernel, network values run on the device between the select and backup kernels,
 and any other object's value.batch(states, backend=backend) is called on the host once per
@@ -27,7 +29,8 @@ __all__ = ["get_move"]
 
 def _plugin_check(state, value, policy, backend):
     game = _search.game_of(backend, state)
-    _search.policy_of(policy)
+    if _search.policy_of(policy)[0] == _search.HOST_POLICY and game != "connect4":
+        raise NotImplementedError("a host policy callable runs on the Connect4 search only")
     kind = _search.value_kind(value)
     if game == "connect4" and kind == "crude":
         raise NotImplementedError("crude_chess_score is a chess value function")
@@ -43,6 +46,12 @@ def get_move(state, value, policy, backend, simulations=1000, c=1.4, batch_size=
     if batch_size < 1:
         raise ValueError("batch_size must be >= 1")
     ge = _device.scratch(simulations, batch_size)
+    if _search.policy_of(policy)[0] == _search.HOST_POLICY:
+        from .games.connect4 import c4_backend as c4
+        with ge.lock:
+            eng = ge.ensure(1, simulations, batch_size)
+            return _search.c4_host_policy_moves(eng, [0], _device.c4_roots([state], c4), simulations, c,
+                                                batch_size, value, policy, backend)[0]
     with ge.lock:
         eng = ge.ensure(1, simulations, batch_size)
         mt, idx, ver, gauss = _device.python_random_state()
