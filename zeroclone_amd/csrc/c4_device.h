@@ -651,27 +651,51 @@ __device__ __forceinline__ void select_flush(const Tree &t, Fresh *fresh, Leaf *
         inv = 0;
         {
             int done = 0;
-            uint32_t n = cnt;
             for (;;) {  // one 64-word view per pass
                 if (rng.off >= (uint32_t)kWin) rng_advance(rng);
                 const uint32_t w = rng_view(rng);  // lane l: word off + l
-                uint64_t gt = ~0ull;               // lanes after the last accepted word
-                int f = -1;
-                for (; done < m; ++done, --n) {
-                    const uint32_t sh = (uint32_t)__clz(n);
-                    const uint64_t A = __ballot((w >> sh) < n) & gt;
-                    if (!A) break;
-                    f = __builtin_ctzll(A);
-                    gt = (uint64_t)0 - (2ull << f);
-                    // the r-th untried move (r = the draw), erased from the list
-                    const uint32_t r = (uint32_t)__builtin_amdgcn_readlane((int)w, f) >> sh;
-                    const uint32_t mi = (ul >> (3 * r)) & 7u;
-                    const uint32_t lowm = (1u << (3 * r)) - 1u;
-                    ul = (ul & lowm) | ((ul >> 3) & ~lowm);
-                    picks |= mi << (3 * done);
-                    inv |= (8u | (uint32_t)done) << (4 * mi);
-                    ucl |= 1u << mi;
+                const int rem = m - done;
+                // acceptance masks of the next (up to 7) draws, n = cnt - done - i: independent
+                // of each other, issued back to back
+                uint64_t A[7];
+#pragma unroll
+                for (int i = 0; i < 7; ++i) {
+                    const uint32_t n = (uint32_t)max((int)cnt - done - i, 1);
+                    A[i] = __ballot((w >> __clz(n)) < n);
                 }
+                // the draws, a scalar chain: each takes the first accepted word after the last
+                uint64_t gt = ~0ull;  // lanes after the last accepted word
+                int f = -1, nd = 0;
+                int fl[7];
+#pragma unroll
+                for (int i = 0; i < 7; ++i) {
+                    fl[i] = 0;
+                    if (i < rem && nd == i) {
+                        const uint64_t acc = A[i] & gt;
+                        if (acc) {
+                            f = __builtin_ctzll(acc);
+                            fl[i] = f;
+                            gt = (uint64_t)0 - (2ull << f);
+                            nd = i + 1;
+                        }
+                    }
+                }
+                // the r-th untried move of each draw (r = the accepted word's value), erased
+                // from the list in turn
+#pragma unroll
+                for (int i = 0; i < 7; ++i) {
+                    if (i < nd) {
+                        const uint32_t n = cnt - (uint32_t)(done + i);
+                        const uint32_t r = (uint32_t)__builtin_amdgcn_readlane((int)w, fl[i]) >> __clz(n);
+                        const uint32_t mi = (ul >> (3 * r)) & 7u;
+                        const uint32_t lowm = (1u << (3 * r)) - 1u;
+                        ul = (ul & lowm) | ((ul >> 3) & ~lowm);
+                        picks |= mi << (3 * (done + i));
+                        inv |= (8u | (uint32_t)(done + i)) << (4 * mi);
+                        ucl |= 1u << mi;
+                    }
+                }
+                done += nd;
                 if (done < m) {  // the view ran out: all of it is consumed
                     rng.off += (uint32_t)kWin;
                     continue;
