@@ -418,13 +418,14 @@ static_assert(sizeof(Fresh) == 48, "Fresh is three 16-byte LDS slots");
 // ------------------------------------------------------------------ node records
 struct Tree {
     uint8_t *nodes;  // this game's records
-    int32_t *W;      // this game's W rows
     __device__ __forceinline__ uint8_t *rec(int nd) const { return nodes + (size_t)nd * kRecBytes; }
     __device__ __forceinline__ uint32_t *hdr(int nd) const { return (uint32_t *)rec(nd); }
     __device__ __forceinline__ uint16_t *child(int nd) const { return (uint16_t *)(rec(nd) + 16); }
     __device__ __forceinline__ int32_t *na(int nd) const { return (int32_t *)(rec(nd) + 32); }
+    // +64: stepwise search: Wa in fp64 (q); rollout search: Wa as int32 (w).  Either way Qa
+    // is formed as Wa / Na when read — the IEEE quotient mcts.cpp:95 stores
     __device__ __forceinline__ double *q(int nd) const { return (double *)(rec(nd) + 64); }
-    __device__ __forceinline__ int32_t *w(int nd) const { return W + (size_t)nd * kSlots; }
+    __device__ __forceinline__ int32_t *w(int nd) const { return (int32_t *)(rec(nd) + 64); }
 };
 
 // Node(state, legal_moves, parent, idx) (mcts.cpp:23-34): all moves untried, in list order.
@@ -443,8 +444,7 @@ __device__ __forceinline__ void node_init(const Tree &t, int nd, int parent, int
     if (lane < kSlots) {
         t.child(nd)[lane] = 0xFFFF;
         t.na(nd)[lane] = 0;
-        t.q(nd)[lane] = 0.0;
-        t.w(nd)[lane] = 0;
+        t.q(nd)[lane] = 0.0;  // Wa (either form) = 0
     }
 }
 
@@ -490,9 +490,9 @@ struct FlushSel {
 
 // The walk from the root over HBM records (select, mcts.cpp:47-63): the UCT child (first
 // maximum, +inf for an unvisited edge) until a node with untried moves or without children.
-// QW = false: the record's +64 slots hold Q (rollout mode, W in the side array);
-// QW = true:  they hold W in fp64 and Q = W / Na is formed here — the same IEEE quotient
-//             mcts.cpp:95 stores, so the UCT inputs are bit-identical.
+// QW = false: the record's +64 slots hold Wa as int32 (rollout search: values are +-1/0);
+// QW = true:  they hold Wa in fp64 (stepwise search).  Q = Wa / Na is formed here — the same
+//             IEEE quotient mcts.cpp:95 stores, so the UCT inputs are bit-identical.
 struct WalkEnd {
     int node, depth, turn;
     uint64_t b0, b1;     // the node's position
@@ -513,7 +513,8 @@ __device__ __forceinline__ WalkEnd walk_hbm(const Tree &t, ConstDouble *logtab, 
         const uint4 h = *(const uint4 *)R;
         ch = ((const uint16_t *)(R + 16))[k];
         const int32_t na = ((const int32_t *)(R + 32))[k];
-        const double qw = ((const double *)(R + 64))[k];
+        // Wa: fp64 (QW) or int32 (rollout search)
+        const double qw = QW ? ((const double *)(R + 64))[k] : (double)((const int32_t *)(R + 64))[k];
         const double lg = logtab[nN];  // log(N), glibc values tabulated on the host
         u = uni(h.y);
         ow = uni(h.w);
@@ -531,7 +532,7 @@ __device__ __forceinline__ WalkEnd walk_hbm(const Tree &t, ConstDouble *logtab, 
             best = __builtin_ctzll(unvisited);
         } else {
             // UCT (mcts.cpp:41-45) = fma(c, sqrt(log(N)/Na), Qa), first max in slot order
-            const double q = QW ? (valid ? qw / (double)na : 0.0) : qw;
+            const double q = valid ? qw / (double)na : 0.0;
             double v = valid ? fma(c, sqrt(lg / (double)na), q) : -INFINITY;
             int bi = (int)k;
             argmax8(v, bi);

@@ -23,7 +23,7 @@ __device__ __forceinline__ uint32_t mbcnt_lo(uint64_t m) {  // set bits of m in 
 }
 
 __device__ __forceinline__ Tree ext_tree(const ExtParams &p, int g) {
-    return Tree{p.a.nodes + (size_t)g * p.M * kRecBytes, p.a.W + (size_t)g * p.M * kSlots};
+    return Tree{p.a.nodes + (size_t)g * p.M * kRecBytes};
 }
 
 __global__ __launch_bounds__(kBlock) void c4_ext_begin_kernel(ExtParams p) {

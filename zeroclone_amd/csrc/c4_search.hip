@@ -421,7 +421,7 @@ __global__ __launch_bounds__(kSearchWaves * kBlock) void c4_search_kernel(Search
     }
 
     const Arena &a = p.a;
-    const Tree t{a.nodes + (size_t)g * p.M * kRecBytes, a.W + (size_t)g * p.M * kSlots};
+    const Tree t{a.nodes + (size_t)g * p.M * kRecBytes};
 
     LRng rng;
     const uint64_t use0 = uni64(a.rngpos[2 * (size_t)g]);
@@ -507,7 +507,6 @@ __global__ __launch_bounds__(kSearchWaves * kBlock) void c4_search_kernel(Search
             const int32_t w1 = w0 + dw;
             t.na(par)[act] = na1;
             t.w(par)[act] = w1;
-            t.q(par)[act] = (double)w1 / (double)na1;  // Qa = Wa / Na
         }
         wave_mem_order();
         stamp.mark(5);
@@ -523,7 +522,6 @@ __global__ __launch_bounds__(kSearchWaves * kBlock) void c4_search_kernel(Search
                     const int32_t na = fresh[x_ch - f0].na, w = fresh[x_ch - f0].w;
                     t.na(x0node)[lane] = na;
                     t.w(x0node)[lane] = w;
-                    t.q(x0node)[lane] = (double)w / (double)na;
                 }
             }
         }
@@ -544,8 +542,7 @@ __global__ __launch_bounds__(kSearchWaves * kBlock) void c4_search_kernel(Search
                     if (slot == 0) *(uint4 *)R = make_uint4(0u, F.u, F.link, F.ow);
                     ((uint16_t *)(R + 16))[slot] = c;
                     ((int32_t *)(R + 32))[slot] = na;
-                    ((double *)(R + 64))[slot] = na ? (double)w / (double)na : 0.0;
-                    t.w(f0 + r)[slot] = w;
+                    ((int32_t *)(R + 64))[slot] = w;
                 }
             }
         }

@@ -70,7 +70,7 @@ void free_chess(zc::ChessArena &c) {
 }
 
 void free_arena(zc::Arena &a) {
-    void *ptrs[] = {a.nodes, a.W,     a.ring,  a.rngpos, a.logtab,  a.phase,    a.roots,    a.move,
+    void *ptrs[] = {a.nodes, a.ring,  a.rngpos, a.logtab,  a.phase,    a.roots,    a.move,
                     a.na,    a.ids,   a.stats, a.ext_ctl, a.ext_paths, a.ext_meta, a.ext_roots};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
@@ -188,7 +188,6 @@ int zc_engine_create(const zc_engine_config *cfg, zc_engine **out) {
     zc::Arena &a = e->a;
     int rc = ZC_OK;
     if (!rc) rc = dalloc(e, &a.nodes, G * M * zc::kRecBytes);
-    if (!rc) rc = dalloc(e, &a.W, G * M * zc::kSlots);
     if (!rc) rc = dalloc(e, &a.ring, G * zc::kRingWords);
     if (!rc) rc = dalloc(e, &a.rngpos, G * 2);
     if (!rc) rc = dalloc(e, &a.logtab, M + 2);

@@ -27,10 +27,11 @@ namespace zc {
 //                          bits 24..27: #moves
 //   +16  u16  child[8]     0xFFFF = null                              (Node::children)
 //   +32  i32  Na[8]                                                    (Node::Na)
-//   +64  f64  [8]          rollout search: Qa = Wa / Na                (Node::Qa)
-//                          stepwise search: Wa in fp64 (Qa is formed as Wa / Na when read)
-// In the rollout search Wa is an integer and lives in a separate [game][M][8] i32 array:
-// only backup touches it.  Boards are not stored: the walk re-applies moves from the root.
+//   +64  [8]  Wa           rollout search: i32 (rollout values are +-1 / 0, so Wa is an
+//                          integer); stepwise search: f64.  Qa (Node::Qa) is formed as
+//                          Wa / Na when the walk reads the edge — the IEEE quotient
+//                          mcts.cpp:95 stores, so UCT's inputs are bit-identical
+// Boards are not stored: the walk re-applies moves from the root.
 constexpr int kRecBytes = 128;
 constexpr int kSlots = 8;
 constexpr int kMaxDepth = 44;          // levels 0..42 (a C4 game has at most 42 plies)
@@ -45,7 +46,6 @@ static_assert(kLookahead + kChunk + 624 + 192 < kRingWords, "ring must retain th
 
 struct Arena {
     uint8_t *nodes = nullptr;     // [G][M][128 B]
-    int32_t *W = nullptr;         // [G][M][8]
     uint32_t *ring = nullptr;     // [G][kRingWords]    raw (untempered) MT words
     uint64_t *rngpos = nullptr;   // [G][2]             {next word to use, words generated}
     double *logtab = nullptr;     // [M+2]              glibc log(n), n = 0..M+1
