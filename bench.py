@@ -11,6 +11,10 @@ labelled as Engine.get_dataset and pooled) and the refill of finished games
 (scripts/train.py:151-170), all on the device (selfplay.C4SelfPlay).  Before the warm-up
 the pool is run until every game slot has finished a game and started another, so the
 timed steps see games of mixed ages (steady-state self-play), not the lockstep opening.
+The K timed steps run as one free-running launch (C4SelfPlay.run, zc_c4_selfplay_async):
+every game plays its K moves at its own pace — the same moves, trajectories and RNG streams
+as K lockstep steps (tests/test_gpu_selfplay_run.py) — so young games (long rollouts) do not
+stall the whole pool once per move.
 
 Games are sharded across ranks by global game id (seed = base + id) — no collective on the
 data path ("scaling": "weak").  `--gpus N` without torchrun spawns N fresh processes (one
@@ -272,7 +276,7 @@ def philox_mode(sp, args) -> dict:
         sp.eng.c4_rollout_mode("exact")
     return {"value": round(r["expansions"] / r["dt"], 1), "unit": "expansions/s",
             "ms_per_step": round(r["dt"] / args.steps * 1e3, 3),
-            "search_ms_per_step": [round(x, 3) for x in r["kernel_ms"]], "expansions": r["expansions"],
+            "selfplay_launch_ms": round(r["launch_ms"], 3), "expansions": r["expansions"],
             "config": f"C2(ii) {sp.G} games x {args.sims} sims, batch {args.batch}: Philox rollout mode"}
 
 
@@ -282,8 +286,7 @@ def burn_in(sp, max_steps: int = 200, check_every: int = 8) -> int:
     >= G everywhere): the timed window then sees games of mixed ages.  Returns the steps."""
     steps = 0
     while steps < max_steps:
-        for _ in range(check_every):
-            sp.step()
+        sp.run(check_every)
         steps += check_every
         if int(sp.traj.slot[:, 1].min().item()) >= sp.G:
             break
@@ -292,47 +295,34 @@ def burn_in(sp, max_steps: int = 200, check_every: int = 8) -> int:
 
 
 def run_steps(sp, steps: int, warmup: int, world: int = 1) -> dict:
-    """W untimed steps, then K timed steps bracketed by barrier + device sync; HIP events
-    around every search launch on the launch stream."""
+    """W untimed moves, then K timed moves bracketed by barrier + device sync.  The K moves
+    are ONE free-running self-play launch (C4SelfPlay.run: every game at its own pace, the
+    same moves as K lockstep steps) followed by the K steps' trajectory recording; HIP
+    events around the launch on its stream."""
     dev = sp.dev
     stream = torch.cuda.current_stream(dev)
-    acc = torch.zeros(4, dtype=torch.int64, device=dev)   # expansions, depth_sum, finished, leaves
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(max(steps, 1))]
-
-    def one(ev):   # warm-up and timed steps run the same code (first use of a torch op loads its kernel)
-        ev[0].record(stream)
-        r = sp.step_search()
-        ev[1].record(stream)
-        sp.step_finish()
-        tally(r)
-
-    def tally(r):
-        acc[0] += sp.stats[:, 0].sum()
-        acc[1] += sp.stats[:, 1].sum()
-        acc[2] += ((r != _native.ZC_C4_ONGOING) & (r != _native.ZC_SLOT_IDLE)).sum()
-        acc[3] += sp.stats[:, 2].sum()
-
-    tally(sp.results)   # load the tally's torch kernels even when warmup == 0 (no step is run)
-    for _ in range(warmup):
-        one(evs[0])
+    ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+    if warmup:
+        sp.run(warmup)
     torch.cuda.synchronize(dev)
-    acc.zero_()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for k in range(steps):
-        one(evs[k])
+    ev[0].record(stream)
+    res = sp.run(steps)
+    ev[1].record(stream)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
-    if int((sp.stats[:, 5] != 0).sum().item()):
+    st = sp.stats
+    if int((st[:, 5] != 0).sum().item()):
         raise RuntimeError("a game reported a nonzero search status")
-    kernel_ms = [a.elapsed_time(b) for a, b in evs]
-    tot = [int(x) for x in acc.tolist()]
-    return {"dt": dt, "kernel_ms": kernel_ms, "expansions": tot[0], "depth_sum": tot[1], "finished": tot[2],
-            "leaves": tot[3]}
+    fin = int(((res != _native.ZC_C4_ONGOING) & (res != _native.ZC_SLOT_IDLE)).sum().item())
+    tot = [int(x) for x in st[:, [0, 1, 2]].sum(0).tolist()]
+    return {"dt": dt, "launch_ms": ev[0].elapsed_time(ev[1]), "expansions": tot[0], "depth_sum": tot[1],
+            "finished": fin, "leaves": tot[2]}
 
 
 def reduce_over_ranks(counts, dt: float, kernel_ms_sum: float, device) -> tuple[list[int], float, float]:
@@ -397,7 +387,7 @@ def run_rank(args, rank: int, world: int, local: int):
     r = run_steps(sp, args.steps, args.warmup, world)
     gather = gather_trajectories(sp, world)
     counts, dt_max, kms = reduce_over_ranks([r["expansions"], r["depth_sum"], r["finished"], r["leaves"]], r["dt"],
-                                            sum(r["kernel_ms"]), dev)
+                                            r["launch_ms"], dev)
     expansions, depth_sum, finished, leaves = counts
     if rank == 0:
         prof, prof_src = search_profile()
@@ -405,7 +395,7 @@ def run_rank(args, rank: int, world: int, local: int):
         traffic_src = "--traffic-bytes" if args.traffic_bytes else prof_src
         launches = args.steps * world
         bytes_launch = bytes_per_expansion_model(expansions, depth_sum) / launches
-        avg_kernel_s = kms / 1e3 / args.steps
+        avg_kernel_s = kms / 1e3 / args.steps   # per move
         achieved = bytes_launch / avg_kernel_s / 1e9
         out = {
             "metric": METRIC,
@@ -432,14 +422,16 @@ def run_rank(args, rank: int, world: int, local: int):
             "roofline": {"bound": "issue", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 5),
                          "traffic": traffic, "traffic_source": traffic_src,
-                         "kernel": "c4_search_kernel", "avg_launch_ms": round(avg_kernel_s * 1e3, 3),
+                         "kernel": "c4_selfplay_kernel (K moves per launch; per-move figures = launch / K)",
+                         "avg_launch_ms": round(avg_kernel_s * 1e3, 3),
                          "bytes_per_launch_model": round(bytes_launch),
                          "model": "SURVEY §8(d): 152*d+96 B per expansion, d counted in-kernel",
                          "issue": dict(prof.get("issue") or {}, source=prof_src) if prof.get("issue") else None,
                          "limiter": "the per-game serial dependency chain (latency + issue arbitration), not HBM: "
                                     "roofline.issue (SQ counters) and DESIGN §4"},
             "extra": {"expansions": expansions, "leaves": leaves, "mean_depth": round(depth_sum / max(expansions, 1), 3),
-                      "games_finished": finished, "search_ms_per_step": [round(x, 3) for x in r["kernel_ms"]],
+                      "games_finished": finished,
+                      "selfplay_launch_ms": round(r["launch_ms"], 3),
                       "trajectory_allgather": gather},
         }
         if world == 1:
@@ -517,7 +509,9 @@ def _spawned(rank: int, args, world: int, port: int):
 def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=60,
+                    help="timed moves (one free-running launch; about a game length, so every slot's "
+                         "games of all ages share the window)")
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--games", type=int, default=4096, help="games per GPU")
     ap.add_argument("--sims", type=int, default=800)

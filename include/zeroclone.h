@@ -103,6 +103,20 @@ int zc_c4_search_async(zc_engine *eng, int32_t first_game, int32_t n_games, cons
                        int32_t *d_out_move, int32_t *d_out_root_na, zc_game_stats *d_out_stats,
                        void *hip_stream);
 
+/* Self-play of games first..first+n-1 for `moves` consecutive moves in ONE launch, each game
+ * at its own pace: per move the search above from d_roots[i], then Engine.play_move +
+ * _evaluate (as zc_c4_play_async), and a finished game restarts from the opening (the refill
+ * of scripts/train.py:151-170 without a game quota).  d_roots is updated in place.  Step k's
+ * post-move position, column and result (ZC_C4_ONGOING / +-1 / 0) go to
+ * d_out_states / d_out_moves / d_out_results[k*n + i] — exactly the inputs of
+ * zc_traj_record_async for that step, which the caller replays in step order.
+ * d_stats[i] sums the moves' counters (reserved = games finished).  Results equal `moves`
+ * rounds of zc_c4_search_async + zc_c4_play_async; games never wait for each other, so a
+ * launch no longer waits once per move for its slowest game. */
+int zc_c4_selfplay_async(zc_engine *eng, int32_t first_game, int32_t n_games, zc_c4_state *d_roots, int32_t sims,
+                         double c, int32_t batch_size, int32_t moves, zc_c4_state *d_out_states,
+                         int16_t *d_out_moves, int32_t *d_out_results, zc_game_stats *d_stats, void *hip_stream);
+
 /* Random source of the Connect4 search's rollouts (all zc_c4_search* calls that follow):
  *   ZC_ROLLOUT_EXACT (default) — the game's CPython MT19937 stream in the reference's order;
  *     results are bit-identical to mcts.get_move.
@@ -451,6 +465,8 @@ int zc_debug_chess_tree(zc_engine *eng, int32_t game, int32_t max_nodes, int32_t
  * the stamped kernel build on (enable != 0) or off for later searches.  Synchronises the
  * device.  Stamped runs are for phase SHARES only, never for timing. */
 int zc_debug_phase_cycles(zc_engine *eng, int32_t enable, int64_t *out8);
+/* The same stamps per game (no reset): out[g * 8 + k] for games 0 .. n_games-1. */
+int zc_debug_phase_cycles_games(zc_engine *eng, int32_t n_games, int64_t *out);
 
 #ifdef __cplusplus
 }

@@ -1,8 +1,8 @@
 #!/usr/bin/env python3
 """The bench's own workload for rocprofv3 passes: C4SelfPlay at 4096 games x 800 sims x bs 32,
 burned in to steady state (every slot has finished a game and started another, as bench.py
-does), then --steps timed moves.  The kernel of interest is c4_search_kernel<false, false>;
-tools/summarize_profile.py picks it out of the trace."""
+does), then --steps timed moves in one free-running launch (c4_selfplay_kernel<false>, the
+last launch of the trace; tools/summarize_profile.py --moves K reports it per move)."""
 import argparse
 import os
 import sys
@@ -28,6 +28,6 @@ burn = bench.burn_in(sp) if a.burn_in else 0
 print(f"burn-in {burn} steps", flush=True)
 r = bench.run_steps(sp, a.steps, warmup=0)
 print(f"steps {a.steps}: {r['expansions'] / r['dt'] / 1e9:.4f} G expansions/s, "
-      f"kernel ms {[round(x, 3) for x in r['kernel_ms']]}, depth {r['depth_sum'] / max(r['expansions'], 1):.3f}",
-      flush=True)
+      f"launch ms {r['launch_ms']:.3f} ({r['launch_ms'] / a.steps:.3f} per move), "
+      f"depth {r['depth_sum'] / max(r['expansions'], 1):.3f}", flush=True)
 sp.close()

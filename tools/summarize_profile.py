@@ -27,7 +27,7 @@ import collections
 import csv
 import json
 
-KERNEL = "c4_search_kernel<false, false>"  # the product kernel (not the stamped diagnostic build)
+KERNEL = "c4_selfplay_kernel<false>"  # the product kernel (K self-play moves per launch)
 N_CU, N_SIMD, N_XCD = 256, 1024, 8
 
 
@@ -56,17 +56,19 @@ def main():
     ap.add_argument("--write")
     ap.add_argument("--pmc")
     ap.add_argument("--kernel", default=KERNEL)
-    ap.add_argument("--last", type=int, default=8, help="launches to average (0 = all)")
+    ap.add_argument("--last", type=int, default=1, help="launches to average (0 = all)")
+    ap.add_argument("--moves", type=int, default=1, help="moves per launch: bytes and times are reported per move")
     ap.add_argument("--note", default="")
     ap.add_argument("--out", required=True)
     a = ap.parse_args()
-    out = {"kernel": a.kernel, "launches_used": a.last or "all"}
+    out = {"kernel": a.kernel, "launches_used": a.last or "all", "moves_per_launch": a.moves}
     if a.note:
         out["note"] = a.note
     if a.stats:
         for r in csv.DictReader(open(a.stats)):
             if a.kernel in r["Name"]:
                 out["rocprof_stats"] = {"calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"]),
+                                        "avg_ns_per_move": float(r["AverageNs"]) / a.moves,
                                         "min_ns": float(r["MinNs"]), "max_ns": float(r["MaxNs"]),
                                         "percent_of_gpu_time": float(r["Percentage"])}
     if a.trace:
@@ -75,12 +77,15 @@ def main():
         durs = [d for _, d in sorted(durs)]
         sel = durs[-a.last:] if a.last else durs
         out["trace_last_avg_ns"] = mean(sel)
+        out["trace_last_avg_ns_per_move"] = mean(sel) / a.moves
     if a.fetch and a.write:
         f = mean([d["FETCH_SIZE"] for d in per_dispatch(a.fetch, a.kernel, a.last)])
         w = mean([d["WRITE_SIZE"] for d in per_dispatch(a.write, a.kernel, a.last)])
+        f, w = f / a.moves, w / a.moves
         out["hbm"] = {"FETCH_SIZE_KiB": f, "WRITE_SIZE_KiB": w,
                       "bytes_per_launch": (2 * f + w) * 1024.0,
                       "bytes_per_launch_uncorrected": (f + w) * 1024.0,
+                      "per": "move",
                       "correction": "read side x2 (gfx950 FETCH_SIZE half-count), KiB -> B"}
     if a.pmc:
         ds = per_dispatch(a.pmc, a.kernel, a.last)

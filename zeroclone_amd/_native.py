@@ -115,6 +115,10 @@ SIGNATURES = [
                                         ctypes.c_void_p]),
     ("zc_c4_ext_backup", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
                                         ctypes.c_void_p, ctypes.c_void_p]),
+    ("zc_c4_selfplay_async", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p,
+                                            ctypes.c_int32, ctypes.c_double, ctypes.c_int32, ctypes.c_int32,
+                                            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                            ctypes.c_void_p]),
     ("zc_c4_hp_walk", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p,
                                      ctypes.c_void_p]),
     ("zc_c4_hp_expand", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
@@ -199,6 +203,7 @@ SIGNATURES = [
                                            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     ("zc_debug_phase_cycles", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, P(ctypes.c_int64)]),
+    ("zc_debug_phase_cycles_games", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, P(ctypes.c_int64)]),
     ("zc_debug_c4_rollout", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p,
                                            ctypes.c_void_p, ctypes.c_void_p]),
 ]
@@ -372,6 +377,15 @@ class NativeEngine:
                                        int(batch_size), ctypes.c_void_p(d_move), ctypes.c_void_p(d_na),
                                        ctypes.c_void_p(d_stats), ctypes.c_void_p(stream or None)))
 
+    def c4_selfplay_async(self, d_roots: int, n: int, sims: int, c: float, batch_size: int, moves: int,
+                          d_states: int, d_moves16: int, d_results: int, d_stats: int, stream: int = 0,
+                          first_game: int = 0) -> None:
+        """`moves` self-play moves per game in one launch (zc_c4_selfplay_async)."""
+        check(lib().zc_c4_selfplay_async(self._h, first_game, n, ctypes.c_void_p(d_roots), int(sims), float(c),
+                                         int(batch_size), int(moves), ctypes.c_void_p(d_states),
+                                         ctypes.c_void_p(d_moves16), ctypes.c_void_p(d_results),
+                                         ctypes.c_void_p(d_stats), ctypes.c_void_p(stream or None)))
+
     def c4_play_async(self, d_states: int, n: int, d_moves: int, d_results: int, reset: bool = True,
                       stream: int = 0) -> None:
         check(lib().zc_c4_play_async(self._h, n, ctypes.c_void_p(d_states), ctypes.c_void_p(d_moves),
@@ -536,6 +550,12 @@ class NativeEngine:
         q = np.ascontiguousarray(q, np.float64)
         out = np.zeros(len(logn), np.float64)
         check(lib().zc_debug_uct(self._h, len(logn), _ptr(logn), _ptr(na), _ptr(q), float(c), _ptr(out)))
+        return out
+
+    def phase_cycles_games(self, n: int) -> np.ndarray:
+        """Per-game stamp cycles [n, 8] accumulated since the last phase_cycles() reset."""
+        out = np.zeros((n, 8), np.int64)
+        check(lib().zc_debug_phase_cycles_games(self._h, int(n), out.ctypes.data_as(P(ctypes.c_int64))))
         return out
 
     def phase_cycles(self, enable: bool):

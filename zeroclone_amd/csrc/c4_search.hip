@@ -375,61 +375,43 @@ __host__ __device__ constexpr size_t c4_search_wave_lds(int bs) {
             kPathSpill + 15) & ~(size_t)15;
 }
 
-// STAMP = diagnostic build: lane 0 adds s_memtime deltas per phase into p.a.phase[g][0..7] =
-// {rng generation at flush start, first walk of a flush, resumed walks, expansion + leaf
-//  bookkeeping, rollouts, backup, publish, -}.
-template <bool STAMP, bool PHILOX>
-__global__ __launch_bounds__(kSearchWaves * kBlock) void c4_search_kernel(SearchParams p) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t s_dyn[];
-    // LDS: order[128] u32 + sel[128][8] (the workgroup's tables), then per wave (game):
-    //      MT ring (1024 raw words), fresh[bs] (48 B), leaves[bs] (24 B),
-    //      paths[bs][kMaxDepth] (u16 node ids)
-    uint32_t *const s_order = (uint32_t *)s_dyn;
+// Per-wave LDS of the search: the MT ring, fresh nodes, pending leaves, their paths.
+struct SearchLds {
+    uint32_t *s_order;  // the workgroup's tables: order[128] u32 + sel[128][8]
+    uint32_t *ring;
+    Fresh *fresh;
+    Leaf *leaves;
+    uint16_t *paths;
+};
+
+__device__ __forceinline__ SearchLds search_lds(uint8_t *s_dyn, int bs) {
     const uint32_t wave = threadIdx.x >> 6;
-    uint8_t *const s_wave = s_dyn + kTabBytes + (size_t)wave * c4_search_wave_lds(p.bs);
-    uint32_t *const s_ring = (uint32_t *)s_wave;
-    Fresh *const fresh = (Fresh *)(s_wave + kLRingBytes);
-    Leaf *const leaves = (Leaf *)(s_wave + kLRingBytes + sizeof(Fresh) * (size_t)p.bs);
-    uint16_t *const paths = (uint16_t *)(s_wave + kLRingBytes + (sizeof(Fresh) + sizeof(Leaf)) * (size_t)p.bs);
-    const uint8_t *const s_sel = sel_table(s_order);
-    load_tables(s_order);
-    __syncthreads();
+    uint8_t *const s_wave = s_dyn + kTabBytes + (size_t)wave * c4_search_wave_lds(bs);
+    SearchLds L;
+    L.s_order = (uint32_t *)s_dyn;
+    L.ring = (uint32_t *)s_wave;
+    L.fresh = (Fresh *)(s_wave + kLRingBytes);
+    L.leaves = (Leaf *)(s_wave + kLRingBytes + sizeof(Fresh) * (size_t)bs);
+    L.paths = (uint16_t *)(s_wave + kLRingBytes + (sizeof(Fresh) + sizeof(Leaf)) * (size_t)bs);
+    return L;
+}
+
+// One whole search (mcts.get_move, mcts.cpp:102-160) of game g from p.roots[gl] (re-read
+// every flush rather than held in registers); the tree ends in t, the stream in rng.
+// STAMP = diagnostic build: lane 0 adds s_memtime deltas per phase into p.a.phase[g][0..7] =
+// {-, first walk of a flush, resumed walks, expansion + leaf bookkeeping, rollouts, backup,
+//  publish, rollout sub-region}.
+template <bool STAMP, bool PHILOX>
+__device__ __forceinline__ void search_move(const SearchParams &p, const SearchLds &L, int gl, int g, const Tree &t,
+                                            LRng &rng, uint32_t tag, Counters &cn, int &status) {
+    const uint32_t lane = lane_id();
+    const uint32_t *const s_order = L.s_order;
+    Fresh *const fresh = L.fresh;
+    Leaf *const leaves = L.leaves;
+    uint16_t *const paths = L.paths;
     // log(N) table read through the constant address space: uniform index -> scalar loads,
     // which do not sit in the vector-memory counter the walk waits on.
     ConstDouble *logtab = (ConstDouble *)p.a.logtab;
-
-    const uint32_t lane = lane_id();
-    const uint32_t k = lane & 7u;
-    const int gl = (int)(blockIdx.x * (blockDim.x >> 6) + wave);  // game within this call (one wave per game)
-    if (gl >= p.n_games) return;
-    const int g = p.game_ids ? uni(p.game_ids[gl]) : p.first_game + gl;
-
-    {
-        const zc_c4_state root = p.roots[gl];
-        const uint64_t rp0 = uni64(root.stones[0]), rp1 = uni64(root.stones[1]);
-        const int rturn = uni(root.turn);
-        if (!valid_state(rp0, rp1, rturn) || legal_mask(rp0 | rp1) == 0) {
-            if (lane == 0) {
-                zc_game_stats st{};
-                st.status = valid_state(rp0, rp1, rturn) ? ZC_STATUS_NO_MOVES : ZC_STATUS_BAD_STATE;
-                p.out_stats[gl] = st;
-                p.out_move[gl] = -1;
-            }
-            if (lane < 7) p.out_na[(size_t)gl * 7 + lane] = 0;
-            return;
-        }
-    }
-
-    const Arena &a = p.a;
-    const Tree t{a.nodes + (size_t)g * p.M * kRecBytes};
-
-    LRng rng;
-    const uint64_t use0 = uni64(a.rngpos[2 * (size_t)g]);
-    lrng_open(rng, s_ring, a.ring + (size_t)g * kRingWords, use0, uni64(a.rngpos[2 * (size_t)g + 1]));
-    const uint32_t tag = uni((uint32_t)use0);  // Philox mode: stream per move
-    Counters cn;
-    int status = 0;
-
     {
         const zc_c4_state root = p.roots[gl];
         node_init(t, 0, 0xFFFF, 0xFF, 0, uni(s_order[legal_mask(uni64(root.stones[0]) | uni64(root.stones[1]))]));
@@ -445,7 +427,6 @@ __global__ __launch_bounds__(kSearchWaves * kBlock) void c4_search_kernel(Search
         // ---- selection + expansion of nb leaves (mcts.cpp:129-147) -------------------------
         FlushSel fs;
         {
-            // the root position, re-read every flush rather than held in registers
             const zc_c4_state root = p.roots[gl];
             select_flush<false, STAMP>(t, fresh, leaves, paths, s_order, logtab, rng, cn, stamp, nnodes,
                                        status, uni64(root.stones[0]), uni64(root.stones[1]), uni(root.turn), done,
@@ -455,8 +436,9 @@ __global__ __launch_bounds__(kSearchWaves * kBlock) void c4_search_kernel(Search
 
         // ---- value.batch: random rollouts in pending order (mcts.cpp:112-124) ---------------
         if (PHILOX)
-            c4_rollouts_philox(leaves, nb, s_sel, make_uint2((uint32_t)p.philox_seed, (uint32_t)(p.philox_seed >> 32)),
-                               (uint32_t)done, tag, (uint32_t)g, cn);
+            c4_rollouts_philox(leaves, nb, sel_table(s_order),
+                               make_uint2((uint32_t)p.philox_seed, (uint32_t)(p.philox_seed >> 32)), (uint32_t)done,
+                               tag, (uint32_t)g, cn);
         else
             c4_rollouts(leaves, nb, rng, s_order, cn, STAMP ? &stamp.ph[7] : nullptr);
         wave_mem_order();
@@ -503,10 +485,8 @@ __global__ __launch_bounds__(kSearchWaves * kBlock) void c4_search_kernel(Search
         }
         if (pre) {
             const int dw = (lane & 1u) ? S : -S;  // Wa -= (-1)^l * S
-            const int32_t na1 = na0 + nb;
-            const int32_t w1 = w0 + dw;
-            t.na(par)[act] = na1;
-            t.w(par)[act] = w1;
+            t.na(par)[act] = na0 + nb;
+            t.w(par)[act] = w0 + dw;
         }
         wave_mem_order();
         stamp.mark(5);
@@ -519,9 +499,8 @@ __global__ __launch_bounds__(kSearchWaves * kBlock) void c4_search_kernel(Search
             if (lane < kSlots) {
                 t.child(x0node)[lane] = (uint16_t)x_ch;
                 if (x_ch != 0xFFFF && (int)x_ch >= f0) {  // edge into a fresh child
-                    const int32_t na = fresh[x_ch - f0].na, w = fresh[x_ch - f0].w;
-                    t.na(x0node)[lane] = na;
-                    t.w(x0node)[lane] = w;
+                    t.na(x0node)[lane] = fresh[x_ch - f0].na;
+                    t.w(x0node)[lane] = fresh[x_ch - f0].w;
                 }
             }
         }
@@ -551,9 +530,14 @@ __global__ __launch_bounds__(kSearchWaves * kBlock) void c4_search_kernel(Search
         done += nb;
     }
     if (STAMP && lane == 0)
-        for (int k_ = 0; k_ < kPhases; ++k_) a.phase[kPhases * (size_t)g + k_] += (int64_t)stamp.ph[k_];
+        for (int k_ = 0; k_ < kPhases; ++k_) p.a.phase[kPhases * (size_t)g + k_] += (int64_t)stamp.ph[k_];
+}
 
-    // ---- best move: first max of child N over the root's move list (mcts.cpp:150-157) ----
+// The move (mcts.cpp:150-157): first max of child N over the root's move list -> its column;
+// lanes 0..6 also get the visits of the child in their column (0 if illegal) in `na_col`.
+__device__ __forceinline__ int best_column(const Tree &t, int &na_col) {
+    const uint32_t lane = lane_id();
+    const uint32_t k = lane & 7u;
     const uint32_t u = uni(t.hdr(0)[1]);
     const uint32_t ow = uni(t.hdr(0)[3]);
     const uint32_t nm = u >> 28;
@@ -561,14 +545,52 @@ __global__ __launch_bounds__(kSearchWaves * kBlock) void c4_search_kernel(Search
     int bi = (int)k;
     argmax8(bv, bi);
     const int best = uni(bi);
-    if (lane < 7) {  // visits per column
-        int pos = -1;
-        for (uint32_t s = 0; s < nm; ++s)
-            if (((ow >> (3 * s)) & 7u) == lane) pos = (int)s;
-        p.out_na[(size_t)gl * 7 + lane] = pos >= 0 ? t.na(0)[pos] : 0;
+    int pos = -1;
+    for (uint32_t s = 0; s < nm; ++s)
+        if (((ow >> (3 * s)) & 7u) == lane) pos = (int)s;
+    na_col = pos >= 0 ? t.na(0)[pos] : 0;
+    return (int)((ow >> (3 * best)) & 7u);
+}
+
+template <bool STAMP, bool PHILOX>
+__global__ __launch_bounds__(kSearchWaves * kBlock) void c4_search_kernel(SearchParams p) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t s_dyn[];
+    const SearchLds L = search_lds(s_dyn, p.bs);
+    load_tables(L.s_order);
+    __syncthreads();
+
+    const uint32_t lane = lane_id();
+    const int gl = (int)(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));  // one wave per game
+    if (gl >= p.n_games) return;
+    const int g = p.game_ids ? uni(p.game_ids[gl]) : p.first_game + gl;
+    {
+        const zc_c4_state root = p.roots[gl];
+        const uint64_t rp0 = uni64(root.stones[0]), rp1 = uni64(root.stones[1]);
+        const int rturn = uni(root.turn);
+        if (!valid_state(rp0, rp1, rturn) || legal_mask(rp0 | rp1) == 0) {
+            if (lane == 0) {
+                zc_game_stats st{};
+                st.status = valid_state(rp0, rp1, rturn) ? ZC_STATUS_NO_MOVES : ZC_STATUS_BAD_STATE;
+                p.out_stats[gl] = st;
+                p.out_move[gl] = -1;
+            }
+            if (lane < 7) p.out_na[(size_t)gl * 7 + lane] = 0;
+            return;
+        }
     }
+    const Arena &a = p.a;
+    const Tree t{a.nodes + (size_t)g * p.M * kRecBytes};
+    LRng rng;
+    const uint64_t use0 = uni64(a.rngpos[2 * (size_t)g]);
+    lrng_open(rng, L.ring, a.ring + (size_t)g * kRingWords, use0, uni64(a.rngpos[2 * (size_t)g + 1]));
+    Counters cn;
+    int status = 0;
+    search_move<STAMP, PHILOX>(p, L, gl, g, t, rng, uni((uint32_t)use0), cn, status);
+    int na_col;
+    const int col = best_column(t, na_col);
+    if (lane < 7) p.out_na[(size_t)gl * 7 + lane] = na_col;
     if (lane == 0) {
-        p.out_move[gl] = (int)((ow >> (3 * best)) & 7u);
+        p.out_move[gl] = col;
         zc_game_stats st{};
         st.status = status;
         st.expansions = cn.expansions;
@@ -577,6 +599,82 @@ __global__ __launch_bounds__(kSearchWaves * kBlock) void c4_search_kernel(Search
         st.rollout_plies = cn.plies;
         st.rollout_blocks = cn.blocks;
         st.rng_words = rng.use();
+        p.out_stats[gl] = st;
+    }
+    lrng_close(rng, a.ring + (size_t)g * kRingWords, use0, a.rngpos + 2 * (size_t)g);
+}
+
+// Self-play without a global step: each wave plays `p.moves` consecutive moves of its game —
+// search, Engine.play_move + _evaluate (engine.py:98-108, 148-153), and the refill of a
+// finished game from the opening (train.py:151-170 with no game quota) — keeping its tree
+// arena, its MT stream (in LDS) and its pace.  Games of different ages take different times
+// per move (young games have the long rollouts); synchronising all games every move makes
+// each launch wait for the slowest game, here the waves only meet at the end of the run.
+// Step k's post-move position / move / result go to out_states[k*n + gl], out_moves[...],
+// out_results[...] (the inputs of zc_traj_record_async for step k, replayed in step order
+// after the launch); out_stats[gl] accumulates over the moves.
+template <bool PHILOX>
+__global__ __launch_bounds__(kSearchWaves * kBlock) void c4_selfplay_kernel(SearchParams p) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t s_dyn[];
+    const SearchLds L = search_lds(s_dyn, p.bs);
+    load_tables(L.s_order);
+    __syncthreads();
+
+    const uint32_t lane = lane_id();
+    const int gl = (int)(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
+    if (gl >= p.n_games) return;
+    const int g = p.first_game + gl;
+    const Arena &a = p.a;
+    const Tree t{a.nodes + (size_t)g * p.M * kRecBytes};
+    LRng rng;
+    const uint64_t use0 = uni64(a.rngpos[2 * (size_t)g]);
+    lrng_open(rng, L.ring, a.ring + (size_t)g * kRingWords, use0, uni64(a.rngpos[2 * (size_t)g + 1]));
+    Counters cn;
+    int status = 0;
+    int finished = 0;
+    for (int mv = 0; mv < p.moves; ++mv) {
+        zc_c4_state root = p.roots[gl];
+        uint64_t s0 = uni64(root.stones[0]), s1 = uni64(root.stones[1]);
+        int turn = uni(root.turn);
+        if (!valid_state(s0, s1, turn) || legal_mask(s0 | s1) == 0) {  // never from play: flagged
+            status = ZC_STATUS_BAD_STATE;
+            break;
+        }
+        search_move<false, PHILOX>(p, L, gl, g, t, rng, uni((uint32_t)(use0 + (uint64_t)(int64_t)rng.use())), cn,
+                                   status);
+        int na_col;
+        const int col = best_column(t, na_col);
+        // play_move + _evaluate (c4_play_kernel): check_win -> turn*2-1 with the new turn
+        const uint64_t bit = drop_bit(s0 | s1, col);
+        if (turn) s1 |= bit; else s0 |= bit;
+        const bool won = has_four(turn ? s1 : s0);
+        turn ^= 1;
+        const int r = won ? turn * 2 - 1 : ((s0 | s1) == kFull ? 0 : ZC_C4_ONGOING);
+        const size_t o = (size_t)mv * p.n_games + gl;
+        if (lane == 0) {
+            zc_c4_state post;
+            post.stones[0] = s0;
+            post.stones[1] = s1;
+            post.turn = turn;
+            post.reserved = 0;
+            p.out_states[o] = post;
+            p.out_moves16[o] = (int16_t)col;
+            p.out_results[o] = r;
+            p.io_roots[gl] = r == ZC_C4_ONGOING ? post : zc_c4_state{{0, 0}, 0, 0};
+        }
+        finished += r != ZC_C4_ONGOING;
+        wave_mem_order();
+    }
+    if (lane == 0) {
+        zc_game_stats st{};
+        st.status = status;
+        st.expansions = cn.expansions;
+        st.depth_sum = cn.depth_sum;
+        st.leaves = (int64_t)p.sims * p.moves;
+        st.rollout_plies = cn.plies;
+        st.rollout_blocks = cn.blocks;
+        st.rng_words = rng.use();
+        st.reserved = finished;
         p.out_stats[gl] = st;
     }
     lrng_close(rng, a.ring + (size_t)g * kRingWords, use0, a.rngpos + 2 * (size_t)g);
@@ -704,6 +802,16 @@ void launch_c4_search(const SearchParams &p, hipStream_t s) {
         else
             hipLaunchKernelGGL((c4_search_kernel<false, false>), grid, block, lds, s, p);
     }
+}
+
+void launch_c4_selfplay(const SearchParams &p, hipStream_t s) {
+    const int wpg = c4_search_wpg(p.bs);
+    const size_t lds = c4_search_lds_bytes(p.bs);
+    const dim3 grid((p.n_games + wpg - 1) / wpg), block(wpg * kBlock);
+    if (p.philox)
+        hipLaunchKernelGGL((c4_selfplay_kernel<true>), grid, block, lds, s, p);
+    else
+        hipLaunchKernelGGL((c4_selfplay_kernel<false>), grid, block, lds, s, p);
 }
 
 void launch_c4_rollout_debug(const Arena &a, int M, int first_game, int n, const zc_c4_state *states,

@@ -306,6 +306,27 @@ int zc_rng_get_state(zc_engine *eng, int32_t game, uint32_t *mt624, int32_t *ind
     return ZC_OK;
 }
 
+int zc_c4_selfplay_async(zc_engine *eng, int32_t first, int32_t n, zc_c4_state *d_roots, int32_t sims, double c,
+                         int32_t bs, int32_t moves, zc_c4_state *d_out_states, int16_t *d_out_moves,
+                         int32_t *d_out_results, zc_game_stats *d_stats, void *hip_stream) {
+    if (!eng || (n && (!d_roots || !d_out_states || !d_out_moves || !d_out_results || !d_stats)))
+        return fail(ZC_EINVAL, "null argument");
+    if (int r = check_search(eng, first, n, sims, c, bs)) return r;
+    if (moves < 1) return fail(ZC_EINVAL, "moves must be >= 1 (got %d)", moves);
+    if (!n) return ZC_OK;
+    std::lock_guard<std::mutex> lk(eng->mu);
+    ZC_HIP(hipSetDevice(eng->cfg.device));
+    zc::SearchParams p = make_params(eng, first, n, d_roots, sims, c, bs, nullptr, nullptr, d_stats);
+    p.moves = moves;
+    p.io_roots = d_roots;
+    p.out_states = d_out_states;
+    p.out_moves16 = d_out_moves;
+    p.out_results = d_out_results;
+    zc::launch_c4_selfplay(p, (hipStream_t)hip_stream);
+    ZC_HIP(hipGetLastError());
+    return ZC_OK;
+}
+
 int zc_c4_search_async(zc_engine *eng, int32_t first, int32_t n, const zc_c4_state *d_roots, int32_t sims, double c,
                        int32_t bs, int32_t *d_move, int32_t *d_na, zc_game_stats *d_stats, void *hip_stream) {
     if (!eng || (n && (!d_roots || !d_move || !d_na || !d_stats))) return fail(ZC_EINVAL, "null argument");
@@ -1257,6 +1278,16 @@ int zc_debug_c4_rollout(zc_engine *eng, int32_t first, int32_t n, const zc_c4_st
     ZC_HIP(hipMemcpyAsync(out_words, dw, (size_t)n * sizeof(int64_t), hipMemcpyDeviceToHost, s));
     ZC_HIP(hipStreamSynchronize(s));
     (void)hipFree(dw);
+    return ZC_OK;
+}
+
+int zc_debug_phase_cycles_games(zc_engine *eng, int32_t n_games, int64_t *out) {
+    if (!eng || !out) return fail(ZC_EINVAL, "null argument");
+    if (n_games < 0 || n_games > eng->cfg.max_games) return fail(ZC_EINVAL, "n_games outside the engine");
+    std::lock_guard<std::mutex> lk(eng->mu);
+    ZC_HIP(hipSetDevice(eng->cfg.device));
+    ZC_HIP(hipDeviceSynchronize());
+    ZC_HIP(hipMemcpy(out, eng->a.phase, (size_t)n_games * zc::kPhases * sizeof(int64_t), hipMemcpyDeviceToHost));
     return ZC_OK;
 }
 

@@ -91,6 +91,12 @@ struct SearchParams {
     int stamp;
     int philox;            // rollouts: 0 = the game's MT19937 stream (exact), 1 = Philox mode
     uint64_t philox_seed;  // Philox key of the Philox rollout mode
+    // self-play run (c4_selfplay_kernel): moves per game, per-step outputs [moves][n_games]
+    int moves;
+    zc_c4_state *io_roots;  // = roots, written after every move
+    zc_c4_state *out_states;
+    int16_t *out_moves16;
+    int32_t *out_results;
 };
 
 struct ExtParams {
@@ -255,6 +261,7 @@ void launch_c4_ext_end(const ExtParams &p, hipStream_t s);
 void launch_c4_hp_walk(const ExtParams &p, hipStream_t s);
 void launch_c4_hp_expand(const ExtParams &p, hipStream_t s);
 void launch_c4_search(const SearchParams &p, hipStream_t s);
+void launch_c4_selfplay(const SearchParams &p, hipStream_t s);
 void launch_c4_rollout_debug(const Arena &a, int M, int first_game, int n, const zc_c4_state *states,
                              int32_t *out_value, int64_t *out_words, hipStream_t s);
 void launch_c4_rollout_seq(const Arena &a, int game, int n, const zc_c4_state *states, int32_t *out_value,

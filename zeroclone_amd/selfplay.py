@@ -117,6 +117,7 @@ class Trajectories:
         """Slot g plays game g (g < quota) or idles; the pool is emptied.  quota None = no
         limit (every finished game's slot starts another)."""
         q = _UNLIMITED if quota is None else int(quota)
+        self.quota = q
         if games_cap is not None and games_cap > self.games_cap:
             self._alloc_pool(games_cap, games_cap * self.max_len)
         ids = torch.arange(self.n, dtype=torch.int32, device=self.dev)
@@ -202,6 +203,30 @@ class C4SelfPlay:
         opening."""
         self.step_search(stream)
         return self.step_finish(stream)
+
+    def run(self, moves: int, stream: int | None = None) -> torch.Tensor:
+        """`moves` moves for every game in ONE launch (zc_c4_selfplay_async: each game at its
+        own pace, finished games refilled from the opening in the kernel), then the
+        trajectory recording of every step, in step order — the same games, pool and labels
+        as `moves` calls of step().  Needs the unlimited quota (start(None)): with a quota the
+        refill depends on other slots' finishes, which step() decides once per step.
+        Returns the per-step results [moves, G]; self.stats sums the moves' counters."""
+        if self.traj is not None and self.traj.quota != _UNLIMITED:
+            raise ValueError("run() plays without a game quota; use step() under simulate_games' quota")
+        s = stream if stream is not None else torch.cuda.current_stream(self.dev).cuda_stream
+        if getattr(self, "_run_k", None) != moves:
+            self._run_states = torch.zeros((moves, self.G, 3), dtype=torch.int64, device=self.dev)
+            self._run_moves = torch.zeros((moves, self.G), dtype=torch.int16, device=self.dev)
+            self._run_results = torch.zeros((moves, self.G), dtype=torch.int32, device=self.dev)
+            self._run_k = moves
+        self.eng.c4_selfplay_async(self.roots.data_ptr(), self.G, self.sims, self.c, self.bs, moves,
+                                   self._run_states.data_ptr(), self._run_moves.data_ptr(),
+                                   self._run_results.data_ptr(), self.stats.data_ptr(), stream=s)
+        if self.record:
+            for k in range(moves):
+                self.traj.record(self._run_states[k].data_ptr(), self._run_moves[k], self._run_results[k], stream=s)
+        self.results.copy_(self._run_results[-1])
+        return self._run_results
 
     def step_search(self, stream: int | None = None) -> torch.Tensor:
         """The search half of a step (zc_c4_search_async); returns the results tensor the
