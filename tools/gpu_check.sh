@@ -37,14 +37,14 @@ for st in "$@"; do
             run hbm_write 600 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/hbm -o write \
                 --pmc WRITE_SIZE -- python3 tools/one_search.py --reps 2 || exit $? ;;
     sprof)  run sprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/sprof -o run --output-format csv \
-                -- python3 tools/prof_search.py --steps 20 || exit $? ;;
+                -- python3 tools/prof_search.py --steps 60 || exit $? ;;
     spmc)   run spmc 600 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/spmc -o pmc \
                 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE \
-                -- python3 tools/prof_search.py --steps 20 || exit $? ;;
+                -- python3 tools/prof_search.py --steps 60 || exit $? ;;
     shbm)   run shbm_fetch 600 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/shbm -o fetch \
-                --pmc FETCH_SIZE -- python3 tools/prof_search.py --steps 20 || exit $?
+                --pmc FETCH_SIZE -- python3 tools/prof_search.py --steps 60 || exit $?
             run shbm_write 600 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/shbm -o write \
-                --pmc WRITE_SIZE -- python3 tools/prof_search.py --steps 20 || exit $? ;;
+                --pmc WRITE_SIZE -- python3 tools/prof_search.py --steps 60 || exit $? ;;
     ab)     run ab 900 env AB_ROOTS=mixed AB_ROUNDS=${AB_ROUNDS:-3} python tools/ab_search.py ${AB_LIBS} || exit $? ;;
     *) echo "unknown stage $st"; exit 2 ;;
   esac

@@ -68,7 +68,6 @@ def main():
         for r in csv.DictReader(open(a.stats)):
             if a.kernel in r["Name"]:
                 out["rocprof_stats"] = {"calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"]),
-                                        "avg_ns_per_move": float(r["AverageNs"]) / a.moves,
                                         "min_ns": float(r["MinNs"]), "max_ns": float(r["MaxNs"]),
                                         "percent_of_gpu_time": float(r["Percentage"])}
     if a.trace:
@@ -111,8 +110,8 @@ def main():
                 b = max(units, key=units.get)
                 iss["bound_unit"] = b.split("_")[0]
                 iss["frac"] = units[b]
-            if a.stats and "rocprof_stats" in out:
-                iss["clock_ghz"] = cyc / out["rocprof_stats"]["avg_ns"]
+            if out.get("trace_last_avg_ns"):   # the same launch(es), timed in the --stats pass
+                iss["clock_ghz"] = cyc / out["trace_last_avg_ns"]
             out["issue"] = iss
     json.dump(out, open(a.out, "w"), indent=1)
     print(json.dumps(out))
