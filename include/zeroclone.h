@@ -315,6 +315,23 @@ int zc_chess_ext_backup(zc_engine *eng, int32_t first_game, int32_t n_games, int
 int zc_chess_ext_end(zc_engine *eng, int32_t first_game, int32_t n_games, uint16_t *d_out_move,
                      int32_t *d_out_root_na, zc_game_stats *d_out_stats, void *hip_stream);
 
+/* Host-policy chess search inside a zc_chess_ext_begin .. end search (as zc_c4_hp_*): the
+ * walk returns the node's position and its untried moves (packed from | to << 6 |
+ * capture value << 12, in the node's untried-list order, the list mcts.cpp:67-70 hands to
+ * the policy); expand takes the index of the caller's pick in that list. */
+typedef struct zc_chess_hp_node {
+    zc_chess_state state;
+    int32_t node;
+    int32_t n_untried;
+    int32_t depth;
+    int32_t reserved;
+    uint16_t untried[ZC_CHESS_MAX_MOVES];
+} zc_chess_hp_node;
+int zc_chess_hp_walk(zc_engine *eng, int32_t game, int32_t flush, int32_t leaf, zc_chess_hp_node *d_node,
+                     void *hip_stream);
+int zc_chess_hp_expand(zc_engine *eng, int32_t game, int32_t flush, int32_t leaf, int32_t untried_index,
+                       zc_chess_state *d_leaf, void *hip_stream);
+
 /* ---- Chess PUCT search (AlphaZero-style; no reference counterpart) -------
  * Selection by Q + c_puct * P * sqrt(sum N) / (1 + N) with priors P from a policy network,
  * virtual loss within a flush, Dirichlet(alpha) noise of weight eps on the root priors

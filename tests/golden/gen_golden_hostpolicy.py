@@ -51,6 +51,46 @@ def main():
     meta = {"generator": "tests/golden/gen_golden_hostpolicy.py", "policies": "tests/c4_policies.py"}
     json.dump({"meta": meta, "cases": cases}, open(os.path.join(HERE, "c4_get_move_hostpolicy.json"), "w"))
     print(len(cases), "cases")
+    chess_main(mcts, vf)
+
+
+def chess_main(mcts, vf):
+    """Chess: the reference's compiled chess backend, Value('crude_chess_score')."""
+    import gen_golden_chess as GC
+    cb = GC.load_ref()
+
+    def run(fen, seed, sims, bs, c, pname):
+        st = cb.state_from_fen(fen)
+        pol = P.ChessRecording(P.make(pname))
+        val = G.RecordingValue(vf.Value("crude_chess_score"))
+        val.counts = {}
+        random.seed(seed)
+        mv = mcts.get_move(st, _Counting(val), pol, cb, sims, c, bs)
+        return {"fen": fen, "seed": seed, "sims": sims, "bs": bs, "c": c, "policy": pname,
+                "move": list(mv[0]) + [mv[1]], "calls": pol.calls, "leaves": val.leaves,
+                "next_word": random.getrandbits(32)}
+
+    cases = []
+    fens = [GC.FENS["start"], GC.FENS["kiwipete"], GC.FENS["pos4"],
+            "r1bqkbnr/pppp1ppp/2n5/4p3/2B1P3/5Q2/PPPP1PPP/RNB1K1NR w KQkq - 2 3"]
+    for i, fen in enumerate(fens):
+        for k, pname in enumerate(P.CHESS_POLICIES):
+            cases.append(run(fen, 100 + 10 * i + k, 48 + 16 * k, (8, 16, 32, 5)[k], 1.4, pname))
+    json.dump({"meta": {"generator": "tests/golden/gen_golden_hostpolicy.py", "policies": "tests/c4_policies.py",
+                        "value": "crude_chess_score"}, "cases": cases},
+              open(os.path.join(HERE, "chess_get_move_hostpolicy.json"), "w"))
+    print(len(cases), "chess cases")
+
+
+class _Counting:
+    """Value.batch pass-through that counts leaves (the reference's states carry no tag)."""
+
+    def __init__(self, rec):
+        self.rec = rec
+
+    def batch(self, states, **kw):
+        self.rec.leaves += len(states)
+        return self.rec.inner.batch(states, **kw)
 
 
 if __name__ == "__main__":

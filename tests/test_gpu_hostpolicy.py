@@ -94,3 +94,24 @@ def test_engine_with_a_host_policy_plays_the_reference_move(golden):
     col = c["move"]
     assert after.board[5][col] == "X" and sum(ch != " " for row in after.board for ch in row) == 1
     assert random.getrandbits(32) == c["next_word"]
+
+
+def test_chess_host_policy_get_move_matches_reference(golden):
+    """Chess: the reference's compiled get_move with the reference chess backend and
+    Value('crude_chess_score') (tests/golden/chess_get_move_hostpolicy.json) — every policy
+    call (size, pick and a checksum of the untried list in order), move, leaves, and Python's
+    `random` afterwards."""
+    from zeroclone_amd.engine.games.chess import chess_backend as cb
+    cases = golden("chess_get_move_hostpolicy.json")["cases"]
+    assert len(cases) >= 16
+    for c in cases:
+        st = cb.state_from_fen(c["fen"])
+        pol = P.ChessRecording(P.make(c["policy"]))
+        val = CountingValue(Value("crude_chess_score"))
+        random.seed(c["seed"])
+        mv = mcts.get_move(st, val, pol, cb, c["sims"], c["c"], c["bs"])
+        key = (c["fen"], c["policy"], c["seed"])
+        assert pol.calls == c["calls"], key
+        assert list(mv[0]) + [mv[1]] == c["move"], key
+        assert val.leaves == c["leaves"], key
+        assert random.getrandbits(32) == c["next_word"], key

@@ -66,6 +66,9 @@ STATS_DTYPE = np.dtype([("expansions", "<i8"), ("depth_sum", "<i8"), ("leaves", 
 CHESS_STATE_DTYPE = np.dtype([("board", "u1", (64,)), ("turn", "u1"), ("fifty", "u1"), ("castle", "u1"),
                               ("reserved", "u1", (5,))])
 CHESS_MAX_MOVES = 256
+# zc_chess_hp_node: the chess host-policy walk's end (include/zeroclone.h)
+CHESS_HP_NODE_DTYPE = np.dtype([("state", CHESS_STATE_DTYPE), ("node", "<i4"), ("n_untried", "<i4"), ("depth", "<i4"),
+                                ("reserved", "<i4"), ("untried", "<u2", (CHESS_MAX_MOVES,))])
 # ChessNode (zc_internal.h): the device tree's node record, as zc_debug_chess_tree copies it
 CHESS_NODE_DTYPE = np.dtype([("st", "u1", (72,)), ("base", "<u4"), ("nmoves", "<u2"), ("nu", "<u2"),
                              ("parent", "<u2"), ("pact", "<u2"), ("depth", "<u2"), ("material", "<i2"),
@@ -152,6 +155,10 @@ SIGNATURES = [
                                            ctypes.c_void_p]),
     ("zc_chess_ext_backup", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
                                            ctypes.c_void_p, ctypes.c_void_p]),
+    ("zc_chess_hp_walk", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                        ctypes.c_void_p, ctypes.c_void_p]),
+    ("zc_chess_hp_expand", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                          ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p]),
     ("zc_chess_ext_end", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p,
                                         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     ("zc_chess_puct_flushes", ctypes.c_int, [ctypes.c_int32, ctypes.c_int32]),
@@ -481,6 +488,14 @@ class NativeEngine:
     def chess_ext_backup(self, first_game: int, n: int, flush: int, d_values: int, stream: int = 0):
         check(lib().zc_chess_ext_backup(self._h, first_game, n, int(flush), ctypes.c_void_p(d_values),
                                         ctypes.c_void_p(stream or None)))
+
+    def chess_hp_walk(self, game: int, flush: int, leaf: int, d_node: int, stream: int = 0) -> None:
+        check(lib().zc_chess_hp_walk(self._h, game, int(flush), int(leaf), ctypes.c_void_p(d_node),
+                                     ctypes.c_void_p(stream or None)))
+
+    def chess_hp_expand(self, game: int, flush: int, leaf: int, index: int, d_leaf: int = 0, stream: int = 0) -> None:
+        check(lib().zc_chess_hp_expand(self._h, game, int(flush), int(leaf), int(index),
+                                       ctypes.c_void_p(d_leaf or None), ctypes.c_void_p(stream or None)))
 
     def chess_ext_end(self, first_game: int, n: int, d_move: int, d_na: int, d_stats: int, stream: int = 0):
         check(lib().zc_chess_ext_end(self._h, first_game, n, ctypes.c_void_p(d_move), ctypes.c_void_p(d_na),

@@ -39,21 +39,13 @@ struct Resume {
     uint32_t stw = 0;            // lanes 0..17: the node's position (zc_chess_state words)
 };
 
-// select + expand + record of ONE simulation (mcts.cpp:129-147).  Returns the leaf node;
-// its depth in `ldepth`; lane l of `pathv` holds the slot of the edge into level l.
-__device__ int simulate(const ChessParams &p, const CTree &t, CLds &L, ConstDouble *logtab, Rng &rng, int done,
-                        int &nnodes, int &slots, int &status, int &ldepth, uint32_t &pathv, Counters &cn,
-                        Resume &rs) {
+// select (mcts.cpp:47-63) from `node` down: the UCT child (first maximum, +inf for an
+// unvisited edge) until a node with untried moves or without moves; lane l of pathv gets the
+// slot of the edge into level l.
+__device__ __forceinline__ void chess_walk(const ChessParams &p, const CTree &t, ConstDouble *logtab, int &node,
+                                           int &depth, int &nN, uint32_t &pathv, int &status) {
     const uint32_t lane = lane_id();
-    int node = 0, depth = 0, nN = done;
-    pathv = 0;
-    if (rs.valid) {
-        node = rs.node;
-        depth = rs.depth;
-        nN = rs.nN;
-        pathv = rs.pathv;
-    }
-    for (; !rs.cached;) {  // select (mcts.cpp:47-63)
+    for (;;) {  // select (mcts.cpp:47-63)
         const ChessNode *N = &t.nodes[node];
         const uint32_t base = uni(N->base);
         const int nm = uni((int)N->nmoves), nu = uni((int)N->nu);
@@ -110,6 +102,23 @@ __device__ int simulate(const ChessParams &p, const CTree &t, CLds &L, ConstDoub
         if (lane == (uint32_t)depth) pathv = base + (uint32_t)best;
         node = nxt;
     }
+}
+
+// select + expand + record of ONE simulation (mcts.cpp:129-147).  Returns the leaf node;
+// its depth in `ldepth`; lane l of `pathv` holds the slot of the edge into level l.
+__device__ int simulate(const ChessParams &p, const CTree &t, CLds &L, ConstDouble *logtab, Rng &rng, int done,
+                        int &nnodes, int &slots, int &status, int &ldepth, uint32_t &pathv, Counters &cn,
+                        Resume &rs) {
+    const uint32_t lane = lane_id();
+    int node = 0, depth = 0, nN = done;
+    pathv = 0;
+    if (rs.valid) {
+        node = rs.node;
+        depth = rs.depth;
+        nN = rs.nN;
+        pathv = rs.pathv;
+    }
+    if (!rs.cached) chess_walk(p, t, logtab, node, depth, nN, pathv, status);
     ChessNode *N = &t.nodes[node];
     const bool hit = rs.cached;
     const int nu = hit ? rs.nu : uni((int)N->nu);
@@ -441,7 +450,114 @@ __global__ __launch_bounds__(64) void chess_ext_end_kernel(ChessParams p) {
     finish(p, ctree(p, g), gl, g, p.ca.ctl + (size_t)g * kCtlWords);
 }
 
+// ---------------------------------------------------------------- host policy (§8(b))
+// One game, one simulation per walk/expand pair, as c4_ext.hip's zc_c4_hp_*: the caller's
+// policy picks among the untried moves between the two launches.
+__global__ __launch_bounds__(64) void chess_hp_walk_kernel(ChessParams p) {
+    const uint32_t lane = lane_id();
+    const int g = p.first_game;
+    const CTree t = ctree(p, g);
+    int32_t *ctl = p.ca.ctl + (size_t)g * kCtlWords;
+    int status = uni(ctl[cStatus]);
+    zc_chess_hp_node *out = p.hp_node;
+    if (status) {
+        if (lane == 0) {
+            out->node = -1;
+            out->n_untried = 0;
+            out->depth = 0;
+        }
+        return;
+    }
+    int node = 0, depth = 0, nN = p.flush * p.bs;
+    uint32_t pathv = 0;
+    chess_walk(p, t, (ConstDouble *)p.a.logtab, node, depth, nN, pathv, status);
+    uint32_t *path = p.ca.paths + ((size_t)g * p.max_batch + p.hp_leaf) * kChessPath;
+    if (lane < (uint32_t)kChessPath) path[lane] = pathv;
+    const ChessNode *N = &t.nodes[node];
+    const int nu = status ? 0 : uni((int)N->nu);
+    const uint32_t base = uni(N->base);
+    for (int i = (int)lane; i < nu; i += 64) out->untried[i] = t.mv[base + t.ut[base + i]];
+    if (lane < 18) ((uint32_t *)&out->state)[lane] = ((const uint32_t *)&N->st)[lane];
+    if (lane == 0) {
+        out->node = node;
+        out->n_untried = nu;
+        out->depth = depth;
+        ctl[cHpNode] = node;
+        ctl[cHpNode + 1] = depth;
+        ctl[cStatus] = status;
+    }
+}
+
+__global__ __launch_bounds__(64) void chess_hp_expand_kernel(ChessParams p) {
+    __shared__ CLds L;
+    const uint32_t lane = lane_id();
+    const int g = p.first_game;
+    const CTree t = ctree(p, g);
+    int32_t *ctl = p.ca.ctl + (size_t)g * kCtlWords;
+    if (uni(ctl[cStatus])) return;
+    const int node = uni(ctl[cHpNode]);
+    int depth = uni(ctl[cHpNode + 1]);
+    int nnodes = uni(ctl[cNodes]), slots = uni(ctl[cSlots]), status = 0;
+    uint32_t *path = p.ca.paths + ((size_t)g * p.max_batch + p.hp_leaf) * kChessPath;
+    ChessNode *N = &t.nodes[node];
+    const int nu = uni((int)N->nu);
+    int leaf = node;
+    if (nu > 0) {
+        const int local = p.hp_index;
+        if (local < 0 || local >= nu) {
+            if (lane == 0) ctl[cStatus] = ZC_STATUS_INTERNAL;
+            return;
+        }
+        // expand (mcts.cpp:65-78) with the caller's pick: untried.erase(begin + local)
+        const uint32_t base = uni(N->base);
+        const int midx = uni((int)t.ut[base + local]);
+        const uint32_t m = uni((uint32_t)t.mv[base + midx]);
+        for (int b = local; b < nu - 1; b += 64) {
+            const int i = b + (int)lane;
+            uint8_t v = 0;
+            if (i < nu - 1) v = t.ut[base + i + 1];
+            wave_sync_mem();
+            if (i < nu - 1) t.ut[base + i] = v;
+        }
+        if (lane == 0) N->nu = (uint16_t)(nu - 1);
+        if (lane < 18) ((uint32_t *)&L.st)[lane] = ((const uint32_t *)&N->st)[lane];
+        wave_sync_mem();
+        if (lane == 0) chessdev::apply_move(L.st, m);
+        wave_sync_mem();
+        const int child = nnodes++;
+        if (child >= p.M) {
+            if (lane == 0) ctl[cStatus] = ZC_STATUS_INTERNAL;
+            return;
+        }
+        create_node(t, L, child, node, midx, depth + 1, slots, status);
+        ++depth;
+        if (lane == 0) {
+            t.ch[base + midx] = (uint16_t)child;
+            path[depth] = base + (uint32_t)midx;
+            ctl[cExp] += 1;
+            ctl[cDepth] += depth;
+        }
+        leaf = child;
+        wave_sync_mem();
+    }
+    if (p.leaves && lane < 18) ((uint32_t *)&p.leaves[0])[lane] = ((const uint32_t *)&t.nodes[leaf].st)[lane];
+    if (lane == 0) {
+        p.ca.meta[(size_t)g * p.max_batch + p.hp_leaf] = (uint32_t)leaf | ((uint32_t)depth << 16);
+        ctl[cNodes] = nnodes;
+        ctl[cSlots] = slots;
+        ctl[cStatus] = status;
+        ctl[cNb] = p.hp_leaf + 1;
+    }
+}
+
 }  // namespace
+
+void launch_chess_hp_walk(const ChessParams &p, hipStream_t s) {
+    hipLaunchKernelGGL(chess_hp_walk_kernel, dim3(1), dim3(64), 0, s, p);
+}
+void launch_chess_hp_expand(const ChessParams &p, hipStream_t s) {
+    hipLaunchKernelGGL(chess_hp_expand_kernel, dim3(1), dim3(64), 0, s, p);
+}
 
 void launch_chess_search(const ChessParams &p, hipStream_t s) {
     hipLaunchKernelGGL(chess_search_kernel, dim3(p.n_games), dim3(64), 0, s, p);

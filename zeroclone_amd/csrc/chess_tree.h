@@ -28,7 +28,7 @@ __device__ __forceinline__ CTree ctree(const ChessParams &p, int g) {
                  a.prior ? a.prior + so : nullptr, a.S};
 }
 
-enum : int { cNodes = 0, cSlots = 1, cStatus = 2, cNb = 3, cExp = 4, cDepth = 5, cUse0 = 6 };
+enum : int { cNodes = 0, cSlots = 1, cStatus = 2, cNb = 3, cExp = 4, cDepth = 5, cUse0 = 6, cHpNode = 8 };
 
 struct CLds {
     ChessScratch s;

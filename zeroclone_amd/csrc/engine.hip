@@ -810,6 +810,43 @@ int zc_chess_ext_end(zc_engine *eng, int32_t first, int32_t n, uint16_t *d_move,
     return ZC_OK;
 }
 
+int zc_chess_hp_walk(zc_engine *eng, int32_t game, int32_t flush, int32_t leaf, zc_chess_hp_node *d_node,
+                     void *hip_stream) {
+    if (!eng || !d_node) return fail(ZC_EINVAL, "null argument");
+    std::lock_guard<std::mutex> lk(eng->mu);
+    if (int r = check_cx(eng, game, 1, flush, true)) return r;
+    const int nb = std::min(eng->cx_bs, eng->cx_sims - flush * eng->cx_bs);
+    if (leaf < 0 || leaf >= nb) return fail(ZC_EINVAL, "leaf %d outside flush %d's [0, %d)", leaf, flush, nb);
+    ZC_HIP(hipSetDevice(eng->cfg.device));
+    zc::ChessParams p = chess_params(eng, game, 1, eng->cx_sims, eng->cx_c, eng->cx_bs, eng->cx_policy, eng->cx_freedom);
+    p.flush = flush;
+    p.hp_leaf = leaf;
+    p.hp_node = d_node;
+    zc::launch_chess_hp_walk(p, (hipStream_t)hip_stream);
+    ZC_HIP(hipGetLastError());
+    return ZC_OK;
+}
+
+int zc_chess_hp_expand(zc_engine *eng, int32_t game, int32_t flush, int32_t leaf, int32_t untried_index,
+                       zc_chess_state *d_leaf, void *hip_stream) {
+    if (!eng) return fail(ZC_EINVAL, "null argument");
+    std::lock_guard<std::mutex> lk(eng->mu);
+    if (int r = check_cx(eng, game, 1, flush, true)) return r;
+    const int nb = std::min(eng->cx_bs, eng->cx_sims - flush * eng->cx_bs);
+    if (leaf < 0 || leaf >= nb) return fail(ZC_EINVAL, "leaf %d outside flush %d's [0, %d)", leaf, flush, nb);
+    if (untried_index < -1 || untried_index >= ZC_CHESS_MAX_MOVES)
+        return fail(ZC_EINVAL, "untried index %d outside [-1, %d)", untried_index, ZC_CHESS_MAX_MOVES);
+    ZC_HIP(hipSetDevice(eng->cfg.device));
+    zc::ChessParams p = chess_params(eng, game, 1, eng->cx_sims, eng->cx_c, eng->cx_bs, eng->cx_policy, eng->cx_freedom);
+    p.flush = flush;
+    p.hp_leaf = leaf;
+    p.hp_index = untried_index;
+    p.leaves = d_leaf;
+    zc::launch_chess_hp_expand(p, (hipStream_t)hip_stream);
+    ZC_HIP(hipGetLastError());
+    return ZC_OK;
+}
+
 // ---------------------------------------------------------------- chess PUCT search
 int zc_chess_puct_flushes(int32_t sims, int32_t bs) {
     if (sims < 2 || bs < 1) return fail(ZC_EINVAL, "PUCT search needs sims >= 2 and batch_size >= 1");

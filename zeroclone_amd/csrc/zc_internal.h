@@ -176,6 +176,9 @@ struct ChessParams {
     const void *logits;         // backup: [n*bs][4096] policy logits (from*64 + to)
     int logits_f16;
     float *out_prior;           // end (optional): root priors after noise [n][ZC_CHESS_MAX_MOVES]
+    // host-policy search (zc_chess_hp_*): leaf index in the flush, untried index, walk output
+    int hp_leaf, hp_index;
+    zc_chess_hp_node *hp_node;
 };
 
 // ---------------------------------------------------------------- Connect4 PUCT search
@@ -231,6 +234,8 @@ void launch_chess_ext_begin(const ChessParams &p, hipStream_t s);
 void launch_chess_ext_select(const ChessParams &p, hipStream_t s);
 void launch_chess_ext_backup(const ChessParams &p, hipStream_t s);
 void launch_chess_ext_end(const ChessParams &p, hipStream_t s);
+void launch_chess_hp_walk(const ChessParams &p, hipStream_t s);
+void launch_chess_hp_expand(const ChessParams &p, hipStream_t s);
 
 void launch_chess_puct_begin(const ChessParams &p, hipStream_t s);
 void launch_chess_puct_select(const ChessParams &p, hipStream_t s);

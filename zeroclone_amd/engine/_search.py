@@ -11,9 +11,10 @@ chess; Connect4 moves carry no capture value, so for Connect4 immediate_value pi
 all untried moves exactly like random (policy_functions.py:14-17 with all values 0) and both
 map to the same device policy.
 
-Any other policy callable (SURVEY §8(b)'s fallback) runs the Connect4 search in host-policy
-mode: the tree stays on the device and every expansion calls policy(untried_moves) on the
-host, where mcts.cpp:65-78 calls it (zc_c4_hp_walk / zc_c4_hp_expand, `c4_host_policy_moves`).
+Any other policy callable (SURVEY §8(b)'s fallback) runs the search in host-policy mode: the
+tree stays on the device and every expansion calls policy(untried_moves) on the host, where
+mcts.cpp:65-78 calls it (zc_c4_hp_* / zc_chess_hp_*: `c4_host_policy_moves`,
+`chess_host_policy_moves`).
 """
 from __future__ import annotations
 
@@ -87,7 +88,7 @@ def chess_moves(eng, ids, states, sims, c, bs, value, policy, backend):
     import torch
     pol, freedom = policy_of(policy)
     if pol == HOST_POLICY:
-        raise NotImplementedError("a host policy callable runs on the Connect4 search only")
+        return chess_host_policy_moves(eng, ids, states, sims, c, bs, value, policy, backend)
     kind = value_kind(value)
     n = len(ids)
     dev = torch.device("cuda", eng.device)
@@ -202,4 +203,59 @@ def c4_host_policy_moves(eng, ids, roots, sims, c, bs, value, policy, backend):
         if int(st[0, 5].item()):
             raise RuntimeError(f"host-policy search failed (status {int(st[0, 5].item())})")
         out.append((int(mv[0].item()), 0))
+    return out
+
+
+def chess_host_policy_moves(eng, ids, states, sims, c, bs, value, policy, backend):
+    """The §8(b) fallback for chess: as c4_host_policy_moves, on the chess tree
+    (zc_chess_hp_walk / zc_chess_hp_expand inside a zc_chess_ext_* search).  The policy gets
+    the untried moves as the reference's move objects ((fr, fc, tr, tc), capture value), in
+    the node's untried order; a game with no legal move gives None."""
+    import torch
+    from .games.chess import chess_backend as cb
+    dev = torch.device("cuda", eng.device)
+    stream = torch.cuda.current_stream(dev)
+    s = stream.cuda_stream
+    node = torch.zeros(_native.CHESS_HP_NODE_DTYPE.itemsize, dtype=torch.uint8, device=dev)
+    leaf = torch.zeros(72, dtype=torch.uint8, device=dev)
+    vals = torch.zeros(bs, dtype=torch.float64, device=dev)
+    mv = torch.zeros(1, dtype=torch.int16, device=dev)
+    na = torch.zeros((1, _native.CHESS_MAX_MOVES), dtype=torch.int32, device=dev)
+    st = torch.zeros((1, _native.STATS_FIELDS), dtype=torch.int64, device=dev)
+    out = []
+    for gi, state in zip(ids, states):
+        root = torch.from_numpy(chess_roots([state]).view(np.uint8).reshape(1, 72).copy()).to(dev)
+        eng.chess_ext_begin(int(gi), 1, root.data_ptr(), sims, c, bs, _native.ZC_POLICY_RANDOM, 0.0, s)
+        live = True
+        for f in range((sims + bs - 1) // bs):
+            nb = min(bs, sims - f * bs)
+            leaves = []
+            for j in range(nb):
+                eng.chess_hp_walk(int(gi), f, j, node.data_ptr(), s)
+                nd = node.cpu().numpy().view(_native.CHESS_HP_NODE_DTYPE)[0]
+                if int(nd["node"]) < 0:
+                    live = False
+                    break
+                k = -1
+                n_un = int(nd["n_untried"])
+                if n_un:
+                    moves = [_native.unpack_chess_move(m) for m in nd["untried"][:n_un]]
+                    k = moves.index(policy(moves))
+                eng.chess_hp_expand(int(gi), f, j, k, leaf.data_ptr(), s)
+                leaves.append(cb.from_zc(leaf.cpu().numpy().view(_native.CHESS_STATE_DTYPE)[0]))
+            if not live:
+                break
+            v = [float(x) for x in value.batch(leaves, backend=backend)]
+            vals[:nb].copy_(torch.tensor(v, dtype=torch.float64))
+            eng.chess_ext_backup(int(gi), 1, f, vals.data_ptr(), s)
+        eng.chess_ext_end(int(gi), 1, mv.data_ptr(), na.data_ptr(), st.data_ptr(), s)
+        stream.synchronize()
+        status = int(st[0, 5].item())
+        if status == _native.ZC_STATUS_NO_MOVES:
+            out.append(None)
+            continue
+        if status:
+            raise RuntimeError(f"host-policy chess search failed (status {status})")
+        m = int(mv[0].item()) & 0xFFFF
+        out.append(None if m == 0xFFFF else _native.unpack_chess_move(m))
     return out

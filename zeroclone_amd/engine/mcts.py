@@ -11,8 +11,8 @@ reference's state.  The GIL is released during device calls (ctypes).
 
 Supported plugins: the Connect4 and chess backends (this package's, or the reference's —
 states with the same fields), Policy('random') / Policy('immediate_value') on the device, any
-other policy callable for Connect4 (called on the host at each expansion, the tree still on
-the device: _search.c4_host_policy_moves), and any value
+other policy callable (called on the host at each expansion, the tree still on the device:
+_search.c4_host_policy_moves / chess_host_policy_moves), and any value
 object: Value('random_rollout') (Connect4) and Value('crude_chess_score') (chess) run inside
 the search kernel, network values run on the device between the select and backup kernels,
 and any other object's value.batch(states, backend=backend) is called on the host once per
@@ -29,8 +29,7 @@ __all__ = ["get_move"]
 
 def _plugin_check(state, value, policy, backend):
     game = _search.game_of(backend, state)
-    if _search.policy_of(policy)[0] == _search.HOST_POLICY and game != "connect4":
-        raise NotImplementedError("a host policy callable runs on the Connect4 search only")
+    _search.policy_of(policy)
     kind = _search.value_kind(value)
     if game == "connect4" and kind == "crude":
         raise NotImplementedError("crude_chess_score is a chess value function")
@@ -47,11 +46,17 @@ def get_move(state, value, policy, backend, simulations=1000, c=1.4, batch_size=
         raise ValueError("batch_size must be >= 1")
     ge = _device.scratch(simulations, batch_size)
     if _search.policy_of(policy)[0] == _search.HOST_POLICY:
-        from .games.connect4 import c4_backend as c4
         with ge.lock:
             eng = ge.ensure(1, simulations, batch_size)
-            return _search.c4_host_policy_moves(eng, [0], _device.c4_roots([state], c4), simulations, c,
-                                                batch_size, value, policy, backend)[0]
+            if game == "connect4":
+                from .games.connect4 import c4_backend as c4
+                return _search.c4_host_policy_moves(eng, [0], _device.c4_roots([state], c4), simulations, c,
+                                                    batch_size, value, policy, backend)[0]
+            mv = _search.chess_host_policy_moves(eng, [0], [state], simulations, c, batch_size, value, policy,
+                                                 backend)[0]
+            if mv is None:
+                raise ValueError("root has no legal move (the reference indexes moves[-1] here)")
+            return mv
     with ge.lock:
         eng = ge.ensure(1, simulations, batch_size)
         mt, idx, ver, gauss = _device.python_random_state()
