@@ -193,13 +193,17 @@ __device__ void c4_rollouts(Leaf *L, int nb, R &rng, const uint32_t *s_order, Co
             uint32_t owp = s_order[(uint32_t)mask & ~pairbits];
             for (;;) {
                 RMARK(6);
-                if (rng.off >= (uint32_t)kWin) rng_advance(rng);
-                const uint32_t wv = rng_view(rng);  // lane l: word off + l
-                uint32_t v = wv >> sh;
-                uint64_t A = __ballot(v < n);  // accepted words
-                if (!A) {
+                uint32_t wv, v;
+                uint64_t A;  // accepted words
+                // a view without an accepted word (2^-64 at worst) is consumed whole; its own
+                // loop keeps the block loop's state off a second back edge
+                for (;;) {
+                    if (rng.off >= (uint32_t)kWin) rng_advance(rng);
+                    wv = rng_view(rng);  // lane l: word off + l
+                    v = wv >> sh;
+                    A = __ballot(v < n);
+                    if (A) break;
                     rng.off += (uint32_t)kWin;
-                    continue;
                 }
                 cn.add(cn.blocks, 1);
                 RMARK(2);
@@ -295,11 +299,13 @@ __device__ void c4_rollouts(Leaf *L, int nb, R &rng, const uint32_t *s_order, Co
                 // one if it was played, and the one the block ended at
                 const bool fa = endlane >= lf;
                 const bool fe = __builtin_amdgcn_readlane((int)fills, (int)endlane) != 0;
-                if (fa | fe) {
+                {  // unconditional (selects), so the block loop carries one copy of its state
                     const uint32_t ce = fe ? (uint32_t)__builtin_amdgcn_readlane((int)col, (int)endlane) : cf;
                     const uint32_t ca = fa ? cf : ce;
-                    mask &= ~((1 << ca) | (1 << ce));
-                    ow = (uint32_t)__builtin_amdgcn_readlane((int)owp, (int)(7u * ca + ce));
+                    const bool ff = fa | fe;
+                    mask = ff ? mask & ~((1 << ca) | (1 << ce)) : mask;
+                    const uint32_t ownew = (uint32_t)__builtin_amdgcn_readlane((int)owp, (int)((7u * ca + ce) & 63u));
+                    ow = ff ? ownew : ow;
                     owp = s_order[(uint32_t)mask & ~pairbits];
                 }
                 n = (ow >> 24) & 15u;
