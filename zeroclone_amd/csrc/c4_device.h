@@ -58,6 +58,9 @@ __device__ __forceinline__ uint64_t uni64(uint64_t x) {
     return ((uint64_t)uni((uint32_t)(x >> 32)) << 32) | (uint64_t)uni((uint32_t)x);
 }
 __device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
+__device__ __forceinline__ uint32_t mbcnt64(uint64_t m) {  // set bits of m in lanes below this one
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
 
 __device__ __forceinline__ void wave_mem_order() {
     // Same-wave hand-offs through memory (one lane stores, another loads) are ordered by
@@ -610,7 +613,7 @@ __device__ __forceinline__ void select_flush(const Tree &t, Fresh *fresh, Leaf *
             if ((u >> bb) & 1u) ul |= bb << (3 * c++);
     }
     int bulk0 = 0;          // first node id of the last bulk (the children of `node`)
-    uint32_t inv = 0;       // slot s of `node` expanded by draw i of that bulk: (8 | i) << 4s
+    uint32_t invl = 0;      // lane k: 8 | i when slot k of `node` was expanded by draw i of that bulk
     uint32_t c_low = 0, c_lmask = 0;  // lane i: child i's order word / legal mask
     int j = 0;
     while (j < nb) {
@@ -626,12 +629,12 @@ __device__ __forceinline__ void select_flush(const Tree &t, Fresh *fresh, Leaf *
                 break;
             }
             const int s = __builtin_ctzll(fm);
-            const int child = bulk0 + (int)((inv >> (4 * s)) & 7u);
+            const int i = __builtin_amdgcn_readlane((int)invl, s) & 7;
+            const int child = bulk0 + i;
             if (node == x0node) {  // leaving X0 for good (walks never go back up)
                 x_u = u;
                 x_ch = ch;
             }
-            const int i = (int)((inv >> (4 * s)) & 7u);
             const uint64_t bit = drop_bit(b0 | b1, (int)((ow >> (3 * s)) & 7u));
             if (turn) b1 |= bit; else b0 |= bit;
             turn ^= 1;
@@ -648,8 +651,7 @@ __device__ __forceinline__ void select_flush(const Tree &t, Fresh *fresh, Leaf *
         }
         // ---- m draws (random.choice over cnt, cnt-1, ... untried moves)
         const int m = min((int)cnt, nb - j);
-        uint32_t picks = 0, ucl = 0;
-        inv = 0;
+        uint32_t rr = 0;  // lane i < m: draw i's value r (the index into the untried list then)
         {
             int done = 0;
             for (;;) {  // one 64-word view per pass
@@ -665,37 +667,28 @@ __device__ __forceinline__ void select_flush(const Tree &t, Fresh *fresh, Leaf *
                     A[i] = __ballot((w >> __clz(n)) < n);
                 }
                 // the draws, a scalar chain: each takes the first accepted word after the last
-                uint64_t gt = ~0ull;  // lanes after the last accepted word
+                uint64_t gt = ~0ull, F = 0;  // lanes after the last accepted word; accepted words
                 int f = -1, nd = 0;
-                int fl[7];
 #pragma unroll
                 for (int i = 0; i < 7; ++i) {
-                    fl[i] = 0;
                     if (i < rem && nd == i) {
                         const uint64_t acc = A[i] & gt;
                         if (acc) {
                             f = __builtin_ctzll(acc);
-                            fl[i] = f;
+                            F |= 1ull << f;
                             gt = (uint64_t)0 - (2ull << f);
                             nd = i + 1;
                         }
                     }
                 }
-                // the r-th untried move of each draw (r = the accepted word's value), erased
-                // from the list in turn
-#pragma unroll
-                for (int i = 0; i < 7; ++i) {
-                    if (i < nd) {
-                        const uint32_t n = cnt - (uint32_t)(done + i);
-                        const uint32_t r = (uint32_t)__builtin_amdgcn_readlane((int)w, fl[i]) >> __clz(n);
-                        const uint32_t mi = (ul >> (3 * r)) & 7u;
-                        const uint32_t lowm = (1u << (3 * r)) - 1u;
-                        ul = (ul & lowm) | ((ul >> 3) & ~lowm);
-                        picks |= mi << (3 * (done + i));
-                        inv |= (8u | (uint32_t)(done + i)) << (4 * mi);
-                        ucl |= 1u << mi;
-                    }
-                }
+                // lane-parallel: accepted word l is draw di = done + (accepted words below it);
+                // its value goes to lane di (a forward permute; lanes outside [done, done + nd)
+                // keep theirs)
+                const bool inF = (F >> lane) & 1ull;
+                const uint32_t di = (uint32_t)done + mbcnt64(F);
+                const uint32_t rl = w >> __clz(max((int)cnt - (int)di, 1));
+                const uint32_t got = (uint32_t)__builtin_amdgcn_ds_permute((int)((inF ? di : 63u) << 2), (int)rl);
+                if ((int)lane >= done && (int)lane < done + nd) rr = got;
                 done += nd;
                 if (done < m) {  // the view ran out: all of it is consumed
                     rng.off += (uint32_t)kWin;
@@ -705,11 +698,28 @@ __device__ __forceinline__ void select_flush(const Tree &t, Fresh *fresh, Leaf *
                 break;
             }
         }
+        // draw i's position in the untried list as it was before the bulk (the erase of
+        // mcts.cpp:72 undone all at once, a Lehmer code: later draws skip the earlier picks)
+        uint32_t pl = rr;
+#pragma unroll
+        for (int i = 5; i >= 0; --i) {
+            const uint32_t pi = (uint32_t)__builtin_amdgcn_readlane((int)pl, i);
+            pl += ((int)lane > i && (int)lane < m && pl >= pi) ? 1u : 0u;
+        }
+        const uint32_t mi_l = (ul >> (3 * (pl & 7u))) & 7u;  // lane i < m: draw i's move index
+        // the expanded slots (OR over lanes 0..7, DPP) and, in lane k, the draw that took slot k
+        uint32_t slotbit = (int)lane < m ? 1u << mi_l : 0u;
+        slotbit |= (uint32_t)dpp<0xB1>((int)slotbit);
+        slotbit |= (uint32_t)dpp<0x4E>((int)slotbit);
+        slotbit |= (uint32_t)dpp<0x141>((int)slotbit);
+        const uint32_t ucl = uni(slotbit);
+        const uint32_t sent = (uint32_t)__builtin_amdgcn_ds_permute((int)(((int)lane < m ? mi_l : 63u) << 2),
+                                                                     (int)(8u | lane));
+        invl = (ucl >> (lane & 7u)) & 1u ? sent : 0u;
         u &= ~ucl;
         // ---- the m children and their leaves, lane i = draw i
         {
-            const uint32_t li = lane & 7u;
-            const uint32_t mi = (picks >> (3 * li)) & 7u;
+            const uint32_t mi = mi_l;
             const int col = (int)((ow >> (3 * mi)) & 7u);
             const uint64_t bit = drop_bit(b0 | b1, col);
             const bool filled = (bit & kTop) != 0;
@@ -732,7 +742,7 @@ __device__ __forceinline__ void select_flush(const Tree &t, Fresh *fresh, Leaf *
             for (int i = 0; i < m; ++i)
                 paths[(j + i) * kMaxDepth + lane] = (uint16_t)(lane == (uint32_t)ldepth ? (uint32_t)(nnodes + i) : pathv);
             // the node's new children
-            const uint32_t pk = (inv >> (4 * k)) & 15u;
+            const uint32_t pk = lane < 8 ? invl : 0u;
             if (pk & 8u) ch = (uint32_t)nnodes + (pk & 7u);
             if (node >= f0) {  // the node's copy in LDS
                 if (lane == 0) fresh[node - f0].u = u;
