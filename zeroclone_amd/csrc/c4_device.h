@@ -565,7 +565,8 @@ __device__ __forceinline__ WalkEnd walk_hbm(const Tree &t, ConstDouble *logtab, 
 // scores +inf, so below X0 that is simply the lowest slot holding a fresh child — no
 // arithmetic, no HBM.  Fresh nodes live in LDS (`fresh`) until the caller publishes them.
 // Leaf j goes to leaves[j] (board, node, depth, turn, legal mask) and its path (node ids of
-// levels 0..depth) to paths[j][*].  QW: as walk_hbm.
+// levels 0..depth) to paths[j][*] (paths = nullptr: not recorded; the fresh part of a path is
+// also the chain of parent links in `fresh`).  QW: as walk_hbm.
 template <bool QW, bool STAMP, class RNG>
 __device__ __forceinline__ void select_flush(const Tree &t, Fresh *fresh, Leaf *leaves, uint16_t *paths,
                                              const uint32_t *s_order, ConstDouble *logtab,
@@ -624,7 +625,9 @@ __device__ __forceinline__ void select_flush(const Tree &t, Fresh *fresh, Leaf *
                 const uint32_t meta = (uint32_t)node | ((uint32_t)depth << 16) | ((uint32_t)turn << 24) |
                                       ((uint32_t)cmask << 25);
                 for (int i = (int)lane; j + i < nb; i += 64) leaves[j + i] = Leaf{b0, b1, meta, 0, ow, 0};
-                for (; j < nb; ++j) paths[j * kMaxDepth + lane] = (uint16_t)pathv;
+                if (paths)
+                    for (int jj = j; jj < nb; ++jj) paths[jj * kMaxDepth + lane] = (uint16_t)pathv;
+                j = nb;
                 wave_mem_order();
                 break;
             }
@@ -739,8 +742,9 @@ __device__ __forceinline__ void select_flush(const Tree &t, Fresh *fresh, Leaf *
             }
             // leaf j+i's path: the walk's path plus the new node (all 64 lanes store: lanes
             // >= kMaxDepth spill into the next leaf's path, written after this, or the spill bytes)
-            for (int i = 0; i < m; ++i)
-                paths[(j + i) * kMaxDepth + lane] = (uint16_t)(lane == (uint32_t)ldepth ? (uint32_t)(nnodes + i) : pathv);
+            if (paths)
+                for (int i = 0; i < m; ++i)
+                    paths[(j + i) * kMaxDepth + lane] = (uint16_t)(lane == (uint32_t)ldepth ? (uint32_t)(nnodes + i) : pathv);
             // the node's new children
             const uint32_t pk = lane < 8 ? invl : 0u;
             if (pk & 8u) ch = (uint32_t)nnodes + (pk & 7u);

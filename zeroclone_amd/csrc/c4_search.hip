@@ -414,7 +414,6 @@ __device__ __forceinline__ void search_move(const SearchParams &p, const SearchL
     const uint32_t *const s_order = L.s_order;
     Fresh *const fresh = L.fresh;
     Leaf *const leaves = L.leaves;
-    uint16_t *const paths = L.paths;
     // log(N) table read through the constant address space: uniform index -> scalar loads,
     // which do not sit in the vector-memory counter the walk waits on.
     ConstDouble *logtab = (ConstDouble *)p.a.logtab;
@@ -434,7 +433,7 @@ __device__ __forceinline__ void search_move(const SearchParams &p, const SearchL
         FlushSel fs;
         {
             const zc_c4_state root = p.roots[gl];
-            select_flush<false, STAMP>(t, fresh, leaves, paths, s_order, logtab, rng, cn, stamp, nnodes,
+            select_flush<false, STAMP>(t, fresh, leaves, nullptr, s_order, logtab, rng, cn, stamp, nnodes,
                                        status, uni64(root.stones[0]), uni64(root.stones[1]), uni(root.turn), done,
                                        nb, p.c, fs);
         }
@@ -480,12 +479,17 @@ __device__ __forceinline__ void search_move(const SearchParams &p, const SearchL
                 sv = (d & 1) ? -v : v;
             }
             S += __popcll(__ballot(sv > 0)) - __popcll(__ballot(sv < 0));
-            for (int l = d0 + 1; __ballot(l <= d); ++l) {
-                if (l <= d) {
-                    const int fi = (int)paths[jj * kMaxDepth + l] - f0;
+            // the fresh edges: from the leaf up to X0's child along the fresh nodes' parent
+            // links (every node below X0 is fresh, X0 and above are not)
+            int nd = jj < nb ? (int)(leaves[jj].meta & 0xFFFFu) : -1, l = d;
+            while (__ballot(nd >= f0)) {
+                if (nd >= f0) {
+                    const int fi = nd - f0;
                     const int vl = ((d - l) & 1) ? -v : v;
                     atomicAdd(&fresh[fi].na, 1);
                     atomicAdd(&fresh[fi].w, -vl);
+                    nd = (int)(fresh[fi].link & 0xFFFFu);
+                    --l;
                 }
             }
         }
