@@ -669,21 +669,19 @@ __device__ __forceinline__ void select_flush(const Tree &t, Fresh *fresh, Leaf *
                     const uint32_t n = (uint32_t)max((int)cnt - done - i, 1);
                     A[i] = __ballot((w >> __clz(n)) < n);
                 }
-                // the draws, a scalar chain: each takes the first accepted word after the last
+                // the draws, a branch-free scalar chain: each takes the lowest accepted word
+                // after the last one (lb = acc & -acc); a draw without one zeroes `gt`, and with
+                // it every later draw of the view
                 uint64_t gt = ~0ull, F = 0;  // lanes after the last accepted word; accepted words
-                int f = -1, nd = 0;
 #pragma unroll
                 for (int i = 0; i < 7; ++i) {
-                    if (i < rem && nd == i) {
-                        const uint64_t acc = A[i] & gt;
-                        if (acc) {
-                            f = __builtin_ctzll(acc);
-                            F |= 1ull << f;
-                            gt = (uint64_t)0 - (2ull << f);
-                            nd = i + 1;
-                        }
-                    }
+                    const uint64_t acc = (i < rem ? A[i] : 0ull) & gt;
+                    const uint64_t lb = acc & (0ull - acc);
+                    F |= lb;
+                    gt = 0ull - (lb << 1);
                 }
+                const int nd = __popcll(F);
+                const int f = 63 - __clzll(F | 1ull);  // the last accepted word (F != 0 when nd > 0)
                 // lane-parallel: accepted word l is draw di = done + (accepted words below it);
                 // its value goes to lane di (a forward permute; lanes outside [done, done + nd)
                 // keep theirs)
@@ -703,12 +701,13 @@ __device__ __forceinline__ void select_flush(const Tree &t, Fresh *fresh, Leaf *
         }
         // draw i's position in the untried list as it was before the bulk (the erase of
         // mcts.cpp:72 undone all at once, a Lehmer code: later draws skip the earlier picks)
+        // (step i compares with draw i's own r: lane i is only adjusted by the later steps i' < i)
         uint32_t pl = rr;
+        uint32_t rpick[6];
 #pragma unroll
-        for (int i = 5; i >= 0; --i) {
-            const uint32_t pi = (uint32_t)__builtin_amdgcn_readlane((int)pl, i);
-            pl += ((int)lane > i && (int)lane < m && pl >= pi) ? 1u : 0u;
-        }
+        for (int i = 0; i < 6; ++i) rpick[i] = (uint32_t)__builtin_amdgcn_readlane((int)rr, i);
+#pragma unroll
+        for (int i = 5; i >= 0; --i) pl += ((int)lane > i && (int)lane < m && pl >= rpick[i]) ? 1u : 0u;
         const uint32_t mi_l = (ul >> (3 * (pl & 7u))) & 7u;  // lane i < m: draw i's move index
         // the expanded slots (OR over lanes 0..7, DPP) and, in lane k, the draw that took slot k
         uint32_t slotbit = (int)lane < m ? 1u << mi_l : 0u;
