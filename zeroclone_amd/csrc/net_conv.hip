@@ -28,6 +28,18 @@
 
 #include "zc_internal.h"
 
+#ifdef ZC_CONV_STAMP
+// diagnostic build only: per wave of conv3x3_stream_kernel, {HW_ID, XCC_ID, start, tile
+// staged, main loop done, end} (s_memtime), read by tools/conv_phases.py
+__device__ uint64_t g_conv_stamp[1 << 20];
+extern "C" int zc_debug_conv_stamps(void *host, int n) {
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_conv_stamp), (size_t)n * sizeof(uint64_t)) == hipSuccess ? 0 : -1;
+}
+#define CSTAMP(k) const uint64_t cst_##k = __builtin_amdgcn_s_memtime()
+#else
+#define CSTAMP(k)
+#endif
+
 namespace zc {
 namespace {
 
@@ -418,6 +430,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
     constexpr int C8 = CIN / 8;
     constexpr int KC = CIN / 16;
     constexpr int NI = kHalfPix * C8 / 256;
+    CSTAMP(0);
     extern __shared__ __attribute__((aligned(16))) _Float16 lds[];
     // [kHalfPix + 16][LD]: the tile, then 16 zero rows.  An off-board pixel reads the zero
     // row in the bank class of the row it would have read, so the 16 lanes of a read group
@@ -467,6 +480,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
 #pragma unroll
         for (int k = 0; k < 16; ++k) acc[t][k] = 0.0f;
     __syncthreads();  // the input tile is in LDS
+    CSTAMP(1);
 
 #pragma unroll
     for (int tap = 0; tap < 9; ++tap) {
@@ -508,6 +522,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
     // residual, ReLU and the fp16 store on whole 256-byte output rows; NP pixels per pass
     constexpr int SL = kCout + 4;
     constexpr int NP = WPE >= 3 ? 64 : 128;
+    CSTAMP(2);
     float *const sacc = (float *)lds;
 #pragma unroll
     for (int h0 = 0; h0 < kHalfPix; h0 += NP) {
@@ -545,6 +560,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
             }
         }
     }
+#ifdef ZC_CONV_STAMP
+    CSTAMP(3);
+    if (lane == 0 && (blockIdx.x * 4 + wave) * 6 + 6 <= (1 << 20)) {
+        uint64_t *d = g_conv_stamp + (size_t)(blockIdx.x * 4 + wave) * 6;
+        d[0] = __builtin_amdgcn_s_getreg(4 | (0 << 6) | (31 << 11));   // HW_ID
+        d[1] = __builtin_amdgcn_s_getreg(20 | (0 << 6) | (15 << 11));  // XCC_ID
+        d[2] = cst_0;
+        d[3] = cst_1;
+        d[4] = cst_2;
+        d[5] = cst_3;
+    }
+#endif
 }
 
 // [9][kCout][cin] -> the stream form's fragments: packed[((tap * KC + kc) * 4 + mb) * 512 +
