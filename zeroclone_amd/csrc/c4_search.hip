@@ -152,7 +152,7 @@ __device__ void c4_rollouts(Leaf *L, int nb, R &rng, const uint32_t *s_order, Co
     const uint32_t pairbits = lane < 49u ? (1u << (lane / 7u)) | (1u << (lane % 7u)) : 0u;
     // per leaf, lane-parallel (lane = leaf of a group of 64): side to move / last mover stones,
     // has_four(last mover) and 41 - stones, read out by readlane when the leaf's turn comes
-    uint64_t me_v = 0, op_v = 0, won_m = 0;
+    uint64_t won_m = 0;
     uint32_t lm_v = 0, ow_v = 0;
     int room_v = 0;
     for (int j = 0; j < nb; ++j) {
@@ -160,20 +160,23 @@ __device__ void c4_rollouts(Leaf *L, int nb, R &rng, const uint32_t *s_order, Co
         const int jl = j & 63;
         if (jl == 0) {
             const int jj = j + (int)lane;
+            uint64_t op_v = 0;
             if (jj < nb) {
                 lm_v = L[jj].meta;
                 ow_v = L[jj].ow;
                 const uint64_t x0 = L[jj].p0, x1 = L[jj].p1;
-                const bool tnv = (lm_v >> 24) & 1u;
-                me_v = tnv ? x1 : x0;
-                op_v = tnv ? x0 : x1;
+                op_v = (lm_v >> 24) & 1u ? x0 : x1;
                 room_v = 41 - __popcll(x0 | x1);
             }
             won_m = __ballot(jj < nb && has_four(op_v));
         }
         const uint32_t lm = (uint32_t)__builtin_amdgcn_readlane((int)lm_v, jl);
-        uint64_t me = in_vgpr(readlane64(me_v, jl));  // side to move
-        uint64_t op = in_vgpr(readlane64(op_v, jl));  // last mover
+        // the leaf's boards straight from LDS into VGPRs (one uniform address per read: a
+        // broadcast), in flight while the first view is gathered
+        const uint32_t tnv = (lm >> 24) & 1u;
+        const uint64_t *const pp = &L[j].p0;
+        uint64_t me = in_vgpr(pp[tnv]);       // side to move
+        uint64_t op = in_vgpr(pp[tnv ^ 1u]);  // last mover
         const uint32_t low0 = (uint32_t)__builtin_amdgcn_readlane((int)ow_v, jl);
         const int room0 = __builtin_amdgcn_readlane(room_v, jl);
         const bool won = (won_m >> jl) & 1u;
