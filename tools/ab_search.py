@@ -15,7 +15,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CHILD = r'''
-import sys, time, torch
+import sys, time, zlib, torch
 sys.path.insert(0, %r)
 import numpy as np
 from zeroclone_amd import _native
@@ -46,14 +46,16 @@ if %r == "mixed":
                 break
         roots[i]["stones"] = st
         roots[i]["turn"] = turn
-ts = []
+ts, h = [], 0
 for r in range(9):
     eng.seed(0, list(range(r * G, (r + 1) * G)))
     t = time.perf_counter()
-    eng.c4_search(roots, S, 1.4, B)
+    out = eng.c4_search(roots, S, 1.4, B)
     ts.append(time.perf_counter() - t)
+    for a in out:  # moves, root visit counts, per-game stats (incl. MT words consumed)
+        h = zlib.crc32(np.ascontiguousarray(a).tobytes(), h)
 ts = sorted(ts[2:])
-print(ts[len(ts) // 2] * 1e3)
+print(ts[len(ts) // 2] * 1e3, h)
 '''
 
 
@@ -61,16 +63,21 @@ def main():
     libs = sys.argv[1:]
     games = int(os.environ.get("AB_GAMES", "4096"))
     res = {lib: [] for lib in libs}
+    hashes = {}
     for rnd in range(int(os.environ.get("AB_ROUNDS", "3"))):
         for lib in libs:
             env = dict(os.environ, ZC_LIB=os.path.join(ROOT, lib))
             out = subprocess.run([sys.executable, "-c", CHILD % (ROOT, games, os.environ.get("AB_ROOTS", "empty"))],
                                  env=env, check=True,
                                  capture_output=True, text=True, timeout=300).stdout
-            res[lib].append(float(out.strip().splitlines()[-1]))
+            ms, h = out.strip().splitlines()[-1].split()
+            res[lib].append(float(ms))
+            hashes.setdefault(lib, set()).add(h)
             print(rnd, lib, res[lib][-1], flush=True)
+    ref = hashes[libs[0]]
     for lib in libs:
-        print(f"{lib}: median {statistics.median(res[lib]):.3f} ms  all {res[lib]}")
+        same = "outputs identical" if hashes[lib] == ref and len(ref) == 1 else "OUTPUTS DIFFER"
+        print(f"{lib}: median {statistics.median(res[lib]):.3f} ms  all {res[lib]}  {same}")
 
 
 if __name__ == "__main__":
