@@ -463,16 +463,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
         }
         for (int z = tid; z < 16 * C8; z += 256) *(h8 *)(sin + (kHalfPix + z / C8) * LD + (z % C8) * 8) = zero;
     }
-    int pb[4], py[4], px[4];
-    bool pv[4];
+    // per MFMA pixel tile t: the pixel's LDS row and its (y, x) packed as y << 8 | x (a pixel
+    // beyond the tile gets y = 64: every shifted view of it is off the board)
+    int prow[4], pyx[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
         const int P = t * 32 + r;
-        pv[t] = P < npix;
-        pb[t] = P / HW;
-        const int rem = P - pb[t] * HW;
-        py[t] = rem / W;
-        px[t] = rem - py[t] * W;
+        const int pb = P / HW, rem = P - pb * HW, py = rem / W;
+        prow[t] = P;
+        pyx[t] = (P < npix ? py << 8 : 64 << 8) | (rem - py * W);
     }
     f16x acc[4];
 #pragma unroll
@@ -488,9 +487,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
         const _Float16 *xb[4];
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
-            const int sy = py[t] + dy, sx = px[t] + dx;
-            const bool sv = pv[t] && (unsigned)sy < (unsigned)H && (unsigned)sx < (unsigned)W;
-            const int row = pb[t] * HW + sy * W + sx;
+            const int sy = (pyx[t] >> 8) + dy, sx = (pyx[t] & 255) + dx;
+            const bool sv = (unsigned)sy < (unsigned)H && (unsigned)sx < (unsigned)W;
+            const int row = prow[t] + dy * W + dx;
             xb[t] = sin + (sv ? row : kHalfPix + (row & 15)) * LD + hh * 8;
         }
         h8 x[4], xn[4];
