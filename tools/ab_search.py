@@ -6,7 +6,7 @@
 Each round runs every variant in its own process (ZC_LIB=<path>), in turn, so that clock
 and thermal drift hit all of them alike; prints the median search time per variant.
 AB_ROOTS=mixed searches from mid-game roots (random depths 0..27, the steady-state mix of
-self-play) instead of the empty board."""
+self-play) instead of the empty board; AB_MODE=philox times the Philox rollout mode."""
 import os
 import statistics
 import subprocess
@@ -21,6 +21,8 @@ import numpy as np
 from zeroclone_amd import _native
 G, S, B = %d, 800, 32
 eng = _native.NativeEngine(max_games=G, max_sims=S, max_batch=B)
+if %r == "philox":
+    eng.c4_rollout_mode("philox", 12345)
 roots = np.zeros(G, _native.C4_STATE_DTYPE)
 if %r == "mixed":
     rs = np.random.default_rng(1234)
@@ -67,7 +69,7 @@ def main():
     for rnd in range(int(os.environ.get("AB_ROUNDS", "3"))):
         for lib in libs:
             env = dict(os.environ, ZC_LIB=os.path.join(ROOT, lib))
-            out = subprocess.run([sys.executable, "-c", CHILD % (ROOT, games, os.environ.get("AB_ROOTS", "empty"))],
+            out = subprocess.run([sys.executable, "-c", CHILD % (ROOT, games, os.environ.get("AB_MODE", "exact"), os.environ.get("AB_ROOTS", "empty"))],
                                  env=env, check=True,
                                  capture_output=True, text=True, timeout=300).stdout
             ms, h = out.strip().splitlines()[-1].split()
