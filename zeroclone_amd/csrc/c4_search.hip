@@ -88,10 +88,6 @@ __device__ __forceinline__ uint32_t ff1(uint64_t m) {
     __asm__("s_ff1_i32_b64 %0, %1" : "=s"(r) : "s"(m));
     return r;
 }
-// DPP row_shr:1 with zero fill: the value of the previous lane of the 16-lane row (0 at its start)
-__device__ __forceinline__ uint32_t row_prev(uint32_t x) {
-    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, false);
-}
 
 // Value.random_rollout (value_functions.py:35-45) for the nb pending leaves of one flush, in
 // pending order (value.batch: mcts.cpp:118).  Per leaf, from the side to move `turn`:
@@ -259,12 +255,12 @@ __device__ void c4_rollouts(Leaf *L, int nb, R &rng, const uint32_t *s_order, Co
                 // compact plies 0..last by parity into lanes 0..31 (a forward lane permute;
                 // other lanes all go to lane 31, which no ply <= 30 uses), then copy them 32
                 // lanes up
-                const uint32_t c = (qk & 1u) * 16u + (qk >> 1);
-                const uint32_t b = 7u * col + row + 1u;
+                const uint32_t c = ((qk & 1u) << 4) | (qk >> 1);
+                const uint32_t b = 7u * col + row;  // the ply's cell (lanes without a ply: masked by V)
                 const uint32_t pl = (uint32_t)__builtin_amdgcn_ds_permute((int)(mask_sel(K, 31u, c) << 2), (int)b);
                 const uint32_t pb = __builtin_amdgcn_permlane32_swap(pl, pl, false, false)[0];
                 const uint64_t V = __ballot(myply <= last);  // lanes holding plies 0..last
-                const uint64_t bit = 1ull << (pb - 1u);
+                const uint64_t bit = 1ull << pb;
                 uint32_t blo = mask_sel0(V, (uint32_t)bit), bhi = mask_sel0(V, (uint32_t)(bit >> 32));
                 scan_or16x2(blo, bhi);
                 const uint64_t mine = ((uint64_t)bhi << 32) | blo;  // this row's stones so far
@@ -280,10 +276,10 @@ __device__ void c4_rollouts(Leaf *L, int nb, R &rng, const uint32_t *s_order, Co
                 rng.off += endlane + 1u;  // words through the block's last ply are consumed
                 // both sides' stones after ply endply: first mover through ply 2*(endply/2)
                 // (row 0, inclusive), second mover through the odd plies <= endply (row 1,
-                // exclusive: lane 16 + (endply+1)/2; zero at the row's start)
-                const uint64_t prev = ((uint64_t)row_prev(bhi) << 32) | row_prev(blo);
+                // inclusive scan at lane 15 + (endply+1)/2; none when endply = 0)
                 const uint64_t a2 = me | readlane64(mine, (int)(endply >> 1));
-                const uint64_t b2 = op | readlane64(prev, (int)((endply + 33u) >> 1));
+                const uint64_t s2 = readlane64(mine, (int)((endply + 31u) >> 1));
+                const uint64_t b2 = op | (endply ? s2 : 0ull);
                 const bool odd = endply & 1u;  // an even number of plies: the first mover is to move again
                 me = odd ? a2 : b2;
                 op = odd ? b2 : a2;
