@@ -212,7 +212,7 @@ __device__ __forceinline__ void rng_advance(Rng &r) {
 template <class R>
 __device__ __forceinline__ uint32_t rng_view(const R &r) {
     const uint32_t j = lane_id() + r.off;
-    const int idx = (int)((j & 63u) << 2);
+    const int idx = (int)(j << 2);  // ds_bpermute reads the lane from address bits 7:2 only
     const uint32_t a = (uint32_t)__builtin_amdgcn_ds_bpermute(idx, (int)r.wt);
     const uint32_t b = (uint32_t)__builtin_amdgcn_ds_bpermute(idx, (int)r.wn);
     return j < 64u ? a : b;

@@ -216,7 +216,7 @@ __device__ void c4_rollouts(Leaf *L, int nb, R &rng, const uint32_t *s_order, Co
                 uint32_t one = mask_sel0(A, 1u << (4 * col));
                 uint32_t same = ((scan_add32(one) - one) >> (4 * col)) & 15u;
                 uint32_t row = (uint32_t)__popcll((occ >> (7 * col)) & 0x3Full) + same;
-                uint32_t nacc = (uint32_t)__popc(in_vgpr((uint32_t)A)) + (uint32_t)__popc(in_vgpr((uint32_t)(A >> 32)));
+                uint32_t nacc = (uint32_t)__popcll(A);
                 bool fills = row == 5u;
                 uint64_t E0 = __ballot(mask_sel0(A, (fills ? 63u : qk) + 1u) > min(cap_r, nacc - 1u));
                 uint32_t l0 = (uint32_t)__builtin_ctzll(E0);
@@ -225,7 +225,7 @@ __device__ void c4_rollouts(Leaf *L, int nb, R &rng, const uint32_t *s_order, Co
                 uint32_t lf = 64u;  // lane of the absorbed fill (64: none)
                 uint32_t ow2 = ow, cf = 0;
                 const uint32_t q0 = (uint32_t)__builtin_amdgcn_readlane((int)qk, (int)l0);
-                const uint32_t f0 = (uint32_t)__builtin_amdgcn_readlane((int)fills, (int)l0);
+                const uint32_t f0 = (uint32_t)(__ballot(fills) >> l0) & 1u;
                 RMARK(3);
                 if (f0 && q0 < cap_r) {
                     lf = l0;
@@ -243,7 +243,7 @@ __device__ void c4_rollouts(Leaf *L, int nb, R &rng, const uint32_t *s_order, Co
                     one = mask_sel0(A, 1u << (4 * col));
                     same = ((scan_add32(one) - one) >> (4 * col)) & 15u;
                     row = (uint32_t)__popcll((occ >> (7 * col)) & 0x3Full) + same;
-                    nacc = (uint32_t)__popc(in_vgpr((uint32_t)A)) + (uint32_t)__popc(in_vgpr((uint32_t)(A >> 32)));
+                    nacc = (uint32_t)__popcll(A);
                     fills = row == 5u && lane > lf;  // the absorbed fill no longer ends the block
                     E0 = __ballot(mask_sel0(A, (fills ? 63u : qk) + 1u) > min(cap_r, nacc - 1u));
                     l0 = (uint32_t)__builtin_ctzll(E0);
