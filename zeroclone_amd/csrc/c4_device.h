@@ -58,6 +58,24 @@ __device__ __forceinline__ uint64_t uni64(uint64_t x) {
     return ((uint64_t)uni((uint32_t)(x >> 32)) << 32) | (uint64_t)uni((uint32_t)x);
 }
 __device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
+// lane-wise select by a wave mask in SGPRs: bit `lane` of m set -> b, else a (or 0)
+__device__ __forceinline__ uint32_t mask_sel(uint64_t m, uint32_t a, uint32_t b) {
+    uint32_t r;
+    __asm__("v_cndmask_b32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(m));
+    return r;
+}
+__device__ __forceinline__ uint32_t mask_sel0(uint64_t m, uint32_t b) {
+    uint32_t r;
+    __asm__("v_cndmask_b32 %0, 0, %1, %2" : "=v"(r) : "v"(b), "s"(m));
+    return r;
+}
+// x + 1 in the lanes of wave mask m (the mask as the add's carry-in)
+__device__ __forceinline__ uint32_t add_in_mask(uint32_t x, uint64_t m) {
+    uint32_t r;
+    uint64_t co;
+    __asm__("v_addc_co_u32_e64 %0, %1, 0, %2, %3" : "=v"(r), "=s"(co) : "v"(x), "s"(m));
+    return r;
+}
 __device__ __forceinline__ uint32_t mbcnt64(uint64_t m) {  // set bits of m in lanes below this one
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
@@ -685,11 +703,10 @@ __device__ __forceinline__ void select_flush(const Tree &t, Fresh *fresh, Leaf *
                 // lane-parallel: accepted word l is draw di = done + (accepted words below it);
                 // its value goes to lane di (a forward permute; lanes outside [done, done + nd)
                 // keep theirs)
-                const bool inF = (F >> lane) & 1ull;
                 const uint32_t di = (uint32_t)done + mbcnt64(F);
                 const uint32_t rl = w >> __clz(max((int)cnt - (int)di, 1));
-                const uint32_t got = (uint32_t)__builtin_amdgcn_ds_permute((int)((inF ? di : 63u) << 2), (int)rl);
-                if ((int)lane >= done && (int)lane < done + nd) rr = got;
+                const uint32_t got = (uint32_t)__builtin_amdgcn_ds_permute((int)(mask_sel(F, 63u, di) << 2), (int)rl);
+                rr = mask_sel(((1ull << nd) - 1ull) << done, rr, got);  // lanes done .. done + nd - 1
                 done += nd;
                 if (done < m) {  // the view ran out: all of it is consumed
                     rng.off += (uint32_t)kWin;
@@ -707,7 +724,10 @@ __device__ __forceinline__ void select_flush(const Tree &t, Fresh *fresh, Leaf *
 #pragma unroll
         for (int i = 0; i < 6; ++i) rpick[i] = (uint32_t)__builtin_amdgcn_readlane((int)rr, i);
 #pragma unroll
-        for (int i = 5; i >= 0; --i) pl += ((int)lane > i && (int)lane < m && pl >= rpick[i]) ? 1u : 0u;
+        for (int i = 5; i >= 0; --i) {
+            const uint64_t later = ((1ull << m) - 1ull) & ~((2ull << i) - 1ull);  // lanes i+1 .. m-1
+            pl = add_in_mask(pl, __ballot(pl >= rpick[i]) & later);
+        }
         const uint32_t mi_l = (ul >> (3 * (pl & 7u))) & 7u;  // lane i < m: draw i's move index
         // the expanded slots (OR over lanes 0..7, DPP) and, in lane k, the draw that took slot k
         uint32_t slotbit = (int)lane < m ? 1u << mi_l : 0u;

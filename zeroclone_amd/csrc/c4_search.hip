@@ -32,17 +32,6 @@ __device__ __forceinline__ uint64_t readlane64(uint64_t x, int l) {
            (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)x, l);
 }
 
-// lane-wise select by a wave mask in SGPRs: bit `lane` of m set -> b, else a (or 0)
-__device__ __forceinline__ uint32_t mask_sel(uint64_t m, uint32_t a, uint32_t b) {
-    uint32_t r;
-    __asm__("v_cndmask_b32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(m));
-    return r;
-}
-__device__ __forceinline__ uint32_t mask_sel0(uint64_t m, uint32_t b) {
-    uint32_t r;
-    __asm__("v_cndmask_b32 %0, 0, %1, %2" : "=v"(r) : "v"(b), "s"(m));
-    return r;
-}
 __device__ __forceinline__ uint32_t mbcnt(uint64_t m) {  // set bits of m in lanes below this one
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
@@ -75,10 +64,6 @@ __device__ __forceinline__ void scan_or16x2(uint32_t &x, uint32_t &y) {
 // Values that are the same in every lane but should live in VGPRs (worked on by the VALU):
 // the scalar unit is shared by the CU's four SIMDs and is the busier of the two here.
 __device__ __forceinline__ uint64_t in_vgpr(uint64_t x) {
-    __asm__("" : "+v"(x));
-    return x;
-}
-__device__ __forceinline__ uint32_t in_vgpr(uint32_t x) {
     __asm__("" : "+v"(x));
     return x;
 }
