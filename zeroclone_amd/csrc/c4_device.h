@@ -548,7 +548,8 @@ __device__ __forceinline__ WalkEnd walk_hbm(const Tree &t, ConstDouble *logtab, 
         const uint32_t nm = u >> 28;
         const bool valid = k < nm && ch != 0xFFFF;
         int best;
-        const uint64_t unvisited = __ballot(valid && na == 0) & 0xFFull;
+        // slots k < nm (a scalar mask) with a child and no visit: masks ANDed, no per-lane bool
+        const uint64_t unvisited = ((1ull << nm) - 1ull) & __ballot(ch != 0xFFFF) & __ballot(na == 0) & 0xFFull;
         if (unvisited) {  // +inf beats everything; first such slot
             best = __builtin_ctzll(unvisited);
         } else {
@@ -638,7 +639,7 @@ __device__ __forceinline__ void select_flush(const Tree &t, Fresh *fresh, Leaf *
     while (j < nb) {
         const uint32_t cnt = untried_count(u);
         if (cnt == 0) {
-            const uint64_t fm = __ballot(k < (u >> 28) && ch != 0xFFFF && (int)ch >= f0) & 0xFFull;
+            const uint64_t fm = ((1ull << (u >> 28)) - 1ull) & __ballot(ch != 0xFFFF) & __ballot((int)ch >= f0) & 0xFFull;
             if (!fm) {  // no child at all: terminal, every remaining leaf of the flush is this node
                 const uint32_t meta = (uint32_t)node | ((uint32_t)depth << 16) | ((uint32_t)turn << 24) |
                                       ((uint32_t)cmask << 25);

@@ -219,8 +219,7 @@ __device__ void c4_rollouts(Leaf *L, int nb, R &rng, const uint32_t *s_order, Co
                     const uint32_t n2 = (ow2 >> 24) & 15u;
                     const uint32_t v2 = wv >> __clz(n2);
                     const uint64_t low = (2ull << lf) - 1ull;  // lanes 0..lf
-                    // one compare: lanes 0..lf get bit 31 set (never < n2)
-                    A = (A & low) | __ballot((v2 | ((lane - lf - 1u) & 0x80000000u)) < n2);
+                    A = (A & low) | (__ballot(v2 < n2) & ~low);
                     v = mask_sel(low, v2, v);
                     const uint32_t owl = mask_sel(low, ow2, ow);
                     qk = mbcnt(A);
