@@ -294,11 +294,14 @@ def burn_in(sp, max_steps: int = 200, check_every: int = 8) -> int:
     return steps
 
 
-def run_steps(sp, steps: int, warmup: int, world: int = 1) -> dict:
-    """W untimed moves, then K timed moves bracketed by barrier + device sync.  The K moves
-    are ONE free-running self-play launch (C4SelfPlay.run: every game at its own pace, the
-    same moves as K lockstep steps) followed by the K steps' trajectory recording; HIP
-    events around the launch on its stream."""
+def run_steps(sp, steps: int, warmup: int, world: int = 1, launch: str = "pooled") -> dict:
+    """W untimed moves, then K timed steps (K x G moves) bracketed by barrier + device sync,
+    as ONE self-play launch followed by its trajectory recording; HIP events around it on its
+    stream.  launch "pooled" (the default, C4SelfPlay.run_pooled): the G games share a budget
+    of K x G moves drawn from a device counter, at most 2K per game — the reference's
+    self-play threads drawing work from one pool (train.py:151-170), every move a full
+    search; "free" (C4SelfPlay.run): exactly K moves per game, so the launch waits for its
+    slowest game."""
     dev = sp.dev
     stream = torch.cuda.current_stream(dev)
     ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
@@ -310,7 +313,10 @@ def run_steps(sp, steps: int, warmup: int, world: int = 1) -> dict:
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     ev[0].record(stream)
-    res = sp.run(steps)
+    if launch == "pooled":
+        res = sp.run_pooled(steps * sp.G, 2 * steps)
+    else:
+        res = sp.run(steps)
     ev[1].record(stream)
     torch.cuda.synchronize(dev)
     if world > 1:
@@ -319,10 +325,12 @@ def run_steps(sp, steps: int, warmup: int, world: int = 1) -> dict:
     st = sp.stats
     if int((st[:, 5] != 0).sum().item()):
         raise RuntimeError("a game reported a nonzero search status")
-    fin = int(((res != _native.ZC_C4_ONGOING) & (res != _native.ZC_SLOT_IDLE)).sum().item())
+    fin = int(((res != _native.ZC_C4_ONGOING) & (res != _native.ZC_SLOT_IDLE)
+               & (res != _native.ZC_SLOT_SKIP)).sum().item())
+    moves = int(((res != _native.ZC_SLOT_IDLE) & (res != _native.ZC_SLOT_SKIP)).sum().item())
     tot = [int(x) for x in st[:, [0, 1, 2]].sum(0).tolist()]
     return {"dt": dt, "launch_ms": ev[0].elapsed_time(ev[1]), "expansions": tot[0], "depth_sum": tot[1],
-            "finished": fin, "leaves": tot[2]}
+            "finished": fin, "leaves": tot[2], "moves": moves}
 
 
 def reduce_over_ranks(counts, dt: float, kernel_ms_sum: float, device) -> tuple[list[int], float, float]:
@@ -384,7 +392,7 @@ def run_rank(args, rank: int, world: int, local: int):
     torch.cuda.set_stream(torch.cuda.Stream(dev))   # every launch and the timing events on one stream
     sp = C4SelfPlay(G, S, c=args.c, batch_size=B, seed=args.seed, rank=rank, device=local, record=True)
     burn = burn_in(sp) if args.burn_in else 0
-    r = run_steps(sp, args.steps, args.warmup, world)
+    r = run_steps(sp, args.steps, args.warmup, world, launch=args.launch)
     gather = gather_trajectories(sp, world)
     counts, dt_max, kms = reduce_over_ranks([r["expansions"], r["depth_sum"], r["finished"], r["leaves"]], r["dt"],
                                             r["launch_ms"], dev)
@@ -412,6 +420,9 @@ def run_rank(args, rank: int, world: int, local: int):
             "data": "synthetic: self-play from the empty board, per-game CPython MT19937 seeds base+game_id",
             "config": {"workload": f"C2/C3 Connect4 self-play, {G} games/GPU, {S} sims/move, batch {B}, "
                                    f"c {args.c}, random_rollout exact-RNG mode, steady state (mixed game ages)",
+                       "launch": (f"pooled: each step = {G} moves drawn by the games from one shared budget "
+                                  f"(K x {G} per launch, <= 2K per game; every move a full {S}-sim search)"
+                                  if args.launch == "pooled" else f"free: K moves per game per launch"),
                        "games_per_gpu": G, "global_games": G * world, "sims": S, "batch_size": B,
                        "world_size": world, "rank_games": rank_ranges(world, G), "burn_in_steps": burn,
                        "parallelism": f"games sharded over {world} GPU(s), 1 process/GPU"},
@@ -422,7 +433,7 @@ def run_rank(args, rank: int, world: int, local: int):
             "roofline": {"bound": "issue", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 5),
                          "traffic": traffic, "traffic_source": traffic_src,
-                         "kernel": "c4_selfplay_kernel (K moves per launch; per-move figures = launch / K)",
+                         "kernel": "c4_selfplay_kernel (K x G moves per launch; per-step figures = launch / K)",
                          "avg_launch_ms": round(avg_kernel_s * 1e3, 3),
                          "bytes_per_launch_model": round(bytes_launch),
                          "model": "SURVEY §8(d): 152*d+96 B per expansion, d counted in-kernel",
@@ -430,12 +441,17 @@ def run_rank(args, rank: int, world: int, local: int):
                          "limiter": "the per-game serial dependency chain (latency + issue arbitration), not HBM: "
                                     "roofline.issue (SQ counters) and DESIGN §4"},
             "extra": {"expansions": expansions, "leaves": leaves, "mean_depth": round(depth_sum / max(expansions, 1), 3),
-                      "games_finished": finished,
+                      "games_finished": finished, "moves": r["moves"],
                       "selfplay_launch_ms": round(r["launch_ms"], 3),
                       "trajectory_allgather": gather},
         }
         if world == 1:
             out["extra"]["phases"] = phases(sp, args, bytes_launch, avg_kernel_s)
+            other = "free" if args.launch == "pooled" else "pooled"
+            ro = run_steps(sp, args.steps, 0, launch=other)
+            out["extra"][f"launch_{other}"] = {"value": round(ro["expansions"] / ro["dt"], 1), "unit": "expansions/s",
+                                               "ms_per_step": round(ro["dt"] / args.steps * 1e3, 3),
+                                               "moves": ro["moves"], "expansions": ro["expansions"]}
         if world == 1 and args.net_steps > 0:
             out["extra"]["c2_philox"] = philox_mode(sp, args)
             out["extra"]["record_overhead"] = record_overhead(sp, args)
@@ -513,6 +529,8 @@ def parse_args(argv=None):
                     help="timed moves (one free-running launch; about a game length, so every slot's "
                          "games of all ages share the window)")
     ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--launch", choices=["pooled", "free"], default="pooled",
+                    help="pooled: the games share K x G moves per launch; free: K moves per game")
     ap.add_argument("--games", type=int, default=4096, help="games per GPU")
     ap.add_argument("--sims", type=int, default=800)
     ap.add_argument("--batch", type=int, default=32)

@@ -117,6 +117,21 @@ int zc_c4_selfplay_async(zc_engine *eng, int32_t first_game, int32_t n_games, zc
                          double c, int32_t batch_size, int32_t moves, zc_c4_state *d_out_states,
                          int16_t *d_out_moves, int32_t *d_out_results, zc_game_stats *d_stats, void *hip_stream);
 
+/* Pooled self-play: the same launch, but the n games share a budget of `budget` moves drawn
+ * one at a time from the device counter *d_ticket (zeroed by this call), as the reference's
+ * self-play threads take work from one pool (scripts/train.py:151-170) — a game that moves
+ * faster plays more moves, so the launch ends when the budget is spent, not when its slowest
+ * game has played `moves_cap` moves.  Each game plays at most moves_cap moves, and its k-th
+ * move is exactly the k-th move of zc_c4_selfplay_async (same search, RNG stream, refill):
+ * only how many moves each game gets differs (decided by the counter, not deterministic).
+ * Steps a game did not reach get result ZC_SLOT_SKIP and move -1 in the [moves_cap][n]
+ * outputs; zc_traj_record_async leaves such slots untouched.  d_stats[i].leaves = sims x the
+ * moves game i played.  budget <= moves_cap * n_games, < 2^31. */
+int zc_c4_selfplay_pooled_async(zc_engine *eng, int32_t first_game, int32_t n_games, zc_c4_state *d_roots,
+                                int32_t sims, double c, int32_t batch_size, int32_t moves_cap, int64_t budget,
+                                int32_t *d_ticket, zc_c4_state *d_out_states, int16_t *d_out_moves,
+                                int32_t *d_out_results, zc_game_stats *d_stats, void *hip_stream);
+
 /* Random source of the Connect4 search's rollouts (all zc_c4_search* calls that follow):
  *   ZC_ROLLOUT_EXACT (default) — the game's CPython MT19937 stream in the reference's order;
  *     results are bit-identical to mcts.get_move.
@@ -446,6 +461,7 @@ typedef struct zc_traj_buffers {
 #define ZC_TRAJ_FINISHED 4   /* games finished                                         */
 #define ZC_TRAJ_OVERFLOW 5   /* bit 0: pool full (games dropped); bit 1: a game longer than max_len */
 #define ZC_SLOT_IDLE 3       /* result of an idle slot                                 */
+#define ZC_SLOT_SKIP 4       /* Connect4 pooled self-play: no move at this step (slot untouched) */
 /* After a move was played on every slot (d_states = positions after the move, d_moves =
  * the moves, int16: Connect4 column / packed chess move): append each position to its
  * slot's game; a finished game is copied to the pool and its slot restarts from d_init (the
@@ -453,7 +469,8 @@ typedef struct zc_traj_buffers {
  * d_results from zc_c4_play_async (reset = 0) and d_flags = d_rep = NULL; chess passes
  * d_flags from zc_chess_terminal_async and d_rep from zc_chess_repetition_async (NULL = no
  * repetition test) and d_results is written (Engine._evaluate).  Idle slots get
- * ZC_SLOT_IDLE.  No engine needed; enqueued on hip_stream. */
+ * ZC_SLOT_IDLE; Connect4 slots whose result is ZC_SLOT_SKIP are left as they are.  No engine
+ * needed; enqueued on hip_stream. */
 int zc_traj_record_async(int32_t n, const zc_traj_buffers *buf, void *d_states, const int16_t *d_moves,
                          int32_t *d_results, const int32_t *d_flags, const int32_t *d_rep, void *hip_stream);
 

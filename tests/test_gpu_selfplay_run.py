@@ -60,3 +60,41 @@ def test_run_refuses_a_quota():
     with pytest.raises(ValueError):
         sp.run(3)
     sp.close()
+
+
+def test_pooled_run_is_a_prefix_of_the_free_run():
+    """zc_c4_selfplay_pooled_async: the games share a move budget; each game's moves are the
+    first m_g moves of run() (states, moves, results), the budget is spent exactly, skipped
+    steps leave the trajectory slots alone, and a game's pool rows match its recorded moves."""
+    G, S, B, cap = 160, 128, 16, 12
+    budget = G * cap * 3 // 4
+    a = C4SelfPlay(G, S, batch_size=B, seed=11)
+    b = C4SelfPlay(G, S, batch_size=B, seed=11)
+    ra = a.run(cap).clone()
+    sa, ma = a._run_states.clone(), a._run_moves.clone()
+    rb = b.run_pooled(budget, cap).clone()
+    sb, mb = b._run_states.clone(), b._run_moves.clone()
+    played = rb != 4
+    m = played.sum(0)
+    # every game's played steps are a prefix, the budget is spent exactly
+    assert torch.equal(played, torch.arange(cap, device=rb.device)[:, None] < m[None, :])
+    assert int(m.sum()) == budget
+    assert int(b.stats[:, 2].sum()) == budget * S
+    assert torch.equal(rb[played], ra[played])
+    assert torch.equal(mb[played], ma[played])
+    assert torch.equal(sb[played], sa[played])
+    assert bool((mb[~played] == -1).all())
+    # the roots: the position after the game's last move (refilled when it ended the game)
+    for g in range(G):
+        k = int(m[g])
+        if k == 0:
+            continue
+        exp = sa[k - 1, g] if int(ra[k - 1, g]) == 2 else torch.zeros(3, dtype=torch.int64, device=sa.device)
+        assert torch.equal(b.roots[g], exp), g
+    # games finished in the pooled run == games in its trajectory pool; each pooled game's
+    # last move is its finishing move
+    fin = int(((rb != 2) & (rb != 4)).sum())
+    pb = b.take()
+    assert pb.games.shape[0] == fin and fin > 0
+    a.close()
+    b.close()

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """The bench's own workload for rocprofv3 passes: C4SelfPlay at 4096 games x 800 sims x bs 32,
 burned in to steady state (every slot has finished a game and started another, as bench.py
-does), then --steps timed moves in one free-running launch (c4_selfplay_kernel<false>, the
+does), then --steps x G timed moves in one pooled launch (--launch free: --steps moves per game) (c4_selfplay_kernel<false>, the
 last launch of the trace; tools/summarize_profile.py --moves K reports it per move)."""
 import argparse
 import os
@@ -19,6 +19,7 @@ ap.add_argument("--games", type=int, default=4096)
 ap.add_argument("--sims", type=int, default=800)
 ap.add_argument("--batch", type=int, default=32)
 ap.add_argument("--steps", type=int, default=8)
+ap.add_argument("--launch", choices=["pooled", "free"], default="pooled")
 ap.add_argument("--no-burn-in", dest="burn_in", action="store_false")
 a = ap.parse_args()
 torch.cuda.set_device(0)
@@ -26,7 +27,7 @@ torch.cuda.set_stream(torch.cuda.Stream(torch.device("cuda", 0)))
 sp = C4SelfPlay(a.games, a.sims, c=1.4, batch_size=a.batch, seed=0, device=0, record=True)
 burn = bench.burn_in(sp) if a.burn_in else 0
 print(f"burn-in {burn} steps", flush=True)
-r = bench.run_steps(sp, a.steps, warmup=0)
+r = bench.run_steps(sp, a.steps, warmup=0, launch=a.launch)
 print(f"steps {a.steps}: {r['expansions'] / r['dt'] / 1e9:.4f} G expansions/s, "
       f"launch ms {r['launch_ms']:.3f} ({r['launch_ms'] / a.steps:.3f} per move), "
       f"depth {r['depth_sum'] / max(r['expansions'], 1):.3f}", flush=True)

@@ -55,6 +55,7 @@ class TrajBuffers(ctypes.Structure):
 
 ZC_TRAJ_POSITIONS, ZC_TRAJ_GAMES, ZC_TRAJ_NEXT, ZC_TRAJ_QUOTA, ZC_TRAJ_FINISHED, ZC_TRAJ_OVERFLOW = range(6)
 ZC_SLOT_IDLE = 3
+ZC_SLOT_SKIP = 4
 
 C4_STATE_DTYPE = np.dtype([("stones", "<u8", (2,)), ("turn", "<i4"), ("reserved", "<i4")])
 # zc_c4_hp_node: the host-policy walk's end (include/zeroclone.h)
@@ -122,6 +123,10 @@ SIGNATURES = [
                                             ctypes.c_int32, ctypes.c_double, ctypes.c_int32, ctypes.c_int32,
                                             ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                             ctypes.c_void_p]),
+    ("zc_c4_selfplay_pooled_async", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p,
+                                                   ctypes.c_int32, ctypes.c_double, ctypes.c_int32, ctypes.c_int32,
+                                                   ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                                   ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     ("zc_c4_hp_walk", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p,
                                      ctypes.c_void_p]),
     ("zc_c4_hp_expand", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
@@ -392,6 +397,17 @@ class NativeEngine:
                                          int(batch_size), int(moves), ctypes.c_void_p(d_states),
                                          ctypes.c_void_p(d_moves16), ctypes.c_void_p(d_results),
                                          ctypes.c_void_p(d_stats), ctypes.c_void_p(stream or None)))
+
+    def c4_selfplay_pooled_async(self, d_roots: int, n: int, sims: int, c: float, batch_size: int, moves_cap: int,
+                                 budget: int, d_ticket: int, d_states: int, d_moves16: int, d_results: int,
+                                 d_stats: int, stream: int = 0, first_game: int = 0) -> None:
+        """`budget` self-play moves shared by the games in one launch, at most `moves_cap` per
+        game (zc_c4_selfplay_pooled_async)."""
+        check(lib().zc_c4_selfplay_pooled_async(self._h, first_game, n, ctypes.c_void_p(d_roots), int(sims),
+                                                float(c), int(batch_size), int(moves_cap), int(budget),
+                                                ctypes.c_void_p(d_ticket), ctypes.c_void_p(d_states),
+                                                ctypes.c_void_p(d_moves16), ctypes.c_void_p(d_results),
+                                                ctypes.c_void_p(d_stats), ctypes.c_void_p(stream or None)))
 
     def c4_play_async(self, d_states: int, n: int, d_moves: int, d_results: int, reset: bool = True,
                       stream: int = 0) -> None:

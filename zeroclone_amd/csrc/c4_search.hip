@@ -625,7 +625,13 @@ __global__ __launch_bounds__(kSearchWaves * kBlock) void c4_selfplay_kernel(Sear
     Counters cn;
     int status = 0;
     int finished = 0;
-    for (int mv = 0; mv < p.moves; ++mv) {
+    int mv = 0;
+    for (; mv < p.moves; ++mv) {
+        if (p.ticket) {  // pooled run: the next move only while the shared budget lasts
+            int tk = 0;
+            if (lane == 0) tk = atomicAdd(p.ticket, 1);
+            if (uni(tk) >= p.budget) break;
+        }
         zc_c4_state root = p.roots[gl];
         uint64_t s0 = uni64(root.stones[0]), s1 = uni64(root.stones[1]);
         int turn = uni(root.turn);
@@ -658,12 +664,19 @@ __global__ __launch_bounds__(kSearchWaves * kBlock) void c4_selfplay_kernel(Sear
         finished += r != ZC_C4_ONGOING;
         wave_mem_order();
     }
+    if (p.ticket) {  // steps this game did not reach: untouched by the trajectory replay
+        for (int k = mv + (int)lane; k < p.moves; k += kBlock) {
+            const size_t o = (size_t)k * p.n_games + gl;
+            p.out_moves16[o] = -1;
+            p.out_results[o] = ZC_SLOT_SKIP;
+        }
+    }
     if (lane == 0) {
         zc_game_stats st{};
         st.status = status;
         st.expansions = cn.expansions;
         st.depth_sum = cn.depth_sum;
-        st.leaves = (int64_t)p.sims * p.moves;
+        st.leaves = (int64_t)p.sims * mv;
         st.rollout_plies = cn.plies;
         st.rollout_blocks = cn.blocks;
         st.rng_words = rng.use();

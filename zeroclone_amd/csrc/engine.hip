@@ -327,6 +327,34 @@ int zc_c4_selfplay_async(zc_engine *eng, int32_t first, int32_t n, zc_c4_state *
     return ZC_OK;
 }
 
+int zc_c4_selfplay_pooled_async(zc_engine *eng, int32_t first, int32_t n, zc_c4_state *d_roots, int32_t sims,
+                                double c, int32_t bs, int32_t moves_cap, int64_t budget, int32_t *d_ticket,
+                                zc_c4_state *d_out_states, int16_t *d_out_moves, int32_t *d_out_results,
+                                zc_game_stats *d_stats, void *hip_stream) {
+    if (!eng || (n && (!d_roots || !d_out_states || !d_out_moves || !d_out_results || !d_stats || !d_ticket)))
+        return fail(ZC_EINVAL, "null argument");
+    if (int r = check_search(eng, first, n, sims, c, bs)) return r;
+    if (moves_cap < 1) return fail(ZC_EINVAL, "moves_cap must be >= 1 (got %d)", moves_cap);
+    if (budget < 0 || budget > (int64_t)moves_cap * n || budget >= ((int64_t)1 << 31))
+        return fail(ZC_EINVAL, "budget %lld outside [0, moves_cap x n_games] or >= 2^31", (long long)budget);
+    if (!n) return ZC_OK;
+    std::lock_guard<std::mutex> lk(eng->mu);
+    ZC_HIP(hipSetDevice(eng->cfg.device));
+    hipStream_t s = (hipStream_t)hip_stream;
+    ZC_HIP(hipMemsetAsync(d_ticket, 0, sizeof(int32_t), s));
+    zc::SearchParams p = make_params(eng, first, n, d_roots, sims, c, bs, nullptr, nullptr, d_stats);
+    p.moves = moves_cap;
+    p.io_roots = d_roots;
+    p.out_states = d_out_states;
+    p.out_moves16 = d_out_moves;
+    p.out_results = d_out_results;
+    p.ticket = d_ticket;
+    p.budget = (int32_t)budget;
+    zc::launch_c4_selfplay(p, s);
+    ZC_HIP(hipGetLastError());
+    return ZC_OK;
+}
+
 int zc_c4_search_async(zc_engine *eng, int32_t first, int32_t n, const zc_c4_state *d_roots, int32_t sims, double c,
                        int32_t bs, int32_t *d_move, int32_t *d_na, zc_game_stats *d_stats, void *hip_stream) {
     if (!eng || (n && (!d_roots || !d_move || !d_na || !d_stats))) return fail(ZC_EINVAL, "null argument");

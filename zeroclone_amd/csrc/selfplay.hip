@@ -81,7 +81,10 @@ __global__ __launch_bounds__(kRecThreads) void traj_record_kernel(int n, zc_traj
         uint64_t *row = (uint64_t *)(states + (size_t)(g < n ? g : 0) * b.row_bytes);
         if (g < n) {
             game = slot[1];
-            if (game < 0) {  // idle slot (quota spent): held at the opening, nothing recorded
+            if (game >= 0 && !flags && results[g] == ZC_SLOT_SKIP) {
+                game = -2;  // pooled self-play: no move on this slot at this step, left as it is
+                slot[3] = 0;
+            } else if (game < 0) {  // idle slot (quota spent): held at the opening, nothing recorded
                 for (int k = 0; k < W; ++k) row[k] = init[k];
                 results[g] = ZC_SLOT_IDLE;
                 slot[3] = 0;

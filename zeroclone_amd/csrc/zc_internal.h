@@ -97,6 +97,9 @@ struct SearchParams {
     zc_c4_state *out_states;
     int16_t *out_moves16;
     int32_t *out_results;
+    // pooled self-play: moves drawn from *ticket while < budget (null: `moves` per game)
+    int32_t *ticket;
+    int32_t budget;
 };
 
 struct ExtParams {

@@ -228,6 +228,33 @@ class C4SelfPlay:
         self.results.copy_(self._run_results[-1])
         return self._run_results
 
+    def run_pooled(self, budget: int, moves_cap: int, stream: int | None = None) -> torch.Tensor:
+        """`budget` moves shared by all games in ONE launch (zc_c4_selfplay_pooled_async): each
+        game takes its next move from a device counter while the budget lasts, at most
+        `moves_cap` moves — the reference's self-play threads drawing games from one pool
+        (scripts/train.py:151-170).  Game i's k-th move is the k-th move run() would play;
+        how many moves each game gets follows the games' pace.  The trajectory recording
+        replays the steps in order (slots without a k-th move: ZC_SLOT_SKIP, untouched).
+        Returns the per-step results [moves_cap, G]; self.stats sums the moves' counters."""
+        if self.traj is not None and self.traj.quota != _UNLIMITED:
+            raise ValueError("run_pooled() plays without a game quota; use step() under simulate_games' quota")
+        s = stream if stream is not None else torch.cuda.current_stream(self.dev).cuda_stream
+        if getattr(self, "_run_k", None) != moves_cap:
+            self._run_states = torch.zeros((moves_cap, self.G, 3), dtype=torch.int64, device=self.dev)
+            self._run_moves = torch.zeros((moves_cap, self.G), dtype=torch.int16, device=self.dev)
+            self._run_results = torch.zeros((moves_cap, self.G), dtype=torch.int32, device=self.dev)
+            self._run_k = moves_cap
+        if getattr(self, "_ticket", None) is None:
+            self._ticket = torch.zeros(1, dtype=torch.int32, device=self.dev)
+        self.eng.c4_selfplay_pooled_async(self.roots.data_ptr(), self.G, self.sims, self.c, self.bs, moves_cap,
+                                          budget, self._ticket.data_ptr(), self._run_states.data_ptr(),
+                                          self._run_moves.data_ptr(), self._run_results.data_ptr(),
+                                          self.stats.data_ptr(), stream=s)
+        if self.record:
+            for k in range(moves_cap):
+                self.traj.record(self._run_states[k].data_ptr(), self._run_moves[k], self._run_results[k], stream=s)
+        return self._run_results
+
     def step_search(self, stream: int | None = None) -> torch.Tensor:
         """The search half of a step (zc_c4_search_async); returns the results tensor the
         finish half will fill."""
