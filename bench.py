@@ -304,7 +304,8 @@ def run_steps(sp, steps: int, warmup: int, world: int = 1, launch: str = "pooled
     slowest game."""
     dev = sp.dev
     stream = torch.cuda.current_stream(dev)
-    ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+    ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
+          torch.cuda.Event(enable_timing=True))
     if warmup:
         sp.run(warmup)
     torch.cuda.synchronize(dev)
@@ -314,9 +315,9 @@ def run_steps(sp, steps: int, warmup: int, world: int = 1, launch: str = "pooled
     t0 = time.perf_counter()
     ev[0].record(stream)
     if launch == "pooled":
-        res = sp.run_pooled(steps * sp.G, 2 * steps)
+        res = sp.run_pooled(steps * sp.G, 2 * steps, kernel_done=ev[2])
     else:
-        res = sp.run(steps)
+        res = sp.run(steps, kernel_done=ev[2])
     ev[1].record(stream)
     torch.cuda.synchronize(dev)
     if world > 1:
@@ -329,7 +330,7 @@ def run_steps(sp, steps: int, warmup: int, world: int = 1, launch: str = "pooled
                & (res != _native.ZC_SLOT_SKIP)).sum().item())
     moves = int(((res != _native.ZC_SLOT_IDLE) & (res != _native.ZC_SLOT_SKIP)).sum().item())
     tot = [int(x) for x in st[:, [0, 1, 2]].sum(0).tolist()]
-    return {"dt": dt, "launch_ms": ev[0].elapsed_time(ev[1]), "expansions": tot[0], "depth_sum": tot[1],
+    return {"dt": dt, "launch_ms": ev[0].elapsed_time(ev[2]), "launch_record_ms": ev[0].elapsed_time(ev[1]), "expansions": tot[0], "depth_sum": tot[1],
             "finished": fin, "leaves": tot[2], "moves": moves}
 
 
@@ -446,7 +447,7 @@ def run_rank(args, rank: int, world: int, local: int):
                       "trajectory_allgather": gather},
         }
         if world == 1:
-            out["extra"]["phases"] = phases(sp, args, bytes_launch, avg_kernel_s)
+            out["extra"]["phases"] = phases(sp, args, bytes_launch, avg_kernel_s, traffic)
             other = "free" if args.launch == "pooled" else "pooled"
             ro = run_steps(sp, args.steps, 0, launch=other)
             out["extra"][f"launch_{other}"] = {"value": round(ro["expansions"] / ro["dt"], 1), "unit": "expansions/s",
@@ -474,7 +475,7 @@ def run_rank(args, rank: int, world: int, local: int):
         dist.destroy_process_group()
 
 
-def phases(sp, args, bytes_launch: float, avg_kernel_s: float) -> dict:
+def phases(sp, args, bytes_launch: float, avg_kernel_s: float, traffic: float | None = None) -> dict:
     """SURVEY §8(d) per-phase times: s_memtime stamps from one extra search with the stamped
     kernel build, shares applied to the unstamped launch time; and the tree-walk-only
     roofline (select + expand-write + backup + publish; rollouts are integer VALU, not HBM)."""
@@ -490,8 +491,14 @@ def phases(sp, args, bytes_launch: float, avg_kernel_s: float) -> dict:
             "walk_roofline": {"t_walk_ms": round(walk * avg_kernel_s * 1e3, 3),
                               "achieved": round(bytes_launch / (walk * avg_kernel_s) / 1e9, 2),
                               "frac": round(bytes_launch / (walk * avg_kernel_s) / 1e9 / HBM_PEAK_GBS, 5),
+                              "measured_frac": (round(traffic / (walk * avg_kernel_s) / 1e9 / HBM_PEAK_GBS, 5)
+                                                if traffic else None),
                               "note": "SURVEY §8(d) roofline definition: model bytes / tree-walk time only "
-                                      "(phase shares from the stamped build: modelled, not a separate clock)"}}
+                                      "(phase shares from the stamped build: modelled, not a separate clock). "
+                                      "The model counts a root-to-leaf re-read per simulation that the kernel "
+                                      "serves from LDS / L2, so frac ~1 is the model's ceiling, not HBM "
+                                      "saturation: measured_frac = the whole kernel's PMC HBM bytes over the "
+                                      "walk time alone"}}
 
 
 def record_overhead(sp, args) -> dict:

@@ -204,7 +204,7 @@ class C4SelfPlay:
         self.step_search(stream)
         return self.step_finish(stream)
 
-    def run(self, moves: int, stream: int | None = None) -> torch.Tensor:
+    def run(self, moves: int, stream: int | None = None, kernel_done=None) -> torch.Tensor:
         """`moves` moves for every game in ONE launch (zc_c4_selfplay_async: each game at its
         own pace, finished games refilled from the opening in the kernel), then the
         trajectory recording of every step, in step order — the same games, pool and labels
@@ -222,13 +222,15 @@ class C4SelfPlay:
         self.eng.c4_selfplay_async(self.roots.data_ptr(), self.G, self.sims, self.c, self.bs, moves,
                                    self._run_states.data_ptr(), self._run_moves.data_ptr(),
                                    self._run_results.data_ptr(), self.stats.data_ptr(), stream=s)
+        if kernel_done is not None:   # an event recorded after the launch, before the recording
+            kernel_done.record()
         if self.record:
             for k in range(moves):
                 self.traj.record(self._run_states[k].data_ptr(), self._run_moves[k], self._run_results[k], stream=s)
         self.results.copy_(self._run_results[-1])
         return self._run_results
 
-    def run_pooled(self, budget: int, moves_cap: int, stream: int | None = None) -> torch.Tensor:
+    def run_pooled(self, budget: int, moves_cap: int, stream: int | None = None, kernel_done=None) -> torch.Tensor:
         """`budget` moves shared by all games in ONE launch (zc_c4_selfplay_pooled_async): each
         game takes its next move from a device counter while the budget lasts, at most
         `moves_cap` moves — the reference's self-play threads drawing games from one pool
@@ -250,6 +252,8 @@ class C4SelfPlay:
                                           budget, self._ticket.data_ptr(), self._run_states.data_ptr(),
                                           self._run_moves.data_ptr(), self._run_results.data_ptr(),
                                           self.stats.data_ptr(), stream=s)
+        if kernel_done is not None:
+            kernel_done.record()
         if self.record:
             for k in range(moves_cap):
                 self.traj.record(self._run_states[k].data_ptr(), self._run_moves[k], self._run_results[k], stream=s)
