@@ -118,7 +118,7 @@ int zc_c4_selfplay_async(zc_engine *eng, int32_t first_game, int32_t n_games, zc
                          int16_t *d_out_moves, int32_t *d_out_results, zc_game_stats *d_stats, void *hip_stream);
 
 /* Pooled self-play: the same launch, but the n games share a budget of `budget` moves drawn
- * one at a time from the device counter *d_ticket (zeroed by this call), as the reference's
+ * one at a time from the device counter d_ticket[0] (d_ticket[0..1] zeroed by this call), as the reference's
  * self-play threads take work from one pool (scripts/train.py:151-170) — a game that moves
  * faster plays more moves, so the launch ends when the budget is spent, not when its slowest
  * game has played `moves_cap` moves.  Each game plays at most moves_cap moves, and its k-th
@@ -126,7 +126,8 @@ int zc_c4_selfplay_async(zc_engine *eng, int32_t first_game, int32_t n_games, zc
  * only how many moves each game gets differs (decided by the counter, not deterministic).
  * Steps a game did not reach get result ZC_SLOT_SKIP and move -1 in the [moves_cap][n]
  * outputs; zc_traj_record_async leaves such slots untouched.  d_stats[i].leaves = sims x the
- * moves game i played.  budget <= moves_cap * n_games, < 2^31. */
+ * moves game i played.  budget <= moves_cap * n_games, < 2^31.  d_ticket: 2 int32 — the
+ * counter, then the most moves any game played (the d_reached of zc_traj_record_steps_async). */
 int zc_c4_selfplay_pooled_async(zc_engine *eng, int32_t first_game, int32_t n_games, zc_c4_state *d_roots,
                                 int32_t sims, double c, int32_t batch_size, int32_t moves_cap, int64_t budget,
                                 int32_t *d_ticket, zc_c4_state *d_out_states, int16_t *d_out_moves,
@@ -473,6 +474,12 @@ typedef struct zc_traj_buffers {
  * needed; enqueued on hip_stream. */
 int zc_traj_record_async(int32_t n, const zc_traj_buffers *buf, void *d_states, const int16_t *d_moves,
                          int32_t *d_results, const int32_t *d_flags, const int32_t *d_rep, void *hip_stream);
+/* Connect4: zc_traj_record_async for `steps` consecutive steps of a self-play launch, in step
+ * order — d_states / d_moves / d_results are its [steps][n] outputs.  With d_reached (device
+ * int32, e.g. d_ticket + 1 of zc_c4_selfplay_pooled_async) the steps k >= *d_reached, which no
+ * game reached, cost only their launches. */
+int zc_traj_record_steps_async(int32_t n, const zc_traj_buffers *buf, void *d_states, const int16_t *d_moves,
+                               int32_t *d_results, int32_t steps, const int32_t *d_reached, void *hip_stream);
 
 /* ---- self-test hooks (used by the parity tests) -------------------------------------
  * UCT score exactly as the search kernel computes it (mcts.cpp:41-45), evaluated ON THE

@@ -21,8 +21,11 @@ def timed(sp, fn):
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     st = sp.stats[:, [0, 2]].sum(0).tolist()
-    moves = int(((res != 4)).sum().item())
-    return {"dt": dt, "expansions": int(st[0]), "leaves": int(st[1]), "moves": moves}
+    per_game = (res != 4).sum(0).float()
+    moves = int(per_game.sum().item())
+    return {"dt": dt, "expansions": int(st[0]), "leaves": int(st[1]), "moves": moves,
+            "per_game_moves": {"min": int(per_game.min()), "max": int(per_game.max()),
+                               "p99": float(per_game.quantile(0.99)), "mean": float(per_game.mean())}}
 
 
 def main():

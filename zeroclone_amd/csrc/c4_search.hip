@@ -665,6 +665,7 @@ __global__ __launch_bounds__(kSearchWaves * kBlock) void c4_selfplay_kernel(Sear
         wave_mem_order();
     }
     if (p.ticket) {  // steps this game did not reach: untouched by the trajectory replay
+        if (lane == 0) atomicMax(p.ticket + 1, mv);
         for (int k = mv + (int)lane; k < p.moves; k += kBlock) {
             const size_t o = (size_t)k * p.n_games + gl;
             p.out_moves16[o] = -1;

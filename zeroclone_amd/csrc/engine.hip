@@ -341,7 +341,7 @@ int zc_c4_selfplay_pooled_async(zc_engine *eng, int32_t first, int32_t n, zc_c4_
     std::lock_guard<std::mutex> lk(eng->mu);
     ZC_HIP(hipSetDevice(eng->cfg.device));
     hipStream_t s = (hipStream_t)hip_stream;
-    ZC_HIP(hipMemsetAsync(d_ticket, 0, sizeof(int32_t), s));
+    ZC_HIP(hipMemsetAsync(d_ticket, 0, 2 * sizeof(int32_t), s));
     zc::SearchParams p = make_params(eng, first, n, d_roots, sims, c, bs, nullptr, nullptr, d_stats);
     p.moves = moves_cap;
     p.io_roots = d_roots;
@@ -629,6 +629,36 @@ int zc_chess_repetition_async(int32_t n, int32_t cap, const uint16_t *d_hist, co
     if (!n) return ZC_OK;
     if (!zc::launch_chess_repetition(n, cap, d_hist, d_len, d_out, (hipStream_t)hip_stream))
         return fail(ZC_EINVAL, "history capacity %d outside [1, 4096]", cap);
+    ZC_HIP(hipGetLastError());
+    return ZC_OK;
+}
+
+namespace {
+int check_traj(int32_t n, const zc_traj_buffers *buf, const void *d_states) {
+    if (n < 0 || !buf) return fail(ZC_EINVAL, "bad argument");
+    const zc_traj_buffers &b = *buf;
+    if (b.row_bytes < 8 || (b.row_bytes & 7) || b.max_len < 2 || b.pool_cap < 0 || b.pool_cap > INT32_MAX ||
+        b.games_cap < 0)
+        return fail(ZC_EINVAL, "bad trajectory buffer shape (row_bytes %d, max_len %d)", b.row_bytes, b.max_len);
+    if (!b.d_hist || !b.d_hmoves || !b.d_slot || !b.d_pool || !b.d_labels || !b.d_pool_moves || !b.d_games ||
+        !b.d_ctl || !b.d_init)
+        return fail(ZC_EINVAL, "null trajectory buffer");
+    if (((uintptr_t)b.d_hist | (uintptr_t)b.d_pool | (uintptr_t)b.d_init | (uintptr_t)d_states) & 7)
+        return fail(ZC_EINVAL, "rows must be 8-byte aligned");
+    return ZC_OK;
+}
+}  // namespace
+
+int zc_traj_record_steps_async(int32_t n, const zc_traj_buffers *buf, void *d_states, const int16_t *d_moves,
+                               int32_t *d_results, int32_t steps, const int32_t *d_reached, void *hip_stream) {
+    if (int r = check_traj(n, buf, d_states)) return r;
+    if (steps < 0) return fail(ZC_EINVAL, "steps must be >= 0 (got %d)", steps);
+    if (n && steps && (!d_states || !d_moves || !d_results)) return fail(ZC_EINVAL, "bad argument");
+    if (!n) return ZC_OK;
+    const size_t row = (size_t)buf->row_bytes;
+    for (int k = 0; k < steps; ++k)
+        zc::launch_traj_record(n, *buf, (uint8_t *)d_states + (size_t)k * n * row, d_moves + (size_t)k * n,
+                               d_results + (size_t)k * n, nullptr, nullptr, (hipStream_t)hip_stream, d_reached, k);
     ZC_HIP(hipGetLastError());
     return ZC_OK;
 }

@@ -66,7 +66,9 @@ __device__ __forceinline__ void block_scan2(int &x, long long &y, int &tx, long 
 // (slot[3], 0 = nothing to copy), the refill of the slot.  The copy is pass 2.
 __global__ __launch_bounds__(kRecThreads) void traj_record_kernel(int n, zc_traj_buffers b, uint8_t *states,
                                                                   const int16_t *moves, int32_t *results,
-                                                                  const int32_t *flags, const int32_t *rep) {
+                                                                  const int32_t *flags, const int32_t *rep,
+                                                                  const int32_t *reached, int step) {
+    if (reached && step >= *reached) return;  // a pooled run's step no game reached (whole block)
     const int W = b.row_bytes / 8;
     const uint64_t *init = (const uint64_t *)b.d_init;
     long long pos_base = b.d_ctl[kTrajPositions], game_base = b.d_ctl[kTrajGames], next = b.d_ctl[kTrajNext];
@@ -162,7 +164,8 @@ __global__ __launch_bounds__(kRecThreads) void traj_record_kernel(int n, zc_traj
 // Pass 2 — one thread per (slot, position): a finished game's positions, labels and moves
 // to its pool place (get_dataset: position i of n gets f * (-1)^(n-1-i), f = 0 for a draw,
 // -1 otherwise); position 0's thread then restarts the slot's history at the opening.
-__global__ void traj_copy_kernel(int n, zc_traj_buffers b) {
+__global__ void traj_copy_kernel(int n, zc_traj_buffers b, const int32_t *reached, int step) {
+    if (reached && step >= *reached) return;
     const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     const int g = (int)(t / b.max_len), i = (int)(t % b.max_len);
     if (g >= n) return;
@@ -187,11 +190,12 @@ __global__ void traj_copy_kernel(int n, zc_traj_buffers b) {
 }  // namespace
 
 void launch_traj_record(int n, const zc_traj_buffers &b, void *states, const int16_t *moves, int32_t *results,
-                        const int32_t *flags, const int32_t *rep, hipStream_t s) {
+                        const int32_t *flags, const int32_t *rep, hipStream_t s, const int32_t *reached, int step) {
     hipLaunchKernelGGL(traj_record_kernel, dim3(1), dim3(kRecThreads), 0, s, n, b, (uint8_t *)states, moves, results,
-                       flags, rep);
+                       flags, rep, reached, step);
     const long long threads = (long long)n * b.max_len;
-    hipLaunchKernelGGL(traj_copy_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s, n, b);
+    hipLaunchKernelGGL(traj_copy_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s, n, b, reached,
+                       step);
 }
 
 }  // namespace zc

@@ -97,7 +97,8 @@ struct SearchParams {
     zc_c4_state *out_states;
     int16_t *out_moves16;
     int32_t *out_results;
-    // pooled self-play: moves drawn from *ticket while < budget (null: `moves` per game)
+    // pooled self-play: moves drawn from ticket[0] while < budget (null: `moves` per game);
+    // ticket[1] = the most moves any game played
     int32_t *ticket;
     int32_t budget;
 };
@@ -278,7 +279,8 @@ void launch_c4_play(int n, zc_c4_state *states, const int32_t *moves, int32_t *r
 enum : int { kTrajPositions = ZC_TRAJ_POSITIONS, kTrajGames = ZC_TRAJ_GAMES, kTrajNext = ZC_TRAJ_NEXT,
              kTrajQuota = ZC_TRAJ_QUOTA, kTrajFinished = ZC_TRAJ_FINISHED, kTrajOverflow = ZC_TRAJ_OVERFLOW };
 void launch_traj_record(int n, const zc_traj_buffers &b, void *states, const int16_t *moves, int32_t *results,
-                        const int32_t *flags, const int32_t *rep, hipStream_t s);
+                        const int32_t *flags, const int32_t *rep, hipStream_t s, const int32_t *reached = nullptr,
+                        int step = 0);
 void launch_uct_debug(int n, const double *logn, const int32_t *na, const double *q, double c, double *out,
                       hipStream_t s);
 

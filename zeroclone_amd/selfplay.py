@@ -136,6 +136,15 @@ class Trajectories:
             ctypes.c_void_p(results.data_ptr()), ctypes.c_void_p(flags.data_ptr() if flags is not None else None),
             ctypes.c_void_p(rep.data_ptr() if rep is not None else None), ctypes.c_void_p(stream or None)))
 
+    def record_steps(self, d_states: int, moves: torch.Tensor, results: torch.Tensor, steps: int,
+                     reached: torch.Tensor | None = None, stream: int = 0):
+        """record() for `steps` consecutive [steps][n] self-play outputs in one call
+        (zc_traj_record_steps_async); steps >= *reached are skipped on the device."""
+        _native.check(_native.lib().zc_traj_record_steps_async(
+            self.n, ctypes.byref(self._buf), ctypes.c_void_p(d_states), ctypes.c_void_p(moves.data_ptr()),
+            ctypes.c_void_p(results.data_ptr()), int(steps),
+            ctypes.c_void_p(reached.data_ptr() if reached is not None else None), ctypes.c_void_p(stream or None)))
+
     def finished(self) -> int:
         """Games finished since start() (one device read)."""
         return int(self.ctl[_native.ZC_TRAJ_FINISHED].item())
@@ -225,8 +234,7 @@ class C4SelfPlay:
         if kernel_done is not None:   # an event recorded after the launch, before the recording
             kernel_done.record()
         if self.record:
-            for k in range(moves):
-                self.traj.record(self._run_states[k].data_ptr(), self._run_moves[k], self._run_results[k], stream=s)
+            self.traj.record_steps(self._run_states.data_ptr(), self._run_moves, self._run_results, moves, stream=s)
         self.results.copy_(self._run_results[-1])
         return self._run_results
 
@@ -247,7 +255,7 @@ class C4SelfPlay:
             self._run_results = torch.zeros((moves_cap, self.G), dtype=torch.int32, device=self.dev)
             self._run_k = moves_cap
         if getattr(self, "_ticket", None) is None:
-            self._ticket = torch.zeros(1, dtype=torch.int32, device=self.dev)
+            self._ticket = torch.zeros(2, dtype=torch.int32, device=self.dev)   # counter, most moves played
         self.eng.c4_selfplay_pooled_async(self.roots.data_ptr(), self.G, self.sims, self.c, self.bs, moves_cap,
                                           budget, self._ticket.data_ptr(), self._run_states.data_ptr(),
                                           self._run_moves.data_ptr(), self._run_results.data_ptr(),
@@ -255,8 +263,8 @@ class C4SelfPlay:
         if kernel_done is not None:
             kernel_done.record()
         if self.record:
-            for k in range(moves_cap):
-                self.traj.record(self._run_states[k].data_ptr(), self._run_moves[k], self._run_results[k], stream=s)
+            self.traj.record_steps(self._run_states.data_ptr(), self._run_moves, self._run_results, moves_cap,
+                                   reached=self._ticket[1:], stream=s)
         return self._run_results
 
     def step_search(self, stream: int | None = None) -> torch.Tensor:
