@@ -62,7 +62,8 @@ def test_run_refuses_a_quota():
     sp.close()
 
 
-def test_pooled_run_is_a_prefix_of_the_free_run():
+@pytest.mark.parametrize("mode", ["exact", "philox"])
+def test_pooled_run_is_a_prefix_of_the_free_run(mode):
     """zc_c4_selfplay_pooled_async: the games share a move budget; each game's moves are the
     first m_g moves of run() (states, moves, results), the budget is spent exactly, skipped
     steps leave the trajectory slots alone, and a game's pool rows match its recorded moves."""
@@ -70,6 +71,8 @@ def test_pooled_run_is_a_prefix_of_the_free_run():
     budget = G * cap * 3 // 4
     a = C4SelfPlay(G, S, batch_size=B, seed=11)
     b = C4SelfPlay(G, S, batch_size=B, seed=11)
+    for sp in (a, b):
+        sp.eng.c4_rollout_mode(mode, 5)
     ra = a.run(cap).clone()
     sa, ma = a._run_states.clone(), a._run_moves.clone()
     rb = b.run_pooled(budget, cap).clone()
@@ -96,5 +99,12 @@ def test_pooled_run_is_a_prefix_of_the_free_run():
     fin = int(((rb != 2) & (rb != 4)).sum())
     pb = b.take()
     assert pb.games.shape[0] == fin and fin > 0
+    # the device's count of the most moves any game played (the record's early exit)
+    assert int(b._ticket[1]) == int(m.max())
+    # each game's RNG stream: where it played every step, the free run's stream exactly
+    full = [g for g in range(G) if int(m[g]) == cap][:4]
+    for g in full:
+        assert a.eng.get_rng_state(g)[0].tolist() == b.eng.get_rng_state(g)[0].tolist()
+        assert a.eng.get_rng_state(g)[1] == b.eng.get_rng_state(g)[1]
     a.close()
     b.close()
