@@ -118,20 +118,27 @@ int zc_c4_selfplay_async(zc_engine *eng, int32_t first_game, int32_t n_games, zc
                          int16_t *d_out_moves, int32_t *d_out_results, zc_game_stats *d_stats, void *hip_stream);
 
 /* Pooled self-play: the same launch, but the n games share a budget of `budget` moves drawn
- * one at a time from the device counter d_ticket[0] (d_ticket[0..1] zeroed by this call), as the reference's
- * self-play threads take work from one pool (scripts/train.py:151-170) — a game that moves
- * faster plays more moves, so the launch ends when the budget is spent, not when its slowest
- * game has played `moves_cap` moves.  Each game plays at most moves_cap moves, and its k-th
+ * one at a time from the device counter d_ticket[0] (d_ticket[0..1] zeroed by this call).  This
+ * is a throughput schedule, not the reference's: scripts/train.py:151-170 is lockstep (every
+ * unfinished game gets one move per play_mcts_parallel call).  A game that moves faster plays
+ * more moves, so the launch ends when the budget is spent, not when its slowest game has
+ * played `moves_cap` moves.  Each game plays at most moves_cap moves, and its k-th
  * move is exactly the k-th move of zc_c4_selfplay_async (same search, RNG stream, refill):
  * only how many moves each game gets differs (decided by the counter, not deterministic).
  * Steps a game did not reach get result ZC_SLOT_SKIP and move -1 in the [moves_cap][n]
  * outputs; zc_traj_record_async leaves such slots untouched.  d_stats[i].leaves = sims x the
- * moves game i played.  budget <= moves_cap * n_games, < 2^31.  d_ticket: 2 int32 — the
+ * moves game i played.  budget <= moves_cap * n_games, < 2^31; n_games <=
+ * zc_c4_pooled_max_games (ZC_EINVAL otherwise).  d_ticket: 2 int32 — the
  * counter, then the most moves any game played (the d_reached of zc_traj_record_steps_async). */
 int zc_c4_selfplay_pooled_async(zc_engine *eng, int32_t first_game, int32_t n_games, zc_c4_state *d_roots,
                                 int32_t sims, double c, int32_t batch_size, int32_t moves_cap, int64_t budget,
                                 int32_t *d_ticket, zc_c4_state *d_out_states, int16_t *d_out_moves,
                                 int32_t *d_out_results, zc_game_stats *d_stats, void *hip_stream);
+
+/* The most games zc_c4_selfplay_pooled_async accepts at this batch size: the games the
+ * self-play grid keeps resident on the device at once (occupancy x compute units).  A pooled
+ * launch hands out its budget only to resident waves, so larger launches are refused. */
+int zc_c4_pooled_max_games(zc_engine *eng, int32_t batch_size, int32_t *out);
 
 /* Random source of the Connect4 search's rollouts (all zc_c4_search* calls that follow):
  *   ZC_ROLLOUT_EXACT (default) — the game's CPython MT19937 stream in the reference's order;
@@ -351,7 +358,10 @@ int zc_chess_hp_expand(zc_engine *eng, int32_t game, int32_t flush, int32_t leaf
 /* ---- Chess PUCT search (AlphaZero-style; no reference counterpart) -------
  * Selection by Q + c_puct * P * sqrt(sum N) / (1 + N) with priors P from a policy network,
  * virtual loss within a flush, Dirichlet(alpha) noise of weight eps on the root priors
- * (Philox stream keyed by seed and game).  Flush 0 evaluates the root alone; then
+ * (Philox stream keyed by seed, counter (game, search number)).  d_search_no (device int32
+ * [n_games], may be NULL = 0 for every game): game i's search number — the noise and the
+ * temperature sample of the search come from it, and end adds 1 to it, so consecutive
+ * searches (or replays of a captured graph) of a game draw fresh noise.  Flush 0 evaluates the root alone; then
  * ceil((sims - 1) / batch_size) flushes of up to batch_size leaves: zc_chess_puct_flushes.
  * select exports leaves/planes as zc_chess_ext_select; backup takes per leaf slot the value
  * for the leaf's side to move and 4096 policy logits indexed from*64 + to (logits_dtype
@@ -361,7 +371,7 @@ int zc_chess_hp_expand(zc_engine *eng, int32_t game, int32_t flush, int32_t leaf
 int zc_chess_puct_flushes(int32_t sims, int32_t batch_size);
 int zc_chess_puct_begin(zc_engine *eng, int32_t first_game, int32_t n_games, const zc_chess_state *d_roots,
                         int32_t sims, double c_puct, int32_t batch_size, float dirichlet_alpha, float dirichlet_eps,
-                        uint64_t seed, void *hip_stream);
+                        uint64_t seed, int32_t *d_search_no, void *hip_stream);
 int zc_chess_puct_select(zc_engine *eng, int32_t first_game, int32_t n_games, int32_t flush,
                          zc_chess_state *d_leaves, void *d_planes, int32_t planes_dtype, int32_t *d_counts,
                          void *hip_stream);
@@ -380,7 +390,7 @@ int zc_chess_puct_end(zc_engine *eng, int32_t first_game, int32_t n_games, float
  * noise, per column [n][7]. */
 int zc_c4_puct_begin(zc_engine *eng, int32_t first_game, int32_t n_games, const zc_c4_state *d_roots, int32_t sims,
                      double c_puct, int32_t batch_size, float dirichlet_alpha, float dirichlet_eps, uint64_t seed,
-                     void *hip_stream);
+                     int32_t *d_search_no, void *hip_stream);
 int zc_c4_puct_select(zc_engine *eng, int32_t first_game, int32_t n_games, int32_t flush, zc_c4_state *d_leaves,
                       void *d_planes, int32_t planes_dtype, int32_t *d_counts, void *hip_stream);
 int zc_c4_puct_backup(zc_engine *eng, int32_t first_game, int32_t n_games, int32_t flush, const double *d_values,
@@ -460,7 +470,8 @@ typedef struct zc_traj_buffers {
 #define ZC_TRAJ_NEXT 2       /* game number the next refill takes                      */
 #define ZC_TRAJ_QUOTA 3      /* games to start in total (simulate_games' total_games)  */
 #define ZC_TRAJ_FINISHED 4   /* games finished                                         */
-#define ZC_TRAJ_OVERFLOW 5   /* bit 0: pool full (games dropped); bit 1: a game longer than max_len */
+#define ZC_TRAJ_OVERFLOW 5   /* bit 0: pool full (games dropped); bit 1: a game longer than max_len;
+                              * bit 2: the quota ran out inside a multi-step record */
 #define ZC_SLOT_IDLE 3       /* result of an idle slot                                 */
 #define ZC_SLOT_SKIP 4       /* Connect4 pooled self-play: no move at this step (slot untouched) */
 /* After a move was played on every slot (d_states = positions after the move, d_moves =
@@ -474,12 +485,53 @@ typedef struct zc_traj_buffers {
  * needed; enqueued on hip_stream. */
 int zc_traj_record_async(int32_t n, const zc_traj_buffers *buf, void *d_states, const int16_t *d_moves,
                          int32_t *d_results, const int32_t *d_flags, const int32_t *d_rep, void *hip_stream);
-/* Connect4: zc_traj_record_async for `steps` consecutive steps of a self-play launch, in step
- * order — d_states / d_moves / d_results are its [steps][n] outputs.  With d_reached (device
- * int32, e.g. d_ticket + 1 of zc_c4_selfplay_pooled_async) the steps k >= *d_reached, which no
- * game reached, cost only their launches. */
+/* zc_traj_record_async for `steps` consecutive steps of a self-play launch (Connect4
+ * zc_c4_selfplay*_async, chess zc_chess_selfplay*_async), with the same pool, game numbers,
+ * labels and slot histories as `steps` single-step calls in step order — d_states / d_moves /
+ * d_results are the launch's [steps][n] outputs (results already evaluated; ZC_SLOT_SKIP = no
+ * move, only after a slot's last move).  Four launches whatever `steps` is: per slot the
+ * finished games' lengths, a scan of (games, positions) over the [steps][n] grid in step-major
+ * order (the order single steps number the games in), then one wave per slot copies its
+ * finished games to their pool places and appends its unfinished game to its history.  With
+ * d_reached (device int32, e.g. d_ticket + 1 of the pooled launches) only the steps
+ * k < *d_reached are read.  Needs the unlimited quota (a refill that would pass the quota sets
+ * ZC_TRAJ_OVERFLOW bit 2).  The launch's rows in d_states are not modified.  d_scratch: device
+ * scratch of at least zc_traj_steps_scratch_bytes(n, steps) bytes, 16-byte aligned. */
+int zc_traj_steps_scratch_bytes(int32_t n, int32_t steps, int64_t *bytes);
 int zc_traj_record_steps_async(int32_t n, const zc_traj_buffers *buf, void *d_states, const int16_t *d_moves,
-                               int32_t *d_results, int32_t steps, const int32_t *d_reached, void *hip_stream);
+                               int32_t *d_results, int32_t steps, const int32_t *d_reached, void *d_scratch,
+                               int64_t scratch_bytes, void *hip_stream);
+
+/* ---- any game backend: SURVEY §8(b)'s fallback (gen_search.hip) ----------------------
+ * mcts.get_move (mcts.cpp:102-160) for a backend the device knows nothing about: the caller
+ * keeps the game states and move objects (backend.get_legal_moves / play_move, the policy
+ * callable and value.batch are called on the host, where mcts.cpp calls them) and this
+ * library keeps the tree — N, Na, Wa, Qa, children, untried lists — and does the selection,
+ * the expansion bookkeeping and the backup on the device.  One search at a time per engine:
+ *   zc_gen_begin(sims, c, batch_size, root_moves)      Node(root, moves) (:104-108)
+ *   per simulation:
+ *     zc_gen_walk(d_out, out_cap)    select (:47-63) -> d_out = {node, #untried, #moves,
+ *                                    depth, status, untried move indices in list order...}
+ *     zc_gen_expand(untried_index, child_moves)   expand (:65-78) with the policy's pick
+ *                                    (list.index of its move among the untried ones) and
+ *                                    len(get_legal_moves(play_move(state, move))); -1 when
+ *                                    the walk ended at a node with nothing untried (the leaf
+ *                                    is that node).  The new node's id is the count of nodes
+ *                                    before it (root = 0), so the caller indexes its states.
+ *     after every batch_size leaves, and at the end: zc_gen_backup(n, d_values) with
+ *     value.batch's results in pending order (:112-127, backprop :80-100)
+ *   zc_gen_end(d_out, d_root_na, na_cap)  d_out = {best root move index (first maximum of
+ *     child N, -1 if none), status, expansions, depth sum, nodes}; root Na per move.
+ * Child move slots come from a pool the caller grows with zc_gen_reserve before an expansion
+ * would overflow it (zc_gen_capacity); zc_gen_begin reserves sims + 1 nodes.  d_values
+ * fp64; all d_ pointers are device memory; calls are stream-ordered. */
+int zc_gen_reserve(zc_engine *eng, int32_t nodes, int64_t slots);
+int zc_gen_capacity(zc_engine *eng, int32_t *nodes, int64_t *slots);
+int zc_gen_begin(zc_engine *eng, int32_t sims, double c, int32_t batch_size, int32_t root_moves, void *hip_stream);
+int zc_gen_walk(zc_engine *eng, int32_t *d_out, int32_t out_cap, void *hip_stream);
+int zc_gen_expand(zc_engine *eng, int32_t untried_index, int32_t child_moves, void *hip_stream);
+int zc_gen_backup(zc_engine *eng, int32_t n_leaves, const double *d_values, void *hip_stream);
+int zc_gen_end(zc_engine *eng, int32_t *d_out, int32_t *d_root_na, int32_t na_cap, void *hip_stream);
 
 /* ---- self-test hooks (used by the parity tests) -------------------------------------
  * UCT score exactly as the search kernel computes it (mcts.cpp:41-45), evaluated ON THE

@@ -89,3 +89,37 @@ def test_schedule_hyperparams_follows_train_py():
     assert schedule_hyperparams(200)["lr"] == 1e-5
     assert schedule_hyperparams(1, games_cap=700, sims_cap=110)["games"] == 700
     assert schedule_hyperparams(1, games_cap=700, sims_cap=110)["simulations"] == 110
+
+
+def test_any_backend_is_routed_to_the_generic_search():
+    """a backend module that is neither Connect4 nor chess is searched by the
+    any-backend path (no NotImplementedError); an object without the contract's functions
+    is refused."""
+    from zeroclone_amd.engine import _search
+    from toy_games import pile_backend, ttt_backend
+    assert _search.game_of(ttt_backend, ttt_backend.create_init_state()) == "generic"
+    assert _search.game_of(pile_backend, pile_backend.create_init_state()) == "generic"
+
+    class NoRules:
+        pass
+    with pytest.raises(TypeError):
+        _search.game_of(NoRules(), object())
+
+
+def test_any_backend_rollout_follows_the_reference(monkeypatch):
+    """Value('random_rollout') on a backend the device does not know plays the backend's own
+    rules with random.choice, as value_functions.py:35-45."""
+    import random
+    from zeroclone_amd.engine.value_functions import Value
+    from toy_games import ttt_backend as T
+    s = T.create_init_state()
+    random.seed(5)
+    got = Value("random_rollout").batch([s, T.play_move(s, 4)], backend=T)
+    random.seed(5)
+    exp = []
+    for st in (s, T.play_move(s, 4)):
+        init = st.turn
+        while not T.check_win(st) and not T.check_draw(st):
+            st = T.play_move(st, random.choice(list(T.get_legal_moves(st))))
+        exp.append((-1 if st.turn == init else 1) if T.check_win(st) else 0)
+    assert got == exp

@@ -205,6 +205,27 @@ def test_c4_puct_graph_capture_replays_the_eager_move(eng):
     mv, na = mv.clone(), na.clone()
     g = ps.capture(r, 97, fn, temperature=1.0)
     ps.na.zero_()
+    ps.search_no.zero_()   # the eager search was search 0 of every game; replay it as search 0
     g.replay()
     torch.cuda.synchronize()
     assert torch.equal(ps.na, na) and torch.equal(ps.move, mv)
+
+
+def test_c4_consecutive_searches_draw_fresh_noise(eng):
+    """Each search of a game advances its search number (on the device, so graph replays do
+    too): two consecutive searches of the same roots draw different root noise and sample at
+    a different point of the visit CDF; resetting the numbers replays the first search."""
+    from zeroclone_amd.valued import C4PuctSearch
+    n = 64
+    ps = C4PuctSearch(eng, n, 8, dirichlet_alpha=0.3, dirichlet_eps=0.25, seed=9)
+    r = _roots([POSITIONS[0]] * n)
+    out = []
+    for _ in range(2):
+        mv, na, _ = ps.run(r, 33, _hash_net, temperature=1.0)
+        out.append((ps.prior.cpu().numpy().copy(), mv.cpu().numpy().copy()))
+    assert ps.search_no.cpu().tolist() == [2] * n
+    assert all(not np.array_equal(out[0][0][i], out[1][0][i]) for i in range(n))
+    assert not np.array_equal(out[0][1], out[1][1])   # 64 temperature samples: some differ
+    ps.search_no.zero_()
+    mv, _, _ = ps.run(r, 33, _hash_net, temperature=1.0)
+    assert np.array_equal(ps.prior.cpu().numpy(), out[0][0]) and np.array_equal(mv.cpu().numpy(), out[0][1])

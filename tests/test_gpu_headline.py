@@ -1,0 +1,124 @@
+"""The headline kernel at its own shape (BASELINE configs[1], the launch bench.py times):
+C4SelfPlay(4096 games, 800 sims, batch 32) burned in to mixed game ages, then one pooled
+launch (run_pooled(3 x 4096, 6)) and one free-running launch (run(3)).  For sampled games
+every move the launch played is replayed through the oracle (oracle.get_move_mt, the
+reference's get_move restated; /root/reference engine/mcts/src/mcts.cpp:102-160 with
+value_functions.py:35-45 rollouts) from the snapshotted root and the game's MT19937 state:
+the move, the post-move position, the result (Engine._evaluate) and the RNG state after the
+launch must all be identical."""
+import numpy as np
+import pytest
+import torch
+
+import oracle
+from zeroclone_amd.selfplay import C4SelfPlay
+
+pytestmark = pytest.mark.gpu
+
+G, S, B = 4096, 800, 32
+SKIP, ONGOING = 4, 2
+
+
+def board_of(row) -> tuple[str, int]:
+    """[stones X, stones O, turn] -> (42-char board, row 0 at the top; turn)."""
+    s0, s1, t = (int(x) for x in row)
+    cells = []
+    for r in range(6):
+        for c in range(7):
+            bit = 1 << (7 * c + (5 - r))
+            cells.append("X" if s0 & bit else ("O" if s1 & bit else "."))
+    return "".join(cells), t & 1
+
+
+def oracle_mt(eng, g):
+    mt, idx = eng.get_rng_state(g)
+    o = oracle.MT(0)
+    o.s.mt[:] = [int(x) for x in mt]
+    o.s.index = idx
+    return o
+
+
+def replay(eng, snap_roots, mts, sample, states, moves, results):
+    """Replays each sampled game's moves through the oracle; returns moves checked."""
+    checked = 0
+    K = results.shape[0]
+    for g in sample:
+        b, t = board_of(snap_roots[g])
+        mt = mts[g]
+        for k in range(K):
+            r = int(results[k, g])
+            if r == SKIP:
+                assert (results[k:, g] == SKIP).all(), g   # a game's moves are a prefix of the steps
+                break
+            col, _, _ = oracle.get_move_mt(b, t, mt, S, 1.4, B)
+            assert int(moves[k, g]) == col, (g, k)
+            b, t = oracle.play(b, t, col)
+            assert board_of(states[k, g]) == (b, t), (g, k)
+            exp = t * 2 - 1 if oracle.check_win(b, t) else (0 if oracle.check_draw(b) else ONGOING)
+            assert r == exp, (g, k, r, exp)
+            if exp != ONGOING:
+                b, t = "." * 42, 0
+            checked += 1
+        mt_dev, idx_dev = eng.get_rng_state(g)
+        assert [int(x) for x in mt_dev] == list(mt.s.mt) and idx_dev == mt.s.index, g
+    return checked
+
+
+@pytest.fixture(scope="module")
+def pool():
+    sp = C4SelfPlay(G, S, batch_size=B, seed=2024, record=True)
+    burn = 0
+    while burn < 200:   # bench.py burn_in: every slot has finished a game and started another
+        sp.run(8)
+        burn += 8
+        if int(sp.traj.slot[:, 1].min().item()) >= G:
+            break
+    sp.take()
+    yield sp
+    sp.close()
+
+
+def test_pooled_launch_matches_oracle_at_headline_shape(pool):
+    sp = pool
+    sample = list(range(0, G, 16))
+    snap = sp.roots.cpu().numpy().copy()
+    mts = {g: oracle_mt(sp.eng, g) for g in sample}
+    ages = [sum(1 for c in board_of(snap[g])[0] if c != ".") for g in sample]
+    assert max(ages) - min(ages) >= 10   # mixed game ages, not the lockstep opening
+    res = sp.run_pooled(3 * G, 6).cpu().numpy()
+    states = sp._run_states.cpu().numpy()
+    moves = sp._run_moves.cpu().numpy()
+    played = (res != SKIP).sum(0)
+    assert int(played.sum()) == 3 * G
+    assert int(sp.stats[:, 5].abs().sum()) == 0
+    checked = replay(sp.eng, snap, mts, sample, states, moves, res)
+    assert checked >= 3 * len(sample) * 0.8
+    # the trajectories recorded from this launch: every finished game's moves are legal
+    # replays ending in its result, labels as Engine.get_dataset
+    b = sp.take()
+    assert b.games.shape[0] == int(((res != ONGOING) & (res != SKIP)).sum())
+
+
+def test_free_launch_matches_oracle_at_headline_shape(pool):
+    sp = pool
+    sample = list(range(7, G, 16))
+    snap = sp.roots.cpu().numpy().copy()
+    mts = {g: oracle_mt(sp.eng, g) for g in sample}
+    res = sp.run(3).cpu().numpy()
+    states = sp._run_states.cpu().numpy()
+    moves = sp._run_moves.cpu().numpy()
+    assert (res != SKIP).all()
+    assert replay(sp.eng, snap, mts, sample, states, moves, res) == 3 * len(sample)
+
+
+def test_pooled_launch_refuses_more_games_than_resident():
+    """A pooled launch hands its budget only to resident waves: a grid larger than the chip
+    holds at once is refused (the later games would never move)."""
+    probe = C4SelfPlay(8, 8, batch_size=B, record=False)
+    cap = probe.eng.c4_pooled_max_games(B)
+    probe.close()
+    assert cap >= G   # the headline shape fits
+    sp = C4SelfPlay(cap + 64, 8, batch_size=B, record=False)
+    with pytest.raises(ValueError):
+        sp.run_pooled(4 * (cap + 64), 8)
+    sp.close()

@@ -122,3 +122,16 @@ def test_puct_with_the_network_end_to_end(eng):
     g.replay()
     torch.cuda.synchronize()
     assert (ps.na.cpu().numpy().sum(axis=1) == 160).all()
+
+
+def test_consecutive_searches_draw_fresh_noise(eng):
+    """ChessPuctSearch: the per-game search number moves the root noise on every search."""
+    from zeroclone_amd.valued import ChessPuctSearch
+    n = 16
+    ps = ChessPuctSearch(eng, n, 8, dirichlet_alpha=0.3, dirichlet_eps=0.25, seed=4)
+    pri = []
+    for _ in range(2):
+        ps.run(roots_of([FENS[0]] * n), 9, hash_net)
+        pri.append(ps.prior.cpu().numpy()[:, :20].copy())
+    assert ps.search_no.cpu().tolist() == [2] * n
+    assert all(not np.array_equal(pri[0][i], pri[1][i]) for i in range(n))

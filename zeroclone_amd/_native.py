@@ -127,8 +127,11 @@ SIGNATURES = [
                                                    ctypes.c_int32, ctypes.c_double, ctypes.c_int32, ctypes.c_int32,
                                                    ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                                    ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    ("zc_c4_pooled_max_games", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, P(ctypes.c_int32)]),
+    ("zc_traj_steps_scratch_bytes", ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, P(ctypes.c_int64)]),
     ("zc_traj_record_steps_async", ctypes.c_int, [ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
-                                                  ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p]),
+                                                  ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p,
+                                                  ctypes.c_int64, ctypes.c_void_p]),
     ("zc_c4_hp_walk", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p,
                                      ctypes.c_void_p]),
     ("zc_c4_hp_expand", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
@@ -171,7 +174,7 @@ SIGNATURES = [
     ("zc_chess_puct_flushes", ctypes.c_int, [ctypes.c_int32, ctypes.c_int32]),
     ("zc_chess_puct_begin", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p,
                                            ctypes.c_int32, ctypes.c_double, ctypes.c_int32, ctypes.c_float,
-                                           ctypes.c_float, ctypes.c_uint64, ctypes.c_void_p]),
+                                           ctypes.c_float, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p]),
     ("zc_chess_puct_select", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
                                             ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p,
                                             ctypes.c_void_p]),
@@ -182,7 +185,7 @@ SIGNATURES = [
                                          ctypes.c_void_p]),
     ("zc_c4_puct_begin", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p,
                                         ctypes.c_int32, ctypes.c_double, ctypes.c_int32, ctypes.c_float,
-                                        ctypes.c_float, ctypes.c_uint64, ctypes.c_void_p]),
+                                        ctypes.c_float, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p]),
     ("zc_c4_puct_select", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
                                          ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p,
                                          ctypes.c_void_p]),
@@ -211,6 +214,14 @@ SIGNATURES = [
     ("zc_c4_from_rows", ctypes.c_int, [ctypes.c_char_p, ctypes.c_int32, P(C4State)]),
     ("zc_c4_to_rows", ctypes.c_int, [P(C4State), ctypes.c_char_p]),
     ("zc_c4_legal_order", ctypes.c_int, [ctypes.c_int32, P(ctypes.c_int32)]),
+    ("zc_gen_reserve", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64]),
+    ("zc_gen_capacity", ctypes.c_int, [ctypes.c_void_p, P(ctypes.c_int32), P(ctypes.c_int64)]),
+    ("zc_gen_begin", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_double, ctypes.c_int32, ctypes.c_int32,
+                                    ctypes.c_void_p]),
+    ("zc_gen_walk", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p]),
+    ("zc_gen_expand", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p]),
+    ("zc_gen_backup", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p]),
+    ("zc_gen_end", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p]),
     ("zc_debug_uct", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p,
                                     ctypes.c_void_p, ctypes.c_double, ctypes.c_void_p]),
     ("zc_debug_chess_tree", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
@@ -411,6 +422,37 @@ class NativeEngine:
                                                 ctypes.c_void_p(d_moves16), ctypes.c_void_p(d_results),
                                                 ctypes.c_void_p(d_stats), ctypes.c_void_p(stream or None)))
 
+    def c4_pooled_max_games(self, batch_size: int) -> int:
+        n = ctypes.c_int32(0)
+        check(lib().zc_c4_pooled_max_games(self._h, int(batch_size), ctypes.byref(n)))
+        return n.value
+
+    # ---- any game backend (zc_gen_*)
+    def gen_reserve(self, nodes: int, slots: int) -> None:
+        check(lib().zc_gen_reserve(self._h, int(nodes), int(slots)))
+
+    def gen_capacity(self):
+        n, s = ctypes.c_int32(0), ctypes.c_int64(0)
+        check(lib().zc_gen_capacity(self._h, ctypes.byref(n), ctypes.byref(s)))
+        return n.value, s.value
+
+    def gen_begin(self, sims: int, c: float, batch_size: int, root_moves: int, stream: int = 0) -> None:
+        check(lib().zc_gen_begin(self._h, int(sims), float(c), int(batch_size), int(root_moves),
+                                 ctypes.c_void_p(stream or None)))
+
+    def gen_walk(self, d_out: int, out_cap: int, stream: int = 0) -> None:
+        check(lib().zc_gen_walk(self._h, ctypes.c_void_p(d_out), int(out_cap), ctypes.c_void_p(stream or None)))
+
+    def gen_expand(self, untried_index: int, child_moves: int, stream: int = 0) -> None:
+        check(lib().zc_gen_expand(self._h, int(untried_index), int(child_moves), ctypes.c_void_p(stream or None)))
+
+    def gen_backup(self, n: int, d_values: int, stream: int = 0) -> None:
+        check(lib().zc_gen_backup(self._h, int(n), ctypes.c_void_p(d_values), ctypes.c_void_p(stream or None)))
+
+    def gen_end(self, d_out: int, d_root_na: int = 0, na_cap: int = 0, stream: int = 0) -> None:
+        check(lib().zc_gen_end(self._h, ctypes.c_void_p(d_out), ctypes.c_void_p(d_root_na or None), int(na_cap),
+                               ctypes.c_void_p(stream or None)))
+
     def c4_play_async(self, d_states: int, n: int, d_moves: int, d_results: int, reset: bool = True,
                       stream: int = 0) -> None:
         check(lib().zc_c4_play_async(self._h, n, ctypes.c_void_p(d_states), ctypes.c_void_p(d_moves),
@@ -520,10 +562,11 @@ class NativeEngine:
                                      ctypes.c_void_p(d_stats), ctypes.c_void_p(stream or None)))
 
     # ---- chess PUCT search (device pointers)
-    def chess_puct_begin(self, first_game, n, d_roots, sims, c_puct, batch_size, alpha, eps, seed, stream=0):
+    def chess_puct_begin(self, first_game, n, d_roots, sims, c_puct, batch_size, alpha, eps, seed, d_search_no=0,
+                        stream=0):
         check(lib().zc_chess_puct_begin(self._h, first_game, n, ctypes.c_void_p(d_roots), int(sims), float(c_puct),
                                         int(batch_size), float(alpha), float(eps), int(seed) & (2**64 - 1),
-                                        ctypes.c_void_p(stream or None)))
+                                        ctypes.c_void_p(d_search_no or None), ctypes.c_void_p(stream or None)))
 
     def chess_puct_select(self, first_game, n, flush, d_leaves=0, d_planes=0, planes_f16=True, d_counts=0, stream=0):
         check(lib().zc_chess_puct_select(self._h, first_game, n, int(flush), ctypes.c_void_p(d_leaves or None),
@@ -541,10 +584,11 @@ class NativeEngine:
                                       ctypes.c_void_p(d_stats), ctypes.c_void_p(stream or None)))
 
     # ---- Connect4 PUCT search (device pointers as ints)
-    def c4_puct_begin(self, first_game, n, d_roots, sims, c_puct, batch_size, alpha, eps, seed, stream=0):
+    def c4_puct_begin(self, first_game, n, d_roots, sims, c_puct, batch_size, alpha, eps, seed, d_search_no=0,
+                        stream=0):
         check(lib().zc_c4_puct_begin(self._h, first_game, n, ctypes.c_void_p(d_roots), int(sims), float(c_puct),
                                      int(batch_size), float(alpha), float(eps), int(seed) & (2**64 - 1),
-                                     ctypes.c_void_p(stream or None)))
+                                     ctypes.c_void_p(d_search_no or None), ctypes.c_void_p(stream or None)))
 
     def c4_puct_select(self, first_game, n, flush, d_leaves=0, d_planes=0, planes_f16=True, d_counts=0, stream=0):
         check(lib().zc_c4_puct_select(self._h, first_game, n, int(flush), ctypes.c_void_p(d_leaves or None),

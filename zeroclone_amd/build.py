@@ -14,7 +14,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 # ZC_LIB: load (and build) another copy of the library, e.g. a variant for an A/B timing run
 LIB = os.environ.get("ZC_LIB") or os.path.join(HERE, "libzeroclone_amd.so")
-SOURCES = ["engine.hip", "c4_search.hip", "c4_ext.hip", "chess.hip", "chess_search.hip", "chess_puct.hip", "net_conv.hip", "selfplay.hip", "c4_puct.hip"]
+SOURCES = ["engine.hip", "c4_search.hip", "c4_ext.hip", "chess.hip", "chess_search.hip", "chess_puct.hip", "net_conv.hip", "selfplay.hip", "c4_puct.hip", "gen_search.hip"]
 HEADERS = ["zc_internal.h", "c4_order_table.h", "c4_device.h", "chess_device.h", "chess_tree.h", "counter_rng.h", "puct_common.h", os.path.join("..", "..", "include", "zeroclone.h")]
 ARCH = os.environ.get("ZC_OFFLOAD_ARCH", "gfx950")
 

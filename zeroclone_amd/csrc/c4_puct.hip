@@ -258,7 +258,7 @@ __global__ __launch_bounds__(64) void c4_puct_backup_kernel(C4PuctParams p) {
                 const float sum = wave_sum_f(e);
                 float pr = e / sum;
                 if (node == 0 && p.dir_eps > 0.0f) {  // Dirichlet(alpha) noise on the root priors
-                    const float gm = valid ? gamma_draw(p.dir_alpha, key, (uint32_t)g, lane) : 0.0f;
+                    const float gm = valid ? gamma_draw(p.dir_alpha, key, (uint32_t)g, lane, search_number(p, gl)) : 0.0f;
                     const float gs = wave_sum_f(gm);
                     pr = (1.0f - p.dir_eps) * pr + p.dir_eps * (gs > 0.0f ? gm / gs : 0.0f);
                 }
@@ -307,7 +307,7 @@ __global__ __launch_bounds__(64) void c4_puct_end_kernel(C4PuctParams p) {
         } else {  // sample proportional to Na^(1/T): inverse CDF over the moves in order
             double tot = 0.0;
             for (int j = 0; j < nm; ++j) tot += pow((double)uni(R->na[j]), 1.0 / (double)p.temperature);
-            const uint4 r = philox(make_uint4((uint32_t)g, 0x5BE0CD19u, 0, 0),
+            const uint4 r = philox(make_uint4((uint32_t)g, 0x5BE0CD19u, search_number(p, gl), 0),
                                    make_uint2((uint32_t)p.seed, (uint32_t)(p.seed >> 32)));
             const double target = (double)u01(r.x) * tot;
             double run = 0.0;
@@ -322,6 +322,7 @@ __global__ __launch_bounds__(64) void c4_puct_end_kernel(C4PuctParams p) {
         }
     }
     if (lane == 0) {
+        if (p.search_no) p.search_no[gl] = (int32_t)(search_number(p, gl) + 1);
         p.out_move[gl] = best >= 0 ? (int)((ow >> (3 * best)) & 7u) : -1;
         zc_game_stats st{};
         st.status = status;

@@ -664,13 +664,12 @@ __global__ __launch_bounds__(kSearchWaves * kBlock) void c4_selfplay_kernel(Sear
         finished += r != ZC_C4_ONGOING;
         wave_mem_order();
     }
-    if (p.ticket) {  // steps this game did not reach: untouched by the trajectory replay
-        if (lane == 0) atomicMax(p.ticket + 1, mv);
-        for (int k = mv + (int)lane; k < p.moves; k += kBlock) {
-            const size_t o = (size_t)k * p.n_games + gl;
-            p.out_moves16[o] = -1;
-            p.out_results[o] = ZC_SLOT_SKIP;
-        }
+    if (p.ticket && lane == 0) atomicMax(p.ticket + 1, mv);
+    // steps this game did not reach (budget spent, or a bad root): skipped by the recording
+    for (int k = mv + (int)lane; k < p.moves; k += kBlock) {
+        const size_t o = (size_t)k * p.n_games + gl;
+        p.out_moves16[o] = -1;
+        p.out_results[o] = ZC_SLOT_SKIP;
     }
     if (lane == 0) {
         zc_game_stats st{};
@@ -819,6 +818,18 @@ void launch_c4_selfplay(const SearchParams &p, hipStream_t s) {
         hipLaunchKernelGGL((c4_selfplay_kernel<true>), grid, block, lds, s, p);
     else
         hipLaunchKernelGGL((c4_selfplay_kernel<false>), grid, block, lds, s, p);
+}
+
+int c4_selfplay_resident_games(int bs, int philox, int *out) {
+    const int wpg = c4_search_wpg(bs);
+    int blocks = 0, dev = 0, cus = 0;
+    const void *fn = philox ? (const void *)c4_selfplay_kernel<true> : (const void *)c4_selfplay_kernel<false>;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, fn, wpg * kBlock, c4_search_lds_bytes(bs)) != hipSuccess)
+        return -1;
+    if (hipGetDevice(&dev) != hipSuccess) return -1;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return -1;
+    *out = blocks * cus * wpg;
+    return 0;
 }
 
 void launch_c4_rollout_debug(const Arena &a, int M, int first_game, int n, const zc_c4_state *states,

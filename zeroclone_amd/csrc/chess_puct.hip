@@ -250,7 +250,7 @@ __global__ __launch_bounds__(64) void puct_backup_kernel(ChessParams p) {
 #pragma unroll
                     for (int q = 0; q < 4; ++q) {
                         const int k = q * 64 + (int)lane;
-                        gm[q] = k < nm ? gamma_draw(p.dir_alpha, key, (uint32_t)g, (uint32_t)k) : 0.0f;
+                        gm[q] = k < nm ? gamma_draw(p.dir_alpha, key, (uint32_t)g, (uint32_t)k, search_number(p, gl)) : 0.0f;
                         gs += gm[q];
                     }
                     gs = wave_sum_f(gs);
@@ -318,7 +318,7 @@ __global__ __launch_bounds__(64) void puct_end_kernel(ChessParams p) {
                 tot += j < nm ? pow((double)t.na[base + j], 1.0 / (double)p.temperature) : 0.0;
             }
             tot = wave_sum_d(tot);
-            const uint4 r = philox(make_uint4((uint32_t)g, 0x5BE0CD19u, 0, 0),
+            const uint4 r = philox(make_uint4((uint32_t)g, 0x5BE0CD19u, search_number(p, gl), 0),
                                    make_uint2((uint32_t)p.seed, (uint32_t)(p.seed >> 32)));
             const double target = (double)u01(r.x) * tot;
             double run = 0.0;
@@ -333,6 +333,7 @@ __global__ __launch_bounds__(64) void puct_end_kernel(ChessParams p) {
         }
     }
     if (lane == 0) {
+        if (p.search_no) p.search_no[gl] = (int32_t)(search_number(p, gl) + 1);
         p.out_move[gl] = (best >= 0 && !status) ? t.mv[base + best] : (uint16_t)0xFFFF;
         zc_game_stats st{};
         st.status = status;

@@ -508,6 +508,10 @@ __global__ __launch_bounds__(64) void chess_hp_expand_kernel(ChessParams p) {
             if (lane == 0) ctl[cStatus] = ZC_STATUS_INTERNAL;
             return;
         }
+        if (nnodes >= p.M) {  // out of tree capacity: reported before the node is changed
+            if (lane == 0) ctl[cStatus] = ZC_STATUS_CAPACITY;
+            return;
+        }
         // expand (mcts.cpp:65-78) with the caller's pick: untried.erase(begin + local)
         const uint32_t base = uni(N->base);
         const int midx = uni((int)t.ut[base + local]);
@@ -525,10 +529,6 @@ __global__ __launch_bounds__(64) void chess_hp_expand_kernel(ChessParams p) {
         if (lane == 0) chessdev::apply_move(L.st, m);
         wave_sync_mem();
         const int child = nnodes++;
-        if (child >= p.M) {
-            if (lane == 0) ctl[cStatus] = ZC_STATUS_INTERNAL;
-            return;
-        }
         create_node(t, L, child, node, midx, depth + 1, slots, status);
         ++depth;
         if (lane == 0) {

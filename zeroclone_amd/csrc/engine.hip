@@ -69,6 +69,14 @@ void free_chess(zc::ChessArena &c) {
     c = zc::ChessArena{};
 }
 
+void free_gen(zc_engine *e) {
+    zc::GenArena &g = e->ga;
+    void *ptrs[] = {g.nodes, g.na, g.wa, g.qa, g.child, g.untried, g.ctl, g.pending};
+    for (void *p : ptrs)
+        if (p) (void)hipFree(p);
+    g = zc::GenArena{};
+}
+
 void free_arena(zc::Arena &a) {
     void *ptrs[] = {a.nodes, a.ring,  a.rngpos, a.logtab,  a.phase,    a.roots,    a.move,
                     a.na,    a.ids,   a.stats, a.ext_ctl, a.ext_paths, a.ext_meta, a.ext_roots};
@@ -233,6 +241,7 @@ int zc_engine_destroy(zc_engine *eng) {
         (void)hipStreamSynchronize(eng->stream);
         free_arena(eng->a);
         free_chess(eng->ca);
+        free_gen(eng);
         void *c4p[] = {eng->c4p_nodes, eng->c4p_ctl, eng->c4p_paths, eng->c4p_meta};
         for (void *q : c4p)
             if (q) (void)hipFree(q);
@@ -340,6 +349,14 @@ int zc_c4_selfplay_pooled_async(zc_engine *eng, int32_t first, int32_t n, zc_c4_
     if (!n) return ZC_OK;
     std::lock_guard<std::mutex> lk(eng->mu);
     ZC_HIP(hipSetDevice(eng->cfg.device));
+    // A wave takes its tickets only once resident: with more games than the chip holds at
+    // once, the first waves could spend the whole budget and the rest never move.  Refused.
+    int resident = 0;
+    if (zc::c4_selfplay_resident_games(bs, eng->rollout_mode == ZC_ROLLOUT_PHILOX, &resident))
+        return fail(ZC_EHIP, "occupancy query failed");
+    if (n > resident)
+        return fail(ZC_EINVAL, "pooled self-play of %d games: at most %d (batch %d) are resident at once, and "
+                    "the rest would never move; use zc_c4_selfplay_async or fewer games per launch", n, resident, bs);
     hipStream_t s = (hipStream_t)hip_stream;
     ZC_HIP(hipMemsetAsync(d_ticket, 0, 2 * sizeof(int32_t), s));
     zc::SearchParams p = make_params(eng, first, n, d_roots, sims, c, bs, nullptr, nullptr, d_stats);
@@ -352,6 +369,18 @@ int zc_c4_selfplay_pooled_async(zc_engine *eng, int32_t first, int32_t n, zc_c4_
     p.budget = (int32_t)budget;
     zc::launch_c4_selfplay(p, s);
     ZC_HIP(hipGetLastError());
+    return ZC_OK;
+}
+
+int zc_c4_pooled_max_games(zc_engine *eng, int32_t batch_size, int32_t *out) {
+    if (!eng || !out) return fail(ZC_EINVAL, "null argument");
+    if (batch_size < 1 || batch_size > eng->cfg.max_batch) return fail(ZC_EINVAL, "bad batch_size %d", batch_size);
+    std::lock_guard<std::mutex> lk(eng->mu);
+    ZC_HIP(hipSetDevice(eng->cfg.device));
+    int r = 0;
+    if (zc::c4_selfplay_resident_games(batch_size, eng->rollout_mode == ZC_ROLLOUT_PHILOX, &r))
+        return fail(ZC_EHIP, "occupancy query failed");
+    *out = r;
     return ZC_OK;
 }
 
@@ -649,16 +678,25 @@ int check_traj(int32_t n, const zc_traj_buffers *buf, const void *d_states) {
 }
 }  // namespace
 
+int zc_traj_steps_scratch_bytes(int32_t n, int32_t steps, int64_t *bytes) {
+    if (n < 0 || steps < 0 || !bytes) return fail(ZC_EINVAL, "bad argument");
+    *bytes = (int64_t)zc::traj_steps_scratch_bytes(n, steps);
+    return ZC_OK;
+}
+
 int zc_traj_record_steps_async(int32_t n, const zc_traj_buffers *buf, void *d_states, const int16_t *d_moves,
-                               int32_t *d_results, int32_t steps, const int32_t *d_reached, void *hip_stream) {
+                               int32_t *d_results, int32_t steps, const int32_t *d_reached, void *d_scratch,
+                               int64_t scratch_bytes, void *hip_stream) {
     if (int r = check_traj(n, buf, d_states)) return r;
     if (steps < 0) return fail(ZC_EINVAL, "steps must be >= 0 (got %d)", steps);
+    if ((int64_t)n * steps >= ((int64_t)1 << 31)) return fail(ZC_EINVAL, "n x steps must be < 2^31");
     if (n && steps && (!d_states || !d_moves || !d_results)) return fail(ZC_EINVAL, "bad argument");
-    if (!n) return ZC_OK;
-    const size_t row = (size_t)buf->row_bytes;
-    for (int k = 0; k < steps; ++k)
-        zc::launch_traj_record(n, *buf, (uint8_t *)d_states + (size_t)k * n * row, d_moves + (size_t)k * n,
-                               d_results + (size_t)k * n, nullptr, nullptr, (hipStream_t)hip_stream, d_reached, k);
+    if (!n || !steps) return ZC_OK;
+    if (!d_scratch || ((uintptr_t)d_scratch & 15) || scratch_bytes < (int64_t)zc::traj_steps_scratch_bytes(n, steps))
+        return fail(ZC_EINVAL, "scratch: %lld bytes at %p, need %zu bytes 16-byte aligned", (long long)scratch_bytes,
+                    d_scratch, zc::traj_steps_scratch_bytes(n, steps));
+    zc::launch_traj_record_steps(n, steps, *buf, d_states, d_moves, d_results, d_reached, d_scratch,
+                                 (hipStream_t)hip_stream);
     ZC_HIP(hipGetLastError());
     return ZC_OK;
 }
@@ -919,6 +957,7 @@ zc::ChessParams puct_params(zc_engine *e, int32_t first, int32_t n) {
     p.dir_alpha = e->px_alpha;
     p.dir_eps = e->px_eps;
     p.seed = e->px_seed;
+    p.search_no = e->px_search_no;
     return p;
 }
 int check_px(zc_engine *e, int32_t first, int32_t n, int32_t flush, bool need_flush) {
@@ -934,7 +973,8 @@ int check_px(zc_engine *e, int32_t first, int32_t n, int32_t flush, bool need_fl
 extern "C" {
 
 int zc_chess_puct_begin(zc_engine *eng, int32_t first, int32_t n, const zc_chess_state *d_roots, int32_t sims,
-                        double c_puct, int32_t bs, float alpha, float eps, uint64_t seed, void *hip_stream) {
+                        double c_puct, int32_t bs, float alpha, float eps, uint64_t seed, int32_t *d_search_no,
+                        void *hip_stream) {
     if (!eng || (n && !d_roots)) return fail(ZC_EINVAL, "null argument");
     if (int r = check_search(eng, first, n, sims, c_puct, bs)) return r;
     if (sims < 2) return fail(ZC_EINVAL, "PUCT search needs sims >= 2 (flush 0 evaluates the root)");
@@ -950,6 +990,7 @@ int zc_chess_puct_begin(zc_engine *eng, int32_t first, int32_t n, const zc_chess
     eng->px_alpha = alpha;
     eng->px_eps = eps;
     eng->px_seed = seed;
+    eng->px_search_no = d_search_no;
     eng->px_active = true;
     if (!n) return ZC_OK;
     zc::ChessParams p = puct_params(eng, first, n);
@@ -1054,6 +1095,7 @@ zc::C4PuctParams c4p_params(zc_engine *e, int32_t first, int32_t n) {
     p.dir_alpha = e->qx_alpha;
     p.dir_eps = e->qx_eps;
     p.seed = e->qx_seed;
+    p.search_no = e->qx_search_no;
     return p;
 }
 int check_qx(zc_engine *e, int32_t first, int32_t n, int32_t flush, bool need_flush) {
@@ -1069,7 +1111,8 @@ int check_qx(zc_engine *e, int32_t first, int32_t n, int32_t flush, bool need_fl
 extern "C" {
 
 int zc_c4_puct_begin(zc_engine *eng, int32_t first, int32_t n, const zc_c4_state *d_roots, int32_t sims,
-                     double c_puct, int32_t bs, float alpha, float eps, uint64_t seed, void *hip_stream) {
+                     double c_puct, int32_t bs, float alpha, float eps, uint64_t seed, int32_t *d_search_no,
+                     void *hip_stream) {
     if (!eng || (n && !d_roots)) return fail(ZC_EINVAL, "null argument");
     if (int r = check_search(eng, first, n, sims, c_puct, bs)) return r;
     if (sims < 2) return fail(ZC_EINVAL, "PUCT search needs sims >= 2 (flush 0 evaluates the root)");
@@ -1085,6 +1128,7 @@ int zc_c4_puct_begin(zc_engine *eng, int32_t first, int32_t n, const zc_c4_state
     eng->qx_alpha = alpha;
     eng->qx_eps = eps;
     eng->qx_seed = seed;
+    eng->qx_search_no = d_search_no;
     eng->qx_active = true;
     if (!n) return ZC_OK;
     zc::C4PuctParams p = c4p_params(eng, first, n);
@@ -1402,6 +1446,154 @@ int zc_debug_phase_cycles(zc_engine *eng, int32_t enable, int64_t *out8) {
     }
     ZC_HIP(hipMemset(eng->a.phase, 0, G * K * sizeof(int64_t)));
     eng->stamp = enable ? 1 : 0;
+    return ZC_OK;
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------- any game backend (gen_search.hip)
+namespace {
+size_t gen_slot_bytes() { return sizeof(int32_t) * 3 + sizeof(double) * 2; }  // na, child, untried, wa, qa
+
+// Grow the any-backend tree to hold `nodes` nodes and `slots` move slots, keeping its
+// content (the device is synchronised first: a search may be in flight).
+int gen_reserve_locked(zc_engine *e, int64_t nodes, int64_t slots) {
+    zc::GenArena &g = e->ga;
+    if (!g.ctl) {
+        if (hipMalloc((void **)&g.ctl, zc::kGenCtlWords * sizeof(int32_t)) != hipSuccess ||
+            hipMalloc((void **)&g.pending, (size_t)e->cfg.max_batch * sizeof(int32_t)) != hipSuccess)
+            return fail(ZC_ENOMEM, "hipMalloc failed (any-backend tree control)");
+        if (hipMemset(g.ctl, 0, zc::kGenCtlWords * sizeof(int32_t)) != hipSuccess) return fail(ZC_EHIP, "memset failed");
+        e->bytes += zc::kGenCtlWords * sizeof(int32_t) + (size_t)e->cfg.max_batch * sizeof(int32_t);
+    }
+    if (nodes <= g.node_cap && slots <= g.slot_cap) return ZC_OK;
+    if (nodes > INT32_MAX || slots > INT32_MAX) return fail(ZC_ECAPACITY, "any-backend tree beyond 2^31 nodes or slots");
+    const int64_t nn = std::max<int64_t>(nodes, g.node_cap), ns = std::max<int64_t>(slots, g.slot_cap);
+    zc::GenArena n = g;
+    bool ok = hipMalloc((void **)&n.nodes, (size_t)nn * sizeof(zc::GenNode)) == hipSuccess;
+    ok = ok && hipMalloc((void **)&n.na, (size_t)ns * sizeof(int32_t)) == hipSuccess;
+    ok = ok && hipMalloc((void **)&n.wa, (size_t)ns * sizeof(double)) == hipSuccess;
+    ok = ok && hipMalloc((void **)&n.qa, (size_t)ns * sizeof(double)) == hipSuccess;
+    ok = ok && hipMalloc((void **)&n.child, (size_t)ns * sizeof(int32_t)) == hipSuccess;
+    ok = ok && hipMalloc((void **)&n.untried, (size_t)ns * sizeof(int32_t)) == hipSuccess;
+    if (!ok) {
+        void *ptrs[] = {n.nodes, n.na, n.wa, n.qa, n.child, n.untried};
+        for (void *p : ptrs)
+            if (p && p != g.nodes && p != g.na && p != g.wa && p != g.qa && p != g.child && p != g.untried)
+                (void)hipFree(p);
+        return fail(ZC_ENOMEM, "hipMalloc failed (any-backend tree of %lld nodes, %lld slots)", (long long)nn,
+                    (long long)ns);
+    }
+    ZC_HIP(hipDeviceSynchronize());
+    if (g.node_cap) {
+        const size_t on = (size_t)g.node_cap, os = (size_t)g.slot_cap;
+        ZC_HIP(hipMemcpy(n.nodes, g.nodes, on * sizeof(zc::GenNode), hipMemcpyDeviceToDevice));
+        ZC_HIP(hipMemcpy(n.na, g.na, os * sizeof(int32_t), hipMemcpyDeviceToDevice));
+        ZC_HIP(hipMemcpy(n.wa, g.wa, os * sizeof(double), hipMemcpyDeviceToDevice));
+        ZC_HIP(hipMemcpy(n.qa, g.qa, os * sizeof(double), hipMemcpyDeviceToDevice));
+        ZC_HIP(hipMemcpy(n.child, g.child, os * sizeof(int32_t), hipMemcpyDeviceToDevice));
+        ZC_HIP(hipMemcpy(n.untried, g.untried, os * sizeof(int32_t), hipMemcpyDeviceToDevice));
+        void *old[] = {g.nodes, g.na, g.wa, g.qa, g.child, g.untried};
+        for (void *p : old) (void)hipFree(p);
+    }
+    e->bytes += (nn - g.node_cap) * (int64_t)sizeof(zc::GenNode) + (ns - g.slot_cap) * (int64_t)gen_slot_bytes();
+    n.node_cap = (int32_t)nn;
+    n.slot_cap = ns;
+    g = n;
+    return ZC_OK;
+}
+
+zc::GenParams gen_params(const zc_engine *e) {
+    zc::GenParams p{};
+    p.sims = e->gx_sims;
+    p.bs = e->gx_bs;
+    p.c = e->gx_c;
+    p.logtab = e->a.logtab;
+    p.a = e->ga;
+    return p;
+}
+
+int check_gx(const zc_engine *e) {
+    if (!e->gx_active) return fail(ZC_EINVAL, "no any-backend search in progress (call zc_gen_begin first)");
+    return ZC_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int zc_gen_reserve(zc_engine *eng, int32_t nodes, int64_t slots) {
+    if (!eng) return fail(ZC_EINVAL, "null argument");
+    if (nodes < 1 || slots < 0) return fail(ZC_EINVAL, "need nodes >= 1 and slots >= 0");
+    std::lock_guard<std::mutex> lk(eng->mu);
+    ZC_HIP(hipSetDevice(eng->cfg.device));
+    return gen_reserve_locked(eng, nodes, slots);
+}
+
+int zc_gen_capacity(zc_engine *eng, int32_t *nodes, int64_t *slots) {
+    if (!eng || !nodes || !slots) return fail(ZC_EINVAL, "null argument");
+    std::lock_guard<std::mutex> lk(eng->mu);
+    *nodes = eng->ga.node_cap;
+    *slots = eng->ga.slot_cap;
+    return ZC_OK;
+}
+
+int zc_gen_begin(zc_engine *eng, int32_t sims, double c, int32_t bs, int32_t root_moves, void *hip_stream) {
+    if (!eng) return fail(ZC_EINVAL, "null argument");
+    if (int r = check_search(eng, 0, 0, sims, c, bs)) return r;
+    if (root_moves < 0) return fail(ZC_EINVAL, "root_moves must be >= 0");
+    std::lock_guard<std::mutex> lk(eng->mu);
+    ZC_HIP(hipSetDevice(eng->cfg.device));
+    if (int r = gen_reserve_locked(eng, (int64_t)sims + 1, std::max<int64_t>(root_moves, eng->ga.slot_cap))) return r;
+    eng->gx_sims = sims;
+    eng->gx_bs = bs;
+    eng->gx_c = c;
+    eng->gx_active = true;
+    zc::launch_gen_begin(gen_params(eng), root_moves, (hipStream_t)hip_stream);
+    ZC_HIP(hipGetLastError());
+    return ZC_OK;
+}
+
+int zc_gen_walk(zc_engine *eng, int32_t *d_out, int32_t out_cap, void *hip_stream) {
+    if (!eng || !d_out) return fail(ZC_EINVAL, "null argument");
+    if (out_cap < 5) return fail(ZC_EINVAL, "out_cap must be >= 5");
+    std::lock_guard<std::mutex> lk(eng->mu);
+    if (int r = check_gx(eng)) return r;
+    ZC_HIP(hipSetDevice(eng->cfg.device));
+    zc::launch_gen_walk(gen_params(eng), d_out, out_cap, (hipStream_t)hip_stream);
+    ZC_HIP(hipGetLastError());
+    return ZC_OK;
+}
+
+int zc_gen_expand(zc_engine *eng, int32_t untried_index, int32_t child_moves, void *hip_stream) {
+    if (!eng) return fail(ZC_EINVAL, "null argument");
+    if (untried_index < -1 || child_moves < 0) return fail(ZC_EINVAL, "bad untried_index / child_moves");
+    std::lock_guard<std::mutex> lk(eng->mu);
+    if (int r = check_gx(eng)) return r;
+    ZC_HIP(hipSetDevice(eng->cfg.device));
+    zc::launch_gen_expand(gen_params(eng), untried_index, child_moves, (hipStream_t)hip_stream);
+    ZC_HIP(hipGetLastError());
+    return ZC_OK;
+}
+
+int zc_gen_backup(zc_engine *eng, int32_t n_leaves, const double *d_values, void *hip_stream) {
+    if (!eng || (n_leaves && !d_values)) return fail(ZC_EINVAL, "null argument");
+    std::lock_guard<std::mutex> lk(eng->mu);
+    if (int r = check_gx(eng)) return r;
+    if (n_leaves < 0 || n_leaves > eng->gx_bs) return fail(ZC_EINVAL, "n_leaves %d outside [0, batch_size]", n_leaves);
+    ZC_HIP(hipSetDevice(eng->cfg.device));
+    zc::launch_gen_backup(gen_params(eng), n_leaves, d_values, (hipStream_t)hip_stream);
+    ZC_HIP(hipGetLastError());
+    return ZC_OK;
+}
+
+int zc_gen_end(zc_engine *eng, int32_t *d_out, int32_t *d_root_na, int32_t na_cap, void *hip_stream) {
+    if (!eng || !d_out) return fail(ZC_EINVAL, "null argument");
+    std::lock_guard<std::mutex> lk(eng->mu);
+    if (int r = check_gx(eng)) return r;
+    ZC_HIP(hipSetDevice(eng->cfg.device));
+    zc::launch_gen_end(gen_params(eng), d_out, d_root_na, d_root_na ? na_cap : 0, (hipStream_t)hip_stream);
+    ZC_HIP(hipGetLastError());
+    eng->gx_active = false;
     return ZC_OK;
 }
 

@@ -176,6 +176,7 @@ struct ChessParams {
     // PUCT search (chess_puct.hip)
     float dir_alpha, dir_eps;   // Dirichlet root noise
     uint64_t seed;              // counter-based RNG key (noise, temperature sampling)
+    int32_t *search_no;         // [n] per-game search number (counter word; end adds 1), or null
     float temperature;          // end: 0 = most visits, > 0 = sample proportional to Na^(1/T)
     const void *logits;         // backup: [n*bs][4096] policy logits (from*64 + to)
     int logits_f16;
@@ -222,6 +223,7 @@ struct C4PuctParams {
     int logits_f16;
     float dir_alpha, dir_eps;
     uint64_t seed;
+    int32_t *search_no;       // [n] per-game search number (counter word; end adds 1), or null
     float temperature;
     int32_t *out_move;        // column
     int32_t *out_na;          // [n][7] visits per column
@@ -232,6 +234,45 @@ void launch_c4_puct_begin(const C4PuctParams &p, hipStream_t s);
 void launch_c4_puct_select(const C4PuctParams &p, hipStream_t s);
 void launch_c4_puct_backup(const C4PuctParams &p, hipStream_t s);
 void launch_c4_puct_end(const C4PuctParams &p, hipStream_t s);
+
+// ---------------------------------------------------------------- any game backend
+// (gen_search.hip; SURVEY §8(b)'s fallback).  The tree of one search; the game states and
+// move objects stay with the caller (Python objects of an arbitrary backend).
+struct GenNode {
+    int32_t base;     // first slot of the node's moves
+    int32_t nmoves;   // Node::moves.size()
+    int32_t nu;       // Node::untried.size()
+    int32_t parent;   // -1 at the root
+    int32_t pact;     // parent_action_idx
+    int32_t n;        // Node::N
+    int32_t depth;
+    int32_t pad;
+};
+enum : int { kGenNodes = 0, kGenSlots = 1, kGenPending = 2, kGenWalked = 3, kGenStatus = 4, kGenExp = 5,
+             kGenDepth = 6, kGenCtlWords = 8 };
+struct GenArena {
+    GenNode *nodes = nullptr;    // [node_cap]
+    int32_t *na = nullptr;       // [slot_cap] Na
+    double *wa = nullptr;        // [slot_cap] Wa
+    double *qa = nullptr;        // [slot_cap] Qa
+    int32_t *child = nullptr;    // [slot_cap] child node, -1 = null
+    int32_t *untried = nullptr;  // [slot_cap] untried move indices of the slot range's node
+    int32_t *ctl = nullptr;      // [kGenCtlWords]
+    int32_t *pending = nullptr;  // [max_batch] the pending flush's leaves
+    int32_t node_cap = 0;
+    int64_t slot_cap = 0;
+};
+struct GenParams {
+    int sims, bs;
+    double c;
+    const double *logtab;
+    GenArena a;
+};
+void launch_gen_begin(const GenParams &p, int root_moves, hipStream_t s);
+void launch_gen_walk(const GenParams &p, int32_t *out, int out_cap, hipStream_t s);
+void launch_gen_expand(const GenParams &p, int local, int child_moves, hipStream_t s);
+void launch_gen_backup(const GenParams &p, int nb, const double *values, hipStream_t s);
+void launch_gen_end(const GenParams &p, int32_t *out, int32_t *root_na, int na_cap, hipStream_t s);
 
 void launch_chess_search(const ChessParams &p, hipStream_t s);     // crude_chess_score, whole move
 void launch_chess_ext_begin(const ChessParams &p, hipStream_t s);
@@ -271,6 +312,7 @@ void launch_c4_hp_walk(const ExtParams &p, hipStream_t s);
 void launch_c4_hp_expand(const ExtParams &p, hipStream_t s);
 void launch_c4_search(const SearchParams &p, hipStream_t s);
 void launch_c4_selfplay(const SearchParams &p, hipStream_t s);
+int c4_selfplay_resident_games(int bs, int philox, int *out);  // games the self-play grid keeps resident
 void launch_c4_rollout_debug(const Arena &a, int M, int first_game, int n, const zc_c4_state *states,
                              int32_t *out_value, int64_t *out_words, hipStream_t s);
 void launch_c4_rollout_seq(const Arena &a, int game, int n, const zc_c4_state *states, int32_t *out_value,
@@ -279,8 +321,10 @@ void launch_c4_play(int n, zc_c4_state *states, const int32_t *moves, int32_t *r
 enum : int { kTrajPositions = ZC_TRAJ_POSITIONS, kTrajGames = ZC_TRAJ_GAMES, kTrajNext = ZC_TRAJ_NEXT,
              kTrajQuota = ZC_TRAJ_QUOTA, kTrajFinished = ZC_TRAJ_FINISHED, kTrajOverflow = ZC_TRAJ_OVERFLOW };
 void launch_traj_record(int n, const zc_traj_buffers &b, void *states, const int16_t *moves, int32_t *results,
-                        const int32_t *flags, const int32_t *rep, hipStream_t s, const int32_t *reached = nullptr,
-                        int step = 0);
+                        const int32_t *flags, const int32_t *rep, hipStream_t s);
+size_t traj_steps_scratch_bytes(int n, int K);
+void launch_traj_record_steps(int n, int K, const zc_traj_buffers &b, const void *states, const int16_t *moves,
+                              const int32_t *results, const int32_t *reached, void *scratch, hipStream_t s);
 void launch_uct_debug(int n, const double *logn, const int32_t *na, const double *q, double c, double *out,
                       hipStream_t s);
 
@@ -304,17 +348,24 @@ struct zc_engine {
     double qx_c = 0;
     float qx_alpha = 0, qx_eps = 0;
     uint64_t qx_seed = 0;
+    int32_t *qx_search_no = nullptr;
     bool qx_active = false;
     // the chess PUCT search in progress
     int px_first = 0, px_n = 0, px_sims = 0, px_bs = 0;
     double px_c = 0;
     float px_alpha = 0, px_eps = 0;
     uint64_t px_seed = 0;
+    int32_t *px_search_no = nullptr;
     bool px_active = false;
     // the chess stepwise search in progress
     int cx_first = 0, cx_n = 0, cx_sims = 0, cx_bs = 0, cx_policy = 0;
     double cx_c = 0, cx_freedom = 0;
     bool cx_active = false;
+    // the any-backend search (zc_gen_*): its tree and the search in progress
+    zc::GenArena ga;
+    int gx_sims = 0, gx_bs = 0;
+    double gx_c = 0;
+    bool gx_active = false;
     // the stepwise search in progress (zc_c4_ext_begin .. end)
     int ext_first = 0, ext_n = 0, ext_sims = 0, ext_bs = 0, ext_flushes_done = 0;
     double ext_c = 0;

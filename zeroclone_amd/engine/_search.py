@@ -15,6 +15,10 @@ Any other policy callable (SURVEY §8(b)'s fallback) runs the search in host-pol
 tree stays on the device and every expansion calls policy(untried_moves) on the host, where
 mcts.cpp:65-78 calls it (zc_c4_hp_* / zc_chess_hp_*: `c4_host_policy_moves`,
 `chess_host_policy_moves`).
+
+Any other game backend (a module with the six functions of engine/README.md:17-24) runs
+`generic_moves`: the tree on the device (zc_gen_*), the backend, policy and value -- Python
+objects the device cannot run -- called on the host exactly where mcts.cpp calls them.
 """
 from __future__ import annotations
 
@@ -37,7 +41,10 @@ def game_of(backend, state) -> str:
     from .games.connect4 import c4_backend as c4
     if c4.is_state(state):
         return "connect4"
-    raise NotImplementedError(f"backend {name!r}: only Connect4 and chess run on the MI355X search path")
+    for fn in ("get_legal_moves", "play_move"):
+        if not callable(getattr(backend, fn, None)):
+            raise TypeError(f"backend {name!r} has no {fn}() (the plugin contract, engine/README.md:17-24)")
+    return "generic"
 
 
 HOST_POLICY = -1   # any other callable: called on the host at each expansion
@@ -259,3 +266,76 @@ def chess_host_policy_moves(eng, ids, states, sims, c, bs, value, policy, backen
         m = int(mv[0].item()) & 0xFFFF
         out.append(None if m == 0xFFFF else _native.unpack_chess_move(m))
     return out
+
+
+def generic_moves(eng, state, sims, c, bs, value, policy, backend):
+    """mcts.get_move (mcts.cpp:102-160) for ANY backend: the tree lives on the
+    device (zc_gen_*: UCT selection, the expansion bookkeeping, the fp64 pending-order
+    backup); the states and moves are the backend's Python objects, kept here by node id.
+    Per simulation, in the reference's order: the device walk (select, :47-63); if the node
+    has untried moves, policy(untried moves in list order), list.index of its pick, the
+    backend's play_move and get_legal_moves (expand, :65-78), then the device expansion;
+    every batch_size leaves value.batch(states, backend=backend) (:112-127) and the device
+    backup.  Returns root_moves[first child with the most visits] (:150-157)."""
+    import torch
+    dev = torch.device("cuda", eng.device)
+    stream = torch.cuda.current_stream(dev)
+    s = stream.cuda_stream
+    root_moves = list(backend.get_legal_moves(state))
+    states, moves = [state], [root_moves]
+    eng.gen_begin(sims, c, bs, len(root_moves), s)
+    n_cap, s_cap = eng.gen_capacity()
+    slots = len(root_moves)
+    out = torch.zeros(5 + max(64, slots), dtype=torch.int32, device=dev)
+    vals = torch.zeros(bs, dtype=torch.float64, device=dev)
+    pending = []
+
+    def flush():
+        if not pending:
+            return
+        v = value.batch(list(pending), backend=backend)
+        v = [float(v[i]) for i in range(len(pending))]
+        vals[:len(v)].copy_(torch.tensor(v, dtype=torch.float64))
+        eng.gen_backup(len(v), vals.data_ptr(), s)
+        pending.clear()
+
+    for _ in range(sims):
+        eng.gen_walk(out.data_ptr(), out.numel(), s)
+        o = out.cpu().numpy()
+        if o[4]:
+            raise RuntimeError(f"any-backend search failed on the device (status {int(o[4])})")
+        node, nu = int(o[0]), int(o[1])
+        if nu and 5 + nu > out.numel():   # a longer untried list than the buffer: walk again (no side effects)
+            out = torch.zeros(5 + nu, dtype=torch.int32, device=dev)
+            eng.gen_walk(out.data_ptr(), out.numel(), s)
+            o = out.cpu().numpy()
+        if nu:
+            untried = [moves[node][int(k)] for k in o[5:5 + nu]]
+            action = policy(untried)
+            local = untried.index(action)
+            new_state = backend.play_move(states[node], action)
+            new_moves = list(backend.get_legal_moves(new_state))
+            if slots + len(new_moves) > s_cap:
+                eng.gen_reserve(n_cap, max(2 * s_cap, slots + len(new_moves), 1024))
+                n_cap, s_cap = eng.gen_capacity()
+            eng.gen_expand(local, len(new_moves), s)
+            slots += len(new_moves)
+            states.append(new_state)
+            moves.append(new_moves)
+            pending.append(new_state)
+        else:
+            eng.gen_expand(-1, 0, s)
+            pending.append(states[node])
+        if len(pending) >= bs:
+            flush()
+    flush()
+    res = torch.zeros(5, dtype=torch.int32, device=dev)
+    eng.gen_end(res.data_ptr(), 0, 0, s)
+    r = res.cpu().numpy()
+    if r[1]:
+        raise RuntimeError(f"any-backend search failed on the device (status {int(r[1])})")
+    if int(r[4]) != len(states):
+        raise RuntimeError("any-backend search: device and host trees disagree")
+    if r[0] < 0:
+        raise ValueError("root has no legal move (the reference indexes moves[-1] here)")
+    return root_moves[int(r[0])]

@@ -17,8 +17,12 @@ object: Value('random_rollout') (Connect4) and Value('crude_chess_score') (chess
 the search kernel, network values run on the device between the select and backup kernels,
 and any other object's value.batch(states, backend=backend) is called on the host once per
 flush, exactly where the reference calls it (mcts.cpp:116).  Such a value function must not
-draw from `random` (the reference's network and crude-score values do not).  Anything else
-raises NotImplementedError: there is no CPU search.
+draw from `random` (the reference's network and crude-score values do not).
+
+Any other game backend (the six functions of engine/README.md:17-24) searches with the tree
+on the device (zc_gen_*) and the backend, policy and value called on the host, in the
+reference's order, drawing from Python's `random` themselves (_search.generic_moves).
+There is no CPU search.
 """
 from __future__ import annotations
 
@@ -31,6 +35,8 @@ def _plugin_check(state, value, policy, backend):
     game = _search.game_of(backend, state)
     _search.policy_of(policy)
     kind = _search.value_kind(value)
+    if game == "generic":
+        return game
     if game == "connect4" and kind == "crude":
         raise NotImplementedError("crude_chess_score is a chess value function")
     if game == "chess" and kind == "rollout":
@@ -45,6 +51,10 @@ def get_move(state, value, policy, backend, simulations=1000, c=1.4, batch_size=
     if batch_size < 1:
         raise ValueError("batch_size must be >= 1")
     ge = _device.scratch(simulations, batch_size)
+    if game == "generic":   # any backend: the tree on the device, the plugins on the host
+        with ge.lock:
+            eng = ge.ensure(1, simulations, batch_size)
+            return _search.generic_moves(eng, state, simulations, c, batch_size, value, policy, backend)
     if _search.policy_of(policy)[0] == _search.HOST_POLICY:
         with ge.lock:
             eng = ge.ensure(1, simulations, batch_size)

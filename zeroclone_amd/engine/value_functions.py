@@ -48,7 +48,10 @@ class Value:
     # ---------------------------------------------------------------- random_rollout
     def random_rollout(self, states, backend):
         if getattr(backend, "ZC_GAME", None) != "connect4" and not _looks_like_c4(backend, states):
-            raise NotImplementedError("random_rollout is implemented for the Connect4 backend only")
+            from ._search import game_of
+            if states and game_of(backend, states[0]) != "generic":
+                raise NotImplementedError("random_rollout runs on the GPU for Connect4 only")
+            return [_backend_rollout(s, backend) for s in states]
         from .games.connect4 import c4_backend as c4
         if not states:
             return []
@@ -144,6 +147,19 @@ def load_value_network(path, model_type: str = "chess_value"):
     net = ValueNetwork(channels, blocks, in_planes=in_planes)
     net.load_state_dict(sd)
     return net
+
+
+def _backend_rollout(state, backend):
+    """value_functions.py:35-45 for a backend the device does not know: its
+    rules are the plugin's Python callables, so the playout calls them where the reference
+    does, drawing from Python's global `random`."""
+    import random
+    initial = state.turn
+    while not backend.check_win(state) and not backend.check_draw(state):
+        state = backend.play_move(state, random.choice(list(backend.get_legal_moves(state))))
+    if backend.check_win(state):
+        return -1 if state.turn == initial else 1
+    return 0
 
 
 def _looks_like_c4(backend, states):

@@ -115,11 +115,14 @@ class Trajectories:
 
     def start(self, quota: int | None, games_cap: int | None = None):
         """Slot g plays game g (g < quota) or idles; the pool is emptied.  quota None = no
-        limit (every finished game's slot starts another)."""
+        limit (every finished game's slot starts another).  With a quota the pool is sized for
+        its worst case (quota games of max_len positions), so simulate_games never drops one."""
         q = _UNLIMITED if quota is None else int(quota)
         self.quota = q
-        if games_cap is not None and games_cap > self.games_cap:
-            self._alloc_pool(games_cap, games_cap * self.max_len)
+        need_g = max(int(games_cap or 0), q if quota is not None else 0)
+        need_p = need_g * self.max_len if quota is not None else 0
+        if need_g > self.games_cap or need_p > self.pool_cap:
+            self._alloc_pool(max(need_g, self.games_cap), max(need_p, self.pool_cap))
         ids = torch.arange(self.n, dtype=torch.int32, device=self.dev)
         self.slot.zero_()
         self.slot[:, 0] = 1
@@ -139,15 +142,27 @@ class Trajectories:
     def record_steps(self, d_states: int, moves: torch.Tensor, results: torch.Tensor, steps: int,
                      reached: torch.Tensor | None = None, stream: int = 0):
         """record() for `steps` consecutive [steps][n] self-play outputs in one call
-        (zc_traj_record_steps_async); steps >= *reached are skipped on the device."""
+        (zc_traj_record_steps_async: four launches whatever `steps` is); only the steps
+        k < *reached are read.  Needs the unlimited quota."""
+        if self.quota != _UNLIMITED:
+            raise ValueError("multi-step recording needs the unlimited quota (start(None))")
+        need = ctypes.c_int64(0)
+        _native.check(_native.lib().zc_traj_steps_scratch_bytes(self.n, int(steps), ctypes.byref(need)))
+        if getattr(self, "_scratch", None) is None or self._scratch.numel() < need.value:
+            self._scratch = torch.empty(max(need.value, 16), dtype=torch.uint8, device=self.dev)
         _native.check(_native.lib().zc_traj_record_steps_async(
             self.n, ctypes.byref(self._buf), ctypes.c_void_p(d_states), ctypes.c_void_p(moves.data_ptr()),
             ctypes.c_void_p(results.data_ptr()), int(steps),
-            ctypes.c_void_p(reached.data_ptr() if reached is not None else None), ctypes.c_void_p(stream or None)))
+            ctypes.c_void_p(reached.data_ptr() if reached is not None else None),
+            ctypes.c_void_p(self._scratch.data_ptr()), self._scratch.numel(), ctypes.c_void_p(stream or None)))
 
     def finished(self) -> int:
-        """Games finished since start() (one device read)."""
-        return int(self.ctl[_native.ZC_TRAJ_FINISHED].item())
+        """Games finished since start() (one device read); raises at once if the pool has
+        overflowed (a game was dropped), rather than at take()."""
+        fin, ov = (int(x) for x in self.ctl[[_native.ZC_TRAJ_FINISHED, _native.ZC_TRAJ_OVERFLOW]].tolist())
+        if ov:
+            self.take()   # raises with the overflow's cause
+        return fin
 
     def take(self) -> TrajBatch:
         """The pooled games, sorted by game number (start order), as device tensors; the pool
@@ -156,7 +171,9 @@ class Trajectories:
         if ctl[_native.ZC_TRAJ_OVERFLOW]:
             raise RuntimeError("trajectory pool overflow: " + ("pool full (take() more often or raise games_cap) "
                                                                if ctl[_native.ZC_TRAJ_OVERFLOW] & 1 else "")
-                               + ("a game longer than max_len" if ctl[_native.ZC_TRAJ_OVERFLOW] & 2 else ""))
+                               + ("a game longer than max_len " if ctl[_native.ZC_TRAJ_OVERFLOW] & 2 else "")
+                               + ("the quota ran out inside a multi-step record" if ctl[_native.ZC_TRAJ_OVERFLOW] & 4
+                                  else ""))
         k, n = int(ctl[_native.ZC_TRAJ_GAMES]), int(ctl[_native.ZC_TRAJ_POSITIONS])
         g = self.games[:k]
         order = torch.argsort(g[:, 0])

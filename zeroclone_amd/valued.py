@@ -202,13 +202,16 @@ class ChessPuctSearch:
         self.na = torch.zeros((n_games, _native.CHESS_MAX_MOVES), dtype=torch.int32, device=self.dev)
         self.prior = torch.zeros((n_games, _native.CHESS_MAX_MOVES), dtype=torch.float32, device=self.dev)
         self.stats = torch.zeros((n_games, _native.STATS_FIELDS), dtype=torch.int64, device=self.dev)
+        # per-game search number: the Philox counter word of the root noise and the
+        # temperature sample; each search adds 1 on the device (graph replays included)
+        self.search_no = torch.zeros(n_games, dtype=torch.int32, device=self.dev)
 
     def enqueue(self, roots: torch.Tensor, sims: int, net_fn, temperature: float = 0.0, first_game: int = 0):
         e, n = self.eng, self.n
         p = lambda t: t.data_ptr() if t is not None else 0  # noqa: E731
         nfl = _native.check(_native.lib().zc_chess_puct_flushes(int(sims), int(self.bs)))
         e.chess_puct_begin(first_game, n, roots.data_ptr(), sims, self.c, self.bs, self.alpha, self.eps, self.seed,
-                           _stream(self.dev))
+                           self.search_no.data_ptr(), stream=_stream(self.dev))
         for f in range(nfl):
             e.chess_puct_select(first_game, n, f, p(self.leaves), p(self.planes),
                                 self.planes.dtype == torch.float16, self.counts.data_ptr(), _stream(self.dev))
@@ -265,6 +268,7 @@ class C4PuctSearch:
         self.na = torch.zeros((n_games, 7), dtype=torch.int32, device=self.dev)
         self.prior = torch.zeros((n_games, 7), dtype=torch.float32, device=self.dev)
         self.stats = torch.zeros((n_games, _native.STATS_FIELDS), dtype=torch.int64, device=self.dev)
+        self.search_no = torch.zeros(n_games, dtype=torch.int32, device=self.dev)   # as ChessPuctSearch
         # the tree arena exists before any graph capture
         z = torch.zeros((1, 3), dtype=torch.int64, device=self.dev)
         eng.c4_puct_begin(0, 0, z.data_ptr(), 2, c_puct, batch_size, dirichlet_alpha, dirichlet_eps, seed)
@@ -274,7 +278,7 @@ class C4PuctSearch:
         p = lambda t: t.data_ptr() if t is not None else 0  # noqa: E731
         nfl = _native.check(_native.lib().zc_chess_puct_flushes(int(sims), int(self.bs)))
         e.c4_puct_begin(first_game, n, roots.data_ptr(), sims, self.c, self.bs, self.alpha, self.eps, self.seed,
-                        _stream(self.dev))
+                        self.search_no.data_ptr(), stream=_stream(self.dev))
         for f in range(nfl):
             e.c4_puct_select(first_game, n, f, p(self.leaves), p(self.planes), self.planes.dtype == torch.float16,
                              self.counts.data_ptr(), _stream(self.dev))
