@@ -120,6 +120,114 @@ def cpu_baseline_chess(sims: int = 400, bs: int = 32, c: float = 1.4, budget_s: 
                       f"{dt:.1f}s (expansions ~= sims from the opening)"}
 
 
+def _cpu_net(planes: int, policy: bool = False):
+    """The network the reference evaluates on a host without a GPU (value_functions.py:61-99:
+    DEVICE "cpu", DTYPE float32; models/chess_value/network.py:24-45), random init, with the
+    process's CPU share as torch's intra-op threads."""
+    from zeroclone_amd.nets import PolicyValueNetwork, ValueNetwork
+    threads = host_cpus()["threads"]
+    torch.set_num_threads(threads)
+    torch.manual_seed(0)
+    if policy:
+        return PolicyValueNetwork().eval(), threads
+    return ValueNetwork(128, 8, in_planes=planes).eval(), threads
+
+
+def _timed_moves(one, budget_s: float):
+    """Calls one(k) for k = 0, 1, ... until budget_s has passed (at least twice); returns
+    (moves, seconds)."""
+    t = time.perf_counter()
+    n = 0
+    while n < 2 or time.perf_counter() - t < budget_s:
+        one(n)
+        n += 1
+    return n, time.perf_counter() - t
+
+
+def cpu_baseline_c4_net(sims: int, bs: int, c: float, budget_s: float = 10.0):
+    """C2(iii) CPU baseline: the oracle's valued Connect4 get_move (oracle/c4_oracle.c,
+    pinned to the reference's get_move on 40 valued goldens) with the fp32 ValueNetwork(128,
+    8, in_planes=2) on the host, one batched forward per flush — the reference's network
+    mode on a CPU box."""
+    import numpy as np
+    import oracle
+    net, threads = _cpu_net(2)
+
+    def vb(boards, turns):
+        x = np.zeros((len(boards), 2, 6, 7), np.float32)
+        for j, (b, t) in enumerate(zip(boards, turns)):
+            a = np.frombuffer(b.encode(), np.uint8).reshape(6, 7)
+            me, op = (ord("X"), ord("O")) if t == 0 else (ord("O"), ord("X"))
+            x[j, 0], x[j, 1] = a == me, a == op
+        with torch.no_grad():
+            return net(torch.from_numpy(x)).reshape(-1).double().tolist()
+
+    n, dt = _timed_moves(lambda k: oracle.get_move_valued("." * 42, 0, oracle.MT(1000 + k), sims, c, bs, vb), budget_s)
+    return {"value": round(n * sims / dt, 1), "unit": "expansions/s", "cores": threads, "kind": "port",
+            "sample": f"{n} Connect4 openings x {sims} sims (expansions ~= sims), batch {bs}, oracle valued get_move + "
+                      f"fp32 ValueNetwork(128, 8, in_planes=2) on {threads} torch threads, {dt:.1f}s"}
+
+
+def cpu_baseline_chess_net(sims: int = 400, bs: int = 32, c: float = 1.4, budget_s: float = 10.0):
+    """C4 (chess value network) CPU baseline: the oracle's chess get_move (random policy,
+    pinned to the reference's on 26 goldens) with the fp32 ValueNetwork(128, 8) over
+    state_to_tensor planes, one batched forward per flush."""
+    import numpy as np
+    import oracle
+    net, threads = _cpu_net(17)
+    root = oracle.chess_init()
+
+    def vb(leaves):
+        x = np.stack([oracle.chess_tensor(oracle.chess_state(b.decode("latin-1"), t, f, cs)) for b, t, f, cs in leaves])
+        with torch.no_grad():
+            return net(torch.from_numpy(x)).reshape(-1).double().tolist()
+
+    n, dt = _timed_moves(lambda k: oracle.chess_get_move(root, oracle.MT(2000 + k), sims, c, bs, value_batch=vb),
+                         budget_s)
+    return {"value": round(n * sims / dt, 1), "unit": "expansions/s", "cores": threads, "kind": "port",
+            "sample": f"{n} chess openings x {sims} sims (expansions ~= sims), batch {bs}, oracle chess get_move + "
+                      f"fp32 ValueNetwork(128, 8) on {threads} torch threads, {dt:.1f}s"}
+
+
+def cpu_baseline_chess_puct(sims: int = 1600, bs: int = 32, c: float = 1.5, budget_s: float = 10.0):
+    """C5 CPU baseline (PUCT has no reference counterpart): oracle/puct_ref.py, the search's
+    executable specification, with the fp32 policy + value network on the host evaluating
+    each flush's leaves in one batch (root noise off: it does not change the work)."""
+    import numpy as np
+    import oracle
+    from oracle import puct_ref
+    net, threads = _cpu_net(17, policy=True)
+    root = oracle.chess_init()
+
+    def one(k):
+        cache = {}
+
+        def key(s):
+            return bytes(s.board) + bytes([s.turn, s.fifty, s.castle])
+
+        def flush(states):
+            if not states:
+                return
+            x = np.stack([oracle.chess_tensor(s) for s in states])
+            with torch.no_grad():
+                v, lg = net(torch.from_numpy(x))
+            for s, vv, ll in zip(states, v.reshape(-1).tolist(), lg.numpy()):
+                cache[key(s)] = (vv, ll)
+
+        def prior(node):
+            ll = cache[key(node.s)][1]
+            idx = [(fr * 8 + fc) * 64 + tr * 8 + tc for fr, fc, tr, tc, _ in node.moves]
+            e = np.exp(ll[idx] - ll[idx].max())
+            return list(e / e.sum())
+
+        puct_ref.search(root, sims, bs, c, lambda s: cache[key(s)][0], prior, flush_fn=flush)
+
+    n, dt = _timed_moves(one, budget_s)
+    return {"value": round(n * (sims - 1) / dt, 1), "unit": "expansions/s", "cores": threads, "kind": "port",
+            "sample": f"{n} chess openings x {sims} sims, batch {bs}, PUCT specification oracle/puct_ref.py + fp32 "
+                      f"PolicyValueNetwork (128 x 8) on {threads} torch threads, {dt:.1f}s"}
+
+
 MFMA_F16_PEAK_TFLOPS = 2500.0  # MI355X dense fp16 MFMA peak, ~2.5 PF (MI355X_MICROARCH.md; no sparsity)
 
 
@@ -353,23 +461,30 @@ def rank_ranges(world: int, games: int) -> list[list[int]]:
 def gather_trajectories(sp, world: int) -> dict:
     """C3's one collective: this rank's finished games' positions (the device
     pool, labels packed with the rows) all-gathered over ranks into the replay buffer."""
+    out, _ = exchange_positions(sp.take_positions(), world, lambda: torch.cuda.synchronize(sp.dev))
+    return out
+
+
+def exchange_positions(local, world: int, sync=lambda: None):
+    """The timed all-gather of `local` position rows (selfplay.positions_of) over the ranks:
+    a warm-up exchange, barrier + sync, the timed one, its time max-reduced over ranks.
+    Returns (report, gathered rows; None at world size 1)."""
     from zeroclone_amd.selfplay import gather_positions
-    local = sp.take_positions()
     out = {"local_rows": int(local.shape[0])}
     if world == 1:
-        return out
+        return out, None
     gather_positions(local)  # warm the communicator
     dist.barrier()
-    torch.cuda.synchronize(sp.dev)
+    sync()
     tg = time.perf_counter()
     allpos = gather_positions(local)
-    torch.cuda.synchronize(sp.dev)
-    gms = torch.tensor([(time.perf_counter() - tg) * 1e3], dtype=torch.float64, device=sp.dev)
+    sync()
+    gms = torch.tensor([(time.perf_counter() - tg) * 1e3], dtype=torch.float64, device=local.device)
     dist.all_reduce(gms, op=dist.ReduceOp.MAX)
     out.update({"rows": int(allpos.shape[0]), "bytes": int(allpos.numel() * allpos.element_size()),
                 "ms": round(float(gms.item()), 3),
                 "collective": "all_gather (counts, padded payload) of finished games' 24-B positions, nccl=RCCL"})
-    return out
+    return out, allpos
 
 
 def search_profile():
@@ -466,6 +581,9 @@ def run_rank(args, rank: int, world: int, local: int):
             out["cpu_baseline"] = cpu_baseline(S, B, args.c)
             if args.net_steps > 0:
                 out["extra"]["c4_chess"]["crude"]["cpu_baseline"] = cpu_baseline_chess()
+                out["extra"]["c2_value_net"]["cpu_baseline"] = cpu_baseline_c4_net(S, B, args.c)
+                out["extra"]["c4_chess"]["value_net"]["cpu_baseline"] = cpu_baseline_chess_net()
+                out["extra"]["c5_chess_puct"]["cpu_baseline"] = cpu_baseline_chess_puct()
         else:
             out["cpu_baseline"] = None
         print(json.dumps(out), flush=True)
@@ -513,6 +631,31 @@ def record_overhead(sp, args) -> dict:
     return {"ms_per_step_recorded": round(on["dt"] / args.steps * 1e3, 3),
             "ms_per_step_unrecorded": round(off["dt"] / args.steps * 1e3, 3),
             "ratio": round(on["dt"] / max(off["dt"], 1e-9), 4)}
+
+
+def visible_gpus(kfd_root: str = "/sys/class/kfd/kfd/topology/nodes") -> int:
+    """GPUs this process may use, counted WITHOUT initialising HIP (the parent must not touch
+    the GPU before it spawns the ranks): the KFD topology's GPU nodes (simd_count > 0),
+    narrowed by ROCR_VISIBLE_DEVICES / HIP_VISIBLE_DEVICES / CUDA_VISIBLE_DEVICES.  Raises
+    when the topology is unreadable: no fallback to hipGetDeviceCount."""
+    try:
+        nodes = [os.path.join(kfd_root, d) for d in os.listdir(kfd_root)]
+    except OSError as e:
+        raise RuntimeError(f"cannot count GPUs without HIP: {kfd_root} unreadable ({e})") from None
+    n = 0
+    for d in nodes:
+        try:
+            with open(os.path.join(d, "properties")) as fh:
+                props = dict(line.split()[:2] for line in fh if len(line.split()) >= 2)
+        except OSError:
+            continue
+        if int(props.get("simd_count", "0")) > 0:
+            n += 1
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            n = min(n, len([x for x in v.split(",") if x.strip() != ""]))
+    return n
 
 
 def _free_port() -> int:
@@ -566,7 +709,10 @@ def main():
     if args.gpus == 1:
         run_rank(args, 0, 1, 0)
         return
-    visible = torch.cuda.device_count()   # counts devices without initialising HIP in this process
+    try:
+        visible = visible_gpus()   # the KFD topology: no HIP call in this (parent) process
+    except RuntimeError as e:
+        raise SystemExit(f"bench.py: {e}")
     if args.gpus > visible:
         raise SystemExit(f"bench.py: --gpus {args.gpus} but only {visible} GPU(s) visible")
     import torch.multiprocessing as mp

@@ -1,5 +1,6 @@
 """A plain-Python restatement of the PUCT searches of zeroclone_amd/csrc/chess_puct.hip and
-c4_puct.hip, for the parity tests (test infrastructure; the rules come from the oracle).  The search has no
+c4_puct.hip, for the parity tests and bench.py's C5 CPU baseline (TEST INFRASTRUCTURE ONLY;
+the rules come from the oracle).  The search has no
 reference counterpart, so this file is its specification in executable
 form: same arithmetic order in fp64, same tie-breaking, same flush / virtual-loss protocol.
 """
@@ -48,9 +49,12 @@ class Node:
         self.evaluated = False
 
 
-def search(state, sims, bs, c, value_fn, prior_fn, rules=ChessRules):
+def search(state, sims, bs, c, value_fn, prior_fn, rules=ChessRules, flush_fn=None):
     """value_fn(state) -> value for the side to move; prior_fn(node) -> priors (list,
-    float) for the node's moves.  Returns (root moves, root visits, chosen index)."""
+    float) for the node's moves.  flush_fn(states), if given, is called once per flush with
+    the states of its non-terminal leaves before any value_fn / prior_fn call of that flush
+    (a batched network fills the cache they read).  Returns (root moves, root visits,
+    chosen index)."""
     root = Node(state, rules)
     flushes = 1 + (sims - 1 + bs - 1) // bs
     for f in range(flushes):
@@ -78,6 +82,8 @@ def search(state, sims, bs, c, value_fn, prior_fn, rules=ChessRules):
                     break
                 node = node.child[best]
             leaves.append((node, path))
+        if flush_fn is not None:
+            flush_fn([node.s for node, _ in leaves if len(node.moves)])
         for node, path in leaves:
             if len(node.moves) == 0:
                 v = -1.0 if rules.win(node.s) else 0.0

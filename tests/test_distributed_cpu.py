@@ -159,8 +159,83 @@ def test_bench_rank_ranges_and_launcher_errors():
     # more GPUs than visible: a clear error before any GPU work (no GPU in this container)
     p = subprocess.run([sys.executable, "bench.py", "--gpus", "2"], cwd=repo, env=env, capture_output=True, text=True,
                        timeout=300)
-    assert p.returncode != 0 and "GPU(s) visible" in p.stderr
+    assert p.returncode != 0 and ("GPU(s) visible" in p.stderr or "cannot count GPUs" in p.stderr)
     # under torchrun the world size must match --gpus
     p = subprocess.run([sys.executable, "bench.py", "--gpus", "4"], cwd=repo, env={**env, "WORLD_SIZE": "2"},
                        capture_output=True, text=True, timeout=300)
     assert p.returncode != 0 and "WORLD_SIZE=2 but --gpus 4" in p.stderr
+
+
+def test_visible_gpus_reads_the_kfd_topology(tmp_path, monkeypatch):
+    """bench.visible_gpus counts GPU nodes of the KFD topology (simd_count > 0) with no HIP
+    call, honours *_VISIBLE_DEVICES, and fails loudly when the topology is missing."""
+    import bench
+    for i, simds in enumerate([0, 1024, 1024, 0, 1024]):   # two CPU nodes, three GPUs
+        d = tmp_path / str(i)
+        d.mkdir()
+        (d / "properties").write_text(f"cpu_cores_count {0 if simds else 64}\nsimd_count {simds}\n")
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        monkeypatch.delenv(var, raising=False)
+    assert bench.visible_gpus(str(tmp_path)) == 3
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "0,1")
+    assert bench.visible_gpus(str(tmp_path)) == 2
+    with pytest.raises(RuntimeError):
+        bench.visible_gpus(str(tmp_path / "absent"))
+
+
+def _games_of_rank(rank):
+    """A TrajBatch of finished Connect4 games as the device pool returns them (rows, labels
+    by Engine.get_dataset, moves, game records), built on the host from real games."""
+    from zeroclone_amd.engine.games.connect4 import c4_backend as c4
+    from zeroclone_amd.selfplay import TrajBatch
+    rng = np.random.default_rng(10 + rank)
+    rows, labels, moves, games = [], [], [], []
+    for gno in range(2 + 3 * rank):
+        st, hist, mv = c4.create_init_state(), [], []
+        res = None
+        while res is None:
+            hist.append(c4.to_zc(st))
+            legal = sorted(c4.get_legal_moves(st))
+            m = legal[rng.integers(len(legal))]
+            mv.append(m[0])
+            st = c4.play_move(st, m)
+            res = (st.turn * 2 - 1) if c4.check_win(st) else (0 if c4.check_draw(st) else None)
+        hist.append(c4.to_zc(st))
+        mv.append(-1)
+        games.append([gno, rank, res, len(rows), len(hist)])
+        rows += [[np.int64(np.uint64(s0)), np.int64(np.uint64(s1)), t] for s0, s1, t in hist]
+        labels += dataset_labels(len(hist), res).astype(np.int32).tolist()
+        moves += mv
+    t = lambda a, dt: torch.tensor(np.asarray(a), dtype=dt)  # noqa: E731
+    return TrajBatch(t(rows, torch.int64), t(labels, torch.int32), t(moves, torch.int16), t(games, torch.int64))
+
+
+def _traj_worker(rank, world, port, out):
+    import bench
+    from zeroclone_amd.selfplay import positions_of
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    rep, rows = bench.exchange_positions(positions_of(_games_of_rank(rank)), world)
+    out[rank] = (rep, rows.numpy().tolist())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_trajectory_exchange_gloo_world2():
+    """bench.py's C3 exchange on TrajBatch-shaped rows from real games: every rank receives
+    every rank's positions in rank order, labels packed as Engine.get_dataset's."""
+    from zeroclone_amd.selfplay import positions_of
+    world, port = 2, _free_port()
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_traj_worker, args=(world, port, out), nprocs=world, join=True)
+    want = np.concatenate([positions_of(_games_of_rank(r)).numpy() for r in range(world)])
+    for r in range(world):
+        rep, rows = out[r]
+        rows = np.asarray(rows, np.int64)
+        assert np.array_equal(rows, want)
+        assert rep["rows"] == len(want) and rep["bytes"] == want.size * 8 and rep["ms"] >= 0
+    lab = (want[:, 2] >> 32).astype(np.int64)
+    b0 = _games_of_rank(0)
+    assert np.array_equal(lab[: b0.labels.shape[0]], b0.labels.numpy())

@@ -9,7 +9,7 @@ import pytest
 import torch
 
 import oracle
-import puct_ref
+from oracle import puct_ref
 from c4_values import bits_from_rows, hash_value
 
 pytestmark = pytest.mark.gpu

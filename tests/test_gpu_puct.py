@@ -7,7 +7,7 @@ import pytest
 import torch
 
 import oracle
-import puct_ref
+from oracle import puct_ref
 
 pytestmark = pytest.mark.gpu
 

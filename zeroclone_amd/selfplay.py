@@ -308,10 +308,7 @@ class C4SelfPlay:
     def take_positions(self) -> torch.Tensor:
         """Positions of the games finished since the last take, in start order: [n, 3] int64
         device rows (stones X, stones O, turn | Engine.get_dataset label << 32)."""
-        b = self.take()
-        rows = b.rows.clone()
-        rows[:, 2] = (rows[:, 2] & 1) | (b.labels.to(torch.int64) << 32)
-        return rows
+        return positions_of(self.take())
 
     def finished_games(self, batch: TrajBatch | None = None):
         """Host view of taken games (tests / inspection): (global slot id, moves, result,
@@ -321,6 +318,14 @@ class C4SelfPlay:
 
     def close(self):
         self.eng.close()
+
+
+def positions_of(b: TrajBatch) -> torch.Tensor:
+    """A Connect4 TrajBatch as the exchange's rows: [n, 3] int64 (stones X, stones O,
+    turn | Engine.get_dataset label << 32), on the batch's device."""
+    rows = b.rows.clone()
+    rows[:, 2] = (rows[:, 2] & 1) | (b.labels.to(torch.int64) << 32)
+    return rows
 
 
 def _host_games(b: TrajBatch, first_id: int, move_fn):
