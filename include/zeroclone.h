@@ -355,6 +355,51 @@ int zc_chess_hp_walk(zc_engine *eng, int32_t game, int32_t flush, int32_t leaf, 
 int zc_chess_hp_expand(zc_engine *eng, int32_t game, int32_t flush, int32_t leaf, int32_t untried_index,
                        zc_chess_state *d_leaf, void *hip_stream);
 
+/* ---- Chess self-play on the device (scripts/train.py:151-170) ------------
+ * Engine.play_move + _evaluate (engine/engine.py:98-108, 148-153) for chess, with the move
+ * histories the repetition draw needs (chess_backend.cpp:364-441) kept in HBM:
+ *   d_roots    [n] the positions to move from (updated: the post-move position, or d_init
+ *              once the game has ended — the refill of a finished game)
+ *   d_hist     [n][2][hist_cap] uint16 each side's moves in play order (packed moves)
+ *   d_hist_len [n][2] int32 (zeroed when a game ends; hist_cap <= 4096)
+ *   d_err      [3] int32, OR-ed: a game longer than hist_cap moves per side | a search out
+ *              of tree capacity | no move at a live root (the game stops moving)
+ * Results are Engine._evaluate's: turn*2-1 (checkmate, turn = side to move after the move),
+ * 0 (stalemate, fifty-move rule, both sides' histories repeating), ZC_C4_ONGOING. */
+typedef struct zc_chess_play_buffers {
+    zc_chess_state *d_roots;
+    const zc_chess_state *d_init;
+    uint16_t *d_hist;
+    int32_t *d_hist_len;
+    int32_t hist_cap, reserved;
+    int32_t *d_err;
+} zc_chess_play_buffers;
+/* One step of n games whose moves a search chose (any mode; d_moves[i] = 0xFFFF: none,
+ * flagged): d_out_states / d_out_results [n] are the post-move positions and results
+ * (the inputs of zc_traj_record_async with d_flags = NULL); d_search_stats (may be NULL)
+ * flags searches out of capacity.  No engine needed. */
+int zc_chess_play_step_async(int32_t n, const zc_chess_play_buffers *b, const uint16_t *d_moves,
+                             const zc_game_stats *d_search_stats, zc_chess_state *d_out_states,
+                             int32_t *d_out_results, void *hip_stream);
+/* Crude-score self-play (zc_chess_search_async's search) of games first..first+n-1 for
+ * `moves` consecutive moves in ONE launch, each game at its own pace: search, step, refill.
+ * Outputs [moves][n] (post-move positions, moves, results: zc_traj_record_steps_async's
+ * inputs); d_stats[i] sums the moves' counters (reserved = games finished).  Equal to
+ * `moves` rounds of zc_chess_search_async + zc_chess_play_step_async. */
+int zc_chess_selfplay_async(zc_engine *eng, int32_t first_game, int32_t n_games, const zc_chess_play_buffers *b,
+                            int32_t sims, double c, int32_t batch_size, int32_t policy, double freedom,
+                            int32_t moves, zc_chess_state *d_out_states, uint16_t *d_out_moves,
+                            int32_t *d_out_results, zc_game_stats *d_stats, void *hip_stream);
+/* Pooled form (as zc_c4_selfplay_pooled_async): the games share `budget` moves drawn from
+ * d_ticket[0], at most moves_cap each; unreached steps get ZC_SLOT_SKIP and move 0xFFFF;
+ * d_ticket[1] = the most moves any game played.  n_games <= zc_chess_pooled_max_games. */
+int zc_chess_selfplay_pooled_async(zc_engine *eng, int32_t first_game, int32_t n_games,
+                                   const zc_chess_play_buffers *b, int32_t sims, double c, int32_t batch_size,
+                                   int32_t policy, double freedom, int32_t moves_cap, int64_t budget,
+                                   int32_t *d_ticket, zc_chess_state *d_out_states, uint16_t *d_out_moves,
+                                   int32_t *d_out_results, zc_game_stats *d_stats, void *hip_stream);
+int zc_chess_pooled_max_games(int32_t hist_cap, int32_t *out);
+
 /* ---- Chess PUCT search (AlphaZero-style; no reference counterpart) -------
  * Selection by Q + c_puct * P * sqrt(sum N) / (1 + N) with priors P from a policy network,
  * virtual loss within a flush, Dirichlet(alpha) noise of weight eps on the root priors

@@ -44,6 +44,13 @@ class EngineConfig(ctypes.Structure):
                 ("max_batch", ctypes.c_int32)]
 
 
+class ChessPlayBuffers(ctypes.Structure):
+    """zc_chess_play_buffers (include/zeroclone.h): a chess self-play pool's device buffers."""
+    _fields_ = [("d_roots", ctypes.c_void_p), ("d_init", ctypes.c_void_p), ("d_hist", ctypes.c_void_p),
+                ("d_hist_len", ctypes.c_void_p), ("hist_cap", ctypes.c_int32), ("reserved", ctypes.c_int32),
+                ("d_err", ctypes.c_void_p)]
+
+
 class TrajBuffers(ctypes.Structure):
     """zc_traj_buffers (include/zeroclone.h): device pointers of a self-play trajectory pool."""
     _fields_ = [("row_bytes", ctypes.c_int32), ("max_len", ctypes.c_int32), ("pool_cap", ctypes.c_int64),
@@ -127,6 +134,18 @@ SIGNATURES = [
                                                    ctypes.c_int32, ctypes.c_double, ctypes.c_int32, ctypes.c_int32,
                                                    ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                                    ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    ("zc_chess_play_step_async", ctypes.c_int, [ctypes.c_int32, P(ChessPlayBuffers), ctypes.c_void_p, ctypes.c_void_p,
+                                                ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    ("zc_chess_selfplay_async", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, P(ChessPlayBuffers),
+                                               ctypes.c_int32, ctypes.c_double, ctypes.c_int32, ctypes.c_int32,
+                                               ctypes.c_double, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p,
+                                               ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    ("zc_chess_selfplay_pooled_async", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32,
+                                                      P(ChessPlayBuffers), ctypes.c_int32, ctypes.c_double,
+                                                      ctypes.c_int32, ctypes.c_int32, ctypes.c_double, ctypes.c_int32,
+                                                      ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                                      ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    ("zc_chess_pooled_max_games", ctypes.c_int, [ctypes.c_int32, P(ctypes.c_int32)]),
     ("zc_c4_pooled_max_games", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, P(ctypes.c_int32)]),
     ("zc_traj_steps_scratch_bytes", ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, P(ctypes.c_int64)]),
     ("zc_traj_record_steps_async", ctypes.c_int, [ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,

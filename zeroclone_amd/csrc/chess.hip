@@ -79,56 +79,16 @@ __global__ __launch_bounds__(64) void chess_terminal_kernel(int n, const zc_ches
     }
 }
 
-// has_repeated_prefix (:148-180; min_pattern_len 2, min_repeats 3) of both sides' move
-// histories, most recent move first.  hist[i][side][k] = that side's k-th move in play order
-// (k < len[i][side] <= cap); out[i] = white's answer | black's << 1 (check_draw's repetition
-// draw is both).  KMP's test — some prefix whose smallest period p >= 2 divides its length
-// at least 3 times — is evaluated as: with M(q) = q + lcp(L, L shifted by q), the longest
-// prefix of period q, some p >= 2 has R = p * floor(M(p) / p) >= 3p and R > M(1).  (Then the
-// smallest period of the R-prefix is not 1, and by Fine and Wilf it divides p, so it repeats
-// >= 3 times; conversely KMP's prefix is such an R or shorter.)  One wave per position, the
-// history staged in LDS, lanes comparing 64 shifted pairs per step.
+// has_repeated_prefix (:148-180) of both sides' move histories (chess_device.h::repetitions):
+// hist[i][side][k] = that side's k-th move in play order (k < len[i][side] <= cap); out[i] =
+// white's answer | black's << 1.  One wave per position, the history staged in LDS.
 __global__ __launch_bounds__(64) void chess_repetition_kernel(int n, int cap, const uint16_t *hist, const int32_t *len,
                                                              int32_t *out) {
     __shared__ uint16_t Lh[kMaxHistory];
     const int i = blockIdx.x;
     if (i >= n) return;
-    const int l = (int)lane();
-    int res = 0;
-    for (int side = 0; side < 2; ++side) {
-        const int m = min(__builtin_amdgcn_readfirstlane(len[2 * i + side]), cap);
-        const uint16_t *h = hist + ((size_t)i * 2 + side) * cap;
-        for (int k = l; k < m; k += 64) Lh[k] = h[m - 1 - k];
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        bool rep = false;
-        if (m >= 6) {
-            int m1 = m;  // M(1): the opening run of one repeated move
-            for (int base = 0; base < m; base += 64) {
-                const int k = base + l;
-                const uint64_t mm = __ballot(k < m && Lh[k] != Lh[0]);
-                if (mm) {
-                    m1 = base + __builtin_ctzll(mm);
-                    break;
-                }
-            }
-            for (int p = 2; 3 * p <= m && !rep; ++p) {
-                int lcp = m - p;
-                for (int base = 0; base < m - p; base += 64) {
-                    const int k = base + l;
-                    const uint64_t mm = __ballot(k < m - p && Lh[k] != Lh[k + p]);
-                    if (mm) {
-                        lcp = base + __builtin_ctzll(mm);
-                        break;
-                    }
-                }
-                const int R = (p + lcp) / p * p;
-                rep = R >= 3 * p && R > m1;
-            }
-        }
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        res |= (rep ? 1 : 0) << side;
-    }
-    if (l == 0) out[i] = res;
+    const int res = repetitions(hist + (size_t)i * 2 * cap, len + 2 * i, cap, Lh);
+    if (lane() == 0) out[i] = res;
 }
 
 // state_to_tensor (:461-521): [17][8][8], planes 0-11 = PNBRQK pnbrqk, 12 = white to move,

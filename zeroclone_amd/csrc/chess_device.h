@@ -499,6 +499,58 @@ __device__ __forceinline__ void apply_move(zc_chess_state &o, uint32_t m) {
     if (tr == 7 && pc == 'p') b[to] = 'q';
 }
 
+// has_repeated_prefix (chess_backend.cpp:148-180; min_pattern_len 2, min_repeats 3) of the
+// m moves h[0..m) in play order, most recent first (one wave; Lh: m u16 of LDS).  KMP's test
+// — some prefix whose smallest period p >= 2 divides its length at least 3 times — is
+// evaluated as: with M(q) = q + lcp(L, L shifted by q), the longest prefix of period q, some
+// p >= 2 has R = p * floor(M(p) / p) >= 3p and R > M(1).  (Then the smallest period of the
+// R-prefix is not 1, and by Fine and Wilf it divides p, so it repeats >= 3 times; conversely
+// KMP's prefix is such an R or shorter.)  Lanes compare 64 shifted pairs per step.
+__device__ __forceinline__ bool repeated_prefix(const uint16_t *h, int m, uint16_t *Lh) {
+    const int l = (int)lane();
+    for (int k = l; k < m; k += 64) Lh[k] = h[m - 1 - k];
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    bool rep = false;
+    if (m >= 6) {
+        int m1 = m;  // M(1): the opening run of one repeated move
+        for (int base = 0; base < m; base += 64) {
+            const int k = base + l;
+            const uint64_t mm = __ballot(k < m && Lh[k] != Lh[0]);
+            if (mm) {
+                m1 = base + __builtin_ctzll(mm);
+                break;
+            }
+        }
+        for (int p = 2; 3 * p <= m && !rep; ++p) {
+            int lcp = m - p;
+            for (int base = 0; base < m - p; base += 64) {
+                const int k = base + l;
+                const uint64_t mm = __ballot(k < m - p && Lh[k] != Lh[k + p]);
+                if (mm) {
+                    lcp = base + __builtin_ctzll(mm);
+                    break;
+                }
+            }
+            const int R = (p + lcp) / p * p;
+            rep = R >= 3 * p && R > m1;
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    return rep;
+}
+
+// Both sides' repetition answers: white's | black's << 1 (check_draw's repetition draw is
+// both, chess_backend.cpp:416-441).  hist[side][k] = that side's k-th move (k < len[side],
+// at most cap read).
+__device__ __forceinline__ int repetitions(const uint16_t *hist, const int32_t *len, int cap, uint16_t *Lh) {
+    int res = 0;
+    for (int side = 0; side < 2; ++side) {
+        const int m = min(__builtin_amdgcn_readfirstlane(len[side]), cap);
+        res |= (repeated_prefix(hist + (size_t)side * cap, m, Lh) ? 1 : 0) << side;
+    }
+    return res;
+}
+
 struct ChessScratch {
     uint8_t board[64];
     uint16_t legal[kMaxLegal];

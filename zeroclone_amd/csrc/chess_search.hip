@@ -266,13 +266,10 @@ __device__ void root_init(const ChessParams &p, const CTree &t, CLds &L, int gl,
     wave_sync_mem();
 }
 
-__device__ void finish(const ChessParams &p, const CTree &t, int gl, int g, const int32_t *ctl) {
+// first max of child N over the root's moves (mcts.cpp:150-155): the slot index, or
+// 0x7FFFFFFF when the root has no child
+__device__ __forceinline__ int best_root_slot(const CTree &t, int nm, uint32_t base) {
     const uint32_t lane = lane_id();
-    const int status = uni(ctl[cStatus]);
-    const ChessNode *R = &t.nodes[0];
-    const int nm = status == ZC_STATUS_NO_MOVES ? 0 : uni((int)R->nmoves);
-    const uint32_t base = uni(R->base);
-    // first max of child N over the root's moves (mcts.cpp:150-155)
     int bv = -1, bi = 0x7FFFFFFF;
     for (int b = 0; b < nm; b += 64) {
         const int j = b + (int)lane;
@@ -291,6 +288,16 @@ __device__ void finish(const ChessParams &p, const CTree &t, int gl, int g, cons
             bi = oi;
         }
     }
+    return uni(bi);
+}
+
+__device__ void finish(const ChessParams &p, const CTree &t, int gl, int g, const int32_t *ctl) {
+    const uint32_t lane = lane_id();
+    const int status = uni(ctl[cStatus]);
+    const ChessNode *R = &t.nodes[0];
+    const int nm = status == ZC_STATUS_NO_MOVES ? 0 : uni((int)R->nmoves);
+    const uint32_t base = uni(R->base);
+    const int bi = best_root_slot(t, nm, base);
     for (int j = (int)lane; j < ZC_CHESS_MAX_MOVES; j += 64)
         p.out_na[(size_t)gl * ZC_CHESS_MAX_MOVES + j] = j < nm ? t.na[base + j] : 0;
     if (lane == 0) {
@@ -353,14 +360,9 @@ __device__ void chess_backup_flush(const ChessParams &p, const CTree &t, int g, 
 }
 
 // ---------------------------------------------------------------- fused: crude_chess_score
-__global__ __launch_bounds__(64) void chess_search_kernel(ChessParams p) {
-    __shared__ CLds L;
-    __shared__ double s_vals[256];
-    const int gl = blockIdx.x;
-    if (gl >= p.n_games) return;
-    const int g = p.first_game + gl;
-    const CTree t = ctree(p, g);
-    int32_t *ctl = p.ca.ctl + (size_t)g * kCtlWords;
+// The whole search of one game from p.roots[gl] (root_init .. the last backup).
+__device__ void crude_search(const ChessParams &p, const CTree &t, CLds &L, double *s_vals, int gl, int g,
+                             int32_t *ctl) {
     ConstDouble *logtab = (ConstDouble *)p.a.logtab;
     root_init(p, t, L, gl, g, ctl);
     const uint32_t *meta = p.ca.meta + (size_t)g * p.max_batch;
@@ -376,7 +378,168 @@ __global__ __launch_bounds__(64) void chess_search_kernel(ChessParams p) {
         chess_backup_flush(p, t, g, ctl, s_vals, nb);
         done += nb;
     }
+}
+
+__global__ __launch_bounds__(64) void chess_search_kernel(ChessParams p) {
+    __shared__ CLds L;
+    __shared__ double s_vals[256];
+    const int gl = blockIdx.x;
+    if (gl >= p.n_games) return;
+    const int g = p.first_game + gl;
+    const CTree t = ctree(p, g);
+    int32_t *ctl = p.ca.ctl + (size_t)g * kCtlWords;
+    crude_search(p, t, L, s_vals, gl, g, ctl);
     finish(p, t, gl, g, ctl);
+}
+
+// ---------------------------------------------------------------- chess self-play
+// Engine.play_move + _evaluate (engine/engine.py:98-108, 148-153) of move m from q.roots[gl]:
+// the position after the move (left in L.st), the mover's history push (play_move's deque,
+// chess_backend.cpp:364-400), check_win / check_draw of the new position (:404-441:
+// checkmate; stalemate, the fifty-move counter, both sides' histories repeating).  Returns
+// the result (turn*2-1 with the new side to move, 0, or ZC_C4_ONGOING).
+__device__ int chess_play_judge(const ChessPlayParams &q, int gl, CLds &L, uint16_t *Lh, uint32_t m, int &err) {
+    const uint32_t lane = lane_id();
+    if (lane < 18) ((uint32_t *)&L.st)[lane] = ((const uint32_t *)&q.roots[gl])[lane];
+    wave_sync_mem();
+    const int mover = uni((int)L.st.turn);
+    if (lane == 0) chessdev::apply_move(L.st, m);
+    wave_sync_mem();
+    L.s.board[lane] = L.st.board[lane];
+    wave_sync_mem();
+    const int turn = uni((int)L.st.turn);
+    bool check;
+    const int k = chessdev::legal_moves_check(L.s.board, turn, L.s.legal, L.s.pseudo, L.s.region, check);
+    uint16_t *h = q.hist + (size_t)gl * 2 * q.cap;
+    int32_t *hl = q.hlen + 2 * (size_t)gl;
+    const int len = uni(hl[mover]);
+    if (len >= q.cap) err |= 1;  // a game longer than the history holds: flagged
+    if (lane == 0) {
+        h[(size_t)mover * q.cap + min(len, q.cap - 1)] = (uint16_t)m;
+        hl[mover] = len + 1;
+    }
+    wave_sync_mem();
+    const int rep = chessdev::repetitions(h, hl, q.cap, Lh);
+    if (k < 0) err |= 8;
+    if (k == 0 && check) return turn * 2 - 1;
+    if ((k == 0 && !check) || uni((int)L.st.fifty) >= 50 || rep == 3) return 0;
+    return ZC_C4_ONGOING;
+}
+
+// After a step of game gl: its outputs at index o, its root to the post-move position or,
+// when the game ended, to the initial position with empty histories (the refill of
+// scripts/train.py:151-170).
+__device__ void chess_play_commit(const ChessPlayParams &q, int gl, const CLds &L, size_t o, uint32_t m, int r) {
+    const uint32_t lane = lane_id();
+    if (lane < 18) {
+        const uint32_t w = ((const uint32_t *)&L.st)[lane];
+        ((uint32_t *)&q.out_states[o])[lane] = w;
+        ((uint32_t *)&q.roots[gl])[lane] = r == ZC_C4_ONGOING ? w : ((const uint32_t *)q.init)[lane];
+    }
+    if (lane == 0) {
+        if (q.out_moves) q.out_moves[o] = (uint16_t)m;
+        q.out_results[o] = r;
+        if (r != ZC_C4_ONGOING) {
+            q.hlen[2 * (size_t)gl] = 0;
+            q.hlen[2 * (size_t)gl + 1] = 0;
+        }
+    }
+    wave_sync_mem();
+}
+
+__device__ __forceinline__ void chess_play_errors(const ChessPlayParams &q, int err) {
+    if (lane_id() == 0 && err) {
+        if (err & 1) atomicOr(q.err + 0, 1);
+        if (err & 2) atomicOr(q.err + 1, 1);
+        if (err & 4) atomicOr(q.err + 2, 1);
+        if (err & 8) atomicOr(q.err + 1, 1);
+    }
+}
+
+// Lockstep: one step of every game whose move some search (any mode) chose: q.in_moves[gl]
+// (0xFFFF = the search found none: flagged, the game left as it is); q.search_stats flags a
+// search that ran out of tree capacity.  Outputs at [gl].
+__global__ __launch_bounds__(64) void chess_play_step_kernel(ChessPlayParams q, int n) {
+    extern __shared__ uint16_t s_hist[];
+    __shared__ CLds L;
+    const int gl = blockIdx.x;
+    if (gl >= n) return;
+    int err = 0;
+    if (q.search_stats && uni((int)q.search_stats[gl].status) == ZC_STATUS_CAPACITY) err |= 2;
+    const uint32_t m = uni((uint32_t)q.in_moves[gl]);
+    if (m == 0xFFFFu) {
+        err |= 4;
+        if (lane_id() < 18) ((uint32_t *)&L.st)[lane_id()] = ((const uint32_t *)&q.roots[gl])[lane_id()];
+        wave_sync_mem();
+        chess_play_commit(q, gl, L, (size_t)gl, m, ZC_C4_ONGOING);
+    } else {
+        const int r = chess_play_judge(q, gl, L, s_hist, m, err);
+        chess_play_commit(q, gl, L, (size_t)gl, m, r);
+    }
+    chess_play_errors(q, err);
+}
+
+// Self-play with the crude score, `q.moves` moves per game in ONE launch (the chess form of
+// c4_search.hip's c4_selfplay_kernel): per move the whole search from the game's root, the
+// step above, the refill.  With q.ticket the games share q.budget moves (pooled); steps a
+// game did not reach are ZC_SLOT_SKIP / move 0xFFFF.  Outputs [moves][n]; q.stats[gl] sums
+// the moves' counters (reserved = games finished).
+__global__ __launch_bounds__(64) void chess_selfplay_kernel(ChessParams p, ChessPlayParams q) {
+    extern __shared__ uint16_t s_hist[];
+    __shared__ CLds L;
+    __shared__ double s_vals[256];
+    const int gl = blockIdx.x;
+    if (gl >= p.n_games) return;
+    const uint32_t lane = lane_id();
+    const int g = p.first_game + gl;
+    const CTree t = ctree(p, g);
+    int32_t *ctl = p.ca.ctl + (size_t)g * kCtlWords;
+    const uint64_t use_start = uni64(p.a.rngpos[2 * (size_t)g]);
+    int64_t exp = 0, depth = 0;
+    int finished = 0, status = 0, err = 0, mv = 0;
+    for (; mv < q.moves; ++mv) {
+        if (q.ticket) {
+            int tk = 0;
+            if (lane == 0) tk = atomicAdd(q.ticket, 1);
+            if (uni(tk) >= q.budget) break;
+        }
+        crude_search(p, t, L, s_vals, gl, g, ctl);
+        status = uni(ctl[cStatus]);
+        exp += uni(ctl[cExp]);
+        depth += uni(ctl[cDepth]);
+        if (status) {  // a root without moves is never live here: flagged, the game stops
+            err |= status == ZC_STATUS_CAPACITY ? 2 : 4;
+            break;
+        }
+        const ChessNode *R = &t.nodes[0];
+        const uint32_t base = uni(R->base);
+        const int bi = best_root_slot(t, uni((int)R->nmoves), base);
+        if (bi == 0x7FFFFFFF) {
+            err |= 4;
+            break;
+        }
+        const uint32_t m = uni((uint32_t)t.mv[base + bi]);
+        const int r = chess_play_judge(q, gl, L, s_hist, m, err);
+        chess_play_commit(q, gl, L, (size_t)mv * p.n_games + gl, m, r);
+        finished += r != ZC_C4_ONGOING;
+    }
+    if (q.ticket && lane == 0) atomicMax(q.ticket + 1, mv);
+    for (int k = mv + (int)lane; k < q.moves; k += 64) {
+        const size_t o = (size_t)k * p.n_games + gl;
+        q.out_moves[o] = 0xFFFF;
+        q.out_results[o] = ZC_SLOT_SKIP;
+    }
+    chess_play_errors(q, err);
+    if (lane == 0) {
+        zc_game_stats st{};
+        st.status = status;
+        st.expansions = exp;
+        st.depth_sum = depth;
+        st.leaves = (int64_t)p.sims * mv;
+        st.rng_words = (int64_t)(p.a.rngpos[2 * (size_t)g] - use_start);
+        st.reserved = finished;
+        q.stats[gl] = st;
+    }
 }
 
 // ---------------------------------------------------------------- stepwise (caller values)
@@ -561,6 +724,22 @@ void launch_chess_hp_expand(const ChessParams &p, hipStream_t s) {
 
 void launch_chess_search(const ChessParams &p, hipStream_t s) {
     hipLaunchKernelGGL(chess_search_kernel, dim3(p.n_games), dim3(64), 0, s, p);
+}
+void launch_chess_play_step(const ChessPlayParams &q, int n, hipStream_t s) {
+    hipLaunchKernelGGL(chess_play_step_kernel, dim3(n), dim3(64), (size_t)q.cap * sizeof(uint16_t), s, q, n);
+}
+void launch_chess_selfplay(const ChessParams &p, const ChessPlayParams &q, hipStream_t s) {
+    hipLaunchKernelGGL(chess_selfplay_kernel, dim3(p.n_games), dim3(64), (size_t)q.cap * sizeof(uint16_t), s, p, q);
+}
+int chess_selfplay_resident_games(int cap, int *out) {
+    int blocks = 0, dev = 0, cus = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, (const void *)chess_selfplay_kernel, 64,
+                                                     (size_t)cap * sizeof(uint16_t)) != hipSuccess)
+        return -1;
+    if (hipGetDevice(&dev) != hipSuccess) return -1;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return -1;
+    *out = blocks * cus;
+    return 0;
 }
 void launch_chess_ext_begin(const ChessParams &p, hipStream_t s) {
     hipLaunchKernelGGL(chess_ext_begin_kernel, dim3(p.n_games), dim3(64), 0, s, p);

@@ -818,6 +818,109 @@ int zc_chess_search_async(zc_engine *eng, int32_t first, int32_t n, const zc_che
     return ZC_OK;
 }
 
+}  // extern "C"
+
+namespace {
+int check_play_buffers(int32_t n, const zc_chess_play_buffers *b) {
+    if (!b) return fail(ZC_EINVAL, "null play buffers");
+    if (n && (!b->d_roots || !b->d_init || !b->d_hist || !b->d_hist_len || !b->d_err))
+        return fail(ZC_EINVAL, "null play buffer");
+    if (b->hist_cap < 1 || b->hist_cap > 4096) return fail(ZC_EINVAL, "hist_cap %d outside [1, 4096]", b->hist_cap);
+    return ZC_OK;
+}
+zc::ChessPlayParams play_params(const zc_chess_play_buffers *b) {
+    zc::ChessPlayParams q{};
+    q.roots = b->d_roots;
+    q.init = b->d_init;
+    q.hist = b->d_hist;
+    q.hlen = b->d_hist_len;
+    q.cap = b->hist_cap;
+    q.err = b->d_err;
+    return q;
+}
+int chess_selfplay_common(zc_engine *eng, int32_t first, int32_t n, const zc_chess_play_buffers *b, int32_t sims,
+                          double c, int32_t bs, int32_t policy, double freedom, int32_t moves, int64_t budget,
+                          int32_t *d_ticket, zc_chess_state *d_out_states, uint16_t *d_out_moves,
+                          int32_t *d_out_results, zc_game_stats *d_stats, void *hip_stream) {
+    if (!eng || (n && (!d_out_states || !d_out_moves || !d_out_results || !d_stats))) return fail(ZC_EINVAL, "null argument");
+    if (int r = check_play_buffers(n, b)) return r;
+    if (int r = check_chess(eng, first, n, sims, c, bs, policy, freedom)) return r;
+    if (bs > 256) return fail(ZC_EINVAL, "batch_size %d > 256 (crude-score chess search)", bs);
+    if (moves < 1) return fail(ZC_EINVAL, "moves must be >= 1 (got %d)", moves);
+    if (d_ticket && (budget < 0 || budget > (int64_t)moves * n || budget >= ((int64_t)1 << 31)))
+        return fail(ZC_EINVAL, "budget %lld outside [0, moves_cap x n_games] or >= 2^31", (long long)budget);
+    if (!n) return ZC_OK;
+    std::lock_guard<std::mutex> lk(eng->mu);
+    ZC_HIP(hipSetDevice(eng->cfg.device));
+    if (int r = ensure_chess(eng)) return r;
+    hipStream_t s = (hipStream_t)hip_stream;
+    if (d_ticket) {
+        int resident = 0;
+        if (zc::chess_selfplay_resident_games(b->hist_cap, &resident)) return fail(ZC_EHIP, "occupancy query failed");
+        if (n > resident)
+            return fail(ZC_EINVAL, "pooled chess self-play of %d games: at most %d are resident at once", n, resident);
+        ZC_HIP(hipMemsetAsync(d_ticket, 0, 2 * sizeof(int32_t), s));
+    }
+    zc::ChessParams p = chess_params(eng, first, n, sims, c, bs, policy, freedom);
+    p.roots = b->d_roots;
+    zc::ChessPlayParams q = play_params(b);
+    q.out_states = d_out_states;
+    q.out_moves = d_out_moves;
+    q.out_results = d_out_results;
+    q.moves = moves;
+    q.ticket = d_ticket;
+    q.budget = (int32_t)budget;
+    q.stats = d_stats;
+    zc::launch_chess_selfplay(p, q, s);
+    ZC_HIP(hipGetLastError());
+    return ZC_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int zc_chess_play_step_async(int32_t n, const zc_chess_play_buffers *b, const uint16_t *d_moves,
+                             const zc_game_stats *d_search_stats, zc_chess_state *d_out_states,
+                             int32_t *d_out_results, void *hip_stream) {
+    if (n < 0 || (n && (!d_moves || !d_out_states || !d_out_results))) return fail(ZC_EINVAL, "bad argument");
+    if (int r = check_play_buffers(n, b)) return r;
+    if (!n) return ZC_OK;
+    zc::ChessPlayParams q = play_params(b);
+    q.in_moves = d_moves;
+    q.search_stats = d_search_stats;
+    q.out_states = d_out_states;
+    q.out_results = d_out_results;
+    zc::launch_chess_play_step(q, n, (hipStream_t)hip_stream);
+    ZC_HIP(hipGetLastError());
+    return ZC_OK;
+}
+
+int zc_chess_selfplay_async(zc_engine *eng, int32_t first, int32_t n, const zc_chess_play_buffers *b, int32_t sims,
+                            double c, int32_t bs, int32_t policy, double freedom, int32_t moves,
+                            zc_chess_state *d_out_states, uint16_t *d_out_moves, int32_t *d_out_results,
+                            zc_game_stats *d_stats, void *hip_stream) {
+    return chess_selfplay_common(eng, first, n, b, sims, c, bs, policy, freedom, moves, 0, nullptr, d_out_states,
+                                 d_out_moves, d_out_results, d_stats, hip_stream);
+}
+
+int zc_chess_selfplay_pooled_async(zc_engine *eng, int32_t first, int32_t n, const zc_chess_play_buffers *b,
+                                   int32_t sims, double c, int32_t bs, int32_t policy, double freedom,
+                                   int32_t moves_cap, int64_t budget, int32_t *d_ticket, zc_chess_state *d_out_states,
+                                   uint16_t *d_out_moves, int32_t *d_out_results, zc_game_stats *d_stats,
+                                   void *hip_stream) {
+    if (n && !d_ticket) return fail(ZC_EINVAL, "null argument");
+    return chess_selfplay_common(eng, first, n, b, sims, c, bs, policy, freedom, moves_cap, budget, d_ticket,
+                                 d_out_states, d_out_moves, d_out_results, d_stats, hip_stream);
+}
+
+int zc_chess_pooled_max_games(int32_t hist_cap, int32_t *out) {
+    if (!out || hist_cap < 1 || hist_cap > 4096) return fail(ZC_EINVAL, "bad argument");
+    int r = 0;
+    if (zc::chess_selfplay_resident_games(hist_cap, &r)) return fail(ZC_EHIP, "occupancy query failed");
+    *out = r;
+    return ZC_OK;
+}
+
 int zc_chess_ext_begin(zc_engine *eng, int32_t first, int32_t n, const zc_chess_state *d_roots, int32_t sims, double c,
                        int32_t bs, int32_t policy, double freedom, void *hip_stream) {
     if (!eng || (n && !d_roots)) return fail(ZC_EINVAL, "null argument");

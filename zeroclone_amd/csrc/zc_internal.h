@@ -274,6 +274,29 @@ void launch_gen_expand(const GenParams &p, int local, int child_moves, hipStream
 void launch_gen_backup(const GenParams &p, int nb, const double *values, hipStream_t s);
 void launch_gen_end(const GenParams &p, int32_t *out, int32_t *root_na, int na_cap, hipStream_t s);
 
+// Chess self-play steps (chess_search.hip): Engine.play_move + _evaluate on the device, the
+// move histories of the repetition draw in HBM, the refill of finished games.
+struct ChessPlayParams {
+    zc_chess_state *roots;        // [n] the positions to move from; updated (post-move or init)
+    const zc_chess_state *init;   // the opening
+    uint16_t *hist;               // [n][2][cap] each side's moves in play order
+    int32_t *hlen;                // [n][2]
+    int cap;
+    int32_t *err;                 // [3] history overflow | search out of capacity | no move
+    const uint16_t *in_moves;     // lockstep step: the searched moves [n]
+    const zc_game_stats *search_stats;  // lockstep step (optional): the search's statuses [n]
+    zc_chess_state *out_states;   // [moves][n] post-move positions
+    uint16_t *out_moves;          // [moves][n]
+    int32_t *out_results;         // [moves][n]
+    int moves;
+    int32_t *ticket;              // pooled: moves drawn while ticket[0] < budget; ticket[1] = most moves
+    int32_t budget;
+    zc_game_stats *stats;         // self-play launch: per-game sums
+};
+void launch_chess_play_step(const ChessPlayParams &q, int n, hipStream_t s);
+void launch_chess_selfplay(const ChessParams &p, const ChessPlayParams &q, hipStream_t s);
+int chess_selfplay_resident_games(int cap, int *out);
+
 void launch_chess_search(const ChessParams &p, hipStream_t s);     // crude_chess_score, whole move
 void launch_chess_ext_begin(const ChessParams &p, hipStream_t s);
 void launch_chess_ext_select(const ChessParams &p, hipStream_t s);

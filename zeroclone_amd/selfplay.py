@@ -191,12 +191,16 @@ class Trajectories:
 class C4SelfPlay:
     """Connect4 self-play pool on one GPU: search (zc_c4_search_async) + play/evaluate
     (zc_c4_play_async) + trajectory recording (zc_traj_record_async), all stream-ordered,
-    no host synchronisation per step."""
+    no host synchronisation per step.  With `net=` the search takes its leaf values from a
+    value network (C4ValuedSearch, C2(iii)); with `puct_net=` it is the PUCT search with a
+    policy + value network (C4PuctSearch, SURVEY §8 a21), moves sampled at `temperature`;
+    both step() only (the network runs between kernels) and capture_step() into one graph."""
 
     MAX_LEN = 43   # the opening + at most 42 moves
 
     def __init__(self, games: int, sims: int, c: float = 1.4, batch_size: int = 32, seed: int = 0,
-                 rank: int = 0, device: int = 0, record: bool = True, games_cap: int | None = None):
+                 rank: int = 0, device: int = 0, record: bool = True, games_cap: int | None = None,
+                 net=None, puct_net=None, temperature: float = 1.0, puct_seed: int = 1):
         self.G, self.sims, self.c, self.bs = games, sims, c, batch_size
         self.dev = torch.device("cuda", device) if isinstance(device, int) else torch.device(device)
         self.eng = _native.NativeEngine(max_games=games, max_sims=sims, max_batch=batch_size,
@@ -215,6 +219,16 @@ class C4SelfPlay:
             cap = games_cap or max(8 * games, 1024)
             self.traj = Trajectories(games, torch.zeros(24, dtype=torch.uint8), self.MAX_LEN, cap,
                                      cap * self.MAX_LEN, self.dev)
+        self.vs = self.value_fn = self.ps = self.net_fn = None
+        self.temperature = float(temperature)
+        if net is not None:
+            from .valued import C4ValuedSearch, NetValue
+            self.vs = C4ValuedSearch(self.eng, games, batch_size, leaves=False)
+            self.value_fn = NetValue(net)
+        if puct_net is not None:
+            from .valued import C4PuctSearch
+            self.ps = C4PuctSearch(self.eng, games, batch_size, seed=puct_seed, leaves=False)
+            self.net_fn = lambda leaves, planes, counts: puct_net(planes)
 
     def start(self, quota: int | None = None):
         """Every slot back to the opening; with a quota, slots beyond it idle and finished
@@ -239,6 +253,8 @@ class C4SelfPlay:
         Returns the per-step results [moves, G]; self.stats sums the moves' counters."""
         if self.traj is not None and self.traj.quota != _UNLIMITED:
             raise ValueError("run() plays without a game quota; use step() under simulate_games' quota")
+        if self.vs is not None or self.ps is not None:
+            raise ValueError("run() fuses the rollout search; network modes step()")
         s = stream if stream is not None else torch.cuda.current_stream(self.dev).cuda_stream
         if getattr(self, "_run_k", None) != moves:
             self._run_states = torch.zeros((moves, self.G, 3), dtype=torch.int64, device=self.dev)
@@ -265,6 +281,8 @@ class C4SelfPlay:
         Returns the per-step results [moves_cap, G]; self.stats sums the moves' counters."""
         if self.traj is not None and self.traj.quota != _UNLIMITED:
             raise ValueError("run_pooled() plays without a game quota; use step() under simulate_games' quota")
+        if self.vs is not None or self.ps is not None:
+            raise ValueError("run_pooled() fuses the rollout search; network modes step()")
         s = stream if stream is not None else torch.cuda.current_stream(self.dev).cuda_stream
         if getattr(self, "_run_k", None) != moves_cap:
             self._run_states = torch.zeros((moves_cap, self.G, 3), dtype=torch.int64, device=self.dev)
@@ -288,9 +306,33 @@ class C4SelfPlay:
         """The search half of a step (zc_c4_search_async); returns the results tensor the
         finish half will fill."""
         s = stream if stream is not None else torch.cuda.current_stream(self.dev).cuda_stream
+        if self.ps is not None or self.vs is not None:
+            if self.ps is not None:
+                mv, _, st = self.ps.enqueue(self.roots, self.sims, self.net_fn, temperature=self.temperature)
+            else:
+                mv, _, st = self.vs.enqueue(self.roots, self.sims, self.c, self.value_fn)
+            self.moves.copy_(mv)
+            self.stats.copy_(st)
+            return self.results
         self.eng.c4_search_async(self.roots.data_ptr(), self.G, self.sims, self.c, self.bs, self.moves.data_ptr(),
                                  self.na.data_ptr(), self.stats.data_ptr(), stream=s)
         return self.results
+
+    def capture_step(self):
+        """One whole step (search with its network, play, record) as a HIP graph; each
+        replay plays the next move of every game."""
+        side = torch.cuda.Stream(self.dev)
+        side.wait_stream(torch.cuda.current_stream(self.dev))
+        with torch.cuda.stream(side):   # the network's kernels warmed outside the capture
+            if self.ps is not None:
+                self.net_fn(None, self.ps.planes, self.ps.counts)
+            elif self.vs is not None:
+                self.value_fn(None, self.vs.planes, self.vs.counts)
+        torch.cuda.current_stream(self.dev).wait_stream(side)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self.step()
+        return g
 
     def step_finish(self, stream: int | None = None) -> torch.Tensor:
         """Play + evaluate the searched moves, record the positions, refill finished games."""
@@ -341,21 +383,25 @@ def _host_games(b: TrajBatch, first_id: int, move_fn):
 
 class ChessSelfPlay:
     """Device-resident chess self-play: the chess form of `C4SelfPlay`.  G games live on one
-    GPU as zc_chess_state rows; one `step()` searches every game (Value('crude_chess_score')
-    in the search kernel, or a value network between the stepwise select and backup
-    kernels), plays the chosen moves (zc_chess_play_async), tests the new positions
-    (zc_chess_terminal_async: check_win, stalemate, fifty-move rule) and both sides' move
-    histories (zc_chess_repetition_async: the repetition half of check_draw,
-    chess_backend.cpp:416-441) on the device, and records the games (zc_traj_record_async:
-    results by Engine._evaluate, engine.py:148-153; finished games restart from the initial
-    position).  Nothing is read back per step; errors (a game longer than the history
-    capacity, a search out of tree capacity, no move at a live root) are collected on the
-    device and raised by `check()` / `take()`."""
+    GPU as zc_chess_state rows; one `step()` searches every game — Value('crude_chess_score')
+    in the search kernel, a value network between the stepwise select and backup kernels
+    (`net=`), or the PUCT search with a policy + value network (`puct_net=`)
+    — then ONE kernel plays the chosen moves, tests the new positions (check_win, stalemate,
+    the fifty-move rule) and both sides' move histories (the repetition half of check_draw,
+    chess_backend.cpp:416-441; histories in HBM) and refills finished games
+    (zc_chess_play_step_async), and the recorder pools the finished games
+    (zc_traj_record_async: Engine._evaluate's results, engine.py:148-153).  With the crude
+    score, `run(K)` / `run_pooled(budget, cap)` play K moves per game (or a shared budget) in
+    ONE launch (zc_chess_selfplay*_async) — the same games as K steps.  Nothing is read back
+    per step; errors (a game longer than the history capacity, a search out of tree
+    capacity, no move at a live root) are collected on the device and raised by `check()` /
+    `take()`.  `capture_step()` records a whole step (search, network, play, record) in one
+    HIP graph."""
 
     def __init__(self, games: int, sims: int, c: float = 1.4, batch_size: int = 32, seed: int = 0,
                  rank: int = 0, device: int = 0, policy: int = _native.ZC_POLICY_IMMEDIATE_VALUE,
                  freedom: float = 3.0, net=None, init_fen: str | None = None, games_cap: int | None = None,
-                 hist_cap: int = 1024):
+                 hist_cap: int = 1024, puct_net=None, temperature: float = 1.0, puct_seed: int = 1):
         self.G, self.sims, self.c, self.bs = games, sims, c, batch_size
         self.policy, self.freedom = int(policy), float(freedom)
         self.dev = torch.device("cuda", device) if isinstance(device, int) else torch.device(device)
@@ -366,26 +412,31 @@ class ChessSelfPlay:
         self.eng.seed(0, [seed + self.first_id + g for g in range(games)])
         init = _native.chess_from_fen(init_fen) if init_fen else _native.chess_init()
         self.init_row = torch.from_numpy(np.frombuffer(init.tobytes(), np.uint8).reshape(1, 72).copy()).to(self.dev)
-        self.init_turn = int(np.asarray(init["turn"]).reshape(-1)[0])
         self.roots = self.init_row.repeat(games, 1).contiguous()
         self.moves = torch.zeros(games, dtype=torch.int16, device=self.dev)
         self.na = torch.zeros((games, _native.CHESS_MAX_MOVES), dtype=torch.int32, device=self.dev)
         self.stats = torch.zeros((games, _native.STATS_FIELDS), dtype=torch.int64, device=self.dev)
-        self.flags = torch.zeros(games, dtype=torch.int32, device=self.dev)
+        self.post = torch.zeros_like(self.roots)
         self.results = torch.zeros(games, dtype=torch.int32, device=self.dev)
-        self.vs = self.value_fn = None
+        self.vs = self.value_fn = self.ps = self.net_fn = None
+        self.temperature = float(temperature)
         if net is not None:
             from .valued import ChessValuedSearch, NetValue
             self.vs = ChessValuedSearch(self.eng, games, batch_size, leaves=False, policy=self.policy,
                                         freedom=self.freedom)
             self.value_fn = NetValue(net)
+        if puct_net is not None:
+            from .valued import ChessPuctSearch
+            self.ps = ChessPuctSearch(self.eng, games, batch_size, seed=puct_seed, leaves=False)
+            self.net_fn = lambda leaves, planes, counts: puct_net(planes)
         self.hist_cap = hist_cap  # moves per side
         self.hist = torch.zeros((games, 2, self.hist_cap), dtype=torch.int16, device=self.dev)
         self.hlen = torch.zeros((games, 2), dtype=torch.int32, device=self.dev)
-        self.turn = torch.full((games,), self.init_turn, dtype=torch.int64, device=self.dev)
-        self.rep = torch.zeros(games, dtype=torch.int32, device=self.dev)
         self.err = torch.zeros(3, dtype=torch.int32, device=self.dev)
-        self._slots = torch.arange(games, device=self.dev)
+        b = _native.ChessPlayBuffers()
+        b.d_roots, b.d_init, b.d_hist = self.roots.data_ptr(), self.init_row.data_ptr(), self.hist.data_ptr()
+        b.d_hist_len, b.hist_cap, b.d_err = self.hlen.data_ptr(), self.hist_cap, self.err.data_ptr()
+        self._pb = b
         max_len = 2 * self.hist_cap + 1
         cap = games_cap or max(8 * games, 1024)
         self.traj = Trajectories(games, self.init_row[0], max_len, cap, cap * 160, self.dev)
@@ -393,38 +444,95 @@ class ChessSelfPlay:
     def start(self, quota: int | None = None):
         self.roots.copy_(self.init_row.expand_as(self.roots))
         self.hlen.zero_()
-        self.turn.fill_(self.init_turn)
         self.traj.start(quota, games_cap=quota)
+
+    def _stream(self, stream):
+        return stream if stream is not None else torch.cuda.current_stream(self.dev).cuda_stream
 
     def step(self, stream: int | None = None) -> torch.Tensor:
         """One move for every game; returns the per-game results tensor (ONGOING = 2,
         IDLE = 3).  Finished games restart from the initial position."""
-        s = stream if stream is not None else torch.cuda.current_stream(self.dev).cuda_stream
-        if self.vs is None:
+        s = self._stream(stream)
+        if self.ps is not None:
+            mv, _, st = self.ps.enqueue(self.roots, self.sims, self.net_fn, temperature=self.temperature)
+        elif self.vs is not None:
+            mv, _, st = self.vs.enqueue(self.roots, self.sims, self.c, self.value_fn)
+        else:
             self.eng.chess_search_async(0, self.G, self.roots.data_ptr(), self.sims, self.c, self.bs, self.policy,
                                         self.freedom, self.moves.data_ptr(), self.na.data_ptr(),
                                         self.stats.data_ptr(), s)
-        else:
-            mv, _, st = self.vs.run(self.roots, self.sims, self.c, self.value_fn)
+            mv, st = self.moves, self.stats
+        if mv is not self.moves:
             self.moves.copy_(mv)
             self.stats.copy_(st)
-        self.eng.chess_play_async(self.G, self.roots.data_ptr(), self.moves.data_ptr(), self.roots.data_ptr(), s)
-        self.eng.chess_terminal_async(self.G, self.roots.data_ptr(), self.flags.data_ptr(), s)
-        # play_move's history push (the mover's deque), then both sides' repetition test
-        at = self.hlen[self._slots, self.turn].clamp(max=self.hist_cap - 1).long()
-        self.hist[self._slots, self.turn, at] = self.moves
-        self.hlen[self._slots, self.turn] += 1
-        self.turn ^= 1
-        _native.check(_native.lib().zc_chess_repetition_async(self.G, self.hist_cap, self.hist.data_ptr(),
-                                                              self.hlen.data_ptr(), self.rep.data_ptr(), s))
-        self.err[0] |= (self.hlen > self.hist_cap).any().to(torch.int32)
-        self.err[1] |= (self.stats[:, 5] == _native.ZC_STATUS_CAPACITY).any().to(torch.int32)
-        self.err[2] |= (self.moves == -1).any().to(torch.int32)
-        self.traj.record(self.roots.data_ptr(), self.moves, self.results, flags=self.flags, rep=self.rep, stream=s)
-        live = (self.results == ONGOING)
-        self.hlen *= live.to(torch.int32)[:, None]
-        self.turn = torch.where(live, self.turn, torch.full_like(self.turn, self.init_turn))
+        _native.check(_native.lib().zc_chess_play_step_async(
+            self.G, ctypes.byref(self._pb), ctypes.c_void_p(self.moves.data_ptr()),
+            ctypes.c_void_p(self.stats.data_ptr()), ctypes.c_void_p(self.post.data_ptr()),
+            ctypes.c_void_p(self.results.data_ptr()), ctypes.c_void_p(s)))
+        self.traj.record(self.post.data_ptr(), self.moves, self.results, stream=s)
         return self.results
+
+    def capture_step(self):
+        """One whole step (search with its network, play, record) as a HIP graph; each
+        replay plays the next move of every game."""
+        side = torch.cuda.Stream(self.dev)
+        side.wait_stream(torch.cuda.current_stream(self.dev))
+        with torch.cuda.stream(side):   # the network's kernels warmed outside the capture
+            if self.ps is not None:
+                self.net_fn(None, self.ps.planes, self.ps.counts)
+            elif self.vs is not None:
+                self.value_fn(None, self.vs.planes, self.vs.counts)
+        torch.cuda.current_stream(self.dev).wait_stream(side)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self.step()
+        return g
+
+    def _run_buffers(self, moves: int):
+        if getattr(self, "_run_k", None) != moves:
+            self._run_states = torch.zeros((moves, self.G, 72), dtype=torch.uint8, device=self.dev)
+            self._run_moves = torch.zeros((moves, self.G), dtype=torch.int16, device=self.dev)
+            self._run_results = torch.zeros((moves, self.G), dtype=torch.int32, device=self.dev)
+            self._run_k = moves
+
+    def run(self, moves: int, stream: int | None = None, kernel_done=None) -> torch.Tensor:
+        """Crude score: `moves` moves for every game in ONE launch (zc_chess_selfplay_async),
+        then the multi-step recording — the same games, pool and labels as `moves` calls of
+        step().  Returns the per-step results [moves, G]; self.stats sums the moves."""
+        return self._launch(moves, None, stream, kernel_done)
+
+    def run_pooled(self, budget: int, moves_cap: int, stream: int | None = None, kernel_done=None) -> torch.Tensor:
+        """Crude score: `budget` moves shared by the games in ONE launch (at most moves_cap
+        each; a throughput schedule, the reference's train.py is lockstep).  Game i's k-th
+        move is the k-th move run() would play."""
+        return self._launch(moves_cap, budget, stream, kernel_done)
+
+    def _launch(self, moves, budget, stream, kernel_done):
+        if self.vs is not None or self.ps is not None:
+            raise ValueError("run()/run_pooled() fuse the crude-score search; network modes step()")
+        if self.traj.quota != _UNLIMITED:
+            raise ValueError("run() plays without a game quota; use step() under simulate_games' quota")
+        s = self._stream(stream)
+        self._run_buffers(moves)
+        args = [self.eng.handle, 0, self.G, ctypes.byref(self._pb), self.sims, self.c, self.bs, self.policy,
+                self.freedom, moves]
+        outs = [ctypes.c_void_p(self._run_states.data_ptr()), ctypes.c_void_p(self._run_moves.data_ptr()),
+                ctypes.c_void_p(self._run_results.data_ptr()), ctypes.c_void_p(self.stats.data_ptr()),
+                ctypes.c_void_p(s)]
+        reached = None
+        if budget is None:
+            _native.check(_native.lib().zc_chess_selfplay_async(*args, *outs))
+        else:
+            if getattr(self, "_ticket", None) is None:
+                self._ticket = torch.zeros(2, dtype=torch.int32, device=self.dev)
+            reached = self._ticket[1:]
+            _native.check(_native.lib().zc_chess_selfplay_pooled_async(
+                *args, int(budget), ctypes.c_void_p(self._ticket.data_ptr()), *outs))
+        if kernel_done is not None:
+            kernel_done.record()
+        self.traj.record_steps(self._run_states.data_ptr(), self._run_moves, self._run_results, moves,
+                               reached=reached, stream=s)
+        return self._run_results
 
     def check(self):
         e = self.err.cpu().tolist()
