@@ -231,146 +231,150 @@ def cpu_baseline_chess_puct(sims: int = 1600, bs: int = 32, c: float = 1.5, budg
 MFMA_F16_PEAK_TFLOPS = 2500.0  # MI355X dense fp16 MFMA peak, ~2.5 PF (MI355X_MICROARCH.md; no sparsity)
 
 
-def net_mode(games: int, sims: int, bs: int, c: float, steps: int, dev) -> dict:
-    """C2(iii): the same search with a random-init value network instead of rollouts
-    (stepwise search zc_c4_ext_*, fp16 ValueNetwork(128, 8, in_planes=2) between the select
-    and backup kernels of every flush), one move per step captured in a HIP graph."""
-    from zeroclone_amd.nets import ValueNetwork, flops_per_position, for_inference
-    from zeroclone_amd.valued import C4ValuedSearch, NetValue
-    torch.manual_seed(0)
-    model = for_inference(ValueNetwork(128, 8, in_planes=2).eval(), dev, torch.float16)
-    eng = _native.NativeEngine(max_games=games, max_sims=sims, max_batch=bs, device=dev.index)
-    eng.seed(0, list(range(games)))
-    vs = C4ValuedSearch(eng, games, bs, leaves=False)
-    roots = torch.zeros((games, 3), dtype=torch.int64, device=dev)
-    g = vs.capture(roots, sims, c, NetValue(model))
-    g.replay()   # warm-up move
-    torch.cuda.synchronize(dev)
-    exp = 0
+def _timed_pool_steps(pool, steps: int, warm: int = 1):
+    """Steady-state network-mode self-play: the pool's whole step (search with its network
+    between the select and backup kernels, play, record) captured as one HIP graph, `warm`
+    untimed replays, then `steps` timed replays.  Returns (expansions, seconds) — the
+    expansions from the pool's device totals (no per-step host read)."""
+    g = pool.capture_step()
+    for _ in range(warm):
+        g.replay()
+    torch.cuda.synchronize(pool.dev)
+    pool.totals.zero_()
     t = time.perf_counter()
     for _ in range(steps):
         g.replay()
-        exp += int(vs.stats[:, 0].sum().item())
+    torch.cuda.synchronize(pool.dev)
     dt = time.perf_counter() - t
-    flushes = (sims + bs - 1) // bs
-    fl = flops_per_position(128, 8, 2, 6, 7) * games * bs * flushes * steps
-    eng.close()
+    exp = int(pool.totals[0].item())
+    return exp, dt
+
+
+MIXED = "steady-state self-play: the pool adopts a burned-in pool's games in progress (mixed ages), "
+
+
+def net_mode(src, games: int, sims: int, bs: int, c: float, steps: int, dev) -> dict:
+    """C2(iii): Connect4 self-play whose search takes its leaf values from a random-init
+    value network (stepwise search zc_c4_ext_*, fp16 ValueNetwork(128, 8, in_planes=2) on
+    this package's MFMA tower between the select and backup kernels of every flush), from the
+    burned-in rollout pool's positions; `steps` timed moves."""
+    from zeroclone_amd.nets import ValueNetwork, flops_per_position, for_inference
+    from zeroclone_amd.selfplay import C4SelfPlay
+    torch.manual_seed(0)
+    model = for_inference(ValueNetwork(128, 8, in_planes=2).eval(), dev, torch.float16)
+    pool = C4SelfPlay(games, sims, c=c, batch_size=bs, seed=7, device=dev.index, net=model)
+    pool.adopt(src)
+    exp, dt = _timed_pool_steps(pool, steps)
+    pool.close()
+    fl = flops_per_position(128, 8, 2, 6, 7) * games * bs * ((sims + bs - 1) // bs) * steps
     return {"value": round(exp / dt, 1), "unit": "expansions/s", "ms_per_move": round(dt / steps * 1e3, 1),
+            "steps": steps, "config": MIXED + f"{games} games x {sims} sims, batch {bs}",
             "net": "ValueNetwork(128, 8, in_planes=2) random init, fp16, BN folded, this package's MFMA conv kernels",
             "net_tflops_lower": round(fl / dt / 1e12, 1),
             "mfma_frac_lower": round(fl / dt / 1e12 / MFMA_F16_PEAK_TFLOPS, 4),
-            "note": "TFLOP/s = network FLOPs / whole move time (search kernels included), so a lower bound "
-                    "on the network's own rate; stepwise search, per-flush leaf planes built on the device"}
+            "note": "TFLOP/s = network FLOPs / whole step time (search, play and record included), so a lower "
+                    "bound on the network's own rate; one HIP graph per step"}
 
 
-def chess_modes(steps: int, dev) -> dict:
-    """BASELINE configs[3] (C4): chess, 1024 games, 400 sims/move — the crude-score search
-    (configs/crude_chess.yaml, value in the kernel) and the value-network search
-    (configs/chess_value.yaml: ValueNetwork(128, 8) random init, fp16, one move per HIP graph)."""
-    import numpy as np
-    from zeroclone_amd.nets import ValueNetwork, flops_per_position, for_inference
-    from zeroclone_amd.valued import ChessValuedSearch, NetValue
-    G, S, B = 1024, 400, 32
-    eng = _native.NativeEngine(max_games=G, max_sims=S, max_batch=B, device=dev.index)
-    eng.seed(0, list(range(G)))
-    rows = np.array([_native.chess_init()] * G, _native.CHESS_STATE_DTYPE).view(np.uint8).reshape(G, 72)
-    roots = torch.from_numpy(rows.copy()).to(dev)
-    mv = torch.zeros(G, dtype=torch.int16, device=dev)
-    na = torch.zeros((G, _native.CHESS_MAX_MOVES), dtype=torch.int32, device=dev)
-    st = torch.zeros((G, _native.STATS_FIELDS), dtype=torch.int64, device=dev)
-    s = torch.cuda.current_stream(dev).cuda_stream
-    crude = lambda: eng.chess_search_async(0, G, roots.data_ptr(), S, 1.4, B, _native.ZC_POLICY_IMMEDIATE_VALUE,  # noqa
-                                           3.0, mv.data_ptr(), na.data_ptr(), st.data_ptr(), s)
-    crude()
-    torch.cuda.synchronize(dev)
-    t = time.perf_counter()
-    exp = 0
-    for _ in range(steps):
-        crude()
-        exp += int(st[:, 0].sum().item())
-    dt = time.perf_counter() - t
-    out = {"crude": {"value": round(exp / dt, 1), "unit": "expansions/s", "ms_per_move": round(dt / steps * 1e3, 2),
-                     "config": "1024 games x 400 sims, crude_chess_score, immediate_value(3), from the opening"}}
-    torch.manual_seed(0)
-    model = for_inference(ValueNetwork(128, 8).eval(), dev, torch.float16)
-    vs = ChessValuedSearch(eng, G, B, leaves=False)
-    g = vs.capture(roots, S, 1.4, NetValue(model))
-    g.replay()
-    torch.cuda.synchronize(dev)
-    t = time.perf_counter()
-    exp = 0
-    for _ in range(steps):
-        g.replay()
-        exp += int(vs.stats[:, 0].sum().item())
-    dt = time.perf_counter() - t
-    fl = flops_per_position(128, 8, 17, 8, 8) * G * B * ((S + B - 1) // B) * steps
-    out["value_net"] = {"value": round(exp / dt, 1), "unit": "expansions/s", "ms_per_move": round(dt / steps * 1e3, 1),
-                        "config": "1024 games x 400 sims, ValueNetwork(128, 8) random init fp16 (MFMA kernels), random policy",
-                        "net_tflops_lower": round(fl / dt / 1e12, 1),
-                        "mfma_frac_lower": round(fl / dt / 1e12 / MFMA_F16_PEAK_TFLOPS, 4)}
-    eng.close()
-    return out
-
-
-def puct_mode(steps: int, dev) -> dict:
-    """BASELINE configs[4] (C5) per GPU: chess PUCT self-play search, 1024 games x 1600 sims,
-    policy + value ResNet (128 x 8, random init, fp16; tower on the MFMA kernels), Dirichlet
-    root noise, one move per HIP graph."""
-    import numpy as np
+def c4_puct_mode(src, games: int, sims: int, bs: int, steps: int, dev) -> dict:
+    """C2 with the PUCT extension (SURVEY §8 a21 on the target game): Connect4 self-play,
+    4096 games x 800 sims, policy (7 column logits) + value ResNet 128x8 random init fp16 on
+    the MFMA tower, Dirichlet root noise (fresh per move: per-game search numbers),
+    temperature 1, from the burned-in rollout pool's positions."""
     from zeroclone_amd.nets import MfmaPolicyValueNetwork, PolicyValueNetwork, flops_per_position
-    from zeroclone_amd.valued import ChessPuctSearch
-    G, S, B = 1024, 1600, 32
-    eng = _native.NativeEngine(max_games=G, max_sims=S, max_batch=B, device=dev.index)
-    rows = np.array([_native.chess_init()] * G, _native.CHESS_STATE_DTYPE).view(np.uint8).reshape(G, 72)
-    roots = torch.from_numpy(rows.copy()).to(dev)
+    from zeroclone_amd.selfplay import C4SelfPlay
     torch.manual_seed(0)
-    net = MfmaPolicyValueNetwork(PolicyValueNetwork().eval(), dev)
-    ps = ChessPuctSearch(eng, G, B, seed=1, leaves=False)
-    fn = lambda leaves, planes, counts: net(planes)  # noqa: E731
-    g = ps.capture(roots, S, fn, temperature=1.0)
-    g.replay()
-    torch.cuda.synchronize(dev)
-    t = time.perf_counter()
-    exp = 0
-    for _ in range(steps):
-        g.replay()
-        exp += int(ps.stats[:, 0].sum().item())
-    dt = time.perf_counter() - t
-    nfl = _native.check(_native.lib().zc_chess_puct_flushes(S, B))
-    fl = flops_per_position(128, 8, 17, 8, 8) * G * B * nfl * steps
-    eng.close()
+    net = MfmaPolicyValueNetwork(PolicyValueNetwork(in_planes=2, board=(6, 7), n_logits=7).eval(), dev)
+    pool = C4SelfPlay(games, sims, batch_size=bs, seed=7, device=dev.index, puct_net=net, temperature=1.0)
+    pool.adopt(src)
+    exp, dt = _timed_pool_steps(pool, steps)
+    pool.close()
+    nfl = _native.check(_native.lib().zc_chess_puct_flushes(sims, bs))
+    fl = flops_per_position(128, 8, 2, 6, 7) * games * bs * nfl * steps
     return {"value": round(exp / dt, 1), "unit": "expansions/s", "ms_per_move": round(dt / steps * 1e3, 1),
-            "config": "C5 per GPU: 1024 games x 1600 sims, PUCT c 1.5, Dirichlet(0.3, 0.25), policy+value ResNet "
-                      "128x8 random init fp16 (MFMA tower), temperature 1",
+            "steps": steps,
+            "config": MIXED + f"C2 + PUCT: {games} games x {sims} sims, c_puct 1.5, Dirichlet(0.3, 0.25), policy "
+                              "(7 logits) + value ResNet 128x8 random init fp16 (MFMA tower), temperature 1",
             "net_tflops_lower": round(fl / dt / 1e12, 1), "mfma_frac_lower": round(fl / dt / 1e12 / MFMA_F16_PEAK_TFLOPS, 4)}
 
 
-def c4_puct_mode(games: int, sims: int, bs: int, steps: int, dev) -> dict:
-    """C2 with the PUCT extension (SURVEY §8 a21 on the target game): 4096 games x 800 sims,
-    policy (7 column logits) + value ResNet 128x8 random init fp16 on the MFMA tower,
-    Dirichlet root noise, temperature 1, one move per HIP graph."""
-    from zeroclone_amd.nets import MfmaPolicyValueNetwork, PolicyValueNetwork, flops_per_position
-    from zeroclone_amd.valued import C4PuctSearch
-    eng = _native.NativeEngine(max_games=games, max_sims=sims, max_batch=bs, device=dev.index)
-    roots = torch.zeros((games, 3), dtype=torch.int64, device=dev)
-    torch.manual_seed(0)
-    net = MfmaPolicyValueNetwork(PolicyValueNetwork(in_planes=2, board=(6, 7), n_logits=7).eval(), dev)
-    ps = C4PuctSearch(eng, games, bs, seed=1, leaves=False)
-    g = ps.capture(roots, sims, lambda leaves, planes, counts: net(planes), temperature=1.0)
-    g.replay()
+def chess_burned_pool(dev, games: int = 1024, sims: int = 400, bs: int = 32, max_moves: int = 600):
+    """The crude-score chess pool (configs/crude_chess.yaml: immediate_value(3)) run with the
+    fused self-play launch until every slot has finished a game and started another (or
+    max_moves): the mixed-age roots of the chess modes."""
+    from zeroclone_amd.selfplay import ChessSelfPlay
+    pool = ChessSelfPlay(games, sims, batch_size=bs, seed=3, device=dev.index)
+    moves = 0
+    while moves < max_moves:
+        pool.run(25)
+        moves += 25
+        if int(pool.traj.slot[:, 1].min().item()) >= games:
+            break
+    pool.take()
+    return pool, moves
+
+
+def chess_modes(steps: int, dev) -> dict:
+    """BASELINE configs[3] (C4): chess self-play, 1024 games, 400 sims/move — the crude-score
+    search (configs/crude_chess.yaml, value in the kernel; the fused pooled launch) and the
+    value-network search (configs/chess_value.yaml: ValueNetwork(128, 8) random init, fp16;
+    one HIP graph per step), both from a burned-in pool (mixed game ages)."""
+    from zeroclone_amd.nets import ValueNetwork, flops_per_position, for_inference
+    from zeroclone_amd.selfplay import ChessSelfPlay
+    G, S, B = 1024, 400, 32
+    crude, burn = chess_burned_pool(dev, G, S, B)
+    K = max(steps, 20)
+    ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
     torch.cuda.synchronize(dev)
     t = time.perf_counter()
-    exp = 0
-    for _ in range(steps):
-        g.replay()
-        exp += int(ps.stats[:, 0].sum().item())
+    ev[0].record()
+    res = crude.run_pooled(K * G, 2 * K, kernel_done=ev[1])
+    torch.cuda.synchronize(dev)
     dt = time.perf_counter() - t
-    nfl = _native.check(_native.lib().zc_chess_puct_flushes(sims, bs))
-    fl = flops_per_position(128, 8, 2, 6, 7) * games * bs * nfl * steps
-    eng.close()
+    exp = int(crude.stats[:, 0].sum().item())
+    moves = int(((res != _native.ZC_SLOT_SKIP)).sum().item())
+    out = {"crude": {"value": round(exp / dt, 1), "unit": "expansions/s", "ms_per_step": round(dt / K * 1e3, 3),
+                     "steps": K, "moves": moves, "launch_ms": round(ev[0].elapsed_time(ev[1]), 2),
+                     "burn_in_moves": burn,
+                     "config": f"steady-state self-play (burned-in pool), {G} games x {S} sims, crude_chess_score, "
+                               f"immediate_value(3); one pooled launch of {K} x {G} moves + its recording"}}
+    torch.manual_seed(0)
+    model = for_inference(ValueNetwork(128, 8).eval(), dev, torch.float16)
+    pool = ChessSelfPlay(G, S, batch_size=B, seed=4, device=dev.index, net=model,
+                         policy=_native.ZC_POLICY_RANDOM, freedom=0.0)
+    pool.adopt(crude)
+    exp, dt = _timed_pool_steps(pool, steps)
+    pool.close()
+    fl = flops_per_position(128, 8, 17, 8, 8) * G * B * ((S + B - 1) // B) * steps
+    out["value_net"] = {"value": round(exp / dt, 1), "unit": "expansions/s", "ms_per_move": round(dt / steps * 1e3, 1),
+                        "steps": steps,
+                        "config": MIXED + f"{G} games x {S} sims, ValueNetwork(128, 8) random init fp16 (MFMA "
+                                          "kernels), random policy",
+                        "net_tflops_lower": round(fl / dt / 1e12, 1),
+                        "mfma_frac_lower": round(fl / dt / 1e12 / MFMA_F16_PEAK_TFLOPS, 4)}
+    out["_pool"] = crude
+    return out
+
+
+def puct_mode(src, steps: int, dev) -> dict:
+    """BASELINE configs[4] (C5) per GPU: chess PUCT self-play, 1024 games x 1600 sims, policy
+    + value ResNet (128 x 8, random init, fp16; tower on the MFMA kernels), Dirichlet root
+    noise, temperature 1, from the burned-in crude pool's positions; one graph per step."""
+    from zeroclone_amd.nets import MfmaPolicyValueNetwork, PolicyValueNetwork, flops_per_position
+    from zeroclone_amd.selfplay import ChessSelfPlay
+    G, S, B = 1024, 1600, 32
+    torch.manual_seed(0)
+    net = MfmaPolicyValueNetwork(PolicyValueNetwork().eval(), dev)
+    pool = ChessSelfPlay(G, S, batch_size=B, seed=6, device=dev.index, puct_net=net, temperature=1.0)
+    pool.adopt(src)
+    exp, dt = _timed_pool_steps(pool, steps)
+    pool.close()
+    nfl = _native.check(_native.lib().zc_chess_puct_flushes(S, B))
+    fl = flops_per_position(128, 8, 17, 8, 8) * G * B * nfl * steps
     return {"value": round(exp / dt, 1), "unit": "expansions/s", "ms_per_move": round(dt / steps * 1e3, 1),
-            "config": f"C2 + PUCT: {games} games x {sims} sims, c_puct 1.5, Dirichlet(0.3, 0.25), policy (7 logits) + "
-                      "value ResNet 128x8 random init fp16 (MFMA tower), temperature 1",
+            "steps": steps,
+            "config": MIXED + "C5 per GPU: 1024 games x 1600 sims, PUCT c 1.5, Dirichlet(0.3, 0.25), policy+value "
+                              "ResNet 128x8 random init fp16 (MFMA tower), temperature 1",
             "net_tflops_lower": round(fl / dt / 1e12, 1), "mfma_frac_lower": round(fl / dt / 1e12 / MFMA_F16_PEAK_TFLOPS, 4)}
 
 
@@ -570,13 +574,16 @@ def run_rank(args, rank: int, world: int, local: int):
                                                "moves": ro["moves"], "expansions": ro["expansions"]}
         if world == 1 and args.net_steps > 0:
             out["extra"]["c2_philox"] = philox_mode(sp, args)
+            out["extra"]["c2_value_net"] = net_mode(sp, G, S, B, args.c, args.net_steps, dev)
+            out["extra"]["c2_puct"] = c4_puct_mode(sp, G, S, B, args.net_steps, dev)
             out["extra"]["record_overhead"] = record_overhead(sp, args)
             sp.close()
             sp = None
-            out["extra"]["c2_value_net"] = net_mode(G, S, B, args.c, args.net_steps, dev)
-            out["extra"]["c2_puct"] = c4_puct_mode(G, S, B, args.net_steps, dev)
-            out["extra"]["c4_chess"] = chess_modes(args.net_steps, dev)
-            out["extra"]["c5_chess_puct"] = puct_mode(args.net_steps, dev)
+            chess = chess_modes(args.net_steps, dev)
+            crude_pool = chess.pop("_pool")
+            out["extra"]["c4_chess"] = chess
+            out["extra"]["c5_chess_puct"] = puct_mode(crude_pool, args.net_steps, dev)
+            crude_pool.close()
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(S, B, args.c)
             if args.net_steps > 0:
@@ -620,14 +627,15 @@ def phases(sp, args, bytes_launch: float, avg_kernel_s: float, traffic: float | 
 
 
 def record_overhead(sp, args) -> dict:
-    """Trajectory recording's cost: the same steps with and without zc_traj_record_async."""
+    """Trajectory recording's cost: the same steady-state steps with and without the
+    recording (zc_traj_record_steps_async).  The unrecorded run leaves the pool's slot
+    histories behind its games, so it runs last, just before the pool is closed."""
+    on = run_steps(sp, args.steps, warmup=1)
     sp.record = False
     try:
         off = run_steps(sp, args.steps, warmup=1)
     finally:
         sp.record = True
-        sp.start()
-    on = run_steps(sp, args.steps, warmup=1)
     return {"ms_per_step_recorded": round(on["dt"] / args.steps * 1e3, 3),
             "ms_per_step_unrecorded": round(off["dt"] / args.steps * 1e3, 3),
             "ratio": round(on["dt"] / max(off["dt"], 1e-9), 4)}
@@ -689,8 +697,9 @@ def parse_args(argv=None):
     ap.add_argument("--no-burn-in", dest="burn_in", action="store_false",
                     help="time from the lockstep opening instead of steady-state self-play")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--net-steps", type=int, default=1,
-                    help="moves of the network / chess modes reported under extra (0 = skip; N=1 only)")
+    ap.add_argument("--net-steps", type=int, default=5,
+                    help="timed steady-state moves of the network / chess modes reported under extra "
+                         "(0 = skip; N=1 only)")
     ap.add_argument("--traffic-bytes", type=float, default=None,
                     help="per-launch HBM bytes of the search kernel from a separate rocprofv3 --pmc pass")
     return ap.parse_args(argv)

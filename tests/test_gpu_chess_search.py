@@ -158,3 +158,32 @@ def test_planes_of_leaves(eng):
         for k in range(0, rows.shape[0], 3):
             st = cb.from_zc(rows[k].view(CHESS_STATE_DTYPE)[0])
             np.testing.assert_array_equal(pl[k], cb.state_to_tensor(st))
+
+
+def test_rng_state_after_chess_search_is_pythons(eng):
+    """zc_rng_get_state after searches that generate their stream only as far as they read
+    (the HBM-ring searches: chess, the stepwise Connect4 search): the returned state is
+    CPython's — the whole 624-word block of the last consumed word, twisted — for every game,
+    across several consecutive searches (random.getstate after as many draws)."""
+    fens = ["rnbqkbnr/pppppppp/8/8/8/8/PPPPPPPP/RNBQKBNR w KQkq - 0 1",
+            "r3k2r/p1ppqpb1/bn2pnp1/3PN3/1p2P3/2N2Q1p/PPPBBPPP/R3K2R w KQkq - 0 1"] * 8
+    n = len(fens)
+    seeds = [31 * g + 5 for g in range(n)]
+    eng.seed(0, seeds)
+    roots = roots_of(fens)
+    mv = torch.zeros(n, dtype=torch.int16, device="cuda")
+    na = torch.zeros((n, 256), dtype=torch.int32, device="cuda")
+    st = torch.zeros((n, 8), dtype=torch.int64, device="cuda")
+    used = [0] * n
+    for sims in (37, 64, 101):
+        eng.chess_search_async(0, n, roots.data_ptr(), sims, 1.4, 16, 0, 0.0, mv.data_ptr(), na.data_ptr(),
+                               st.data_ptr())
+        torch.cuda.synchronize()
+        for g in range(n):
+            used[g] += int(st[g, 4])
+            r = random.Random(seeds[g])
+            for _ in range(used[g]):
+                r.getrandbits(32)
+            want = r.getstate()[1]
+            mt, idx = eng.get_rng_state(g)
+            assert [int(x) for x in mt] == list(want[:624]) and idx == want[624], (sims, g)

@@ -32,7 +32,7 @@ def test_chess_run_equals_lockstep_steps(fen):
     assert torch.equal(a.roots, b.roots) and torch.equal(a.hlen, b.hlen)
     assert torch.equal(a.hist, b.hist)
     pa, pb = pool(a), pool(b)
-    if fen is not None:
+    if fen in (FIFTY_NEXT, KQK):   # games that end within the window
         assert pa[0].shape[0] > 0
     for x, y in zip(pa, pb):
         assert torch.equal(x, y)

@@ -307,9 +307,17 @@ int zc_rng_get_state(zc_engine *eng, int32_t game, uint32_t *mt624, int32_t *ind
                           hipMemcpyDeviceToHost, eng->stream));
     ZC_HIP(hipStreamSynchronize(eng->stream));
     // Python's state after consuming word `use-1`: the 624-word block holding it, and the
-    // offset of the next word inside that block (624 = block exhausted).
+    // offset of the next word inside that block (624 = block exhausted).  CPython twists a
+    // whole block at once; the kernels generate words only as far as they read, so the
+    // block's words beyond pos[1] (words generated) are completed here by the recurrence.
     const uint64_t use = pos[0];
     const uint64_t blk = use == 0 ? 0 : (use - 1) / 624;
+    for (uint64_t p = std::max<uint64_t>(pos[1], 624); p < (blk + 1) * 624; ++p) {
+        const uint32_t m = zc::kRingWords - 1;
+        const uint32_t a = ring[(p - 624) & m], b = ring[(p - 623) & m], x = ring[(p - 227) & m];
+        const uint32_t y = (a & 0x80000000u) | (b & 0x7fffffffu);
+        ring[p & m] = x ^ (y >> 1) ^ ((b & 1u) ? 0x9908b0dfu : 0u);
+    }
     for (int i = 0; i < 624; ++i) mt624[i] = ring[(blk * 624 + (uint64_t)i) & (zc::kRingWords - 1)];
     *index = (int32_t)(use - blk * 624);
     return ZC_OK;

@@ -219,6 +219,7 @@ class C4SelfPlay:
             cap = games_cap or max(8 * games, 1024)
             self.traj = Trajectories(games, torch.zeros(24, dtype=torch.uint8), self.MAX_LEN, cap,
                                      cap * self.MAX_LEN, self.dev)
+        self.totals = torch.zeros(2, dtype=torch.int64, device=self.dev)   # expansions, depth sum since reset
         self.vs = self.value_fn = self.ps = self.net_fn = None
         self.temperature = float(temperature)
         if net is not None:
@@ -313,10 +314,23 @@ class C4SelfPlay:
                 mv, _, st = self.vs.enqueue(self.roots, self.sims, self.c, self.value_fn)
             self.moves.copy_(mv)
             self.stats.copy_(st)
-            return self.results
-        self.eng.c4_search_async(self.roots.data_ptr(), self.G, self.sims, self.c, self.bs, self.moves.data_ptr(),
-                                 self.na.data_ptr(), self.stats.data_ptr(), stream=s)
+        else:
+            self.eng.c4_search_async(self.roots.data_ptr(), self.G, self.sims, self.c, self.bs,
+                                     self.moves.data_ptr(), self.na.data_ptr(), self.stats.data_ptr(), stream=s)
+        self.totals += self.stats[:, :2].sum(0)
         return self.results
+
+    def adopt(self, other: "C4SelfPlay"):
+        """Take over another pool's games in progress (positions and their recorded
+        histories, game numbers; this pool's streams and pool stay its own) — e.g. a
+        network-mode pool starting from a burned-in rollout pool's mixed game ages."""
+        self.roots.copy_(other.roots)
+        if self.traj is not None and other.traj is not None:
+            t, o = self.traj, other.traj
+            t.hist.copy_(o.hist)
+            t.hmoves.copy_(o.hmoves)
+            t.slot.copy_(o.slot)
+            t.ctl[_native.ZC_TRAJ_NEXT] = o.ctl[_native.ZC_TRAJ_NEXT]
 
     def capture_step(self):
         """One whole step (search with its network, play, record) as a HIP graph; each
@@ -418,6 +432,7 @@ class ChessSelfPlay:
         self.stats = torch.zeros((games, _native.STATS_FIELDS), dtype=torch.int64, device=self.dev)
         self.post = torch.zeros_like(self.roots)
         self.results = torch.zeros(games, dtype=torch.int32, device=self.dev)
+        self.totals = torch.zeros(2, dtype=torch.int64, device=self.dev)   # expansions, depth sum since reset
         self.vs = self.value_fn = self.ps = self.net_fn = None
         self.temperature = float(temperature)
         if net is not None:
@@ -470,7 +485,22 @@ class ChessSelfPlay:
             ctypes.c_void_p(self.stats.data_ptr()), ctypes.c_void_p(self.post.data_ptr()),
             ctypes.c_void_p(self.results.data_ptr()), ctypes.c_void_p(s)))
         self.traj.record(self.post.data_ptr(), self.moves, self.results, stream=s)
+        self.totals += self.stats[:, :2].sum(0)
         return self.results
+
+    def adopt(self, other: "ChessSelfPlay"):
+        """Take over another pool's games in progress: positions, both sides' move histories
+        (the repetition draw), recorded histories and game numbers (same hist_cap)."""
+        if other.hist_cap != self.hist_cap:
+            raise ValueError("adopt() needs the same hist_cap")
+        self.roots.copy_(other.roots)
+        self.hist.copy_(other.hist)
+        self.hlen.copy_(other.hlen)
+        t, o = self.traj, other.traj
+        t.hist.copy_(o.hist)
+        t.hmoves.copy_(o.hmoves)
+        t.slot.copy_(o.slot)
+        t.ctl[_native.ZC_TRAJ_NEXT] = o.ctl[_native.ZC_TRAJ_NEXT]
 
     def capture_step(self):
         """One whole step (search with its network, play, record) as a HIP graph; each
