@@ -128,3 +128,16 @@ def test_c4_value_and_puct_selfplay_pools():
             assert np.array_equal(lab[off:off + n].astype(np.float32), dataset_labels(n, r))
         a.close()
         b.close()
+
+
+def test_chess_pooled_launch_refuses_more_games_than_resident():
+    from zeroclone_amd import _native
+    import ctypes
+    n = ctypes.c_int32(0)
+    _native.check(_native.lib().zc_chess_pooled_max_games(64, ctypes.byref(n)))
+    cap = n.value
+    assert cap >= 1024   # C4 / C5's 1024 games per GPU fit
+    sp = ChessSelfPlay(cap + 64, 4, batch_size=4, hist_cap=64)
+    with pytest.raises(ValueError):
+        sp.run_pooled(2 * (cap + 64), 4)
+    sp.close()
