@@ -20,7 +20,7 @@
 //
 // Node = one 192-byte record, slot k (a move, in the node's move-list order) in lane k:
 // everything a selection step reads is one coalesced load per field.  One wave per game.
-// Specification in executable form: tests/puct_ref.py (C4Rules).
+// Specification in executable form: oracle/puct_ref.py (C4Rules).
 #include <hip/hip_fp16.h>
 
 #include "c4_device.h"
