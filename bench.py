@@ -487,7 +487,8 @@ def exchange_positions(local, world: int, sync=lambda: None):
     dist.all_reduce(gms, op=dist.ReduceOp.MAX)
     out.update({"rows": int(allpos.shape[0]), "bytes": int(allpos.numel() * allpos.element_size()),
                 "ms": round(float(gms.item()), 3),
-                "collective": "all_gather (counts, padded payload) of finished games' 24-B positions, nccl=RCCL"})
+                "collective": "all_gather (counts, padded payload) of finished games' 24-B positions, "
+                              + ("nccl=RCCL" if dist.get_backend() == "nccl" else dist.get_backend())})
     return out, allpos
 
 
@@ -503,8 +504,13 @@ def search_profile():
 
 
 def run_rank(args, rank: int, world: int, local: int):
+    if args.share_device:   # rehearsal: every rank on GPU 0 (RCCL needs one GPU per rank)
+        local = 0
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(args.dist_backend)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     from zeroclone_amd.selfplay import C4SelfPlay
@@ -526,7 +532,7 @@ def run_rank(args, rank: int, world: int, local: int):
         avg_kernel_s = kms / 1e3 / args.steps   # per move
         achieved = bytes_launch / avg_kernel_s / 1e9
         out = {
-            "metric": METRIC,
+            "metric": METRIC if not args.share_device else "REHEARSAL (ranks share one GPU; not the metric): " + METRIC,
             "value": round(expansions / dt_max, 1),
             "unit": "expansions/s",
             "n_gpus": world,
@@ -545,7 +551,8 @@ def run_rank(args, rank: int, world: int, local: int):
                                   if args.launch == "pooled" else f"free: K moves per game per launch"),
                        "games_per_gpu": G, "global_games": G * world, "sims": S, "batch_size": B,
                        "world_size": world, "rank_games": rank_ranges(world, G), "burn_in_steps": burn,
-                       "parallelism": f"games sharded over {world} GPU(s), 1 process/GPU"},
+                       "parallelism": (f"games sharded over {world} GPU(s), 1 process/GPU" if not args.share_device
+                                       else f"rehearsal: {world} ranks sharing GPU 0 over {args.dist_backend}")},
             # The search kernel is a per-game serial chain: SQ counters show neither HBM nor
             # an issue port saturated (profiles/: ~0.07 of HBM bandwidth, SALU ~0.36 / VALU
             # ~0.27 issue) — latency and issue arbitration bound it.  achieved / peak / frac
@@ -700,6 +707,11 @@ def parse_args(argv=None):
     ap.add_argument("--net-steps", type=int, default=5,
                     help="timed steady-state moves of the network / chess modes reported under extra "
                          "(0 = skip; N=1 only)")
+    ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
+                    help="torch.distributed backend of the N-rank run (nccl = RCCL over xGMI)")
+    ap.add_argument("--share-device", action="store_true",
+                    help="rehearsal of the N-rank path on a one-GPU box: every rank on GPU 0 (use gloo); "
+                         "the line is marked as a rehearsal, never the metric")
     ap.add_argument("--traffic-bytes", type=float, default=None,
                     help="per-launch HBM bytes of the search kernel from a separate rocprofv3 --pmc pass")
     return ap.parse_args(argv)
@@ -722,8 +734,10 @@ def main():
         visible = visible_gpus()   # the KFD topology: no HIP call in this (parent) process
     except RuntimeError as e:
         raise SystemExit(f"bench.py: {e}")
-    if args.gpus > visible:
+    if args.gpus > visible and not (args.share_device and visible >= 1):
         raise SystemExit(f"bench.py: --gpus {args.gpus} but only {visible} GPU(s) visible")
+    if args.share_device and args.dist_backend == "nccl":
+        raise SystemExit("bench.py: --share-device needs --dist-backend gloo (RCCL wants one GPU per rank)")
     import torch.multiprocessing as mp
     mp.spawn(_spawned, args=(args, args.gpus, _free_port()), nprocs=args.gpus, join=True)
 
