@@ -134,7 +134,7 @@ __device__ void c4_rollouts(Leaf *L, int nb, R &rng, const uint32_t *s_order, Co
     // per leaf, lane-parallel (lane = leaf of a group of 64): side to move / last mover stones,
     // has_four(last mover) and 41 - stones, read out by readlane when the leaf's turn comes
     uint64_t won_m = 0;
-    uint32_t lm_v = 0, ow_v = 0;
+    uint32_t lm_v = 0, ow_v = 0, hp_v = 0;
     int room_v = 0;
     for (int j = 0; j < nb; ++j) {
         RMARK(6);  // regions: 1 leaf setup, 2 view, 3 first segment, 4 absorbed fill, 5 win test, 6 block tail
@@ -148,6 +148,9 @@ __device__ void c4_rollouts(Leaf *L, int nb, R &rng, const uint32_t *s_order, Co
                 const uint64_t x0 = L[jj].p0, x1 = L[jj].p1;
                 op_v = (lm_v >> 24) & 1u ? x0 : x1;
                 room_v = 41 - __popcll(x0 | x1);
+                const uint64_t oc = x0 | x1;  // column heights, 4 bits per column
+                hp_v = 0;
+                for (int c = 0; c < 7; ++c) hp_v |= (uint32_t)__popcll((oc >> (7 * c)) & 0x3Full) << (4 * c);
             }
             won_m = __ballot(jj < nb && has_four(op_v));
         }
@@ -158,6 +161,7 @@ __device__ void c4_rollouts(Leaf *L, int nb, R &rng, const uint32_t *s_order, Co
         const uint64_t *const pp = &L[j].p0;
         uint64_t me = in_vgpr(pp[tnv]);       // side to move
         uint64_t op = in_vgpr(pp[tnv ^ 1u]);  // last mover
+        uint32_t hp = (uint32_t)__builtin_amdgcn_readlane((int)hp_v, jl);  // column heights, carried across blocks
         const uint32_t low0 = (uint32_t)__builtin_amdgcn_readlane((int)ow_v, jl);
         const int room0 = __builtin_amdgcn_readlane(room_v, jl);
         const bool won = (won_m >> jl) & 1u;
@@ -191,16 +195,16 @@ __device__ void c4_rollouts(Leaf *L, int nb, R &rng, const uint32_t *s_order, Co
                 }
                 cn.add(cn.blocks, 1);
                 RMARK(2);
-                const uint64_t occ = me | op;
                 const uint32_t cap_r = min((uint32_t)room, 30u);  // last ply index the board allows
                 uint32_t qk = mbcnt(A);                            // this lane's ply in the block
-                uint32_t col = (ow >> (3 * (v & 7u))) & 7u;        // its column (if accepted)
-                // earlier plies in the same column: 4-bit per-column counters, prefix-summed
-                // (a nibble can only overflow past 15 plies in one column, i.e. after that
-                // column filled — beyond the block's end, so never read)
+                uint32_t col = (ow >> (3 * v)) & 7u;  // its column (if accepted; v < 8 as n < 8)
+                // the ply's row: the column's height (hp, 4 bits per column, carried from block
+                // to block) + earlier plies in the same column (4-bit per-column counters,
+                // prefix-summed).  A nibble only overflows into the next column's after its own
+                // column filled — beyond the block's end, in lanes never read.
                 uint32_t one = mask_sel0(A, 1u << (4 * col));
-                uint32_t same = ((scan_add32(one) - one) >> (4 * col)) & 15u;
-                uint32_t row = (uint32_t)__popcll((occ >> (7 * col)) & 0x3Full) + same;
+                uint32_t sc = scan_add32(one);
+                uint32_t row = ((sc - one + hp) >> (4 * col)) & 15u;  // the column's height + earlier plies in it
                 uint32_t nacc = (uint32_t)__popcll(A);
                 bool fills = row == 5u;
                 uint64_t E0 = __ballot(mask_sel0(A, (fills ? 63u : qk) + 1u) > min(cap_r, nacc - 1u));
@@ -223,10 +227,10 @@ __device__ void c4_rollouts(Leaf *L, int nb, R &rng, const uint32_t *s_order, Co
                     v = mask_sel(low, v2, v);
                     const uint32_t owl = mask_sel(low, ow2, ow);
                     qk = mbcnt(A);
-                    col = (owl >> (3 * (v & 7u))) & 7u;
+                    col = (owl >> (3 * v)) & 7u;
                     one = mask_sel0(A, 1u << (4 * col));
-                    same = ((scan_add32(one) - one) >> (4 * col)) & 15u;
-                    row = (uint32_t)__popcll((occ >> (7 * col)) & 0x3Full) + same;
+                    sc = scan_add32(one);
+                    row = ((sc - one + hp) >> (4 * col)) & 15u;
                     nacc = (uint32_t)__popcll(A);
                     fills = row == 5u && lane > lf;  // the absorbed fill no longer ends the block
                     E0 = __ballot(mask_sel0(A, (fills ? 63u : qk) + 1u) > min(cap_r, nacc - 1u));
@@ -261,12 +265,13 @@ __device__ void c4_rollouts(Leaf *L, int nb, R &rng, const uint32_t *s_order, Co
                 // both sides' stones after ply endply: first mover through ply 2*(endply/2)
                 // (row 0, inclusive), second mover through the odd plies <= endply (row 1,
                 // inclusive scan at lane 15 + (endply+1)/2; none when endply = 0)
-                const uint64_t a2 = me | readlane64(mine, (int)(endply >> 1));
                 const uint64_t s2 = readlane64(mine, (int)((endply + 31u) >> 1));
+                const uint64_t a2 = me | readlane64(mine, (int)(endply >> 1));
                 const uint64_t b2 = op | (endply ? s2 : 0ull);
                 const bool odd = endply & 1u;  // an even number of plies: the first mover is to move again
                 me = odd ? a2 : b2;
                 op = odd ? b2 : a2;
+                hp += (uint32_t)__builtin_amdgcn_readlane((int)sc, (int)endlane);  // plies per column through endlane
                 q += (int)endply + 1;
                 room -= (int)endply + 1;
                 RMARK(5);
@@ -281,7 +286,7 @@ __device__ void c4_rollouts(Leaf *L, int nb, R &rng, const uint32_t *s_order, Co
                 // the legal set (and its CPython order) after the block's fills: the absorbed
                 // one if it was played, and the one the block ended at
                 const bool fa = endlane >= lf;
-                const bool fe = __builtin_amdgcn_readlane((int)fills, (int)endlane) != 0;
+                const bool fe = (__ballot(fills) >> endlane) & 1u;
                 {  // unconditional (selects), so the block loop carries one copy of its state
                     const uint32_t ce = fe ? (uint32_t)__builtin_amdgcn_readlane((int)col, (int)endlane) : cf;
                     const uint32_t ca = fa ? cf : ce;
