@@ -166,7 +166,7 @@ __device__ void c4_rollouts(Leaf *L, int nb, R &rng, const uint32_t *s_order, Co
         const int room0 = __builtin_amdgcn_readlane(room_v, jl);
         const bool won = (won_m >> jl) & 1u;
         int val = 0;
-        int q = 0;  // plies played in this rollout
+        int q = 0;  // plies played in this rollout (room0 - room when it ends)
         RMARK(1);
         if (won) {  // has_four(last mover)
             val = -1;
@@ -213,10 +213,10 @@ __device__ void c4_rollouts(Leaf *L, int nb, R &rng, const uint32_t *s_order, Co
                 // the new legal set
                 uint32_t lf = 64u;  // lane of the absorbed fill (64: none)
                 uint32_t ow2 = ow, cf = 0;
-                const uint32_t q0 = (uint32_t)__builtin_amdgcn_readlane((int)qk, (int)l0);
-                const uint32_t f0 = (uint32_t)(__ballot(fills) >> l0) & 1u;
+                // (one lane test, one mask bit: fills with ply < cap_r, at l0)
+                const uint64_t FA = __ballot(qk < cap_r) & __ballot(fills);
                 RMARK(3);
-                if (f0 && q0 < cap_r) {
+                if ((FA >> l0) & 1u) {
                     lf = l0;
                     cf = (uint32_t)__builtin_amdgcn_readlane((int)col, (int)lf);
                     ow2 = (uint32_t)__builtin_amdgcn_readlane((int)owp, (int)(8u * cf));
@@ -272,11 +272,10 @@ __device__ void c4_rollouts(Leaf *L, int nb, R &rng, const uint32_t *s_order, Co
                 me = odd ? a2 : b2;
                 op = odd ? b2 : a2;
                 hp += (uint32_t)__builtin_amdgcn_readlane((int)sc, (int)endlane);  // plies per column through endlane
-                q += (int)endply + 1;
                 room -= (int)endply + 1;
                 RMARK(5);
                 if (Ew) {  // the ply's mover completed four
-                    val = (q & 1) ? 1 : -1;
+                    val = ((room0 - room) & 1) ? 1 : -1;  // an odd number of plies: the leaf's side won
                     break;
                 }
                 if (room < 0) {  // check_draw: board full
@@ -299,6 +298,7 @@ __device__ void c4_rollouts(Leaf *L, int nb, R &rng, const uint32_t *s_order, Co
                 n = (ow >> 24) & 15u;
                 sh = (uint32_t)__clz(n);
             }
+            q = room0 - room;
         }
         L[j].val = val;  // uniform: every lane stores
         cn.add(cn.plies, q);
