@@ -90,3 +90,34 @@ def test_packed_conv_is_bit_identical_to_the_staged_form():
                                                         b.data_ptr(), relu, None))
             torch.cuda.synchronize()
             assert torch.equal(a.view(torch.int16), b.view(torch.int16)), (h, w, cin, n, use_res, relu)
+
+
+@pytest.mark.parametrize("shape", [(17, 8, 8), (2, 6, 7)])
+@pytest.mark.parametrize("n", [1, 7, 301, 4099])
+def test_fused_tower_is_bit_identical_to_layered(shape, n):
+    """zc_net_tower_async (the whole tower in one launch, activations on chip) against the
+    layer-by-layer packed launches: the tower's output activation bit for bit, ragged last
+    tiles included."""
+    from zeroclone_amd.nets import MfmaValueNetwork
+    c, h, w = shape
+    net = MfmaValueNetwork(_net(c, seed=100 + n))
+    x = (torch.rand(n, c, h, w, device="cuda") < 0.3).half()
+    a, _ = net.tower(x, fused=False)
+    want = a.clone()
+    a.fill_(0)
+    got, _ = net.tower(x, fused=True)
+    torch.cuda.synchronize()
+    assert got.shape == (n, h * w, 128)
+    assert torch.equal(got, want)
+    assert want.abs().sum().item() > 0
+
+
+def test_fused_tower_rejects_unsupported_shapes():
+    from zeroclone_amd import _native
+    L = _native.lib()
+    buf = torch.zeros(1024, dtype=torch.float16, device="cuda")
+    bias = torch.zeros(128, dtype=torch.float32, device="cuda")
+    for (h, w, cin0, nconv) in [(5, 5, 32, 17), (8, 8, 128, 17), (8, 8, 32, 16), (8, 8, 32, 0)]:
+        rc = L.zc_net_tower_async(1, h, w, cin0, nconv, buf.data_ptr(), buf.data_ptr(), bias.data_ptr(),
+                                  buf.data_ptr(), None)
+        assert rc != 0, (h, w, cin0, nconv)

@@ -25,6 +25,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
+#include <type_traits>
 
 #include "zc_internal.h"
 
@@ -573,6 +574,183 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
 #endif
 }
 
+// Fused tower (zc_net_tower_async): the stem and every residual block of one tile of boards
+// in ONE workgroup, the activations resident in LDS from the input planes to the tower's
+// output — no HBM round trip between layers (a layer-by-layer launch moves ~1.6 GB of
+// activations per 32768 boards per layer and stalls each workgroup on its load and store
+// phases).  The MFMA loop is the streamed-weight form's (each wave its 32 output channels x
+// the tile's 128 pixels, fragments from L2 one tap ahead, activation reads one k-step ahead);
+// the epilogue goes straight from the accumulators into the next layer's input buffer:
+//   layer 0 (stem)        buf1 (input planes) -> buf0
+//   layer 2k+1 (conv1)    buf0 (x)            -> buf1 (h)
+//   layer 2k+2 (conv2)    buf1 (h)            -> buf0 (x := relu(conv + bias + x), in place:
+//                          each output pixel reads only its own residual, and no wave reads x
+//                          during conv2)
+// with one barrier per layer.  LDS: buf0 [128][136], 16 zero rows, buf1 [128][136] (73,984
+// B; two workgroups per CU).  Off-board taps of either buffer read the shared zero rows, in
+// the bank class of the row they would have read.  Every value is computed with the same
+// operations in the same order as the layer-by-layer packed form: bit-identical outputs
+// (tests/test_gpu_net.py).
+constexpr int kTowerLD = kCout + 8;
+constexpr int kTowerZero = kHalfPix;        // first zero row
+constexpr int kTowerBuf1 = kHalfPix + 16;   // buf1's first row
+constexpr size_t kTowerLds = (size_t)(2 * kHalfPix + 16) * kTowerLD * sizeof(_Float16);
+
+// One layer's MFMA loop: acc[t] += sum over taps and k of W * X (X from the LDS buffer at
+// row `src`).  a[0..KC) holds the layer's tap-0 fragments on entry; on exit it holds the
+// next layer's (KCN fragments from wn, when wn != nullptr and KCN == KC: in the ring at the
+// last tap; otherwise loaded after the loop).
+template <int H, int W, int KC, int KCN>
+__device__ __forceinline__ void tower_mfma(const _Float16 *lds, int src, const _Float16 *wa, const _Float16 *wn,
+                                           h8 (&a)[8], const int (&prow)[4], const int (&pyx)[4], int hh,
+                                           f16x (&acc)[4]) {
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) {
+        const int dy = tap / 3 - 1, dx = tap % 3 - 1;
+        const _Float16 *xb[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const int sy = (pyx[t] >> 8) + dy, sx = (pyx[t] & 255) + dx;
+            const bool sv = (unsigned)sy < (unsigned)H && (unsigned)sx < (unsigned)W;
+            const int row = prow[t] + dy * W + dx;
+            xb[t] = lds + (sv ? src + row : kTowerZero + (row & 15)) * kTowerLD + hh * 8;
+        }
+        h8 x[4], xn[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) x[t] = *(const h8 *)(xb[t]);
+#pragma unroll
+        for (int kc = 0; kc < KC; ++kc) {
+            if (kc + 1 < KC) {
+#pragma unroll
+                for (int t = 0; t < 4; ++t) xn[t] = *(const h8 *)(xb[t] + (kc + 1) * 16);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[kc], x[t], acc[t], 0, 0, 0);
+            __builtin_amdgcn_sched_barrier(0);
+            if (tap + 1 < 9) a[kc] = *(const h8 *)(wa + (size_t)((tap + 1) * KC + kc) * 2048);
+            else if (KCN == KC && wn) a[kc] = *(const h8 *)(wn + (size_t)kc * 2048);
+            if (kc + 1 < KC) {
+#pragma unroll
+                for (int t = 0; t < 4; ++t) x[t] = xn[t];
+            }
+        }
+    }
+    if (KCN != KC && wn) {
+#pragma unroll
+        for (int kc = 0; kc < KCN; ++kc) a[kc] = *(const h8 *)(wn + (size_t)kc * 2048);
+    }
+}
+
+// acc + bias (+ the residual already in dst), ReLU, fp16 -> dst rows (the stream form's
+// epilogue arithmetic, per lane: 4 channels x one pixel per store)
+__device__ __forceinline__ void tower_epilogue(_Float16 *dst, const float4 (&bv)[4], bool res, int npix, int wave,
+                                               int r, int hh, const f16x (&acc)[4]) {
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        const int P = t * 32 + r;
+        if (P >= npix) continue;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int co = wave * 32 + 8 * g + 4 * hh;
+            h4 *const o = (h4 *)(dst + P * kTowerLD + co);
+            float v[4] = {acc[t][4 * g + 0] + bv[g].x, acc[t][4 * g + 1] + bv[g].y, acc[t][4 * g + 2] + bv[g].z,
+                          acc[t][4 * g + 3] + bv[g].w};
+            if (res) {
+                const h4 rv = *o;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) v[e] += (float)rv[e];
+            }
+            h4 ov;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) ov[e] = (_Float16)fmaxf(v[e], 0.0f);
+            *o = ov;
+        }
+    }
+}
+
+template <int H, int W, int BPH, int CIN0>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void tower_kernel(
+    int nboards, int nconv, const _Float16 *__restrict__ in, const _Float16 *__restrict__ wall,
+    const float *__restrict__ ball, _Float16 *__restrict__ out) {
+    constexpr int HW = H * W;
+    static_assert(BPH * HW <= kHalfPix, "tile too large");
+    constexpr int KC0 = CIN0 / 16;
+    constexpr size_t kW0 = (size_t)9 * CIN0 * kCout, kW = (size_t)9 * kCout * kCout;  // halfs per layer
+    extern __shared__ __attribute__((aligned(16))) _Float16 lds[];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int b0 = blockIdx.x * BPH;
+    const int npix = min(BPH, nboards - b0) * HW;
+    const h8 zero = {0, 0, 0, 0, 0, 0, 0, 0};
+    const int r = lane & 31, hh = lane >> 5;
+    const _Float16 *const wl0 = wall + (size_t)wave * 512 + lane * 8;  // this wave's fragments, layer 0
+    h8 a[8];
+#pragma unroll
+    for (int kc = 0; kc < KC0; ++kc) a[kc] = *(const h8 *)(wl0 + (size_t)kc * 2048);
+    {
+        constexpr int C8 = CIN0 / 8;
+        const _Float16 *src = in + (size_t)b0 * HW * CIN0;
+#pragma unroll
+        for (int q = 0; q < kHalfPix * C8 / 256; ++q) {
+            const int i = tid + q * 256, row = i / C8, c8 = i - row * C8;
+            const h8 t = *(const h8 *)(src + min(row, npix - 1) * CIN0 + c8 * 8);
+            *(h8 *)(lds + (kTowerBuf1 + row) * kTowerLD + c8 * 8) = row < npix ? t : zero;
+        }
+        for (int z = tid; z < 16 * kTowerLD / 8; z += 256) *(h8 *)(lds + kTowerZero * kTowerLD + z * 8) = zero;
+    }
+    int prow[4], pyx[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        const int P = t * 32 + r;
+        const int pb = P / HW, rem = P - pb * HW, py = rem / W;
+        prow[t] = P;
+        pyx[t] = (P < npix ? py << 8 : 64 << 8) | (rem - py * W);
+    }
+    __syncthreads();  // the input tile and the zero rows are in LDS
+    // layer l: src -> dst, then a barrier (dst complete before layer l+1 reads it; dst was
+    // layer l-1's src, which every wave finished reading before the previous barrier)
+    auto layer = [&](int l, auto kc_tag) {
+        constexpr int KC = decltype(kc_tag)::value;
+        // per-lane pixel coordinates re-derived inside the layer (opaque to the compiler), so
+        // that the 36 tap addresses are not hoisted out of the layer loop into registers
+        int pr[4], py[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            pr[t] = prow[t];
+            py[t] = pyx[t];
+            __asm__ volatile("" : "+v"(pr[t]), "+v"(py[t]));
+        }
+        f16x acc[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+            for (int k = 0; k < 16; ++k) acc[t][k] = 0.0f;
+        const int src = (l & 1) ? 0 : kTowerBuf1, dst = (l & 1) ? kTowerBuf1 : 0;
+        const _Float16 *const wa = l == 0 ? wl0 : wl0 + kW0 + (size_t)(l - 1) * kW;
+        const _Float16 *const wn = l + 1 < nconv ? wl0 + kW0 + (size_t)l * kW : nullptr;  // layer l+1's
+        float4 bv[4];  // this wave's bias slice, in flight during the MFMA loop
+#pragma unroll
+        for (int g = 0; g < 4; ++g) bv[g] = *(const float4 *)(ball + (size_t)l * kCout + wave * 32 + 8 * g + 4 * hh);
+        tower_mfma<H, W, KC, 8>(lds, src, wa, wn, a, pr, py, hh, acc);
+        tower_epilogue(lds + dst * kTowerLD, bv, l >= 2 && !(l & 1), npix, wave, r, hh, acc);
+        __syncthreads();
+    };
+    layer(0, std::integral_constant<int, KC0>{});
+    for (int l = 1; l < nconv; ++l) layer(l, std::integral_constant<int, 8>{});
+    // the tower's output (the last layer's dst: buf0, nconv odd) -> HBM, whole 256-byte rows
+#pragma unroll
+    for (int q = 0; q < kHalfPix * (kCout / 8) / 256; ++q) {
+        const int i = tid + q * 256, P = i >> 4, c0 = (i & 15) * 8;
+        if (P < npix) *(h8 *)(out + ((size_t)b0 * HW + P) * kCout + c0) = *(const h8 *)(lds + P * kTowerLD + c0);
+    }
+}
+
+template <int H, int W, int BPH>
+void launch_tower(int n, int nconv, const void *in, const void *wall, const float *ball, void *out, hipStream_t s) {
+    hipLaunchKernelGGL((tower_kernel<H, W, BPH, 32>), dim3((n + BPH - 1) / BPH), dim3(256), kTowerLds, s, n, nconv,
+                       (const _Float16 *)in, (const _Float16 *)wall, ball, (_Float16 *)out);
+}
+
 // [9][kCout][cin] -> the stream form's fragments: packed[((tap * KC + kc) * 4 + mb) * 512 +
 // lane * 8 + e] = w[tap][mb * 32 + lane % 32][kc * 16 + 8 * (lane / 32) + e].
 __global__ void pack_conv_weight_kernel(int cin, const _Float16 *__restrict__ w, _Float16 *__restrict__ packed) {
@@ -697,6 +875,15 @@ bool launch_net_conv3x3_packed(int n, int h, int w, int cin, const void *in, con
     else if (h == 8 && w == 8 && cin == 32) launch_stream<8, 8, 2, 32>(n, in, wp, bias, res, out, relu, s);
     else if (h == 6 && w == 7 && cin == 128) launch_stream<6, 7, 3, 128>(n, in, wp, bias, res, out, relu, s);
     else if (h == 6 && w == 7 && cin == 32) launch_stream<6, 7, 3, 32>(n, in, wp, bias, res, out, relu, s);
+    else return false;
+    return true;
+}
+
+bool launch_net_tower(int n, int h, int w, int cin0, int nconv, const void *in, const void *wall, const float *ball,
+                      void *out, hipStream_t s) {
+    if (cin0 != 32 || nconv < 1 || !(nconv & 1)) return false;
+    if (h == 8 && w == 8) launch_tower<8, 8, 2>(n, nconv, in, wall, ball, out, s);
+    else if (h == 6 && w == 7) launch_tower<6, 7, 3>(n, nconv, in, wall, ball, out, s);
     else return false;
     return true;
 }

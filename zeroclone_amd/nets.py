@@ -152,6 +152,9 @@ class MfmaValueNetwork:
             _native.check(_native.lib().zc_net_conv3x3_pack_async(wt.shape[2], wt.data_ptr(), wp.data_ptr(),
                                                                   ctypes_stream(self.dev)))
             self.wp.append(wp)
+        # the same packed weights back to back and the biases [nconv][128], for the fused tower
+        self.wall = torch.cat([w.reshape(-1) for w in self.wp]).contiguous()
+        self.ball = torch.stack(self.b).contiguous()
         torch.cuda.current_stream(self.dev).synchronize()
         self.fcw = f.fc.weight.detach().float().reshape(-1).contiguous().to(self.dev)
         self.fcb = float(f.fc.bias.detach().float().item())
@@ -166,8 +169,10 @@ class MfmaValueNetwork:
                                torch.empty(n, dtype=torch.float64, device=self.dev))
         return self._bufs[key]
 
-    def tower(self, planes):
-        """Stem + residual blocks: the final activation, NHWC fp16 [n, h*w, 128]."""
+    def tower(self, planes, fused: bool = True):
+        """Stem + residual blocks: the final activation, NHWC fp16 [n, h*w, 128].  fused: one
+        launch for the whole tower (zc_net_tower_async); otherwise one launch per layer
+        (zc_net_conv3x3_packed_async) — bit-identical."""
         import torch
         from . import _native
         L = _native.lib()
@@ -179,6 +184,10 @@ class MfmaValueNetwork:
         x0, a, t, b, vals = self._buffers(n, hw)
         s = ctypes_stream(self.dev)
         _native.check(L.zc_net_planes_to_nhwc_async(n, c, hw, self.cpad, planes.data_ptr(), x0.data_ptr(), s))
+        if fused:
+            _native.check(L.zc_net_tower_async(n, h, w, self.cpad, len(self.wp), x0.data_ptr(), self.wall.data_ptr(),
+                                               self.ball.data_ptr(), a.data_ptr(), s))
+            return a, vals
 
         def conv(i, src, dst, res):
             _native.check(L.zc_net_conv3x3_packed_async(n, h, w, src.shape[2], src.data_ptr(), self.wp[i].data_ptr(),
