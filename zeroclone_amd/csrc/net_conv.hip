@@ -604,10 +604,9 @@ template <int H, int W, int KC, int KCN>
 __device__ __forceinline__ void tower_mfma(const _Float16 *lds, int src, const _Float16 *wa, const _Float16 *wn,
                                            h8 (&a)[8], const int (&prow)[4], const int (&pyx)[4], int hh,
                                            f16x (&acc)[4]) {
-#pragma unroll
-    for (int tap = 0; tap < 9; ++tap) {
+    // tap `tap`'s activation rows of the 4 pixel tiles (off-board: a zero row)
+    auto rows = [&](int tap, const _Float16 *(&xb)[4]) {
         const int dy = tap / 3 - 1, dx = tap % 3 - 1;
-        const _Float16 *xb[4];
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
             const int sy = (pyx[t] >> 8) + dy, sx = (pyx[t] & 255) + dx;
@@ -615,14 +614,25 @@ __device__ __forceinline__ void tower_mfma(const _Float16 *lds, int src, const _
             const int row = prow[t] + dy * W + dx;
             xb[t] = lds + (sv ? src + row : kTowerZero + (row & 15)) * kTowerLD + hh * 8;
         }
-        h8 x[4], xn[4];
+    };
+    const _Float16 *xb[4];
+    rows(0, xb);
+    h8 x[4], xn[4];
 #pragma unroll
-        for (int t = 0; t < 4; ++t) x[t] = *(const h8 *)(xb[t]);
+    for (int t = 0; t < 4; ++t) x[t] = *(const h8 *)(xb[t]);
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) {
+        // the next tap's rows: its first fragments are read during this tap's last k-step
+        const _Float16 *xbn[4];
+        if (tap + 1 < 9) rows(tap + 1, xbn);
 #pragma unroll
         for (int kc = 0; kc < KC; ++kc) {
             if (kc + 1 < KC) {
 #pragma unroll
                 for (int t = 0; t < 4; ++t) xn[t] = *(const h8 *)(xb[t] + (kc + 1) * 16);
+            } else if (tap + 1 < 9) {
+#pragma unroll
+                for (int t = 0; t < 4; ++t) xn[t] = *(const h8 *)(xbn[t]);
             }
             __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -630,10 +640,12 @@ __device__ __forceinline__ void tower_mfma(const _Float16 *lds, int src, const _
             __builtin_amdgcn_sched_barrier(0);
             if (tap + 1 < 9) a[kc] = *(const h8 *)(wa + (size_t)((tap + 1) * KC + kc) * 2048);
             else if (KCN == KC && wn) a[kc] = *(const h8 *)(wn + (size_t)kc * 2048);
-            if (kc + 1 < KC) {
 #pragma unroll
-                for (int t = 0; t < 4; ++t) x[t] = xn[t];
-            }
+            for (int t = 0; t < 4; ++t) x[t] = xn[t];
+        }
+        if (tap + 1 < 9) {
+#pragma unroll
+            for (int t = 0; t < 4; ++t) xb[t] = xbn[t];
         }
     }
     if (KCN != KC && wn) {
