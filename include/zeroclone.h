@@ -465,8 +465,10 @@ int zc_debug_c4_puct_tree(zc_engine *eng, int32_t game, int32_t max_nodes, void 
  *     from input to output; bit-identical to the layer-by-layer packed launches.  d_in =
  *     [n][h*w][cin0] fp16 (zc_net_planes_to_nhwc_async), d_packed = the packed weights of the
  *     nconv layers back to back (stem 9*cin0*128 halfs, then 9*128*128 per layer), d_bias =
- *     [nconv][128] f32, d_out = [n][h*w][128] fp16; all 16-byte aligned.  cin0 = 32, nconv
- *     odd, (h, w) in {(8, 8), (6, 7)}.
+ *     [nconv][128] f32, d_out = [n][h*w][128] fp16 or NULL; all 16-byte aligned.  With
+ *     d_values (fp64 [n]) the value head runs in the same launch on the on-chip activation
+ *     (d_fc_w [128] f32, fc_b; bit-identical to zc_net_value_head_async), so a value-only
+ *     network needs no d_out.  cin0 = 32, nconv odd, (h, w) in {(8, 8), (6, 7)}.
  *   zc_net_planes_to_nhwc_async: state_to_tensor planes [n][cin][h*w] fp16 -> [n][h*w][cpad],
  *     zero padded; cpad a multiple of 8 (16-byte rows), d_out 16-byte aligned.
  *   zc_net_value_head_async: mean over pixels -> dot(fc_w[128]) + fc_b -> tanh, as fp64
@@ -480,7 +482,8 @@ int zc_net_conv3x3_packed_async(int32_t n_boards, int32_t h, int32_t w, int32_t 
                                 const void *d_packed_weight, const float *d_bias, const void *d_residual, void *d_out,
                                 int32_t relu, void *hip_stream);
 int zc_net_tower_async(int32_t n_boards, int32_t h, int32_t w, int32_t cin0, int32_t nconv, const void *d_in,
-                       const void *d_packed_weights, const float *d_biases, void *d_out, void *hip_stream);
+                       const void *d_packed_weights, const float *d_biases, void *d_out, const float *d_fc_w,
+                       float fc_b, double *d_values, void *hip_stream);
 int zc_net_planes_to_nhwc_async(int32_t n, int32_t cin, int32_t hw, int32_t cpad, const void *d_planes, void *d_out,
                                 void *hip_stream);
 int zc_net_value_head_async(int32_t n, int32_t hw, const void *d_act, const float *d_fc_w, float fc_b, double *d_values,

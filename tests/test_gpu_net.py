@@ -119,5 +119,21 @@ def test_fused_tower_rejects_unsupported_shapes():
     bias = torch.zeros(128, dtype=torch.float32, device="cuda")
     for (h, w, cin0, nconv) in [(5, 5, 32, 17), (8, 8, 128, 17), (8, 8, 32, 16), (8, 8, 32, 0)]:
         rc = L.zc_net_tower_async(1, h, w, cin0, nconv, buf.data_ptr(), buf.data_ptr(), bias.data_ptr(),
-                                  buf.data_ptr(), None)
+                                  buf.data_ptr(), None, 0.0, None, None)
         assert rc != 0, (h, w, cin0, nconv)
+
+
+@pytest.mark.parametrize("shape", [(17, 8, 8), (2, 6, 7)])
+@pytest.mark.parametrize("n", [1, 5, 1003])
+def test_fused_value_head_is_bit_identical(shape, n):
+    """The value head inside the tower launch (on the on-chip activation) against the layered
+    tower + zc_net_value_head_async: the fp64 values bit for bit."""
+    from zeroclone_amd.nets import MfmaValueNetwork
+    c, h, w = shape
+    net = MfmaValueNetwork(_net(c, seed=200 + n))
+    x = (torch.rand(n, c, h, w, device="cuda") < 0.3).half()
+    want = net(x, fused=False).clone()
+    got = net(x).clone()
+    torch.cuda.synchronize()
+    assert torch.equal(got, want)
+    assert want.abs().sum().item() > 0

@@ -1384,12 +1384,14 @@ int zc_net_conv3x3_packed_async(int32_t n, int32_t h, int32_t w, int32_t cin, co
 }
 
 int zc_net_tower_async(int32_t n, int32_t h, int32_t w, int32_t cin0, int32_t nconv, const void *d_in,
-                       const void *d_packed, const float *d_bias, void *d_out, void *hip_stream) {
-    if (n < 0 || (n && (!d_in || !d_packed || !d_bias || !d_out)) || ((uintptr_t)d_packed & 15) ||
-        ((uintptr_t)d_in & 15) || ((uintptr_t)d_out & 15) || ((uintptr_t)d_bias & 15))
+                       const void *d_packed, const float *d_bias, void *d_out, const float *d_fc_w, float fc_b,
+                       double *d_values, void *hip_stream) {
+    if (n < 0 || (n && (!d_in || !d_packed || !d_bias || (!d_out && !d_values) || (d_values && !d_fc_w))) ||
+        ((uintptr_t)d_packed & 15) || ((uintptr_t)d_in & 15) || ((uintptr_t)d_out & 15) || ((uintptr_t)d_bias & 15))
         return fail(ZC_EINVAL, "bad argument");
     if (!n) return ZC_OK;
-    if (!zc::launch_net_tower(n, h, w, cin0, nconv, d_in, d_packed, d_bias, d_out, (hipStream_t)hip_stream))
+    if (!zc::launch_net_tower(n, h, w, cin0, nconv, d_in, d_packed, d_bias, d_out, d_values ? d_fc_w : nullptr, fc_b,
+                              d_values, (hipStream_t)hip_stream))
         return fail(ZC_EINVAL, "tower shape (h %d, w %d, cin0 %d, %d convs) not supported", h, w, cin0, nconv);
     ZC_HIP(hipGetLastError());
     return ZC_OK;

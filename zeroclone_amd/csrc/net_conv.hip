@@ -592,60 +592,61 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
 // operations in the same order as the layer-by-layer packed form: bit-identical outputs
 // (tests/test_gpu_net.py).
 constexpr int kTowerLD = kCout + 8;
-constexpr int kTowerZero = kHalfPix;        // first zero row
-constexpr int kTowerBuf1 = kHalfPix + 16;   // buf1's first row
-constexpr size_t kTowerLds = (size_t)(2 * kHalfPix + 16) * kTowerLD * sizeof(_Float16);
+// NT pixel MFMA tiles (32 pixels each) per wave and workgroup: buffer rows TP = 32 NT
+template <int NT> constexpr int tower_zero() { return 32 * NT; }             // first zero row
+template <int NT> constexpr int tower_buf1() { return 32 * NT + 16; }        // buf1's first row
+template <int NT> constexpr size_t tower_lds() { return (size_t)(64 * NT + 16) * kTowerLD * sizeof(_Float16); }
 
 // One layer's MFMA loop: acc[t] += sum over taps and k of W * X (X from the LDS buffer at
 // row `src`).  a[0..KC) holds the layer's tap-0 fragments on entry; on exit it holds the
 // next layer's (KCN fragments from wn, when wn != nullptr and KCN == KC: in the ring at the
 // last tap; otherwise loaded after the loop).
-template <int H, int W, int KC, int KCN>
+template <int H, int W, int NT, int KC, int KCN>
 __device__ __forceinline__ void tower_mfma(const _Float16 *lds, int src, const _Float16 *wa, const _Float16 *wn,
-                                           h8 (&a)[8], const int (&prow)[4], const int (&pyx)[4], int hh,
-                                           f16x (&acc)[4]) {
+                                           h8 (&a)[8], const int (&prow)[NT], const int (&pyx)[NT], int hh,
+                                           f16x (&acc)[NT]) {
     // tap `tap`'s activation rows of the 4 pixel tiles (off-board: a zero row)
-    auto rows = [&](int tap, const _Float16 *(&xb)[4]) {
+    auto rows = [&](int tap, const _Float16 *(&xb)[NT]) {
         const int dy = tap / 3 - 1, dx = tap % 3 - 1;
 #pragma unroll
-        for (int t = 0; t < 4; ++t) {
+        for (int t = 0; t < NT; ++t) {
             const int sy = (pyx[t] >> 8) + dy, sx = (pyx[t] & 255) + dx;
             const bool sv = (unsigned)sy < (unsigned)H && (unsigned)sx < (unsigned)W;
             const int row = prow[t] + dy * W + dx;
-            xb[t] = lds + (sv ? src + row : kTowerZero + (row & 15)) * kTowerLD + hh * 8;
+            xb[t] = lds + (sv ? src + row : tower_zero<NT>() + (row & 15)) * kTowerLD + hh * 8;
         }
     };
-    const _Float16 *xb[4];
+    const _Float16 *xb[NT];
     rows(0, xb);
-    h8 x[4], xn[4];
+    h8 x[NT], xn[NT];
 #pragma unroll
-    for (int t = 0; t < 4; ++t) x[t] = *(const h8 *)(xb[t]);
+    for (int t = 0; t < NT; ++t) x[t] = *(const h8 *)(xb[t]);
 #pragma unroll
     for (int tap = 0; tap < 9; ++tap) {
         // the next tap's rows: its first fragments are read during this tap's last k-step
-        const _Float16 *xbn[4];
+        const _Float16 *xbn[NT];
         if (tap + 1 < 9) rows(tap + 1, xbn);
 #pragma unroll
         for (int kc = 0; kc < KC; ++kc) {
             if (kc + 1 < KC) {
 #pragma unroll
-                for (int t = 0; t < 4; ++t) xn[t] = *(const h8 *)(xb[t] + (kc + 1) * 16);
+                for (int t = 0; t < NT; ++t) xn[t] = *(const h8 *)(xb[t] + (kc + 1) * 16);
             } else if (tap + 1 < 9) {
 #pragma unroll
-                for (int t = 0; t < 4; ++t) xn[t] = *(const h8 *)(xbn[t]);
+                for (int t = 0; t < NT; ++t) xn[t] = *(const h8 *)(xbn[t]);
             }
             __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-            for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[kc], x[t], acc[t], 0, 0, 0);
+            for (int t = 0; t < NT; ++t) acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[kc], x[t], acc[t], 0, 0, 0);
             __builtin_amdgcn_sched_barrier(0);
             if (tap + 1 < 9) a[kc] = *(const h8 *)(wa + (size_t)((tap + 1) * KC + kc) * 2048);
             else if (KCN == KC && wn) a[kc] = *(const h8 *)(wn + (size_t)kc * 2048);
 #pragma unroll
-            for (int t = 0; t < 4; ++t) x[t] = xn[t];
+            for (int t = 0; t < NT; ++t) x[t] = xn[t];
         }
         if (tap + 1 < 9) {
 #pragma unroll
-            for (int t = 0; t < 4; ++t) xb[t] = xbn[t];
+            for (int t = 0; t < NT; ++t) xb[t] = xbn[t];
         }
     }
     if (KCN != KC && wn) {
@@ -656,10 +657,11 @@ __device__ __forceinline__ void tower_mfma(const _Float16 *lds, int src, const _
 
 // acc + bias (+ the residual already in dst), ReLU, fp16 -> dst rows (the stream form's
 // epilogue arithmetic, per lane: 4 channels x one pixel per store)
+template <int NT>
 __device__ __forceinline__ void tower_epilogue(_Float16 *dst, const float4 (&bv)[4], bool res, int npix, int wave,
-                                               int r, int hh, const f16x (&acc)[4]) {
+                                               int r, int hh, const f16x (&acc)[NT]) {
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
+    for (int t = 0; t < NT; ++t) {
         const int P = t * 32 + r;
         if (P >= npix) continue;
 #pragma unroll
@@ -681,12 +683,14 @@ __device__ __forceinline__ void tower_epilogue(_Float16 *dst, const float4 (&bv)
     }
 }
 
-template <int H, int W, int BPH, int CIN0>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void tower_kernel(
+template <int H, int W, int BPH, int CIN0, int NT, int WPE>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE))) void tower_kernel(
     int nboards, int nconv, const _Float16 *__restrict__ in, const _Float16 *__restrict__ wall,
-    const float *__restrict__ ball, _Float16 *__restrict__ out) {
+    const float *__restrict__ ball, _Float16 *__restrict__ out, const float *__restrict__ fcw, float fcb,
+    double *__restrict__ values) {
     constexpr int HW = H * W;
-    static_assert(BPH * HW <= kHalfPix, "tile too large");
+    static_assert(BPH * HW <= 32 * NT, "tile too large");
+    constexpr int TP = 32 * NT;
     constexpr int KC0 = CIN0 / 16;
     constexpr size_t kW0 = (size_t)9 * CIN0 * kCout, kW = (size_t)9 * kCout * kCout;  // halfs per layer
     extern __shared__ __attribute__((aligned(16))) _Float16 lds[];
@@ -703,16 +707,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         constexpr int C8 = CIN0 / 8;
         const _Float16 *src = in + (size_t)b0 * HW * CIN0;
 #pragma unroll
-        for (int q = 0; q < kHalfPix * C8 / 256; ++q) {
+        for (int q = 0; q < (TP * C8 + 255) / 256; ++q) {
             const int i = tid + q * 256, row = i / C8, c8 = i - row * C8;
+            if (row >= TP) break;
             const h8 t = *(const h8 *)(src + min(row, npix - 1) * CIN0 + c8 * 8);
-            *(h8 *)(lds + (kTowerBuf1 + row) * kTowerLD + c8 * 8) = row < npix ? t : zero;
+            *(h8 *)(lds + (tower_buf1<NT>() + row) * kTowerLD + c8 * 8) = row < npix ? t : zero;
         }
-        for (int z = tid; z < 16 * kTowerLD / 8; z += 256) *(h8 *)(lds + kTowerZero * kTowerLD + z * 8) = zero;
+        for (int z = tid; z < 16 * kTowerLD / 8; z += 256) *(h8 *)(lds + tower_zero<NT>() * kTowerLD + z * 8) = zero;
     }
-    int prow[4], pyx[4];
+    int prow[NT], pyx[NT];
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
+    for (int t = 0; t < NT; ++t) {
         const int P = t * 32 + r;
         const int pb = P / HW, rem = P - pb * HW, py = rem / W;
         prow[t] = P;
@@ -725,42 +730,69 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         constexpr int KC = decltype(kc_tag)::value;
         // per-lane pixel coordinates re-derived inside the layer (opaque to the compiler), so
         // that the 36 tap addresses are not hoisted out of the layer loop into registers
-        int pr[4], py[4];
+        int pr[NT], py[NT];
 #pragma unroll
-        for (int t = 0; t < 4; ++t) {
+        for (int t = 0; t < NT; ++t) {
             pr[t] = prow[t];
             py[t] = pyx[t];
             __asm__ volatile("" : "+v"(pr[t]), "+v"(py[t]));
         }
-        f16x acc[4];
+        f16x acc[NT];
 #pragma unroll
-        for (int t = 0; t < 4; ++t)
+        for (int t = 0; t < NT; ++t)
 #pragma unroll
             for (int k = 0; k < 16; ++k) acc[t][k] = 0.0f;
-        const int src = (l & 1) ? 0 : kTowerBuf1, dst = (l & 1) ? kTowerBuf1 : 0;
+        const int src = (l & 1) ? 0 : tower_buf1<NT>(), dst = (l & 1) ? tower_buf1<NT>() : 0;
         const _Float16 *const wa = l == 0 ? wl0 : wl0 + kW0 + (size_t)(l - 1) * kW;
         const _Float16 *const wn = l + 1 < nconv ? wl0 + kW0 + (size_t)l * kW : nullptr;  // layer l+1's
         float4 bv[4];  // this wave's bias slice, in flight during the MFMA loop
 #pragma unroll
         for (int g = 0; g < 4; ++g) bv[g] = *(const float4 *)(ball + (size_t)l * kCout + wave * 32 + 8 * g + 4 * hh);
-        tower_mfma<H, W, KC, 8>(lds, src, wa, wn, a, pr, py, hh, acc);
+        tower_mfma<H, W, NT, KC, 8>(lds, src, wa, wn, a, pr, py, hh, acc);
         tower_epilogue(lds + dst * kTowerLD, bv, l >= 2 && !(l & 1), npix, wave, r, hh, acc);
         __syncthreads();
     };
     layer(0, std::integral_constant<int, KC0>{});
     for (int l = 1; l < nconv; ++l) layer(l, std::integral_constant<int, 8>{});
-    // the tower's output (the last layer's dst: buf0, nconv odd) -> HBM, whole 256-byte rows
+    // the tower's output is the last layer's dst (buf0, nconv odd)
+    if (values) {
+        // the value head on it, one wave per board: value_head_kernel's arithmetic in its
+        // order (lane l sums channels 8 (l & 15) .. +8 over pixels l / 16, +4, ...), from LDS
+        const int c0 = (lane & 15) * 8;
+        for (int bi = wave; bi < npix / HW; bi += 4) {
+            const _Float16 *act = lds + bi * HW * kTowerLD + c0;
+            float sum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+            for (int p = lane >> 4; p < HW; p += 4) {
+                const h8 v = *(const h8 *)(act + p * kTowerLD);
 #pragma unroll
-    for (int q = 0; q < kHalfPix * (kCout / 8) / 256; ++q) {
-        const int i = tid + q * 256, P = i >> 4, c0 = (i & 15) * 8;
-        if (P < npix) *(h8 *)(out + ((size_t)b0 * HW + P) * kCout + c0) = *(const h8 *)(lds + P * kTowerLD + c0);
+                for (int e = 0; e < 8; ++e) sum[e] += (float)v[e];
+            }
+            float d = 0.f;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                float t = sum[e] + __shfl_xor(sum[e], 16);
+                t += __shfl_xor(t, 32);
+                d += t * fcw[c0 + e];
+            }
+            d /= (float)HW;
+            for (int o = 8; o > 0; o >>= 1) d += __shfl_xor(d, o);
+            if (lane == 0) values[b0 + bi] = (double)tanhf(d + fcb);
+        }
+    }
+    if (out) {  // -> HBM, whole 256-byte rows
+#pragma unroll
+        for (int q = 0; q < TP * (kCout / 8) / 256; ++q) {
+            const int i = tid + q * 256, P = i >> 4, c0 = (i & 15) * 8;
+            if (P < npix) *(h8 *)(out + ((size_t)b0 * HW + P) * kCout + c0) = *(const h8 *)(lds + P * kTowerLD + c0);
+        }
     }
 }
 
-template <int H, int W, int BPH>
-void launch_tower(int n, int nconv, const void *in, const void *wall, const float *ball, void *out, hipStream_t s) {
-    hipLaunchKernelGGL((tower_kernel<H, W, BPH, 32>), dim3((n + BPH - 1) / BPH), dim3(256), kTowerLds, s, n, nconv,
-                       (const _Float16 *)in, (const _Float16 *)wall, ball, (_Float16 *)out);
+template <int H, int W, int BPH, int NT, int WPE>
+void launch_tower(int n, int nconv, const void *in, const void *wall, const float *ball, void *out, const float *fcw,
+                  float fcb, double *values, hipStream_t s) {
+    hipLaunchKernelGGL((tower_kernel<H, W, BPH, 32, NT, WPE>), dim3((n + BPH - 1) / BPH), dim3(256), tower_lds<NT>(), s,
+                       n, nconv, (const _Float16 *)in, (const _Float16 *)wall, ball, (_Float16 *)out, fcw, fcb, values);
 }
 
 // [9][kCout][cin] -> the stream form's fragments: packed[((tap * KC + kc) * 4 + mb) * 512 +
@@ -892,10 +924,12 @@ bool launch_net_conv3x3_packed(int n, int h, int w, int cin, const void *in, con
 }
 
 bool launch_net_tower(int n, int h, int w, int cin0, int nconv, const void *in, const void *wall, const float *ball,
-                      void *out, hipStream_t s) {
+                      void *out, const float *fcw, float fcb, double *values, hipStream_t s) {
     if (cin0 != 32 || nconv < 1 || !(nconv & 1)) return false;
-    if (h == 8 && w == 8) launch_tower<8, 8, 2>(n, nconv, in, wall, ball, out, s);
-    else if (h == 6 && w == 7) launch_tower<6, 7, 3>(n, nconv, in, wall, ball, out, s);
+    // 128-pixel tiles at two workgroups per CU; 64-pixel tiles (one chess board) at 3 or 4
+    // workgroups per CU measured 10 % slower (tools/ab_tower.py)
+    if (h == 8 && w == 8) launch_tower<8, 8, 2, 4, 2>(n, nconv, in, wall, ball, out, fcw, fcb, values, s);
+    else if (h == 6 && w == 7) launch_tower<6, 7, 3, 4, 2>(n, nconv, in, wall, ball, out, fcw, fcb, values, s);
     else return false;
     return true;
 }

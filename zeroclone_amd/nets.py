@@ -169,10 +169,12 @@ class MfmaValueNetwork:
                                torch.empty(n, dtype=torch.float64, device=self.dev))
         return self._bufs[key]
 
-    def tower(self, planes, fused: bool = True):
+    def tower(self, planes, fused: bool = True, head: bool = False, activation: bool = True):
         """Stem + residual blocks: the final activation, NHWC fp16 [n, h*w, 128].  fused: one
         launch for the whole tower (zc_net_tower_async); otherwise one launch per layer
-        (zc_net_conv3x3_packed_async) — bit-identical."""
+        (zc_net_conv3x3_packed_async) — bit-identical.  head (fused only): the value head runs
+        in the same launch into the returned fp64 values; activation=False skips writing the
+        activation (a value-only network needs none)."""
         import torch
         from . import _native
         L = _native.lib()
@@ -186,8 +188,12 @@ class MfmaValueNetwork:
         _native.check(L.zc_net_planes_to_nhwc_async(n, c, hw, self.cpad, planes.data_ptr(), x0.data_ptr(), s))
         if fused:
             _native.check(L.zc_net_tower_async(n, h, w, self.cpad, len(self.wp), x0.data_ptr(), self.wall.data_ptr(),
-                                               self.ball.data_ptr(), a.data_ptr(), s))
+                                               self.ball.data_ptr(), a.data_ptr() if activation or not head else None,
+                                               self.fcw.data_ptr() if head else None, self.fcb,
+                                               vals.data_ptr() if head else None, s))
             return a, vals
+        if head:
+            raise ValueError("head=True needs the fused tower")
 
         def conv(i, src, dst, res):
             _native.check(L.zc_net_conv3x3_packed_async(n, h, w, src.shape[2], src.data_ptr(), self.wp[i].data_ptr(),
@@ -200,9 +206,13 @@ class MfmaValueNetwork:
             a, b = b, a
         return a, vals
 
-    def __call__(self, planes):
+    def __call__(self, planes, fused: bool = True):
+        """fp64 values [n]: the tower and the value head in one launch (fused), or the layered
+        tower + zc_net_value_head_async — bit-identical."""
         from . import _native
-        a, vals = self.tower(planes)
+        if fused:
+            return self.tower(planes, head=True, activation=False)[1]
+        a, vals = self.tower(planes, fused=False)
         n, hw = a.shape[0], a.shape[1]
         _native.check(_native.lib().zc_net_value_head_async(n, hw, a.data_ptr(), self.fcw.data_ptr(), self.fcb,
                                                             vals.data_ptr(), ctypes_stream(self.dev)))
@@ -267,12 +277,8 @@ class MfmaPolicyValueNetwork:
 
     def __call__(self, planes):
         import torch
-        from . import _native
-        a, vals = self.tower.tower(planes)
+        a, vals = self.tower.tower(planes, head=True)  # the activation and the values, one launch
         n, hw = a.shape[0], a.shape[1]
-        _native.check(_native.lib().zc_net_value_head_async(n, hw, a.data_ptr(), self.tower.fcw.data_ptr(),
-                                                            self.tower.fcb, vals.data_ptr(),
-                                                            ctypes_stream(self.tower.dev)))
         p = torch.relu(torch.addmm(self.b1, a.reshape(n * hw, -1), self.w1)).reshape(n, -1)
         logits = torch.addmm(self.b2, p, self.w2)
         return vals, logits
