@@ -591,6 +591,7 @@ def run_rank(args, rank: int, world: int, local: int):
             out["extra"]["c4_chess"] = chess
             out["extra"]["c5_chess_puct"] = puct_mode(crude_pool, args.net_steps, dev)
             crude_pool.close()
+            out["extra"]["net_tower"] = tower_mode(dev)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(S, B, args.c)
             if args.net_steps > 0:
@@ -631,6 +632,35 @@ def phases(sp, args, bytes_launch: float, avg_kernel_s: float, traffic: float | 
                                       "serves from LDS / L2, so frac ~1 is the model's ceiling, not HBM "
                                       "saturation: measured_frac = the whole kernel's PMC HBM bytes over the "
                                       "walk time alone"}}
+
+
+def tower_mode(dev, reps: int = 5) -> dict:
+    """The value tower alone (ValueNetwork(128, 8) random init, chess 8x8 x 32768 boards = one
+    C4 flush of 1024 games x 32 leaves): the fused launch (zc_net_tower_async, what every
+    network mode runs) and the layer-by-layer packed launches, timed with HIP events on the
+    launch stream; TFLOP/s over the MFMA work (stem on its 32 padded planes + 16 layers)."""
+    from zeroclone_amd.nets import MfmaValueNetwork, ValueNetwork, flops_per_position
+    torch.manual_seed(0)
+    net = MfmaValueNetwork(ValueNetwork(128, 8, in_planes=17), dev)
+    n = 32768
+    x = (torch.rand(n, 17, 8, 8, device=dev) < 0.3).half()
+    flop = flops_per_position(128, 8, 32, 8, 8) * n
+    out = {"boards": n, "board": "8x8", "net": "ValueNetwork(128, 8), fp16, BN folded"}
+    for fused in (True, False):
+        net.tower(x, fused=fused)
+        ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+        torch.cuda.synchronize(dev)
+        ev[0].record()
+        for _ in range(reps):
+            net.tower(x, fused=fused)
+        ev[1].record()
+        torch.cuda.synchronize(dev)
+        ms = ev[0].elapsed_time(ev[1]) / reps
+        key = "fused" if fused else "layered"
+        out[key] = {"ms": round(ms, 3), "tflops": round(flop / ms / 1e9, 1),
+                    "frac_of_2p5PF": round(flop / ms / 1e9 / MFMA_F16_PEAK_TFLOPS, 4)}
+    out["pmc"] = "profiles/r03_tower_pmc.json (MFMA busy, held clock)"
+    return out
 
 
 def record_overhead(sp, args) -> dict:
