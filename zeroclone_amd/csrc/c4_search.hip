@@ -362,6 +362,238 @@ __device__ void c4_rollouts_philox(Leaf *L, int nb, const uint8_t *s_sel, uint2 
     }
 }
 
+// ------------------------------------------------------------------ planned flush expansion
+// select_flush (c4_device.h) walks the flush's fresh nodes one at a time: per node a view of
+// draws, a Lehmer decode, the children built and stored, then a descent — ~2.9 k cycles per
+// node at 16 waves per CU, 14 % of the search.  But below X0 the flush's shape does not depend
+// on the draws: a node takes min(#untried, leaves left) draws, and once every untried move of
+// it is drawn the next walk enters its LOWEST untried slot (its fresh children all score
+// +inf; old children have Na >= 1), whatever the draws were — for X0 the lowest untried
+// slot, for a fresh node slot 0.  So the chain of nodes X0 = C0, C1, ... (boards, move
+// counts, draws per node) is known before any draw is decoded; only the node IDS on the chain
+// (C_{i+1} = the child of the draw that took that slot) depend on the draws.
+// select_flush_plan therefore (1) walks the chain on the scalar unit, running each node's
+// draws (the same ballots + branch-free chain as select_flush) over a shared view and
+// recording the node in an LDS table; (2) builds every fresh node and leaf in ONE
+// lane-parallel pass, lane d = draw d = node f0 + d: its node's table entry, its r value, the
+// Lehmer decode inside its node's draws, its parent id (the draw of the previous chain node
+// that took position 0 of that node's untried list), its child's board, order word and
+// records; (3) patches the chain nodes' child slots and untried words (LDS atomics) and
+// X0's.  Same tree, same leaves, same stream consumption as select_flush (nb < 64: one lane
+// per draw; the rollout search only — select_flush records leaf paths for the stepwise search).
+struct ChainNode {
+    uint64_t p0, p1;  // the node's stones
+    uint32_t ow;      // its move-list order word
+    uint32_t info;    // n (draws are over n, n-1, ...) | m << 4 | first draw << 8 | depth << 16 | turn << 24 | legal << 25
+    uint32_t ul;      // its untried list (move indices in list order, 3 bits each)
+    uint32_t pad;
+};
+static_assert(sizeof(ChainNode) == 32, "chain table entry");
+
+__device__ __forceinline__ uint64_t lanes_in(int lo, int hi) {  // lanes lo .. hi-1 (0 <= lo <= hi <= 64)
+    const uint64_t below_hi = hi >= 64 ? ~0ull : (1ull << hi) - 1ull;
+    return below_hi & ~((1ull << lo) - 1ull);
+}
+
+template <bool STAMP, class RNG>
+__device__ __forceinline__ void select_flush_plan(const Tree &t, Fresh *fresh, Leaf *leaves, ChainNode *chain,
+                                                  const uint32_t *s_order, ConstDouble *logtab, RNG &rng,
+                                                  Counters &cn, Stamp<STAMP> &stamp, int &nnodes, int &status,
+                                                  uint64_t rp0, uint64_t rp1, int rturn, int done, int nb, double c,
+                                                  FlushSel &fs) {
+    const uint32_t lane = lane_id();
+    const int f0 = nnodes;
+    for (int i = (int)lane; i < nb; i += 64) {  // fresh slots: no children, zero in-edge counters
+        fresh[i].na = 0;
+        fresh[i].w = 0;
+        *(uint4 *)fresh[i].ch = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
+    }
+    const WalkEnd we = walk_hbm<false>(t, logtab, rp0, rp1, rturn, done, c, status);
+    fs.f0 = f0;
+    fs.x0node = we.node;
+    fs.d0 = we.depth;
+    fs.ppath = we.pathv;
+    fs.x_u = we.u;
+    fs.x_ch = we.ch;
+    fs.x0_dirty = false;
+    stamp.mark(1);
+    const uint32_t cnt0 = untried_count(we.u);
+    if (cnt0 == 0) {  // X0 has no move (full board): every leaf of the flush is X0
+        const uint32_t meta = (uint32_t)we.node | ((uint32_t)we.depth << 16) | ((uint32_t)we.turn << 24) |
+                              ((uint32_t)legal_mask(we.b0 | we.b1) << 25);
+        for (int i = (int)lane; i < nb; i += 64) leaves[i] = Leaf{we.b0, we.b1, meta, 0, we.ow, 0};
+        wave_mem_order();
+        stamp.mark(3);
+        return;
+    }
+
+    // ---- (1) the chain, its draws and its table
+    constexpr uint32_t kIdentList = 0x1AC688u;  // 0, 1, ..., 6
+    uint64_t b0 = we.b0, b1 = we.b1;
+    int turn = we.turn, depth = we.depth;
+    uint32_t ow = we.ow, cm = (uint32_t)legal_mask(b0 | b1), n = cnt0, ul = 0;
+    {
+        uint32_t k = 0;
+        for (uint32_t bb = 0; bb < 7; ++bb)
+            if ((we.u >> bb) & 1u) ul |= bb << (3 * k++);
+    }
+    int d = 0, i = 0, T = -1;  // draws so far, chain node, the terminal chain node (full board)
+    uint64_t Sm = 0;           // bit s: a chain node's first draw
+    uint32_t raw = 0;          // lane d: the accepted word of draw d
+    if (rng.off >= (uint32_t)kWin) rng_advance(rng);
+    uint32_t w = rng_view(rng);  // lane l: word off + l
+    uint64_t gt = ~0ull, Fv = 0;  // the view: lanes after the last accepted word; accepted words
+    int dv0 = 0;                  // first draw of the view
+    for (;;) {
+        const int m = min((int)n, nb - d);
+        if (lane == 0)
+            chain[i] = ChainNode{b0, b1, ow,
+                                 n | ((uint32_t)m << 4) | ((uint32_t)d << 8) | ((uint32_t)depth << 16) |
+                                     ((uint32_t)turn << 24) | (cm << 25),
+                                 ul, 0u};
+        if (m == 0) {  // a chain node without moves: the flush's remaining leaves are all it
+            T = i;
+            break;
+        }
+        Sm |= 1ull << d;
+        int k = 0;
+        for (;;) {  // this node's draws over n - k, n - k - 1, ... (a view at a time)
+            const int rem = m - k, cnt = (int)n - k;
+            uint64_t A[7];
+#pragma unroll
+            for (int s = 0; s < 7; ++s) {
+                const uint32_t nn = (uint32_t)max(cnt - s, 1);
+                A[s] = __ballot((w >> __clz(nn)) < nn);
+            }
+            uint64_t F = 0;
+#pragma unroll
+            for (int s = 0; s < 7; ++s) {
+                const uint64_t acc = (s < rem ? A[s] : 0ull) & gt;
+                const uint64_t lb = acc & (0ull - acc);
+                F |= lb;
+                gt = 0ull - (lb << 1);
+            }
+            Fv |= F;
+            const int nd = __popcll(F);
+            k += nd;
+            d += nd;
+            if (k < m) {  // the view ran out: all of it is consumed; its draws go to their lanes
+                const uint32_t di = (uint32_t)dv0 + mbcnt64(Fv);
+                const uint32_t got =
+                    (uint32_t)__builtin_amdgcn_ds_permute((int)(mask_sel(Fv, 63u, di) << 2), (int)w);
+                raw = mask_sel(lanes_in(dv0, d), raw, got);
+                rng.off += (uint32_t)kWin;
+                rng_advance(rng);
+                w = rng_view(rng);
+                gt = ~0ull;
+                Fv = 0;
+                dv0 = d;
+                continue;
+            }
+            // the node's draws are done: the next node's draws start after its last word (the
+            // chain zeroes `gt` in the steps past `rem`)
+            gt = 0ull - (2ull << (63 - __clzll(Fv)));
+            break;
+        }
+        if (d >= nb) break;
+        // the next walk enters this node's lowest untried slot
+        const int col = (int)((ow >> (3 * (ul & 7u))) & 7u);
+        const uint64_t bit = drop_bit(b0 | b1, col);
+        if (turn) b1 |= bit; else b0 |= bit;
+        turn ^= 1;
+        ++depth;
+        if (bit & kTop) {
+            cm &= ~(1u << col);
+            ow = uni(s_order[cm]);
+        }
+        n = (ow >> 24) & 15u;
+        ul = kIdentList;
+        ++i;
+    }
+    {  // the last view's draws (it always has one: a view is only left once it ran out)
+        const uint32_t di = (uint32_t)dv0 + mbcnt64(Fv);
+        const uint32_t got = (uint32_t)__builtin_amdgcn_ds_permute((int)(mask_sel(Fv, 63u, di) << 2), (int)w);
+        raw = mask_sel(lanes_in(dv0, d), raw, got);
+        rng.off += (uint32_t)(63 - __clzll(Fv | 1ull)) + 1u;
+    }
+    const int D = d;  // fresh nodes f0 .. f0 + D - 1
+    wave_mem_order();
+    stamp.mark(2);
+
+    // ---- (2) every fresh node and leaf, lane d = draw d
+    const bool act = (int)lane < D;
+    const uint32_t seg = act ? mbcnt64(Sm) + (uint32_t)((Sm >> lane) & 1ull) - 1u : 0u;
+    const ChainNode e = chain[seg];
+    const uint32_t s_i = (e.info >> 8) & 0xFFu;
+    const uint32_t dd = lane - s_i;  // the draw's index inside its node
+    const uint32_t r = raw >> __clz(act ? (e.info & 15u) - dd : 1u);
+    // draw dd's position in the node's untried list as it was before the node's draws
+    // (select_flush's Lehmer decode, each lane against its own node's earlier draws)
+    uint32_t rp[6];
+#pragma unroll
+    for (int s = 0; s < 6; ++s) rp[s] = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((s_i + (uint32_t)s) << 2), (int)r);
+    uint32_t pl = r;
+#pragma unroll
+    for (int s = 5; s >= 0; --s) pl += (dd > (uint32_t)s && pl >= rp[s]) ? 1u : 0u;
+    const uint32_t mi = (e.ul >> (3 * (pl & 7u))) & 7u;
+    const uint64_t Z = __ballot(act && pl == 0);  // per chain node: the draw holding its lowest untried slot
+    const uint64_t zl = Z & ((1ull << s_i) - 1ull);
+    const int parent = seg == 0 ? we.node : f0 + 63 - __clzll(zl | 1ull);
+    {
+        const uint32_t col = (e.ow >> (3 * mi)) & 7u;
+        const uint64_t bit = drop_bit(e.p0 | e.p1, (int)col);
+        const uint32_t tn = (e.info >> 24) & 1u, ldepth = ((e.info >> 16) & 0xFFu) + 1u;
+        const bool filled = (bit & kTop) != 0;
+        const uint32_t c_lmask = (e.info >> 25) & ~(filled ? 1u << col : 0u);
+        uint32_t c_low = e.ow;
+        if (act && filled) c_low = s_order[c_lmask];
+        if (act) {
+            *(uint4 *)&fresh[lane] = make_uint4(untried_init((c_low >> 24) & 15u), c_low,
+                                                (uint32_t)parent | (mi << 16) | (ldepth << 24), c_lmask);
+            leaves[lane] = Leaf{tn ? e.p0 : (e.p0 | bit), tn ? (e.p1 | bit) : e.p1,
+                                ((uint32_t)f0 + lane) | (ldepth << 16) | ((tn ^ 1u) << 24) | (c_lmask << 25), 0,
+                                c_low, 0};
+        }
+    }
+    if (T >= 0) {  // the terminal chain node (entered from the full node before it)
+        const ChainNode et = chain[T];
+        const uint32_t meta = (uint32_t)(f0 + 63 - __clzll(Z | 1ull)) | (((et.info >> 16) & 0xFFu) << 16) |
+                              (((et.info >> 24) & 1u) << 24) | ((et.info >> 25) << 25);
+        for (int jj = D + (int)lane; jj < nb; jj += 64) leaves[jj] = Leaf{et.p0, et.p1, meta, 0, et.ow, 0};
+    }
+    wave_mem_order();
+    // ---- (3) the chain nodes' child slots and untried words; X0's
+    if (act && seg != 0) {
+        Fresh &P = fresh[parent - f0];
+        P.ch[mi] = (uint16_t)(f0 + (int)lane);
+        atomicAnd(&P.u, ~(1u << mi));
+    }
+    uint32_t slotbit = (act && seg == 0) ? 1u << mi : 0u;  // X0's draws are lanes 0 .. m0-1 (< 8)
+    slotbit |= (uint32_t)dpp<0xB1>((int)slotbit);
+    slotbit |= (uint32_t)dpp<0x4E>((int)slotbit);
+    slotbit |= (uint32_t)dpp<0x141>((int)slotbit);
+    const uint32_t ucl = uni(slotbit);
+    const uint32_t sent =
+        (uint32_t)__builtin_amdgcn_ds_permute((int)(((act && seg == 0) ? mi : 63u) << 2), (int)((uint32_t)f0 + lane));
+    fs.x_ch = ((ucl >> (lane & 7u)) & 1u) ? sent : we.ch;
+    fs.x_u = we.u & ~ucl;
+    fs.x0_dirty = true;
+    nnodes = f0 + D;
+    wave_mem_order();
+    {  // the flush's expansions and their depths (as select_flush)
+        int dsum = 0;
+        for (int base = 0; base < D; base += 64) {
+            const int q = base + (int)lane;
+            const uint32_t dep = q < D ? fresh[q].link >> 24 : 0u;
+#pragma unroll
+            for (int bit = 0; bit < 6; ++bit) dsum += __popcll(__ballot((dep >> bit) & 1u)) << bit;
+        }
+        cn.add(cn.expansions, D);
+        cn.add(cn.depth_sum, dsum);
+    }
+    stamp.mark(3);
+}
+
 // ------------------------------------------------------------------ the search kernel
 constexpr int kSearchWaves = 4;  // games (waves) per workgroup
 __host__ __device__ constexpr size_t c4_search_wave_lds(int bs) {
@@ -421,9 +653,19 @@ __device__ __forceinline__ void search_move(const SearchParams &p, const SearchL
         FlushSel fs;
         {
             const zc_c4_state root = p.roots[gl];
-            select_flush<false, STAMP>(t, fresh, leaves, nullptr, s_order, logtab, rng, cn, stamp, nnodes,
-                                       status, uni64(root.stones[0]), uni64(root.stones[1]), uni(root.turn), done,
-                                       nb, p.c, fs);
+#ifndef ZC_NO_PLAN
+#define ZC_NO_PLAN 0
+#endif
+            // one lane per draw and lane 63 free as the permutes' discard slot (bs < 64); the chain
+            // table lives in the leaf-path area, which this search does not use
+            if (!ZC_NO_PLAN && p.bs < 64)
+                select_flush_plan<STAMP>(t, fresh, leaves, (ChainNode *)L.paths, s_order, logtab, rng, cn, stamp,
+                                         nnodes, status, uni64(root.stones[0]), uni64(root.stones[1]),
+                                         uni(root.turn), done, nb, p.c, fs);
+            else
+                select_flush<false, STAMP>(t, fresh, leaves, nullptr, s_order, logtab, rng, cn, stamp, nnodes,
+                                           status, uni64(root.stones[0]), uni64(root.stones[1]), uni(root.turn),
+                                           done, nb, p.c, fs);
         }
         const int f0 = fs.f0, d0 = fs.d0;
 
