@@ -46,7 +46,7 @@ def run(lib, S, B):
     env = dict(os.environ, ZC_LIB=os.path.join(ROOT, lib))
     out = subprocess.run([sys.executable, "-c", CHILD % (ROOT, S, B)], env=env, check=True, capture_output=True, text=True, timeout=300).stdout
     return json.loads(out.strip().splitlines()[-1])
-for S, B in [(7, 7), (9, 3), (40, 8), (200, 8), (800, 32), (300, 64)]:
+for S, B in [(7, 7), (9, 3), (40, 8), (200, 8), (800, 32), (300, 64), (500, 63)]:
     a, b = run(sys.argv[1], S, B), run(sys.argv[2], S, B)
     bad = [i for i in range(len(a["mv"])) if (a["mv"][i], a["words"][i], a["exp"][i]) != (b["mv"][i], b["words"][i], b["exp"][i])]
     print(S, B, "differ:", len(bad), "of", len(a["mv"]))

@@ -442,6 +442,7 @@ __device__ __forceinline__ void select_flush_plan(const Tree &t, Fresh *fresh, L
     uint32_t raw = 0;          // lane d: the accepted word of draw d
     if (rng.off >= (uint32_t)kWin) rng_advance(rng);
     uint32_t w = rng_view(rng);  // lane l: word off + l
+    uint32_t t3 = w >> 29;
     uint64_t gt = ~0ull, Fv = 0;  // the view: lanes after the last accepted word; accepted words
     int dv0 = 0;                  // first draw of the view
     for (;;) {
@@ -458,20 +459,23 @@ __device__ __forceinline__ void select_flush_plan(const Tree &t, Fresh *fresh, L
         Sm |= 1ull << d;
         int k = 0;
         for (;;) {  // this node's draws over n - k, n - k - 1, ... (a view at a time)
-            const int rem = m - k, cnt = (int)n - k;
+            const int rem = m - k, cnt = (int)n - k;  // rem: 1 .. 7
+            // _randbelow(nn) accepts a word when (w >> (32 - bit_length(nn))) < nn, i.e. when its
+            // top three bits t3 are below T(nn) = 4, 4, 6, 4, 5, 6, 7 for nn = 1 .. 7 (nn = 1, 2:
+            // the top bit / two bits; nn = 3: the top two bits < 3).  Step s draws over cnt - s
+            // moves: its threshold is nibble s of P (0 past rem: no word accepted).
+            const uint32_t P = (0x04464567u >> (4u * (uint32_t)(7 - cnt))) & ((1u << (4u * (uint32_t)rem)) - 1u);
             uint64_t A[7];
 #pragma unroll
-            for (int s = 0; s < 7; ++s) {
-                const uint32_t nn = (uint32_t)max(cnt - s, 1);
-                A[s] = __ballot((w >> __clz(nn)) < nn);
-            }
+            for (int s = 0; s < 7; ++s) A[s] = __ballot(t3 < ((P >> (4u * s)) & 15u));
+            // the draws, a scalar chain: each takes the lowest accepted word after the last one
+            // (s_ff1; none: -1, and gt = -2 << 63 = 0 stops the later steps), its bit = acc & ~gt
             uint64_t F = 0;
 #pragma unroll
             for (int s = 0; s < 7; ++s) {
-                const uint64_t acc = (s < rem ? A[s] : 0ull) & gt;
-                const uint64_t lb = acc & (0ull - acc);
-                F |= lb;
-                gt = 0ull - (lb << 1);
+                const uint64_t acc = A[s] & gt;
+                gt = (~1ull) << (ff1(acc) & 63u);
+                F |= acc & ~gt;
             }
             Fv |= F;
             const int nd = __popcll(F);
@@ -485,14 +489,15 @@ __device__ __forceinline__ void select_flush_plan(const Tree &t, Fresh *fresh, L
                 rng.off += (uint32_t)kWin;
                 rng_advance(rng);
                 w = rng_view(rng);
+                t3 = w >> 29;
                 gt = ~0ull;
                 Fv = 0;
                 dv0 = d;
                 continue;
             }
-            // the node's draws are done: the next node's draws start after its last word (the
-            // chain zeroes `gt` in the steps past `rem`)
-            gt = 0ull - (2ull << (63 - __clzll(Fv)));
+            // the node's draws are done: the next node's start after its last word (the steps
+            // past rem zeroed gt)
+            gt = (~1ull) << (63 - __clzll(Fv));
             break;
         }
         if (d >= nb) break;
