@@ -395,6 +395,74 @@ __device__ __forceinline__ uint64_t lanes_in(int lo, int hi) {  // lanes lo .. h
     return below_hi & ~((1ull << lo) - 1ull);
 }
 
+// walk_hbm (c4_device.h) for the rollout search, with the next level's record fetched while
+// the current level's UCT is computed: lane 8c + k loads slot k (child, Na, Wa) and header word
+// k & 3 of child c's record as soon as the node's children are known, so the memory latency of
+// a level hides under the previous level's fp64 arithmetic; the chosen child's slots then move
+// to lanes k by three bpermutes.  Same walk, same path, same result.
+__device__ __forceinline__ WalkEnd walk_hbm_prefetch(const Tree &t, ConstDouble *logtab, uint64_t rp0, uint64_t rp1,
+                                                     int rturn, int done, double c, int &status) {
+    const uint32_t lane = lane_id();
+    const uint32_t k = lane & 7u, cs = lane >> 3;  // the slot this lane scores / the child it fetches
+    int node = 0, depth = 0, turn = rturn, nN = done;  // nN = N(node) = Na of its in-edge
+    uint64_t b0 = rp0, b1 = rp1;
+    uint32_t pathv = (lane == 0) ? 0x00FF0000u : 0u;
+    const uint8_t *R0 = t.rec(0);
+    uint32_t u = uni(((const uint32_t *)R0)[1]), ow = uni(((const uint32_t *)R0)[3]);
+    uint32_t ch = ((const uint16_t *)(R0 + 16))[k];
+    int32_t na = ((const int32_t *)(R0 + 32))[k];
+    int32_t wa = ((const int32_t *)(R0 + 64))[k];
+    for (;;) {  // select (mcts.cpp:47-63) over HBM records
+        if (untried_count(u)) break;  // untried moves left: expand here
+        if (depth >= kMaxDepth - 2) {  // unreachable (a C4 tree is <= 42 deep); never spin
+            status = ZC_STATUS_INTERNAL;
+            u = 0;
+            break;
+        }
+        const uint32_t nm = u >> 28;
+        // the children's records, in flight during the selection below
+        const uint32_t cid = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(cs << 2), (int)ch);
+        uint32_t pch = 0xFFFFu, phd = 0u;
+        int32_t pna = 0, pwa = 0;
+        if (cs < nm && cid != 0xFFFFu) {
+            const uint8_t *Rc = t.rec((int)cid);
+            phd = ((const uint32_t *)Rc)[lane & 3u];
+            pch = ((const uint16_t *)(Rc + 16))[k];
+            pna = ((const int32_t *)(Rc + 32))[k];
+            pwa = ((const int32_t *)(Rc + 64))[k];
+        }
+        const double lg = logtab[nN];  // log(N), glibc values tabulated on the host
+        const bool valid = k < nm && ch != 0xFFFF;
+        int best;
+        const uint64_t unvisited = ((1ull << nm) - 1ull) & __ballot(ch != 0xFFFF) & __ballot(na == 0) & 0xFFull;
+        if (unvisited) {  // +inf beats everything; first such slot
+            best = __builtin_ctzll(unvisited);
+        } else {
+            // UCT (mcts.cpp:41-45) = fma(c, sqrt(log(N)/Na), Qa), first max in slot order
+            const double q = valid ? (double)wa / (double)na : 0.0;
+            double v = valid ? fma(c, sqrt(lg / (double)na), q) : -INFINITY;
+            int bi = (int)k;
+            argmax8(v, bi);
+            if ((__ballot(v == -INFINITY) & 1ull) != 0) break;  // no child: terminal leaf
+            best = uni(bi);
+        }
+        nN = __builtin_amdgcn_readlane(na, best);
+        const uint64_t bit = drop_bit(b0 | b1, (int)((ow >> (3 * best)) & 7u));
+        if (turn) b1 |= bit; else b0 |= bit;
+        turn ^= 1;
+        node = __builtin_amdgcn_readlane((int)ch, best);
+        ++depth;
+        if (lane == (uint32_t)depth) pathv = (uint32_t)node | ((uint32_t)best << 16);
+        const int src = (int)((8u * (uint32_t)best + k) << 2);
+        ch = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)pch);
+        na = __builtin_amdgcn_ds_bpermute(src, pna);
+        wa = __builtin_amdgcn_ds_bpermute(src, pwa);
+        u = (uint32_t)__builtin_amdgcn_readlane((int)phd, 8 * best + 1);
+        ow = (uint32_t)__builtin_amdgcn_readlane((int)phd, 8 * best + 3);
+    }
+    return WalkEnd{node, depth, turn, b0, b1, pathv, u, ow, ch};
+}
+
 template <bool STAMP, class RNG>
 __device__ __forceinline__ void select_flush_plan(const Tree &t, Fresh *fresh, Leaf *leaves, ChainNode *chain,
                                                   const uint32_t *s_order, ConstDouble *logtab, RNG &rng,
@@ -408,7 +476,11 @@ __device__ __forceinline__ void select_flush_plan(const Tree &t, Fresh *fresh, L
         fresh[i].w = 0;
         *(uint4 *)fresh[i].ch = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
     }
-    const WalkEnd we = walk_hbm<false>(t, logtab, rp0, rp1, rturn, done, c, status);
+#ifndef ZC_WALK_PREFETCH
+#define ZC_WALK_PREFETCH 1
+#endif
+    const WalkEnd we = ZC_WALK_PREFETCH ? walk_hbm_prefetch(t, logtab, rp0, rp1, rturn, done, c, status)
+                                        : walk_hbm<false>(t, logtab, rp0, rp1, rturn, done, c, status);
     fs.f0 = f0;
     fs.x0node = we.node;
     fs.d0 = we.depth;
