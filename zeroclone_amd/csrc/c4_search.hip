@@ -193,7 +193,9 @@ __device__ void c4_rollouts(Leaf *L, int nb, R &rng, const uint32_t *s_order, Co
                     if (A) break;
                     rng.off += (uint32_t)kWin;
                 }
+#ifndef ZC_DIAG_WASTE
                 cn.add(cn.blocks, 1);
+#endif
                 RMARK(2);
                 const uint32_t cap_r = min((uint32_t)room, 30u);  // last ply index the board allows
                 uint32_t qk = mbcnt(A);                            // this lane's ply in the block
@@ -262,6 +264,10 @@ __device__ void c4_rollouts(Leaf *L, int nb, R &rng, const uint32_t *s_order, Co
                 const uint32_t endlane = min(ff1(Ew), l0);
                 const uint32_t endply = (uint32_t)__builtin_amdgcn_readlane((int)qk, (int)endlane);
                 rng.off += endlane + 1u;  // words through the block's last ply are consumed
+#ifdef ZC_DIAG_WASTE
+                cn.add(cn.blocks, lf < 64u && endlane < lf ? 1 : 0);
+                cn.add(cn.plies, lf < 64u ? 1 : 0);
+#endif
                 // both sides' stones after ply endply: first mover through ply 2*(endply/2)
                 // (row 0, inclusive), second mover through the odd plies <= endply (row 1,
                 // inclusive scan at lane 15 + (endply+1)/2; none when endply = 0)
@@ -301,7 +307,9 @@ __device__ void c4_rollouts(Leaf *L, int nb, R &rng, const uint32_t *s_order, Co
             q = room0 - room;
         }
         L[j].val = val;  // uniform: every lane stores
+#ifndef ZC_DIAG_WASTE
         cn.add(cn.plies, q);
+#endif
     }
 }
 
