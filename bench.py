@@ -492,15 +492,17 @@ def exchange_positions(local, world: int, sync=lambda: None):
     return out, allpos
 
 
+# the committed rocprofv3 summary of the current search kernel (tools/summarize_profile.py:
+# HBM bytes per launch from separate FETCH_SIZE / WRITE_SIZE passes, SQ issue counters)
+SEARCH_PROFILE = os.path.join("profiles", "r03_plan_c4_search_summary.json")
+
+
 def search_profile():
-    """The newest committed rocprofv3 summary of the search kernel (tools/summarize_profile.py:
-    HBM bytes per launch from separate FETCH_SIZE / WRITE_SIZE passes, SQ issue counters)."""
-    import glob
-    prof = sorted(glob.glob(os.path.join(HERE, "profiles", "r*_c4_search_summary.json")))
-    if not prof:
+    path = os.path.join(HERE, SEARCH_PROFILE)
+    if not os.path.exists(path):
         return {}, None
-    with open(prof[-1]) as fh:
-        return json.load(fh), os.path.relpath(prof[-1], HERE)
+    with open(path) as fh:
+        return json.load(fh), SEARCH_PROFILE
 
 
 def run_rank(args, rank: int, world: int, local: int):
