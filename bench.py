@@ -624,16 +624,16 @@ def phases(sp, args, bytes_launch: float, avg_kernel_s: float, traffic: float | 
     return {"share": {k: round(v, 4) for k, v in share.items()},
             "ms_per_launch": {k: round(v * avg_kernel_s * 1e3, 3) for k, v in share.items()},
             "walk_roofline": {"t_walk_ms": round(walk * avg_kernel_s * 1e3, 3),
-                              "achieved": round(bytes_launch / (walk * avg_kernel_s) / 1e9, 2),
-                              "frac": round(bytes_launch / (walk * avg_kernel_s) / 1e9 / HBM_PEAK_GBS, 5),
+                              "model_gbs": round(bytes_launch / (walk * avg_kernel_s) / 1e9, 2),
+                              "model_frac": round(bytes_launch / (walk * avg_kernel_s) / 1e9 / HBM_PEAK_GBS, 5),
                               "measured_frac": (round(traffic / (walk * avg_kernel_s) / 1e9 / HBM_PEAK_GBS, 5)
                                                 if traffic else None),
                               "note": "SURVEY §8(d) roofline definition: model bytes / tree-walk time only "
                                       "(phase shares from the stamped build: modelled, not a separate clock). "
                                       "The model counts a root-to-leaf re-read per simulation that the kernel "
-                                      "serves from LDS / L2, so frac ~1 is the model's ceiling, not HBM "
-                                      "saturation: measured_frac = the whole kernel's PMC HBM bytes over the "
-                                      "walk time alone"}}
+                                      "serves from LDS / L2 (or never reads: the planned flush), so model_frac "
+                                      "can exceed 1 and is NOT a measured HBM rate; measured_frac = the whole "
+                                      "kernel's PMC HBM bytes over the walk time alone"}}
 
 
 def tower_mode(dev, reps: int = 5) -> dict:
