@@ -183,6 +183,42 @@ def test_full_size_batch_matches_oracle(eng):
     assert (stats["leaves"] == sims).all() and (stats["status"] == 0).all()
 
 
+@pytest.mark.parametrize("bs", [1, 2, 7, 8, 13, 32, 63, 64, 100])
+def test_planned_flush_deep_roots_match_oracle(eng, bs):
+    """The planned flush (select_flush_plan, batch sizes < 64; select_flush at 64 and up) from
+    deep roots: chains that reach a full board (a terminal chain node takes the rest of the
+    flush's leaves), nodes with one to seven moves, fills on the chain, draws spanning views.
+    Every game's move, root visits and stream words equal the oracle's."""
+    n, sims = 768, 240
+    rng = random.Random(500 + bs)
+    boards = []
+    while len(boards) < n:
+        b, t = "." * 42, 0
+        lean = rng.sample(range(7), rng.randint(1, 3))  # columns filled first: chains hit full columns
+        ok = True
+        for _ in range(rng.randint(18, 41)):
+            legal = [col for col in range(7) if b[col] == "."]
+            pref = [col for col in legal if col in lean]
+            b, t = oracle.play(b, t, rng.choice(pref if pref and rng.random() < 0.7 else legal))
+            if oracle.check_win(b, t):
+                ok = rng.random() < 0.1  # a few already-won roots stay (get_move still searches them)
+                break
+        if ok and not oracle.check_draw(b):
+            boards.append((b, t))
+    seeds = [7919 * g + bs for g in range(n)]
+    eng.seed(0, seeds)
+    from zeroclone_amd._native import C4_STATE_DTYPE
+    st = np.zeros(n, C4_STATE_DTYPE)
+    for i, (b, t) in enumerate(boards):
+        st[i] = to_state(b, t)
+    mv, na, stats = eng.c4_search(st, sims, 1.4, bs)
+    omv, ona, ocons = oracle.get_move_batch([b for b, _ in boards], [t for _, t in boards], seeds, sims, 1.4, bs,
+                                            threads=16)
+    assert np.array_equal(mv, omv)
+    assert np.array_equal(na, ona)
+    assert np.array_equal(stats["rng_words"], ocons.astype(np.int64))
+
+
 def test_invalid_roots_raise(eng):
     full = "XOXOXOX" * 6
     with pytest.raises(ValueError):
