@@ -268,16 +268,6 @@ __device__ void c4_rollouts(Leaf *L, int nb, R &rng, const uint32_t *s_order, Co
                 cn.add(cn.blocks, lf < 64u && endlane < lf ? 1 : 0);
                 cn.add(cn.plies, lf < 64u ? 1 : 0);
 #endif
-                // both sides' stones after ply endply: first mover through ply 2*(endply/2)
-                // (row 0, inclusive), second mover through the odd plies <= endply (row 1,
-                // inclusive scan at lane 15 + (endply+1)/2; none when endply = 0)
-                const uint64_t s2 = readlane64(mine, (int)((endply + 31u) >> 1));
-                const uint64_t a2 = me | readlane64(mine, (int)(endply >> 1));
-                const uint64_t b2 = op | (endply ? s2 : 0ull);
-                const bool odd = endply & 1u;  // an even number of plies: the first mover is to move again
-                me = odd ? a2 : b2;
-                op = odd ? b2 : a2;
-                hp += (uint32_t)__builtin_amdgcn_readlane((int)sc, (int)endlane);  // plies per column through endlane
                 room -= (int)endply + 1;
                 RMARK(5);
                 if (Ew) {  // the ply's mover completed four
@@ -288,6 +278,19 @@ __device__ void c4_rollouts(Leaf *L, int nb, R &rng, const uint32_t *s_order, Co
                     val = 0;
                     break;
                 }
+                // the rollout goes on (most end in their first block, so this is off the common
+                // path): both sides' stones after ply endply — first mover through ply
+                // 2*(endply/2) (row 0, inclusive), second mover through the odd plies <= endply
+                // (row 1, inclusive scan at lane 15 + (endply+1)/2; none when endply = 0)
+                {
+                    const uint64_t s2 = readlane64(mine, (int)((endply + 31u) >> 1));
+                    const uint64_t a2 = me | readlane64(mine, (int)(endply >> 1));
+                    const uint64_t b2 = op | (endply ? s2 : 0ull);
+                    const bool odd = endply & 1u;  // an even number of plies: the first mover is to move again
+                    me = odd ? a2 : b2;
+                    op = odd ? b2 : a2;
+                }
+                hp += (uint32_t)__builtin_amdgcn_readlane((int)sc, (int)endlane);  // plies per column through endlane
                 // the legal set (and its CPython order) after the block's fills: the absorbed
                 // one if it was played, and the one the block ended at
                 const bool fa = endlane >= lf;
