@@ -209,7 +209,9 @@ __device__ void c4_rollouts(Leaf *L, int nb, R &rng, const uint32_t *s_order, Co
                 uint32_t row = ((sc - one + hp) >> (4 * col)) & 15u;  // the column's height + earlier plies in it
                 uint32_t nacc = (uint32_t)__popcll(A);
                 bool fills = row == 5u;
-                uint64_t E0 = __ballot(mask_sel0(A, (fills ? 63u : qk) + 1u) > min(cap_r, nacc - 1u));
+                // the block's end: its first fill, or the first ply past the cap / the view's last
+                // accepted word (masks ANDed on the scalar unit, one lane compare)
+                uint64_t E0 = A & (__ballot(fills) | __ballot(qk >= min(cap_r, nacc - 1u)));
                 uint32_t l0 = (uint32_t)__builtin_ctzll(E0);
                 // the first fill, with room for more plies: re-draw the words after it under
                 // the new legal set
@@ -226,16 +228,14 @@ __device__ void c4_rollouts(Leaf *L, int nb, R &rng, const uint32_t *s_order, Co
                     const uint32_t v2 = wv >> __clz(n2);
                     const uint64_t low = (2ull << lf) - 1ull;  // lanes 0..lf
                     A = (A & low) | (__ballot(v2 < n2) & ~low);
-                    v = mask_sel(low, v2, v);
-                    const uint32_t owl = mask_sel(low, ow2, ow);
                     qk = mbcnt(A);
-                    col = (owl >> (3 * v)) & 7u;
+                    col = mask_sel(low, (ow2 >> (3 * v2)) & 7u, col);  // lanes after lf: the new order
                     one = mask_sel0(A, 1u << (4 * col));
                     sc = scan_add32(one);
                     row = ((sc - one + hp) >> (4 * col)) & 15u;
                     nacc = (uint32_t)__popcll(A);
                     fills = row == 5u && lane > lf;  // the absorbed fill no longer ends the block
-                    E0 = __ballot(mask_sel0(A, (fills ? 63u : qk) + 1u) > min(cap_r, nacc - 1u));
+                    E0 = A & (__ballot(fills) | __ballot(qk >= min(cap_r, nacc - 1u)));
                     l0 = (uint32_t)__builtin_ctzll(E0);
                 }
                 RMARK(4);
