@@ -217,10 +217,9 @@ __device__ void c4_rollouts(Leaf *L, int nb, R &rng, const uint32_t *s_order, Co
                 // the new legal set
                 uint32_t lf = 64u;  // lane of the absorbed fill (64: none)
                 uint32_t ow2 = ow, cf = 0;
-                // (one lane test, one mask bit: fills with ply < cap_r, at l0)
-                const uint64_t FA = __ballot(qk < cap_r) & __ballot(fills);
+                uint32_t last = (uint32_t)__builtin_amdgcn_readlane((int)qk, (int)l0);  // the block's last ply before any win
                 RMARK(3);
-                if ((FA >> l0) & 1u) {
+                if (((__ballot(fills) >> l0) & 1u) && last < cap_r) {  // a fill with room for more plies
                     lf = l0;
                     cf = (uint32_t)__builtin_amdgcn_readlane((int)col, (int)lf);
                     ow2 = (uint32_t)__builtin_amdgcn_readlane((int)owp, (int)(8u * cf));
@@ -237,11 +236,10 @@ __device__ void c4_rollouts(Leaf *L, int nb, R &rng, const uint32_t *s_order, Co
                     fills = row == 5u && lane > lf;  // the absorbed fill no longer ends the block
                     E0 = A & (__ballot(fills) | __ballot(qk >= min(cap_r, nacc - 1u)));
                     l0 = (uint32_t)__builtin_ctzll(E0);
+                    last = (uint32_t)__builtin_amdgcn_readlane((int)qk, (int)l0);
                 }
                 RMARK(4);
-                // the block's last ply before any win
-                const uint32_t last = (uint32_t)__builtin_amdgcn_readlane((int)qk, (int)l0);
-                const uint64_t K = __ballot(mask_sel(A, 255u, qk) <= last);  // lanes of plies 0..last
+                const uint64_t K = A & __ballot(qk <= last);  // lanes of plies 0..last
                 // compact plies 0..last by parity into lanes 0..31 (a forward lane permute;
                 // other lanes all go to lane 31, which no ply <= 30 uses), then copy them 32
                 // lanes up
@@ -250,17 +248,19 @@ __device__ void c4_rollouts(Leaf *L, int nb, R &rng, const uint32_t *s_order, Co
                 const uint32_t pl = (uint32_t)__builtin_amdgcn_ds_permute((int)(mask_sel(K, 31u, c) << 2), (int)b);
                 const uint32_t pb = __builtin_amdgcn_permlane32_swap(pl, pl, false, false)[0];
                 const uint64_t V = __ballot(myply <= last);  // lanes holding plies 0..last
-                const uint64_t bit = 1ull << pb;
-                uint32_t blo = mask_sel0(V, (uint32_t)bit), bhi = mask_sel0(V, (uint32_t)(bit >> 32));
+                // lanes past `last` hold garbage cells; each row's plies ascend along its lanes, so
+                // their bits only reach their own (masked) prefixes
+                const uint64_t bit = 1ull << (pb & 63u);
+                uint32_t blo = (uint32_t)bit, bhi = (uint32_t)(bit >> 32);
                 scan_or16x2(blo, bhi);
                 const uint64_t mine = ((uint64_t)bhi << 32) | blo;  // this row's stones so far
                 const uint64_t bd = (first_row ? me : op) | mine;
                 const uint64_t m1 = bd & (bd >> d1), m2 = bd & (bd >> d2);
                 const uint64_t f4 = (m1 & (m1 >> (2 * d1))) | (m2 & (m2 >> (2 * d2)));
-                const uint64_t W = __ballot(mask_sel0(V, (uint32_t)f4 | (uint32_t)(f4 >> 32)) != 0u);
+                const uint64_t W = V & __ballot(f4 != 0ull);
                 // back to word order: the accepted lane of ply qk won if its compacted lane did
                 const uint32_t W32 = (uint32_t)W | (uint32_t)(W >> 32);
-                const uint64_t Ew = __ballot(mask_sel0(K, (W32 >> c) & 1u) != 0u);
+                const uint64_t Ew = K & __ballot(((W32 >> c) & 1u) != 0u);
                 const uint32_t endlane = min(ff1(Ew), l0);
                 const uint32_t endply = (uint32_t)__builtin_amdgcn_readlane((int)qk, (int)endlane);
                 rng.off += endlane + 1u;  // words through the block's last ply are consumed
