@@ -170,6 +170,7 @@ struct Rng {
     uint32_t wx;     // raw x[window start + 128 + lane], in flight until the window advances
     __device__ __forceinline__ int32_t use() const { return wrel + (int32_t)off; }  // relative to use0
     __device__ __forceinline__ uint32_t slot(int32_t rel) const { return (base + (uint32_t)rel) & kRingMask; }
+    __device__ __forceinline__ uint32_t cur() const { return wt; }
 };
 
 __device__ __forceinline__ int32_t rng_generate(uint32_t *ring, uint32_t base, int32_t grel, int32_t target) {
@@ -264,8 +265,11 @@ struct LRng {
     int32_t wrel;    // window start - use0
     uint32_t off;    // next word to consume = window start + off, off in [0, 128)
     int32_t hrel;    // words [.., use0 + hrel) were in the ring at the start (hrel >= 192 - off)
-    uint32_t wt;     // tempered x[W + lane]
-    uint32_t wn;     // tempered x[W + 64 + lane]
+    // the two tempered windows stay in their registers: wa/wb hold x[W + lane] and
+    // x[W + 64 + lane] when ph == 0, the other way round when ph == 64 (an advance overwrites
+    // the older one in place and flips ph: no register rotation, so no loop-carried copies)
+    uint32_t wa, wb, ph;
+    __device__ __forceinline__ uint32_t cur() const { return ph ? wb : wa; }  // tempered x[W + lane]
     uint32_t wx;     // raw x[W + 128 + lane]
     uint32_t ia, ib, im;  // raw x[p-624], x[p-623], x[p-227] for p = W + 192 + lane (the next step)
     __device__ __forceinline__ int32_t use() const { return wrel + (int32_t)off; }
@@ -317,18 +321,30 @@ __device__ __forceinline__ void lrng_open(LRng &r, uint32_t *lds, const uint32_t
     wave_mem_order();
     lrng_generate_abs(lds, g, target);
     r.hrel = (int32_t)(g - use0);
-    r.wt = temper(lds[r.slot(r.wrel + (int32_t)lane)]);
-    r.wn = temper(lds[r.slot(r.wrel + kWin + (int32_t)lane)]);
+    r.wa = temper(lds[r.slot(r.wrel + (int32_t)lane)]);
+    r.wb = temper(lds[r.slot(r.wrel + kWin + (int32_t)lane)]);
+    r.ph = 0;
     r.wx = lds[r.slot(r.wrel + 2 * kWin + (int32_t)lane)];
     lrng_prefetch(r);
+}
+
+// rng_view for the LDS stream: the window holding word off + l is wa or wb by ph
+__device__ __forceinline__ uint32_t rng_view(const LRng &r) {
+    const uint32_t j = lane_id() + r.off;
+    const int idx = (int)(j << 2);
+    const uint32_t a = (uint32_t)__builtin_amdgcn_ds_bpermute(idx, (int)r.wa);
+    const uint32_t b = (uint32_t)__builtin_amdgcn_ds_bpermute(idx, (int)r.wb);
+    return (j ^ r.ph) < 64u ? a : b;
 }
 
 // Move the windows on by 64 words (precondition: off >= 64); one recurrence step.
 __device__ __forceinline__ void rng_advance(LRng &r) {
     r.wrel += kWin;
     r.off -= (uint32_t)kWin;
-    r.wt = r.wn;
-    r.wn = temper(r.wx);
+    const uint32_t t = temper(r.wx);  // the new second window replaces the old first one
+    if (r.ph) r.wb = t;
+    else r.wa = t;
+    r.ph ^= 64u;
     const int32_t p = r.wrel + 128 + (int32_t)lane_id();
     uint32_t x = mt_twist(r.ia, r.ib, r.im);
     if (r.wrel + 128 < r.hrel) {  // only inside the seeded block: words already in the ring
@@ -373,7 +389,7 @@ __device__ __forceinline__ uint32_t rng_below(R &r, uint32_t n) {
     const uint32_t lane = lane_id();
     for (;;) {
         if (r.off >= (uint32_t)kWin) rng_advance(r);
-        const uint32_t v = r.wt >> sh;
+        const uint32_t v = r.cur() >> sh;
         // one compare: words before `off` get bit 31 set (never < n)
         const uint64_t bal = __ballot((v | ((lane - r.off) & 0x80000000u)) < n);
         if (bal) {
@@ -395,7 +411,7 @@ __device__ __forceinline__ uint32_t rng_below_pick(R &r, uint32_t n, const uint8
     const uint32_t lane = lane_id();
     for (;;) {
         if (r.off >= (uint32_t)kWin) rng_advance(r);
-        const uint32_t v = r.wt >> sh;
+        const uint32_t v = r.cur() >> sh;
         const uint32_t pick = row[v & 7u];
         const uint64_t bal = __ballot((v | ((lane - r.off) & 0x80000000u)) < n);
         if (bal) {

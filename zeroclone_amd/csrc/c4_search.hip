@@ -126,7 +126,6 @@ __device__ void c4_rollouts(Leaf *L, int nb, R &rng, const uint32_t *s_order, Co
     uint64_t t_ = ZC_RSTAMP && sub ? __builtin_amdgcn_s_memtime() : 0;
     const uint32_t lane = lane_id();
     const uint32_t lrow = lane >> 4;
-    const uint32_t myply = 2u * (lane & 15u) + (lrow & 1u);  // ply of this lane in the compacted layout
     const bool first_row = (lrow & 1u) == 0;                  // rows 0, 2: the block's first mover
     const uint32_t d1 = lrow < 2 ? 1u : 6u, d2 = lrow < 2 ? 7u : 8u;
     // lane 7a + b (< 49): the columns {a, b} (a == b: one column) whose fills a block may see
@@ -183,15 +182,20 @@ __device__ void c4_rollouts(Leaf *L, int nb, R &rng, const uint32_t *s_order, Co
                 RMARK(6);
                 uint32_t wv, v;
                 uint64_t A;  // accepted words
-                // a view without an accepted word (2^-64 at worst) is consumed whole; its own
-                // loop keeps the block loop's state off a second back edge
-                for (;;) {
-                    if (rng.off >= (uint32_t)kWin) rng_advance(rng);
-                    wv = rng_view(rng);  // lane l: word off + l
-                    v = wv >> sh;
-                    A = __ballot(v < n);
-                    if (A) break;
-                    rng.off += (uint32_t)kWin;
+                // a view without an accepted word (2^-64 at worst) is consumed whole, in a loop
+                // of its own off the common path (no loop-carried copies of the stream position)
+                if (rng.off >= (uint32_t)kWin) rng_advance(rng);
+                wv = rng_view(rng);  // lane l: word off + l
+                v = wv >> sh;
+                A = __ballot(v < n);
+                if (__builtin_expect(A == 0ull, 0)) {
+                    do {
+                        rng.off += (uint32_t)kWin;
+                        rng_advance(rng);
+                        wv = rng_view(rng);
+                        v = wv >> sh;
+                        A = __ballot(v < n);
+                    } while (A == 0ull);
                 }
 #ifndef ZC_DIAG_WASTE
                 cn.add(cn.blocks, 1);
@@ -208,21 +212,25 @@ __device__ void c4_rollouts(Leaf *L, int nb, R &rng, const uint32_t *s_order, Co
                 uint32_t sc = scan_add32(one);
                 uint32_t row = ((sc - one + hp) >> (4 * col)) & 15u;  // the column's height + earlier plies in it
                 uint32_t nacc = (uint32_t)__popcll(A);
-                bool fills = row == 5u;
+                // the fills, kept as a wave mask (a per-lane bool merged across the absorption
+                // would be materialised and compared again)
+                uint64_t F = __ballot(row == 5u);
                 // the block's end: its first fill, or the first ply past the cap / the view's last
                 // accepted word (masks ANDed on the scalar unit, one lane compare)
-                uint64_t E0 = A & (__ballot(fills) | __ballot(qk >= min(cap_r, nacc - 1u)));
+                uint64_t E0 = A & (F | __ballot(qk >= min(cap_r, nacc - 1u)));
                 uint32_t l0 = (uint32_t)__builtin_ctzll(E0);
+                // the fills with room for more plies after them: the block's end is one of these
+                // exactly when it is the first of them
+                const uint64_t G = A & F & __ballot(qk < cap_r);
                 // the first fill, with room for more plies: re-draw the words after it under
                 // the new legal set
                 uint32_t lf = 64u;  // lane of the absorbed fill (64: none)
-                uint32_t ow2 = ow, cf = 0;
-                uint32_t last = (uint32_t)__builtin_amdgcn_readlane((int)qk, (int)l0);  // the block's last ply before any win
+                uint32_t cf = 0;
                 RMARK(3);
-                if (((__ballot(fills) >> l0) & 1u) && last < cap_r) {  // a fill with room for more plies
+                if (ff1(G) == l0) {  // a fill with room for more plies
                     lf = l0;
                     cf = (uint32_t)__builtin_amdgcn_readlane((int)col, (int)lf);
-                    ow2 = (uint32_t)__builtin_amdgcn_readlane((int)owp, (int)(8u * cf));
+                    const uint32_t ow2 = (uint32_t)__builtin_amdgcn_readlane((int)owp, (int)(8u * cf));
                     const uint32_t n2 = (ow2 >> 24) & 15u;
                     const uint32_t v2 = wv >> __clz(n2);
                     const uint64_t low = (2ull << lf) - 1ull;  // lanes 0..lf
@@ -233,23 +241,21 @@ __device__ void c4_rollouts(Leaf *L, int nb, R &rng, const uint32_t *s_order, Co
                     sc = scan_add32(one);
                     row = ((sc - one + hp) >> (4 * col)) & 15u;
                     nacc = (uint32_t)__popcll(A);
-                    fills = row == 5u && lane > lf;  // the absorbed fill no longer ends the block
-                    E0 = A & (__ballot(fills) | __ballot(qk >= min(cap_r, nacc - 1u)));
+                    F = __ballot(row == 5u) & ~low;  // the absorbed fill no longer ends the block
+                    E0 = A & (F | __ballot(qk >= min(cap_r, nacc - 1u)));
                     l0 = (uint32_t)__builtin_ctzll(E0);
-                    last = (uint32_t)__builtin_amdgcn_readlane((int)qk, (int)l0);
                 }
                 RMARK(4);
-                const uint64_t K = A & __ballot(qk <= last);  // lanes of plies 0..last
-                // compact plies 0..last by parity into lanes 0..31 (a forward lane permute;
-                // other lanes all go to lane 31, which no ply <= 30 uses), then copy them 32
-                // lanes up
-                const uint32_t c = ((qk & 1u) << 4) | (qk >> 1);
-                const uint32_t b = 7u * col + row;  // the ply's cell (lanes without a ply: masked by V)
-                const uint32_t pl = (uint32_t)__builtin_amdgcn_ds_permute((int)(mask_sel(K, 31u, c) << 2), (int)b);
+                // compact EVERY accepted word's ply by parity: ply q < 32 to lane (q & 1)*16 + q/2
+                // (a forward lane permute; the other lanes, and plies >= 32, land in lanes 32..63),
+                // then copy lanes 0..31 up over lanes 32..63.  No ply past the block's last one (at
+                // lane l0) needs masking: each row's plies ascend along its lanes, so a later ply's
+                // stones only reach its own prefix, and its win can only show up in a word lane
+                // beyond l0 (the end is min(first win, l0) below)
+                const uint32_t c = ((qk & 1u) << 4) | ((qk >> 1) & 15u) | (qk & 32u);
+                const uint32_t b = __umul24(col, 7u) + row;  // the ply's cell (a 24-bit mad, not a 64-bit one)
+                const uint32_t pl = (uint32_t)__builtin_amdgcn_ds_permute((int)(mask_sel(A, 63u, c) << 2), (int)b);
                 const uint32_t pb = __builtin_amdgcn_permlane32_swap(pl, pl, false, false)[0];
-                const uint64_t V = __ballot(myply <= last);  // lanes holding plies 0..last
-                // lanes past `last` hold garbage cells; each row's plies ascend along its lanes, so
-                // their bits only reach their own (masked) prefixes
                 const uint64_t bit = 1ull << (pb & 63u);
                 uint32_t blo = (uint32_t)bit, bhi = (uint32_t)(bit >> 32);
                 scan_or16x2(blo, bhi);
@@ -257,11 +263,13 @@ __device__ void c4_rollouts(Leaf *L, int nb, R &rng, const uint32_t *s_order, Co
                 const uint64_t bd = (first_row ? me : op) | mine;
                 const uint64_t m1 = bd & (bd >> d1), m2 = bd & (bd >> d2);
                 const uint64_t f4 = (m1 & (m1 >> (2 * d1))) | (m2 & (m2 >> (2 * d2)));
-                const uint64_t W = V & __ballot(f4 != 0ull);
+                const uint64_t W = __ballot(f4 != 0ull);
                 // back to word order: the accepted lane of ply qk won if its compacted lane did
                 const uint32_t W32 = (uint32_t)W | (uint32_t)(W >> 32);
-                const uint64_t Ew = K & __ballot(((W32 >> c) & 1u) != 0u);
-                const uint32_t endlane = min(ff1(Ew), l0);
+                const uint64_t Ew = A & __ballot(((W32 >> (c & 31u)) & 1u) != 0u);
+                const uint32_t ew = ff1(Ew);
+                const uint32_t endlane = min(ew, l0);
+                const bool win = ew <= l0;  // (ff1 of an empty mask is 0xFFFFFFFF)
                 const uint32_t endply = (uint32_t)__builtin_amdgcn_readlane((int)qk, (int)endlane);
                 rng.off += endlane + 1u;  // words through the block's last ply are consumed
 #ifdef ZC_DIAG_WASTE
@@ -270,7 +278,7 @@ __device__ void c4_rollouts(Leaf *L, int nb, R &rng, const uint32_t *s_order, Co
 #endif
                 room -= (int)endply + 1;
                 RMARK(5);
-                if (Ew) {  // the ply's mover completed four
+                if (win) {  // the ply's mover completed four
                     val = ((room0 - room) & 1) ? 1 : -1;  // an odd number of plies: the leaf's side won
                     break;
                 }
@@ -294,7 +302,7 @@ __device__ void c4_rollouts(Leaf *L, int nb, R &rng, const uint32_t *s_order, Co
                 // the legal set (and its CPython order) after the block's fills: the absorbed
                 // one if it was played, and the one the block ended at
                 const bool fa = endlane >= lf;
-                const bool fe = (__ballot(fills) >> endlane) & 1u;
+                const bool fe = (F >> endlane) & 1u;
                 {  // unconditional (selects), so the block loop carries one copy of its state
                     const uint32_t ce = fe ? (uint32_t)__builtin_amdgcn_readlane((int)col, (int)endlane) : cf;
                     const uint32_t ca = fa ? cf : ce;
