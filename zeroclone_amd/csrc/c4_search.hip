@@ -131,28 +131,27 @@ __device__ void c4_rollouts(Leaf *L, int nb, R &rng, const uint32_t *s_order, Co
     // lane 7a + b (< 49): the columns {a, b} (a == b: one column) whose fills a block may see
     const uint32_t pairbits = lane < 49u ? (1u << (lane / 7u)) | (1u << (lane % 7u)) : 0u;
     // per leaf, lane-parallel (lane = leaf of a group of 64): side to move / last mover stones,
-    // has_four(last mover) and 41 - stones, read out by readlane when the leaf's turn comes
-    uint64_t won_m = 0;
-    uint32_t lm_v = 0, ow_v = 0, hp_v = 0;
-    int room_v = 0;
-    for (int j = 0; j < nb; ++j) {
-        RMARK(6);  // regions: 1 leaf setup, 2 view, 3 first segment, 4 absorbed fill, 5 win test, 6 block tail
-        const int jl = j & 63;
-        if (jl == 0) {
-            const int jj = j + (int)lane;
-            uint64_t op_v = 0;
-            if (jj < nb) {
-                lm_v = L[jj].meta;
-                ow_v = L[jj].ow;
-                const uint64_t x0 = L[jj].p0, x1 = L[jj].p1;
-                op_v = (lm_v >> 24) & 1u ? x0 : x1;
-                room_v = 41 - __popcll(x0 | x1);
-                const uint64_t oc = x0 | x1;  // column heights, 4 bits per column
-                hp_v = 0;
-                for (int c = 0; c < 7; ++c) hp_v |= (uint32_t)__popcll((oc >> (7 * c)) & 0x3Full) << (4 * c);
-            }
-            won_m = __ballot(jj < nb && has_four(op_v));
+    // 41 - stones (-2: has_four(last mover), the leaf is won), read out by readlane when the
+    // leaf's turn comes
+    for (int g = 0; g < nb; g += 64) {
+      uint32_t lm_v = 0, ow_v = 0, hp_v = 0;
+      int room_v = 0;
+      {
+        const int jj = g + (int)lane;
+        if (jj < nb) {
+            lm_v = L[jj].meta;
+            ow_v = L[jj].ow;
+            const uint64_t x0 = L[jj].p0, x1 = L[jj].p1;
+            const uint64_t op_v = (lm_v >> 24) & 1u ? x0 : x1;
+            room_v = has_four(op_v) ? -2 : 41 - __popcll(x0 | x1);
+            const uint64_t oc = x0 | x1;  // column heights, 4 bits per column
+            for (int c = 0; c < 7; ++c) hp_v |= (uint32_t)__popcll((oc >> (7 * c)) & 0x3Full) << (4 * c);
         }
+      }
+      const int jend = min(nb, g + 64);
+      for (int j = g; j < jend; ++j) {
+        RMARK(6);  // regions: 1 leaf setup, 2 view, 3 first segment, 4 absorbed fill, 5 win test, 6 block tail
+        const int jl = j - g;
         const uint32_t lm = (uint32_t)__builtin_amdgcn_readlane((int)lm_v, jl);
         // the leaf's boards straight from LDS into VGPRs (one uniform address per read: a
         // broadcast), in flight while the first view is gathered
@@ -163,7 +162,7 @@ __device__ void c4_rollouts(Leaf *L, int nb, R &rng, const uint32_t *s_order, Co
         uint32_t hp = (uint32_t)__builtin_amdgcn_readlane((int)hp_v, jl);  // column heights, carried across blocks
         const uint32_t low0 = (uint32_t)__builtin_amdgcn_readlane((int)ow_v, jl);
         const int room0 = __builtin_amdgcn_readlane(room_v, jl);
-        const bool won = (won_m >> jl) & 1u;
+        const bool won = room0 == -2;
         int val = 0;
         int q = 0;  // plies played in this rollout (room0 - room when it ends)
         RMARK(1);
@@ -174,7 +173,7 @@ __device__ void c4_rollouts(Leaf *L, int nb, R &rng, const uint32_t *s_order, Co
             int mask = (int)(lm >> 25);
             uint32_t ow = low0;
             uint32_t n = (ow >> 24) & 15u;
-            uint32_t sh = (uint32_t)__clz(n);
+            uint32_t sh = (uint32_t)__builtin_clz(n);  // n >= 1 (room >= 0)
             // order words of the legal set minus the columns of `pairbits`, for the fills
             // (read as soon as the legal set is known, well before a fill needs it)
             uint32_t owp = s_order[(uint32_t)mask & ~pairbits];
@@ -313,7 +312,7 @@ __device__ void c4_rollouts(Leaf *L, int nb, R &rng, const uint32_t *s_order, Co
                     owp = s_order[(uint32_t)mask & ~pairbits];
                 }
                 n = (ow >> 24) & 15u;
-                sh = (uint32_t)__clz(n);
+                sh = (uint32_t)__builtin_clz(n);
             }
             q = room0 - room;
         }
@@ -321,6 +320,7 @@ __device__ void c4_rollouts(Leaf *L, int nb, R &rng, const uint32_t *s_order, Co
 #ifndef ZC_DIAG_WASTE
         cn.add(cn.plies, q);
 #endif
+      }
     }
 }
 
