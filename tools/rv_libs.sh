@@ -1,6 +1,9 @@
 #!/bin/bash
 # Builds zeroclone_amd/lib_rv<k>.so for each ZC_RV mask given (c4_search.hip under -DZC_RV=k,
-# linked with the other objects of the in-tree build) for tools/ab_search.py A/B runs.
+# linked with the other objects of the in-tree build) for tools/ab_search.py A/B runs.  The
+# product source carries no ZC_RV variants: while experimenting, guard each candidate with
+# `if (ZC_RV & bit)` (default ZC_RV 0 = the current kernel), A/B it, then bake in or drop it
+# (DESIGN §4 "late rollout trims" lists what was measured).
 set -e
 cd "$(dirname "$0")/.."
 objs=$(ls zeroclone_amd/build_obj/*.o | grep -v c4_search.o)
