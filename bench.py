@@ -494,7 +494,7 @@ def exchange_positions(local, world: int, sync=lambda: None):
 
 # the committed rocprofv3 summary of the current search kernel (tools/summarize_profile.py:
 # HBM bytes per launch from separate FETCH_SIZE / WRITE_SIZE passes, SQ issue counters)
-SEARCH_PROFILE = os.path.join("profiles", "r03_late_c4_search_summary.json")
+SEARCH_PROFILE = os.path.join("profiles", "r03_end_c4_search_summary.json")
 
 
 def search_profile():

@@ -8,7 +8,7 @@ cd "$(dirname "$0")/.."
 python zeroclone_amd/build.py > /dev/null
 objs=$(ls zeroclone_amd/build_obj/*.o | grep -v c4_search.o)
 for k in 1 2 3 4 5 6; do
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math \
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -mllvm -amdgpu-sched-strategy=iterative-ilp \
     -DZC_RSTAMP=$k -c zeroclone_amd/csrc/c4_search.hip -o /tmp/c4s_rs$k.o &
 done
 wait

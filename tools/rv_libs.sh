@@ -8,7 +8,7 @@ set -e
 cd "$(dirname "$0")/.."
 objs=$(ls zeroclone_amd/build_obj/*.o | grep -v c4_search.o)
 for k in "$@"; do
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math \
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -mllvm -amdgpu-sched-strategy=iterative-ilp \
     -DZC_RV=$k -c zeroclone_amd/csrc/c4_search.hip -o /tmp/c4s_rv$k.o &
 done
 wait
