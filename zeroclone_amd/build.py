@@ -37,7 +37,8 @@ def _stale() -> bool:
 FLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math", "-Wall"]
 # per-source extras: the search kernels are one long dependent chain per wave; LLVM's iterative
 # ILP machine scheduler orders them 1 % faster than the default (same-box A/B, outputs identical,
-# profiles/r03_ab_sched.log; max-memory-clause and iterative-maxocc were 0.9 % slower)
+# profiles/r03_ab_sched.log; max-memory-clause and iterative-maxocc were 0.9 % slower).  Only
+# there: ROCm 7.2's clang crashes in register allocation with it on chess_search.hip.
 SOURCE_FLAGS = {"c4_search.hip": ["-mllvm", "-amdgpu-sched-strategy=iterative-ilp"]}
 
 
