@@ -410,10 +410,10 @@ def run_steps(sp, steps: int, warmup: int, world: int = 1, launch: str = "pooled
     """W untimed moves, then K timed steps (K x G moves) bracketed by barrier + device sync,
     as ONE self-play launch followed by its trajectory recording; HIP events around it on its
     stream.  launch "pooled" (the default, C4SelfPlay.run_pooled): the G games share a budget
-    of K x G moves drawn from a device counter, at most 2K per game — the reference's
-    self-play threads drawing work from one pool (train.py:151-170), every move a full
-    search; "free" (C4SelfPlay.run): exactly K moves per game, so the launch waits for its
-    slowest game."""
+    of K x G moves drawn from a device counter, at most 2K per game, every move a full search
+    — a throughput schedule (train.py:151-170 itself is lockstep: one move per unfinished
+    game per call; each game's moves are exactly its free-run moves); "free"
+    (C4SelfPlay.run): exactly K moves per game, so the launch waits for its slowest game."""
     dev = sp.dev
     stream = torch.cuda.current_stream(dev)
     ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),

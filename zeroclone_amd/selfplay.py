@@ -275,8 +275,9 @@ class C4SelfPlay:
     def run_pooled(self, budget: int, moves_cap: int, stream: int | None = None, kernel_done=None) -> torch.Tensor:
         """`budget` moves shared by all games in ONE launch (zc_c4_selfplay_pooled_async): each
         game takes its next move from a device counter while the budget lasts, at most
-        `moves_cap` moves — the reference's self-play threads drawing games from one pool
-        (scripts/train.py:151-170).  Game i's k-th move is the k-th move run() would play;
+        `moves_cap` moves.  A throughput schedule, not the reference's: scripts/train.py:151-170
+        is lockstep (one move per unfinished game per call).  Game i's k-th move is the k-th move
+        run() would play;
         how many moves each game gets follows the games' pace.  The trajectory recording
         replays the steps in order (slots without a k-th move: ZC_SLOT_SKIP, untouched).
         Returns the per-step results [moves_cap, G]; self.stats sums the moves' counters."""
