@@ -355,6 +355,35 @@ int zc_chess_hp_walk(zc_engine *eng, int32_t game, int32_t flush, int32_t leaf, 
 int zc_chess_hp_expand(zc_engine *eng, int32_t game, int32_t flush, int32_t leaf, int32_t untried_index,
                        zc_chess_state *d_leaf, void *hip_stream);
 
+/* ---- Value('random_rollout') on the chess backend (engine/value_functions.py:35-45 with
+ * engine/games/chess/src/chess_backend.cpp: check_win / check_draw incl. the repetition draw
+ * over both move histories, random.choice(list(get_legal_moves)), play_move) --------------
+ * Histories: d_hist [k][2][hist_cap] uint16 packed moves of white / black in play order
+ * (oldest first: the reference's deques reversed), d_hist_len [k][2].  A rollout's history
+ * may hold ZC_CHESS_ROLL_CAP moves per side; beyond that (or a move list overflow) the
+ * rollout stops and d_status[i] = ZC_STATUS_CAPACITY.  Values: -1 / +1 / 0 for the side to
+ * move at the rolled-out state.
+ * zc_chess_rollouts_async replaces Value.batch (:20-22) called directly: the n_states states
+ * (their own histories, k = n_states) rolled out in order on game `game`'s stream;
+ * d_values[n_states], d_status[1] (may be NULL).
+ * zc_chess_ext_rollouts, after zc_chess_ext_select(flush) (or the flush's zc_chess_hp_*
+ * simulations): every game's pending leaves in pending order on its stream — the flush of
+ * mcts.cpp:112-127 with this value — the leaf histories being the root's (k = n_games, game
+ * first + i at i) plus the path's moves; d_values[n*bs] as zc_chess_ext_backup takes them,
+ * d_status[n] (may be NULL).
+ * zc_chess_ext_leaf_moves: the path of every pending leaf of the flush (what a host
+ * Value.batch needs to rebuild the leaf's histories): d_moves[(i*bs + j)*64 + l - 1] = the
+ * move into level l, d_depth[i*bs + j] = the leaf's depth (0 past the flush's leaves). */
+#define ZC_CHESS_ROLL_CAP 2048
+int zc_chess_rollouts_async(zc_engine *eng, int32_t game, int32_t n_states, const zc_chess_state *d_states,
+                            const uint16_t *d_hist, const int32_t *d_hist_len, int32_t hist_cap, double *d_values,
+                            int32_t *d_status, void *hip_stream);
+int zc_chess_ext_rollouts(zc_engine *eng, int32_t first_game, int32_t n_games, int32_t flush, const uint16_t *d_hist,
+                          const int32_t *d_hist_len, int32_t hist_cap, double *d_values, int32_t *d_status,
+                          void *hip_stream);
+int zc_chess_ext_leaf_moves(zc_engine *eng, int32_t first_game, int32_t n_games, int32_t flush, uint16_t *d_moves,
+                            int32_t *d_depth, void *hip_stream);
+
 /* ---- Chess self-play on the device (scripts/train.py:151-170) ------------
  * Engine.play_move + _evaluate (engine/engine.py:98-108, 148-153) for chess, with the move
  * histories the repetition draw needs (chess_backend.cpp:364-441) kept in HBM:

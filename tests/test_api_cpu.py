@@ -59,20 +59,26 @@ def test_engine_surface_without_gpu():
     assert len(e.states) == 3
 
 
-def test_unsupported_plugins_fail_loudly():
+def test_unknown_plugins_fail_where_the_reference_fails():
+    """An unknown Value name constructs (value_functions.py:9-14 only looks up an optional
+    init_<name>) and fails when called, with AttributeError (:17-18); an unknown Policy name
+    fails at the first expansion the same way (policy_functions.py:6-8).  Every known
+    backend x value combination is accepted by the plugin check (the §8(b) fallback: chess
+    random_rollout on the device, crude_chess_score on Connect4 through the host value path);
+    without a GPU the search itself then refuses to run."""
+    from zeroclone_amd import _native
     from zeroclone_amd.engine import Policy, Value, mcts
-    with pytest.raises(NotImplementedError):
-        Value("mystery_value")
+    from zeroclone_amd.engine.games.chess import chess_backend as cb
+    mystery = Value("mystery_value")
+    with pytest.raises(AttributeError):
+        mystery.batch([c4.create_init_state()], backend=c4)
     v = Value("random_rollout")
     with pytest.raises(AttributeError):   # as the reference's Policy.__call__ getattr fails
         mcts.get_move(c4.create_init_state(), v, Policy("mystery_policy"), c4, 10)
-    with pytest.raises(NotImplementedError):   # chess value on a Connect4 game
-        mcts.get_move(c4.create_init_state(), Value("crude_chess_score"), Policy("random"), c4, 10)
-
-    class Other:
-        __name__ = "chess_backend"
-    with pytest.raises(NotImplementedError):
-        mcts.get_move(c4.create_init_state(), v, Policy("random"), Other(), 10)
+    mcts._plugin_check(c4.create_init_state(), Value("crude_chess_score"), Policy("random"), c4)
+    assert mcts._plugin_check(cb.create_init_state(), v, Policy("random"), cb) == "chess"
+    with pytest.raises(_native.ZeroCloneError):   # no CPU search: the GPU engine is required
+        mcts.get_move(cb.create_init_state(), v, Policy("random"), cb, 10)
 
 
 def test_schedule_hyperparams_follows_train_py():

@@ -1,0 +1,169 @@
+"""GPU parity of the §8(b) fallback for value plugins whose semantics go through Python's
+`random` (tests/golden/fallback_get_move.json, from the reference's own compiled get_move and
+chess backend by tests/golden/gen_golden_fallback.py):
+
+* Value('random_rollout') on the chess backend — called directly (value_functions.py:35-45:
+  the device rollout kernel, zc_chess_rollouts_async, both sides' histories for the
+  repetition draw) and inside get_move (zc_chess_ext_rollouts between the select and backup
+  kernels; every flush's values, the root visit counts, the move);
+* value objects that draw from `random` (tests/fallback_values.py) on Connect4 and chess —
+  value.batch on the host once per flush with Python's `random` handed the game's device
+  stream (_device.game_stream), chess leaves carrying their move histories;
+and in every case the next word of Python's stream after the call."""
+import json
+import os
+import random
+
+import numpy as np
+import pytest
+import torch
+
+import fallback_values as FV
+from zeroclone_amd import _native
+from zeroclone_amd.engine import Policy, Value, mcts
+from zeroclone_amd.engine import _device, _search
+from zeroclone_amd.engine.games.chess import chess_backend as cb
+from zeroclone_amd.engine.games.connect4 import c4_backend as c4
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+@pytest.fixture(scope="module")
+def fx():
+    with open(os.path.join(HERE, "golden", "fallback_get_move.json")) as fh:
+        return json.load(fh)
+
+
+def chess_state(e):
+    c = int(e["castle"])
+    return cb.State([ord(ch) for ch in e["board"]], e["turn"], e["fifty"], c & 1, c & 2, c & 4, c & 8,
+                    cb.moves_from_hist(e["hw"]), cb.moves_from_hist(e["hb"]))
+
+
+def c4_state(board, turn):
+    return c4.State([[(" " if ch == "." else ch) for ch in board[r * 7:(r + 1) * 7]] for r in range(6)], turn)
+
+
+def policy_of(case):
+    if case["policy"] == "immediate_value":
+        return Policy("immediate_value", policy_freedom=case["freedom"])
+    return Policy("random")
+
+
+def test_chess_random_rollout_batch_matches_reference(fx):
+    """Value('random_rollout').batch on chess states, in order, on Python's stream: every value
+    and the stream afterwards — repetition-prone knight shuffles, a fifty-move counter at 47,
+    bare kings and minor pieces (no legal move), mid-game and endgame positions."""
+    total = 0
+    for case in fx["chess_rollouts"]:
+        states = [chess_state(e) for e in case["states"]]
+        random.seed(case["seed"])
+        vals = Value("random_rollout").batch(states, backend=cb)
+        assert vals == case["values"], case["seed"]
+        assert random.getrandbits(32) == case["next_word"], case["seed"]
+        total += sum(case["plies"])
+    assert total > 5000   # the rollouts really played long games
+
+
+def test_chess_get_move_with_random_rollout_matches_reference(fx):
+    for case in fx["chess_search"]:
+        st = chess_state(case["state"])
+        random.seed(case["seed"])
+        mv = mcts.get_move(st, Value("random_rollout"), policy_of(case), cb, case["sims"], case["c"], case["bs"])
+        assert [*mv[0], mv[1]] == case["move"], case["seed"]
+        assert random.getrandbits(32) == case["next_word"], case["seed"]
+
+
+def _chess_stepwise(st, seed, sims, c, bs, pol, freedom, fn_factory):
+    """The stepwise chess search get_move runs, on a fresh engine seeded with Python's state
+    after random.seed(seed); returns (root Na, every flush's values)."""
+    from zeroclone_amd.valued import ChessValuedSearch
+    eng = _native.NativeEngine(max_games=1, max_sims=sims, max_batch=bs)
+    random.seed(seed)
+    mt, idx, _, _ = _device.python_random_state()
+    eng.set_rng_state(0, mt, idx)
+    vs = ChessValuedSearch(eng, 1, bs, policy=pol, freedom=freedom, planes=False, leaves=True)
+    fn = fn_factory(eng, vs)
+    log = []
+
+    class Logged:
+        def flush_values(self, first, n, f, stream):
+            v = fn.flush_values(first, n, f, stream)
+            k = int(vs.counts[0].item())
+            log.extend(float(x) for x in v[:k].cpu().tolist())
+            return v
+
+    roots = torch.from_numpy(_search.chess_roots([st]).view(np.uint8).reshape(1, 72).copy()).cuda()
+    _, na, stats = vs.run(roots, sims, c, Logged())
+    na = na.cpu().numpy()[0]
+    eng.close()
+    return na, log, stats.cpu().numpy()[0]
+
+
+def test_chess_rollout_search_root_visits_and_values(fx):
+    """Root visit counts and the rollout value of every leaf, flush by flush, equal the
+    reference's (the leaf histories — root's + path — decide the repetition draws)."""
+    for case in fx["chess_search"]:
+        st = chess_state(case["state"])
+        pol = _native.ZC_POLICY_IMMEDIATE_VALUE if case["policy"] == "immediate_value" else _native.ZC_POLICY_RANDOM
+        na, vals, stats = _chess_stepwise(
+            st, case["seed"], case["sims"], case["c"], case["bs"], pol, case["freedom"],
+            lambda eng, vs: _search._ChessRolloutValue(eng, [st], case["bs"], vs.dev))
+        assert vals == case["values"], case["seed"]
+        assert list(na[:len(case["root_na"])]) == case["root_na"], case["seed"]
+        assert int(stats[5]) == 0
+
+
+def test_c4_host_values_drawing_random_match_reference(fx):
+    """A value object that draws from `random` with the built-in Policy('random'): the
+    expansion draws (device) and the value's draws (host) interleave as in the reference."""
+    for case in fx["c4_hostvalue"]:
+        st = c4_state(case["board"], case["turn"])
+        random.seed(case["seed"])
+        mv = mcts.get_move(st, FV.VALUES[case["value"]](), Policy("random"), c4, case["sims"], case["c"], case["bs"])
+        assert mv[0] == case["move"], case["seed"]
+        assert random.getrandbits(32) == case["next_word"], case["seed"]
+
+
+def test_c4_host_value_root_visits_match_reference(fx):
+    from zeroclone_amd.valued import C4ValuedSearch, HostValue
+    for case in fx["c4_hostvalue"]:
+        st = c4_state(case["board"], case["turn"])
+        eng = _native.NativeEngine(max_games=1, max_sims=case["sims"], max_batch=case["bs"])
+        random.seed(case["seed"])
+        mt, idx, _, _ = _device.python_random_state()
+        eng.set_rng_state(0, mt, idx)
+        vs = C4ValuedSearch(eng, 1, case["bs"], planes=False)
+        r = torch.from_numpy(_device.c4_roots([st], c4).view(np.int64).reshape(1, 3).copy()).cuda()
+        _, na, _ = vs.run(r, case["sims"], case["c"], HostValue(FV.VALUES[case["value"]](), c4, eng, 0))
+        na = na.cpu().numpy()[0]
+        order = case["order"]
+        assert [int(na[col]) for col in order] == case["root_na"], case["seed"]
+        eng.close()
+
+
+def test_chess_host_values_match_reference(fx):
+    """Chess with value objects that draw from `random` and read the leaves' move histories:
+    the move, the root visit counts and Python's stream afterwards."""
+    for case in fx["chess_hostvalue"]:
+        st = chess_state(case["state"])
+        random.seed(case["seed"])
+        mv = mcts.get_move(st, FV.VALUES[case["value"]](), policy_of(case), cb, case["sims"], case["c"], case["bs"])
+        assert [*mv[0], mv[1]] == case["move"], case["seed"]
+        assert random.getrandbits(32) == case["next_word"], case["seed"]
+        pol = _native.ZC_POLICY_IMMEDIATE_VALUE if case["policy"] == "immediate_value" else _native.ZC_POLICY_RANDOM
+        value = FV.VALUES[case["value"]]()
+        na, vals, _ = _chess_stepwise(st, case["seed"], case["sims"], case["c"], case["bs"], pol, case["freedom"],
+                                      lambda eng, vs: _search._ChessHostValue(value, cb, eng, vs, [st]))
+        assert list(na[:len(case["root_na"])]) == case["root_na"], case["seed"]
+        assert vals == case["values"], case["seed"]
+
+
+def test_chess_rollouts_fill_history_capacity_loudly():
+    """A history longer than a rollout can hold is refused, not truncated."""
+    st = cb.create_init_state()
+    st.hist_white = [((6, 0, 5, 0), 0.0)] * (_native.CHESS_ROLL_CAP + 1)
+    with pytest.raises((RuntimeError, ValueError)):
+        Value("random_rollout").batch([st], backend=cb)

@@ -74,6 +74,7 @@ STATS_DTYPE = np.dtype([("expansions", "<i8"), ("depth_sum", "<i8"), ("leaves", 
 CHESS_STATE_DTYPE = np.dtype([("board", "u1", (64,)), ("turn", "u1"), ("fifty", "u1"), ("castle", "u1"),
                               ("reserved", "u1", (5,))])
 CHESS_MAX_MOVES = 256
+CHESS_ROLL_CAP = 2048   # ZC_CHESS_ROLL_CAP: moves per side a chess rollout's history holds
 # zc_chess_hp_node: the chess host-policy walk's end (include/zeroclone.h)
 CHESS_HP_NODE_DTYPE = np.dtype([("state", CHESS_STATE_DTYPE), ("node", "<i4"), ("n_untried", "<i4"), ("depth", "<i4"),
                                 ("reserved", "<i4"), ("untried", "<u2", (CHESS_MAX_MOVES,))])
@@ -190,6 +191,14 @@ SIGNATURES = [
                                           ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p]),
     ("zc_chess_ext_end", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p,
                                         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    ("zc_chess_rollouts_async", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p,
+                                               ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p,
+                                               ctypes.c_void_p, ctypes.c_void_p]),
+    ("zc_chess_ext_rollouts", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                             ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p,
+                                             ctypes.c_void_p, ctypes.c_void_p]),
+    ("zc_chess_ext_leaf_moves", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                               ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     ("zc_chess_puct_flushes", ctypes.c_int, [ctypes.c_int32, ctypes.c_int32]),
     ("zc_chess_puct_begin", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p,
                                            ctypes.c_int32, ctypes.c_double, ctypes.c_int32, ctypes.c_float,
@@ -583,6 +592,24 @@ class NativeEngine:
     def chess_ext_end(self, first_game: int, n: int, d_move: int, d_na: int, d_stats: int, stream: int = 0):
         check(lib().zc_chess_ext_end(self._h, first_game, n, ctypes.c_void_p(d_move), ctypes.c_void_p(d_na),
                                      ctypes.c_void_p(d_stats), ctypes.c_void_p(stream or None)))
+
+    # ---- Value('random_rollout') on chess (device pointers)
+    def chess_rollouts_async(self, game: int, n: int, d_states: int, d_hist: int, d_hist_len: int, hist_cap: int,
+                             d_values: int, d_status: int = 0, stream: int = 0):
+        check(lib().zc_chess_rollouts_async(self._h, int(game), int(n), ctypes.c_void_p(d_states),
+                                            ctypes.c_void_p(d_hist), ctypes.c_void_p(d_hist_len), int(hist_cap),
+                                            ctypes.c_void_p(d_values), ctypes.c_void_p(d_status or None),
+                                            ctypes.c_void_p(stream or None)))
+
+    def chess_ext_rollouts(self, first_game: int, n: int, flush: int, d_hist: int, d_hist_len: int, hist_cap: int,
+                           d_values: int, d_status: int = 0, stream: int = 0):
+        check(lib().zc_chess_ext_rollouts(self._h, first_game, n, int(flush), ctypes.c_void_p(d_hist),
+                                          ctypes.c_void_p(d_hist_len), int(hist_cap), ctypes.c_void_p(d_values),
+                                          ctypes.c_void_p(d_status or None), ctypes.c_void_p(stream or None)))
+
+    def chess_ext_leaf_moves(self, first_game: int, n: int, flush: int, d_moves: int, d_depth: int, stream: int = 0):
+        check(lib().zc_chess_ext_leaf_moves(self._h, first_game, n, int(flush), ctypes.c_void_p(d_moves),
+                                            ctypes.c_void_p(d_depth), ctypes.c_void_p(stream or None)))
 
     # ---- chess PUCT search (device pointers)
     def chess_puct_begin(self, first_game, n, d_roots, sims, c_puct, batch_size, alpha, eps, seed, d_search_no=0,

@@ -713,6 +713,197 @@ __global__ __launch_bounds__(64) void chess_hp_expand_kernel(ChessParams p) {
     }
 }
 
+// ---------------------------------------------------------------- random_rollout on chess
+// Value('random_rollout') (engine/value_functions.py:35-45) with the chess backend: while
+// not check_win and not check_draw (chess_backend.cpp:404-441), play
+// random.choice(list(get_legal_moves(state))) (:184-360; _randbelow on the game's stream);
+// at the end -1 if the side to move (the loser of a checkmate) is the leaf's side to move,
+// +1 for the other side's checkmate, 0 for a draw.
+//
+// check_draw's repetition half, has_repeated_prefix(hist, 2, 3) on both sides' histories
+// (:148-180, KMP over the deque, most recent move first), is kept incrementally.  With the
+// history a[0..n) in play order, KMP's test — some prefix of the deque whose smallest period
+// p >= 2 divides its length at least 3 times — holds iff for some p >= 2 the last 3p moves
+// have period p and are not all equal (<=: Fine and Wilf put the smallest period of the
+// 3p-suffix below p, dividing it; =>: the 3p'-prefix of KMP's prefix is such a suffix).  So
+// each side keeps c_p = the number of trailing i with a[i] == a[i-p], for every p <= n (one
+// LDS counter per p, lanes over p): a push of x updates c_p = (x == a[n-p]) ? c_p + 1 : 0, and
+// the test is c_p >= 2p and c_1 < 3p - 1 for some p >= 2.  O(n / 64) per ply.
+struct RollSide {
+    uint16_t *a;    // moves in play order
+    uint16_t *cnt;  // cnt[p], p in [1, kRollCap]
+    int n, c1;
+    bool rep;
+};
+
+__device__ __forceinline__ void roll_side_init(RollSide &s) {
+    const uint32_t lane = lane_id();
+    bool hit = false;
+    for (int b = 0; b < s.n; b += 64) {
+        const int p = b + (int)lane + 1;
+        if (p <= s.n) {
+            int c = 0;
+            for (int i = s.n - 1; i >= p && s.a[i] == s.a[i - p]; --i) ++c;
+            s.cnt[p] = (uint16_t)c;
+        }
+    }
+    if (lane == 0 && s.n + 1 <= kRollCap) s.cnt[s.n + 1] = 0;
+    wave_sync_mem();
+    s.c1 = s.n >= 1 ? uni((int)s.cnt[1]) : 0;
+    for (int b = 0; b < s.n; b += 64) {
+        const int p = b + (int)lane + 1;
+        if (p >= 2 && p <= s.n && (int)s.cnt[p] >= 2 * p && s.c1 < 3 * p - 1) hit = true;
+    }
+    s.rep = __ballot(hit) != 0;
+}
+
+// play_move's history push (chess_backend.cpp:374) of move x, and the new repetition answer.
+__device__ __forceinline__ void roll_side_push(RollSide &s, uint16_t x) {
+    const uint32_t lane = lane_id();
+    const int n = s.n;
+    s.c1 = (n >= 1 && uni((int)s.a[n - 1]) == (int)x) ? s.c1 + 1 : 0;
+    bool hit = false;
+    for (int b = 0; b < n; b += 64) {
+        const int p = b + (int)lane + 1;
+        if (p <= n) {
+            int c = s.cnt[p];
+            c = s.a[n - p] == x ? c + 1 : 0;
+            s.cnt[p] = (uint16_t)c;
+            if (p >= 2 && c >= 2 * p && s.c1 < 3 * p - 1) hit = true;
+        }
+    }
+    wave_sync_mem();
+    if (lane == 0) {
+        s.a[n] = x;
+        if (n + 2 <= kRollCap) s.cnt[n + 2] = 0;   // c_p of a period the history reaches next push
+    }
+    wave_sync_mem();
+    s.n = n + 1;
+    s.rep = __ballot(hit) != 0;
+}
+
+// One rollout from the position in L.st with histories w (white's) / k (black's).  Returns
+// the value; status ZC_STATUS_CAPACITY when a history outgrows kRollCap or a position its
+// move list.
+template <class R>
+__device__ int chess_rollout(CLds &L, RollSide &w, RollSide &k, R &rng, int &status) {
+    const uint32_t lane = lane_id();
+    roll_side_init(w);
+    roll_side_init(k);
+    const int t0 = uni((int)L.st.turn);
+    for (;;) {
+        L.s.board[lane] = L.st.board[lane];
+        wave_sync_mem();
+        const int turn = uni((int)L.st.turn);
+        bool check;
+        const int nl = chessdev::legal_moves_check(L.s.board, turn, L.s.legal, L.s.pseudo, L.s.region, check);
+        if (nl < 0) {
+            status = ZC_STATUS_CAPACITY;
+            return 0;
+        }
+        if (nl == 0 && check) return turn == t0 ? -1 : 1;                        // check_win
+        if (nl == 0 || uni((int)L.st.fifty) >= 50 || (w.rep && k.rep)) return 0;   // check_draw
+        const uint32_t r = rng_below(rng, (uint32_t)nl);
+        const uint16_t m = (uint16_t)uni((int)L.s.legal[r]);
+        if ((turn ? k.n : w.n) >= kRollCap) {
+            status = ZC_STATUS_CAPACITY;
+            return 0;
+        }
+        if (turn) roll_side_push(k, m);
+        else roll_side_push(w, m);
+        if (lane == 0) chessdev::apply_move(L.st, m);
+        wave_sync_mem();
+    }
+}
+
+// Rollouts in order on game g's stream: the tree's pending leaves of p.flush (from_tree:
+// histories = the root's + the path's moves, pushed by alternating movers from the root's
+// side to move) or the p.n_states given states with their own histories.
+__global__ __launch_bounds__(64) void chess_rollouts_kernel(ChessParams p, int from_tree) {
+    extern __shared__ uint16_t s_roll[];   // a[2][kRollCap], cnt[2][kRollCap + 1]
+    __shared__ CLds L;
+    const uint32_t lane = lane_id();
+    const int gl = blockIdx.x;
+    if (gl >= p.n_games) return;
+    const int g = p.first_game + gl;
+    int32_t *ctl = p.ca.ctl + (size_t)g * kCtlWords;
+    const CTree t = ctree(p, g);
+    int status = 0;
+    int nb;
+    if (from_tree) {
+        nb = uni(ctl[cStatus]) ? 0 : uni(ctl[cNb]);
+    } else {
+        nb = p.n_states;
+    }
+    Rng rng;
+    const uint64_t use_now = uni64(p.a.rngpos[2 * (size_t)g]);
+    rng_open(rng, p.a.ring + (size_t)g * kRingWords, use_now, uni64(p.a.rngpos[2 * (size_t)g + 1]));
+    const uint32_t *paths = p.ca.paths + (size_t)g * p.max_batch * kChessPath;
+    const uint32_t *meta = p.ca.meta + (size_t)g * p.max_batch;
+    const int t0 = from_tree ? uni((int)t.nodes[0].st.turn) : 0;
+    for (int j = 0; j < nb && !status; ++j) {
+        const int hi = from_tree ? gl : j;   // whose histories
+        const uint16_t *hs = p.rhist + (size_t)hi * 2 * p.rhcap;
+        RollSide w{s_roll, s_roll + 2 * kRollCap, min(uni(p.rhlen[2 * hi]), p.rhcap), 0, false};
+        RollSide k{s_roll + kRollCap, s_roll + 2 * kRollCap + kRollCap + 1, min(uni(p.rhlen[2 * hi + 1]), p.rhcap), 0,
+                   false};
+        int d = 0;
+        const uint32_t *pw = nullptr;
+        if (from_tree) {
+            const uint32_t m = uni(meta[j]);
+            d = (int)(m >> 16);
+            pw = paths + (size_t)j * kChessPath;
+            const ChessNode *N = &t.nodes[m & 0xFFFFu];
+            if (lane < 18) ((uint32_t *)&L.st)[lane] = ((const uint32_t *)&N->st)[lane];
+        } else if (lane < 18) {
+            ((uint32_t *)&L.st)[lane] = ((const uint32_t *)&p.rstates[j])[lane];
+        }
+        const int wt = (t0 == 0 ? (d + 1) / 2 : d / 2), bt = d - wt;   // path moves per side
+        if (w.n + wt > kRollCap || k.n + bt > kRollCap) {
+            status = ZC_STATUS_CAPACITY;
+            break;
+        }
+        for (int i = (int)lane; i < w.n; i += 64) w.a[i] = hs[i];
+        for (int i = (int)lane; i < k.n; i += 64) k.a[i] = hs[p.rhcap + i];
+        wave_sync_mem();
+        if (lane >= 1 && lane <= (uint32_t)d) {   // the move into level l was played by (t0 + l - 1) & 1
+            const uint16_t mv = t.mv[pw[lane]];
+            const int side = (t0 + (int)lane - 1) & 1;
+            (side ? k.a + k.n : w.a + w.n)[(lane - 1) >> 1] = mv;
+        }
+        wave_sync_mem();
+        w.n += wt;
+        k.n += bt;
+        const int v = chess_rollout(L, w, k, rng, status);
+        if (lane == 0) p.rvalues[(size_t)gl * (from_tree ? p.bs : 0) + j] = (double)v;
+    }
+    wave_sync_mem();
+    if (lane == 0) {
+        rng_close(rng, use_now, p.a.rngpos + 2 * (size_t)g);
+        if (p.rstatus) p.rstatus[gl] = status;
+    }
+}
+
+// The moves from the root to each pending leaf of the flush (the host-value leaves' move
+// histories): moves[leaf][l - 1] = the move into level l, depth[leaf].
+__global__ __launch_bounds__(64) void chess_leaf_moves_kernel(ChessParams p) {
+    const uint32_t lane = lane_id();
+    const int gl = blockIdx.x;
+    if (gl >= p.n_games) return;
+    const int g = p.first_game + gl;
+    const int32_t *ctl = p.ca.ctl + (size_t)g * kCtlWords;
+    const CTree t = ctree(p, g);
+    const int nb = uni(ctl[cStatus]) ? 0 : uni(ctl[cNb]);
+    const uint32_t *paths = p.ca.paths + (size_t)g * p.max_batch * kChessPath;
+    const uint32_t *meta = p.ca.meta + (size_t)g * p.max_batch;
+    for (int j = 0; j < p.bs; ++j) {
+        const size_t o = (size_t)gl * p.bs + j;
+        const int d = j < nb ? (int)(uni(meta[j]) >> 16) : 0;
+        if (lane == 0) p.path_depth[o] = d;
+        if (lane >= 1 && lane <= (uint32_t)d) p.path_moves[o * kChessPath + lane - 1] = t.mv[paths[(size_t)j * kChessPath + lane]];
+    }
+}
+
 }  // namespace
 
 void launch_chess_hp_walk(const ChessParams &p, hipStream_t s) {
@@ -752,6 +943,13 @@ void launch_chess_ext_backup(const ChessParams &p, hipStream_t s) {
 }
 void launch_chess_ext_end(const ChessParams &p, hipStream_t s) {
     hipLaunchKernelGGL(chess_ext_end_kernel, dim3(p.n_games), dim3(64), 0, s, p);
+}
+void launch_chess_rollouts(const ChessParams &p, bool from_tree, hipStream_t s) {
+    const size_t lds = (size_t)(4 * kRollCap + 2) * sizeof(uint16_t);
+    hipLaunchKernelGGL(chess_rollouts_kernel, dim3(p.n_games), dim3(64), lds, s, p, from_tree ? 1 : 0);
+}
+void launch_chess_leaf_moves(const ChessParams &p, hipStream_t s) {
+    hipLaunchKernelGGL(chess_leaf_moves_kernel, dim3(p.n_games), dim3(64), 0, s, p);
 }
 
 }  // namespace zc

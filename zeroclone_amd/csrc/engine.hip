@@ -1054,6 +1054,66 @@ int zc_chess_hp_expand(zc_engine *eng, int32_t game, int32_t flush, int32_t leaf
     return ZC_OK;
 }
 
+int zc_chess_rollouts_async(zc_engine *eng, int32_t game, int32_t n_states, const zc_chess_state *d_states,
+                            const uint16_t *d_hist, const int32_t *d_hist_len, int32_t hist_cap, double *d_values,
+                            int32_t *d_status, void *hip_stream) {
+    if (!eng || (n_states && (!d_states || !d_hist || !d_hist_len || !d_values))) return fail(ZC_EINVAL, "null argument");
+    if (int r = check_games(eng, game, 1)) return r;
+    if (n_states < 0 || hist_cap < 1) return fail(ZC_EINVAL, "n_states must be >= 0 and hist_cap >= 1");
+    if (!n_states) return ZC_OK;
+    std::lock_guard<std::mutex> lk(eng->mu);
+    ZC_HIP(hipSetDevice(eng->cfg.device));
+    if (int r = ensure_chess(eng)) return r;
+    zc::ChessParams p = chess_params(eng, game, 1, 1, 1.0, 1, 0, 0.0);
+    p.rstates = d_states;
+    p.n_states = n_states;
+    p.rhist = d_hist;
+    p.rhlen = d_hist_len;
+    p.rhcap = hist_cap;
+    p.rvalues = d_values;
+    p.rstatus = d_status;
+    zc::launch_chess_rollouts(p, false, (hipStream_t)hip_stream);
+    ZC_HIP(hipGetLastError());
+    return ZC_OK;
+}
+
+int zc_chess_ext_rollouts(zc_engine *eng, int32_t first, int32_t n, int32_t flush, const uint16_t *d_hist,
+                          const int32_t *d_hist_len, int32_t hist_cap, double *d_values, int32_t *d_status,
+                          void *hip_stream) {
+    if (!eng || (n && (!d_hist || !d_hist_len || !d_values))) return fail(ZC_EINVAL, "null argument");
+    if (hist_cap < 1) return fail(ZC_EINVAL, "hist_cap must be >= 1");
+    std::lock_guard<std::mutex> lk(eng->mu);
+    if (int r = check_cx(eng, first, n, flush, true)) return r;
+    if (!n) return ZC_OK;
+    ZC_HIP(hipSetDevice(eng->cfg.device));
+    zc::ChessParams p = chess_params(eng, first, n, eng->cx_sims, eng->cx_c, eng->cx_bs, eng->cx_policy, eng->cx_freedom);
+    p.flush = flush;
+    p.rhist = d_hist;
+    p.rhlen = d_hist_len;
+    p.rhcap = hist_cap;
+    p.rvalues = d_values;
+    p.rstatus = d_status;
+    zc::launch_chess_rollouts(p, true, (hipStream_t)hip_stream);
+    ZC_HIP(hipGetLastError());
+    return ZC_OK;
+}
+
+int zc_chess_ext_leaf_moves(zc_engine *eng, int32_t first, int32_t n, int32_t flush, uint16_t *d_moves,
+                            int32_t *d_depth, void *hip_stream) {
+    if (!eng || (n && (!d_moves || !d_depth))) return fail(ZC_EINVAL, "null argument");
+    std::lock_guard<std::mutex> lk(eng->mu);
+    if (int r = check_cx(eng, first, n, flush, true)) return r;
+    if (!n) return ZC_OK;
+    ZC_HIP(hipSetDevice(eng->cfg.device));
+    zc::ChessParams p = chess_params(eng, first, n, eng->cx_sims, eng->cx_c, eng->cx_bs, eng->cx_policy, eng->cx_freedom);
+    p.flush = flush;
+    p.path_moves = d_moves;
+    p.path_depth = d_depth;
+    zc::launch_chess_leaf_moves(p, (hipStream_t)hip_stream);
+    ZC_HIP(hipGetLastError());
+    return ZC_OK;
+}
+
 // ---------------------------------------------------------------- chess PUCT search
 int zc_chess_puct_flushes(int32_t sims, int32_t bs) {
     if (sims < 2 || bs < 1) return fail(ZC_EINVAL, "PUCT search needs sims >= 2 and batch_size >= 1");

@@ -184,6 +184,17 @@ struct ChessParams {
     // host-policy search (zc_chess_hp_*): leaf index in the flush, untried index, walk output
     int hp_leaf, hp_index;
     zc_chess_hp_node *hp_node;
+    // random_rollout on chess (zc_chess_rollouts_async / zc_chess_ext_rollouts): the states'
+    // (or the roots') move histories [n][2][rhcap] in play order, lengths [n][2]; values out
+    const zc_chess_state *rstates;   // direct rollouts: the n_states states (else the tree's leaves)
+    int n_states;
+    const uint16_t *rhist;
+    const int32_t *rhlen;
+    int rhcap;
+    double *rvalues;
+    int32_t *rstatus;
+    uint16_t *path_moves;            // zc_chess_ext_leaf_moves: [n*bs][kChessPath]
+    int32_t *path_depth;             // [n*bs]
 };
 
 // ---------------------------------------------------------------- Connect4 PUCT search
@@ -302,6 +313,9 @@ void launch_chess_ext_begin(const ChessParams &p, hipStream_t s);
 void launch_chess_ext_select(const ChessParams &p, hipStream_t s);
 void launch_chess_ext_backup(const ChessParams &p, hipStream_t s);
 void launch_chess_ext_end(const ChessParams &p, hipStream_t s);
+constexpr int kRollCap = ZC_CHESS_ROLL_CAP;   // random_rollout on chess: moves per side a rollout's history holds
+void launch_chess_rollouts(const ChessParams &p, bool from_tree, hipStream_t s);
+void launch_chess_leaf_moves(const ChessParams &p, hipStream_t s);
 void launch_chess_hp_walk(const ChessParams &p, hipStream_t s);
 void launch_chess_hp_expand(const ChessParams &p, hipStream_t s);
 

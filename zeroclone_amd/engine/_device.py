@@ -55,6 +55,19 @@ def scratch(sims: int, batch: int, device: int = 0) -> GrowingEngine:
         return ge
 
 
+def value_engine(device: int = 0) -> GrowingEngine:
+    """The one-game engine of direct Value.batch calls (Value('random_rollout') on a list of
+    states): separate from the get_move scratch engine, since a host plugin may call such a
+    Value in the middle of a search on the scratch engine (growing it there would destroy the
+    search's tree)."""
+    with _lock:
+        key = ("value", device)
+        ge = _scratch.get(key)
+        if ge is None:
+            ge = _scratch[key] = GrowingEngine(1, 1, 1, device)
+        return ge
+
+
 def python_random_state():
     version, internal, gauss = random.getstate()
     return np.asarray(internal[:624], dtype=np.uint32), int(internal[624]), version, gauss
@@ -62,6 +75,34 @@ def python_random_state():
 
 def set_python_random_state(mt, idx, version, gauss):
     random.setstate((version, tuple(int(x) for x in mt) + (int(idx),), gauss))
+
+
+class game_stream:
+    """Python's global `random` becomes engine game g's device stream for the duration of the
+    block — a host plugin called where the reference calls it (value.batch once per flush,
+    mcts.cpp:116) draws the words the reference would draw, after the device's own — then the
+    advanced stream goes back to the device and Python's previous state is restored.
+    random.gauss's cached second value travels with the game (eng.py_gauss)."""
+
+    def __init__(self, eng, g: int):
+        self.eng, self.g = eng, int(g)
+
+    def __enter__(self):
+        self.saved = random.getstate()
+        mt, idx = self.eng.get_rng_state(self.g)
+        gauss = getattr(self.eng, "py_gauss", {}).get(self.g)
+        set_python_random_state(mt, idx, self.saved[0], gauss)
+        return self
+
+    def __exit__(self, *exc):
+        mt, idx, _, gauss = python_random_state()
+        random.setstate(self.saved)
+        if exc[0] is None:
+            self.eng.set_rng_state(self.g, mt, idx)
+            if not hasattr(self.eng, "py_gauss"):
+                self.eng.py_gauss = {}
+            self.eng.py_gauss[self.g] = gauss
+        return False
 
 
 def c4_roots(states, c4) -> np.ndarray:

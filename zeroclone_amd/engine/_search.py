@@ -113,9 +113,17 @@ def chess_moves(eng, ids, states, sims, c, bs, value, policy, backend):
         torch.cuda.current_stream(dev).synchronize()
     else:
         from ..valued import ChessValuedSearch, NetValue
-        vs = ChessValuedSearch(eng, n, bs, policy=pol, freedom=freedom, planes=(kind == "net"))
-        fn = NetValue(value.zc_model) if kind == "net" else _ChessHostValue(value, backend)
+        vs = ChessValuedSearch(eng, n, bs, policy=pol, freedom=freedom, planes=(kind == "net"),
+                               leaves=(kind == "host"))
+        if kind == "net":
+            fn = NetValue(value.zc_model)
+        elif kind == "rollout":
+            fn = _ChessRolloutValue(eng, states, bs, dev)
+        else:
+            fn = _ChessHostValue(value, backend, eng, vs, states)
         mv, na, st = vs.run(roots, sims, c, fn, first_game=first)
+        if kind == "rollout":
+            fn.check()
     st = st.cpu().numpy()
     bad = st[:, 5]
     if (bad == _native.ZC_STATUS_CAPACITY).any():
@@ -124,22 +132,81 @@ def chess_moves(eng, ids, states, sims, c, bs, value, policy, backend):
     return [None if m == 0xFFFF else _native.unpack_chess_move(m) for m in mv]
 
 
-class _ChessHostValue:
-    def __init__(self, value, backend):
-        self.value, self.backend = value, backend
+class _ChessRolloutValue:
+    """Value('random_rollout') on chess inside the stepwise search (value_functions.py:35-45
+    at mcts.cpp:116): every flush's pending leaves are rolled out on the device in pending
+    order on their game's stream (zc_chess_ext_rollouts), right after the flush's expansion
+    draws; a leaf's move histories are its root's plus the path's moves."""
 
-    def __call__(self, leaves, planes, counts):
+    def __init__(self, eng, states, bs, dev):
         import torch
         from .games.chess import chess_backend as cb
-        rows = leaves.cpu().numpy()
-        cnt = counts.cpu().numpy()
-        bs = rows.shape[0] // cnt.shape[0]
+        hist, hlen = cb.pack_histories(states)
+        self.eng = eng
+        self.h, self.hl = torch.from_numpy(hist).to(dev), torch.from_numpy(hlen).to(dev)
+        self.values = torch.zeros(len(states) * bs, dtype=torch.float64, device=dev)
+        self.status = torch.zeros(len(states), dtype=torch.int32, device=dev)
+
+    def flush_values(self, first, n, f, stream):
+        self.eng.chess_ext_rollouts(first, n, f, self.h.data_ptr(), self.hl.data_ptr(), self.h.shape[2],
+                                    self.values.data_ptr(), self.status.data_ptr(), stream)
+        return self.values
+
+    def check(self):
+        if int(self.status.max().item()):
+            raise RuntimeError(f"chess rollout exceeded {_native.CHESS_ROLL_CAP} moves per side in its history")
+
+
+def chess_leaf_states(eng, first, n, f, bs, rows, counts, roots):
+    """The flush's pending leaves as chess_backend States with the move histories the
+    reference's leaf State carries: the root's, plus the path's moves pushed at the front of
+    the mover's history (play_move, chess_backend.cpp:374) — zc_chess_ext_leaf_moves.
+    Returns one list of States per game."""
+    import torch
+    from .games.chess import chess_backend as cb
+    dev = torch.device("cuda", eng.device)
+    moves = torch.zeros((n * bs, 64), dtype=torch.int16, device=dev)
+    depth = torch.zeros(n * bs, dtype=torch.int32, device=dev)
+    eng.chess_ext_leaf_moves(first, n, f, moves.data_ptr(), depth.data_ptr(),
+                             torch.cuda.current_stream(dev).cuda_stream)
+    mv, dp = moves.cpu().numpy().view(np.uint16), depth.cpu().numpy()
+    out = []
+    for i, k in enumerate(counts):
+        root = roots[i]
+        t0 = int(root.turn)
+        games = []
+        for j in range(int(k)):
+            o = i * bs + j
+            hw, hb = list(root.hist_white), list(root.hist_black)
+            for lv in range(int(dp[o])):
+                m = _native.unpack_chess_move(int(mv[o, lv]))
+                (hw if (t0 + lv) % 2 == 0 else hb).insert(0, m)
+            games.append(cb.from_zc(rows[o].view(_native.CHESS_STATE_DTYPE)[0], hw, hb))
+        out.append(games)
+    return out
+
+
+class _ChessHostValue:
+    """Any other value object on chess: value.batch(leaf States, backend=) per game per
+    flush on the host (mcts.cpp:116), the leaves carrying their move histories, Python's
+    `random` being the game's device stream during the call (_device.game_stream)."""
+
+    def __init__(self, value, backend, eng, vs, roots):
+        self.value, self.backend, self.eng, self.vs, self.roots = value, backend, eng, vs, roots
+
+    def flush_values(self, first, n, f, stream):
+        import torch
+        from ._device import game_stream
+        vs = self.vs
+        rows = vs.leaves.cpu().numpy()
+        cnt = vs.counts.cpu().numpy()
         out = np.zeros(rows.shape[0], np.float64)
-        for i, k in enumerate(cnt):
-            if k:
-                states = [cb.from_zc(r.view(_native.CHESS_STATE_DTYPE)[0]) for r in rows[i * bs: i * bs + k]]
-                out[i * bs: i * bs + k] = [float(v) for v in self.value.batch(states, backend=self.backend)]
-        return torch.from_numpy(out).to(leaves.device)
+        for i, states in enumerate(chess_leaf_states(self.eng, first, n, f, vs.bs, rows, cnt, self.roots)):
+            if states:
+                with game_stream(self.eng, first + i):
+                    v = self.value.batch(states, backend=self.backend)
+                out[i * vs.bs: i * vs.bs + len(states)] = [float(x) for x in v]
+        return torch.from_numpy(out).to(vs.dev)
 
 
 def c4_moves(eng, ids, roots, sims, c, bs, value, backend):
@@ -156,7 +223,7 @@ def c4_moves(eng, ids, roots, sims, c, bs, value, backend):
         raise ValueError("stepwise searches take a contiguous range of engine games")
     vs = C4ValuedSearch(eng, n, bs, planes=(kind == "net"))
     r = torch.from_numpy(roots.view(np.int64).reshape(n, 3).copy()).to(vs.dev)
-    fn = NetValue(value.zc_model) if kind == "net" else HostValue(value, backend)
+    fn = NetValue(value.zc_model) if kind == "net" else HostValue(value, backend, eng, first)
     mv, _, st = vs.run(r, sims, c, fn, first_game=first)
     st = st.cpu().numpy()
     if st[:, 5].any():
@@ -249,9 +316,10 @@ def chess_host_policy_moves(eng, ids, states, sims, c, bs, value, policy, backen
                     moves = [_native.unpack_chess_move(m) for m in nd["untried"][:n_un]]
                     k = moves.index(policy(moves))
                 eng.chess_hp_expand(int(gi), f, j, k, leaf.data_ptr(), s)
-                leaves.append(cb.from_zc(leaf.cpu().numpy().view(_native.CHESS_STATE_DTYPE)[0]))
+                leaves.append(leaf.cpu().numpy().copy())
             if not live:
                 break
+            leaves = chess_leaf_states(eng, int(gi), 1, f, bs, np.stack(leaves), [nb], [state])[0]
             v = [float(x) for x in value.batch(leaves, backend=backend)]
             vals[:nb].copy_(torch.tensor(v, dtype=torch.float64))
             eng.chess_ext_backup(int(gi), 1, f, vals.data_ptr(), s)

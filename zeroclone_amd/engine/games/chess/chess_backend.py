@@ -172,6 +172,23 @@ def state_to_tensor(state):
     return _run(fn, [state], (1, 17, 8, 8), torch.float32)[0]
 
 
+def pack_histories(states, cap: int | None = None):
+    """Both sides' move histories of `states` as the device takes them: uint16 [n, 2, cap]
+    packed moves in play order (the State's lists are most recent first, as the reference's
+    deques) and their lengths int32 [n, 2]."""
+    cap = cap or max([1] + [max(len(s.hist_white), len(s.hist_black)) for s in states])
+    h = np.zeros((len(states), 2, cap), np.uint16)
+    n = np.zeros((len(states), 2), np.int32)
+    for i, s in enumerate(states):
+        for side, lst in enumerate((s.hist_white, s.hist_black)):
+            if len(lst) > cap:
+                raise ValueError(f"a history of {len(lst)} moves exceeds {cap}")
+            for k, ((fr, fc, tr, tc), v) in enumerate(reversed(list(lst))):
+                h[i, side, k] = _native.pack_chess_move(fr, fc, tr, tc, v)
+            n[i, side] = len(lst)
+    return h, n
+
+
 def moves_from_hist(h: str):
     """Decode a history string of the golden fixtures (5 digits per move, most recent first)."""
     return [((int(h[i]), int(h[i + 1]), int(h[i + 2]), int(h[i + 3])), float(h[i + 4])) for i in range(0, len(h), 5)]

@@ -12,12 +12,15 @@ reference's state.  The GIL is released during device calls (ctypes).
 Supported plugins: the Connect4 and chess backends (this package's, or the reference's —
 states with the same fields), Policy('random') / Policy('immediate_value') on the device, any
 other policy callable (called on the host at each expansion, the tree still on the device:
-_search.c4_host_policy_moves / chess_host_policy_moves), and any value
-object: Value('random_rollout') (Connect4) and Value('crude_chess_score') (chess) run inside
-the search kernel, network values run on the device between the select and backup kernels,
-and any other object's value.batch(states, backend=backend) is called on the host once per
-flush, exactly where the reference calls it (mcts.cpp:116).  Such a value function must not
-draw from `random` (the reference's network and crude-score values do not).
+_search.c4_host_policy_moves / chess_host_policy_moves), and any value object:
+Value('random_rollout') runs on the device (Connect4: inside the search kernel; chess: a
+rollout kernel between the select and backup kernels, the leaves' move histories rebuilt from
+the root's and the path), Value('crude_chess_score') inside the chess search kernel, network
+values on the device between the select and backup kernels, and any other object's
+value.batch(states, backend=backend) on the host once per flush, exactly where the reference
+calls it (mcts.cpp:116) — with Python's `random` handed the game's device stream for the
+call (_device.game_stream), so a value that draws random numbers draws the reference's, and
+chess leaves carrying their move histories.
 
 Any other game backend (the six functions of engine/README.md:17-24) searches with the tree
 on the device (zc_gen_*) and the backend, policy and value called on the host, in the
@@ -34,13 +37,9 @@ __all__ = ["get_move"]
 def _plugin_check(state, value, policy, backend):
     game = _search.game_of(backend, state)
     _search.policy_of(policy)
-    kind = _search.value_kind(value)
-    if game == "generic":
-        return game
-    if game == "connect4" and kind == "crude":
-        raise NotImplementedError("crude_chess_score is a chess value function")
-    if game == "chess" and kind == "rollout":
-        raise NotImplementedError("random_rollout runs on the GPU for Connect4 only")
+    _search.value_kind(value)
+    # every combination runs: e.g. crude_chess_score on Connect4 goes to the host value path
+    # and fails where the reference's does (chr() of a board row, value_functions.py:54)
     return game
 
 
@@ -71,6 +70,7 @@ def get_move(state, value, policy, backend, simulations=1000, c=1.4, batch_size=
         eng = ge.ensure(1, simulations, batch_size)
         mt, idx, ver, gauss = _device.python_random_state()
         eng.set_rng_state(0, mt, idx)
+        eng.py_gauss = {0: gauss}
         if game == "connect4":
             from .games.connect4 import c4_backend as c4
             mv = _search.c4_moves(eng, [0], _device.c4_roots([state], c4), simulations, c, batch_size, value,
@@ -80,5 +80,5 @@ def get_move(state, value, policy, backend, simulations=1000, c=1.4, batch_size=
             if mv is None:
                 raise ValueError("root has no legal move (the reference indexes moves[-1] here)")
         mt, idx = eng.get_rng_state(0)
-        _device.set_python_random_state(mt, idx, ver, gauss)
+        _device.set_python_random_state(mt, idx, ver, eng.py_gauss.get(0, gauss))
     return mv

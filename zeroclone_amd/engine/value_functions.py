@@ -31,11 +31,9 @@ class Value:
         self.name = name
         self.init_args = kwargs
         self.zc_model = None
-        if name not in SUPPORTED:
-            raise NotImplementedError(
-                f"value function {name!r} is not implemented on the MI355X path "
-                f"(supported: {', '.join(SUPPORTED)}); see DESIGN.md")
-        if name.startswith("network"):
+        # as the reference (value_functions.py:9-14): an unknown name constructs, and fails
+        # with AttributeError when called (:17-18)
+        if name in SUPPORTED and name.startswith("network"):
             self._init_network()
 
     def __call__(self, state, **kwargs):
@@ -49,15 +47,16 @@ class Value:
     def random_rollout(self, states, backend):
         if getattr(backend, "ZC_GAME", None) != "connect4" and not _looks_like_c4(backend, states):
             from ._search import game_of
-            if states and game_of(backend, states[0]) != "generic":
-                raise NotImplementedError("random_rollout runs on the GPU for Connect4 only")
+            game = game_of(backend, states[0]) if states else "generic"
+            if game == "chess":
+                return _chess_rollouts(states)
             return [_backend_rollout(s, backend) for s in states]
         from .games.connect4 import c4_backend as c4
         if not states:
             return []
-        ge = _device.scratch(1, 32)
+        ge = _device.value_engine()
         with ge.lock:
-            eng = ge.ensure(1, 1, 32)
+            eng = ge.ensure(1, 1, 1)
             mt, idx, ver, gauss = _device.python_random_state()
             eng.set_rng_state(0, mt, idx)
             vals, _ = eng.c4_rollouts(_device.c4_roots(states, c4), game=0)
@@ -160,6 +159,44 @@ def _backend_rollout(state, backend):
     if backend.check_win(state):
         return -1 if state.turn == initial else 1
     return 0
+
+
+def _chess_rollouts(states):
+    """value_functions.py:35-45 on the chess backend, for a direct Value.batch call: the
+    states are rolled out IN ORDER on the GPU (zc_chess_rollouts_async: the chess rules, both
+    sides' histories for the repetition draw) on a CPython-compatible MT19937 stream taken from
+    (and returned to) Python's global `random`."""
+    import numpy as np
+    import torch
+    from .games.chess import chess_backend as cb
+    from ._search import chess_roots
+    if not states:
+        return []
+    hist, hlen = cb.pack_histories(states)
+    ge = _device.value_engine()
+    with ge.lock:
+        eng = ge.ensure(1, 1, 1)
+        dev = torch.device("cuda", eng.device)
+        rows = torch.from_numpy(chess_roots(states).view(np.uint8).reshape(len(states), 72).copy()).to(dev)
+        h, n = torch.from_numpy(hist).to(dev), torch.from_numpy(hlen).to(dev)
+        vals = torch.zeros(len(states), dtype=torch.float64, device=dev)
+        status = torch.zeros(1, dtype=torch.int32, device=dev)
+        mt, idx, ver, gauss = _device.python_random_state()
+        eng.set_rng_state(0, mt, idx)
+        s = torch.cuda.current_stream(dev)
+        eng.chess_rollouts_async(0, len(states), rows.data_ptr(), h.data_ptr(), n.data_ptr(), hist.shape[2],
+                                 vals.data_ptr(), status.data_ptr(), s.cuda_stream)
+        s.synchronize()
+        if int(status.item()):
+            raise RuntimeError(f"chess rollout exceeded {_native_roll_cap()} moves per side in its history")
+        mt, idx = eng.get_rng_state(0)
+        _device.set_python_random_state(mt, idx, ver, gauss)
+        return [int(v) for v in vals.cpu().tolist()]
+
+
+def _native_roll_cap():
+    from .. import _native
+    return _native.CHESS_ROLL_CAP
 
 
 def _looks_like_c4(backend, states):

@@ -107,12 +107,16 @@ class NetValue:
 
 class HostValue:
     """Any reference-style Value object: value.batch(states, backend=backend) per game per
-    flush, on c4_backend states built from the device leaves."""
+    flush, on c4_backend states built from the device leaves.  With `eng`, Python's global
+    `random` is game first_game + i's device stream during the call (the flush's expansion
+    draws already taken, as in mcts.cpp:112-127), so a value object that draws from `random`
+    gets the reference's numbers and the search continues after them."""
 
-    def __init__(self, value, backend):
-        self.value, self.backend = value, backend
+    def __init__(self, value, backend, eng=None, first_game: int = 0):
+        self.value, self.backend, self.eng, self.first = value, backend, eng, first_game
 
     def __call__(self, leaves, planes, counts):
+        from .engine._device import game_stream
         from .engine.games.connect4 import c4_backend as zb
         rows = leaves.cpu().numpy().view(np.uint64)
         cnt = counts.cpu().numpy()
@@ -122,7 +126,12 @@ class HostValue:
             if k == 0:
                 continue
             states = [zb.from_zc(int(r[0]), int(r[1]), int(r[2]) & 1) for r in rows[i * bs: i * bs + k]]
-            out[i * bs: i * bs + k] = [float(v) for v in self.value.batch(states, backend=self.backend)]
+            if self.eng is None:
+                v = self.value.batch(states, backend=self.backend)
+            else:
+                with game_stream(self.eng, self.first + i):
+                    v = self.value.batch(states, backend=self.backend)
+            out[i * bs: i * bs + k] = [float(x) for x in v]
         return torch.from_numpy(out).to(leaves.device)
 
 
@@ -161,7 +170,10 @@ class ChessValuedSearch:
             e.chess_ext_select(first_game, n, f, p(self.leaves), p(self.planes),
                                self.planes is None or self.planes.dtype == torch.float16, self.counts.data_ptr(),
                                _stream(self.dev))
-            v = value_fn(self.leaves, self.planes, self.counts)
+            if hasattr(value_fn, "flush_values"):   # values computed on the device from the tree itself
+                v = value_fn.flush_values(first_game, n, f, _stream(self.dev))
+            else:
+                v = value_fn(self.leaves, self.planes, self.counts)
             if v is not self.values:
                 self.values.copy_(v.reshape(-1))
             e.chess_ext_backup(first_game, n, f, self.values.data_ptr(), _stream(self.dev))
