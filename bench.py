@@ -54,8 +54,10 @@ def bytes_per_expansion_model(expansions: int, depth_sum: int) -> int:
 
 def host_cpus() -> dict:
     """What the CPU baseline ran on: the threads used (the process's CPU share: the
-    scheduler affinity, capped by OMP_NUM_THREADS where the box sets it), nproc, the model."""
-    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    scheduler affinity, capped by OMP_NUM_THREADS where the box sets it), nproc, the model,
+    and why (the affinity mask the process was given)."""
+    aff_set = sorted(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else list(range(os.cpu_count() or 1))
+    aff = len(aff_set)
     omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
     model = platform.processor() or ""
     try:
@@ -66,31 +68,91 @@ def host_cpus() -> dict:
                     break
     except OSError:
         pass
-    return {"threads": max(1, min(aff, omp) if omp else aff), "nproc": os.cpu_count(), "affinity": aff,
-            "cpu_model": model}
+    threads = max(1, min(aff, omp) if omp else aff)
+    why = (f"the process's CPU share: sched_getaffinity allows {aff} of nproc {os.cpu_count()} CPUs "
+           f"({_ranges(aff_set)})" + (f", OMP_NUM_THREADS={omp}" if omp else "")
+           + f" -> {threads} threads")
+    return {"threads": threads, "nproc": os.cpu_count(), "affinity": aff, "affinity_mask": _ranges(aff_set),
+            "cpu_model": model, "why": why}
 
 
-def cpu_baseline(sims: int, bs: int, c: float, budget_s: float = 15.0):
+def _ranges(xs) -> str:
+    out, i = [], 0
+    while i < len(xs):
+        j = i
+        while j + 1 < len(xs) and xs[j + 1] == xs[j] + 1:
+            j += 1
+        out.append(str(xs[i]) if i == j else f"{xs[i]}-{xs[j]}")
+        i = j + 1
+    return ",".join(out)
+
+
+def c4_row_board(row) -> tuple[str, int]:
+    """[stones X, stones O, turn] -> (42-char board, row 0 at the top, '.' empty; turn)."""
+    s0, s1, t = (int(x) for x in row)
+    cells = []
+    for r in range(6):
+        for col in range(7):
+            bit = 1 << (7 * col + (5 - r))
+            cells.append("X" if s0 & bit else ("O" if s1 & bit else "."))
+    return "".join(cells), t & 1
+
+
+def pool_snapshot(sp, n: int = 1024) -> dict:
+    """The burned-in pool's state at the timed window's start, for the like-for-like CPU
+    baseline: n games spread over the pool (every G/n-th slot), their positions and their
+    MT19937 states."""
+    import oracle
+    step = max(1, sp.G // n)
+    idx = list(range(0, sp.G, step))[:n]
+    rows = sp.roots.cpu().numpy()
+    boards, turns, mts = [], [], []
+    for g in idx:
+        b, t = c4_row_board(rows[g])
+        boards.append(b)
+        turns.append(t)
+        mt, k = sp.eng.get_rng_state(g)
+        o = oracle.MT(0)
+        o.s.mt[:] = [int(x) for x in mt]
+        o.s.index = k
+        mts.append(o)
+    return {"boards": boards, "turns": turns, "mts": mts, "slots": idx}
+
+
+def cpu_baseline(sims: int, bs: int, c: float, snap: dict, budget_s: float = 15.0):
     """The oracle port (oracle/c4_oracle.c, bit-exact to the reference's get_move on the
-    committed fixtures), one game per pthread task across the host's CPU share."""
+    committed fixtures) on the SAME workload as the GPU window: games taken from the
+    burned-in pool's snapshot (mixed ages, their own MT19937 states), each playing
+    consecutive self-play moves (search, play, evaluate, refill) — one game per pthread task
+    across the host's CPU share.  Expansions are counted as the GPU counts them (nodes
+    created)."""
+    import copy
     import oracle
     hc = host_cpus()
     threads = hc["threads"]
-    n0 = threads
+    boards, turns, mts = snap["boards"], snap["turns"], snap["mts"]
+    n0 = min(len(boards), threads)
     t = time.perf_counter()
-    oracle.get_move_batch(["." * 42] * n0, [0] * n0, list(range(n0)), sims, c, bs, threads=threads)
-    rate0 = n0 * sims / max(time.perf_counter() - t, 1e-6)
-    n = int(max(threads, min(65536, rate0 * budget_s / sims)))
-    n = max(threads, (n // threads) * threads)
+    e0 = oracle.selfplay_batch(boards[:n0], turns[:n0], [copy.deepcopy(m) for m in mts[:n0]], 1, sims, c, bs,
+                               threads=threads)
+    rate0 = float(e0.sum()) / max(time.perf_counter() - t, 1e-6)
+    per_move = float(e0.sum()) / n0
+    moves = 4
+    n = int(min(len(boards), max(threads, rate0 * budget_s / (per_move * moves))))
+    n = max(min(threads, len(boards)), (n // threads) * threads)
+    ms = [copy.deepcopy(m) for m in mts[:n]]
     t = time.perf_counter()
-    oracle.get_move_batch(["." * 42] * n, [0] * n, list(range(1000, 1000 + n)), sims, c, bs, threads=threads)
+    exp = oracle.selfplay_batch(boards[:n], turns[:n], ms, moves, sims, c, bs, threads=threads)
     dt = time.perf_counter() - t
-    return {"value": round(n * sims / dt, 1), "unit": "expansions/s", "cores": threads, "kind": "port",
-            "nproc": hc["nproc"], "cpu_model": hc["cpu_model"],
+    ages = [sum(ch != "." for ch in b) for b in boards[:n]]
+    return {"value": round(float(exp.sum()) / dt, 1), "unit": "expansions/s", "cores": threads, "kind": "port",
+            "nproc": hc["nproc"], "cpu_model": hc["cpu_model"], "threads_why": hc["why"],
             "port": "oracle/c4_oracle.c: C restatement pinned bit-exact to the reference's own get_move outputs "
                     "(tests/golden/c4_get_move.json, 150 cases incl. 800 sims) and rollouts",
-            "sample": f"{n} games x 1 move x {sims} sims from the opening (expansions = sims there), "
-                      f"batch {bs}, {threads} pthreads, {dt:.1f}s"}
+            "sample": f"{n} games of the burned-in GPU pool's snapshot (the timed window's mixed-age roots, plies "
+                      f"{min(ages)}-{max(ages)}, and their own MT19937 states) x {moves} consecutive self-play moves "
+                      f"each (search, play, evaluate, refill), {sims} sims, batch {bs}; expansions counted as nodes "
+                      f"created; {threads} pthreads, {dt:.1f}s"}
 
 
 def cpu_baseline_chess(sims: int = 400, bs: int = 32, c: float = 1.4, budget_s: float = 10.0):
@@ -492,17 +554,36 @@ def exchange_positions(local, world: int, sync=lambda: None):
     return out, allpos
 
 
-# the committed rocprofv3 summary of the current search kernel (tools/summarize_profile.py:
-# HBM bytes per launch from separate FETCH_SIZE / WRITE_SIZE passes, SQ issue counters)
-SEARCH_PROFILE = os.path.join("profiles", "r03_end_c4_search_summary.json")
+# the committed rocprofv3 summaries (tools/summarize_profile.py, stamped with the sha256 of the
+# library they profiled): the self-play kernel (HBM bytes per launch from separate FETCH_SIZE /
+# WRITE_SIZE passes, SQ issue counters) and the walk-only replay kernel (tools/prof_walk.py)
+SEARCH_PROFILE = os.path.join("profiles", "r04_c4_search_summary.json")
+WALK_PROFILE = os.path.join("profiles", "r04_walk_summary.json")
 
 
-def search_profile():
-    path = os.path.join(HERE, SEARCH_PROFILE)
+def lib_sha() -> str:
+    import hashlib
+    with open(_native.LIB, "rb") as fh:
+        return hashlib.sha256(fh.read()).hexdigest()
+
+
+def load_profile(rel: str):
+    """(summary, source) of a committed profile; the source says STALE when the summary's
+    library stamp differs from the library this process loaded (its counters then describe
+    other code)."""
+    path = os.path.join(HERE, rel)
     if not os.path.exists(path):
         return {}, None
     with open(path) as fh:
-        return json.load(fh), SEARCH_PROFILE
+        prof = json.load(fh)
+    stamp = prof.get("lib_sha256")
+    if stamp != lib_sha():
+        return prof, f"{rel} (STALE: profiled library {str(stamp)[:12]}, loaded {lib_sha()[:12]})"
+    return prof, rel
+
+
+def search_profile():
+    return load_profile(SEARCH_PROFILE)
 
 
 def run_rank(args, rank: int, world: int, local: int):
@@ -520,6 +601,7 @@ def run_rank(args, rank: int, world: int, local: int):
     torch.cuda.set_stream(torch.cuda.Stream(dev))   # every launch and the timing events on one stream
     sp = C4SelfPlay(G, S, c=args.c, batch_size=B, seed=args.seed, rank=rank, device=local, record=True)
     burn = burn_in(sp) if args.burn_in else 0
+    snap = pool_snapshot(sp) if (world == 1 and not args.no_cpu_baseline) else None
     r = run_steps(sp, args.steps, args.warmup, world, launch=args.launch)
     gather = gather_trajectories(sp, world)
     counts, dt_max, kms = reduce_over_ranks([r["expansions"], r["depth_sum"], r["finished"], r["leaves"]], r["dt"],
@@ -529,6 +611,7 @@ def run_rank(args, rank: int, world: int, local: int):
         prof, prof_src = search_profile()
         traffic = args.traffic_bytes or (prof.get("hbm") or {}).get("bytes_per_launch")
         traffic_src = "--traffic-bytes" if args.traffic_bytes else prof_src
+        traffic_stale = bool(traffic_src and "STALE" in traffic_src)
         launches = args.steps * world
         bytes_launch = bytes_per_expansion_model(expansions, depth_sum) / launches
         avg_kernel_s = kms / 1e3 / args.steps   # per move
@@ -561,7 +644,7 @@ def run_rank(args, rank: int, world: int, local: int):
             # keep SURVEY §8(d)'s algorithmic HBM roofline; `issue` is the counter roofline.
             "roofline": {"bound": "issue", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 5),
-                         "traffic": traffic, "traffic_source": traffic_src,
+                         "traffic": traffic, "traffic_source": traffic_src, "traffic_stale": traffic_stale,
                          "kernel": "c4_selfplay_kernel (K x G moves per launch; per-step figures = launch / K)",
                          "avg_launch_ms": round(avg_kernel_s * 1e3, 3),
                          "bytes_per_launch_model": round(bytes_launch),
@@ -575,12 +658,18 @@ def run_rank(args, rank: int, world: int, local: int):
                       "trajectory_allgather": gather},
         }
         if world == 1:
-            out["extra"]["phases"] = phases(sp, args, bytes_launch, avg_kernel_s, traffic)
+            out["extra"]["phases"] = phases(sp, args, bytes_launch, avg_kernel_s)
             other = "free" if args.launch == "pooled" else "pooled"
             ro = run_steps(sp, args.steps, 0, launch=other)
             out["extra"][f"launch_{other}"] = {"value": round(ro["expansions"] / ro["dt"], 1), "unit": "expansions/s",
                                                "ms_per_step": round(ro["dt"] / args.steps * 1e3, 3),
                                                "moves": ro["moves"], "expansions": ro["expansions"]}
+            lock = out["value"] if args.launch == "free" else out["extra"]["launch_free"]["value"]
+            out["extra"]["reference_schedule"] = {
+                "value": lock, "unit": "expansions/s",
+                "note": "scripts/train.py:151-170's lockstep schedule (every game exactly K moves per launch, the "
+                        "launch ends with its slowest game) on the same pool and kernel; the headline `value` is the "
+                        "pooled schedule (the games share K x G moves; each game's moves are its lockstep moves)"}
         if world == 1 and args.net_steps > 0:
             out["extra"]["c2_philox"] = philox_mode(sp, args)
             out["extra"]["c2_value_net"] = net_mode(sp, G, S, B, args.c, args.net_steps, dev)
@@ -595,7 +684,7 @@ def run_rank(args, rank: int, world: int, local: int):
             crude_pool.close()
             out["extra"]["net_tower"] = tower_mode(dev)
         if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(S, B, args.c)
+            out["cpu_baseline"] = cpu_baseline(S, B, args.c, snap)
             if args.net_steps > 0:
                 out["extra"]["c4_chess"]["crude"]["cpu_baseline"] = cpu_baseline_chess()
                 out["extra"]["c2_value_net"]["cpu_baseline"] = cpu_baseline_c4_net(S, B, args.c)
@@ -610,30 +699,99 @@ def run_rank(args, rank: int, world: int, local: int):
         dist.destroy_process_group()
 
 
-def phases(sp, args, bytes_launch: float, avg_kernel_s: float, traffic: float | None = None) -> dict:
-    """SURVEY §8(d) per-phase times: s_memtime stamps from one extra search with the stamped
-    kernel build, shares applied to the unstamped launch time; and the tree-walk-only
-    roofline (select + expand-write + backup + publish; rollouts are integer VALU, not HBM)."""
+def phases(sp, args, bytes_launch: float, avg_kernel_s: float) -> dict:
+    """SURVEY §8(d) per-phase times (s_memtime stamps from one extra search with the stamped
+    kernel build, shares applied to the unstamped launch time) and the tree walk MEASURED on
+    its own: the walk-only replay kernel (walk_measure: the same search from a snapshot with
+    the recorded rollout values in place of the rollouts, identical tree) timed with HIP
+    events here, its HBM bytes per expansion from the committed rocprofv3 passes over the same
+    workload (WALK_PROFILE: FETCH_SIZE x2 + WRITE_SIZE, tools/prof_walk.py)."""
     sp.eng.phase_cycles(True)
     sp.step()
     torch.cuda.synchronize(sp.dev)
     ph = sp.eng.phase_cycles(False)
     tot_c = max(sum(ph.values()), 1)
     share = {k: v / tot_c for k, v in ph.items() if k != "sub"}
-    walk = sum(share[k] for k in ("rng", "walk_first", "walk_resumed", "expand", "backup", "publish"))
+    w = walk_measure(sp, reps=3)
+    wprof, wsrc = load_profile(WALK_PROFILE)
+    hbm = wprof.get("hbm") or {}
+    run = wprof.get("run") or {}
+    walk = {"kernel": "c4_walk_kernel<2> (replay) vs c4_search_kernel<false, false> (the full lockstep search)",
+            "walk_ms": w["walk_ms"], "search_ms": w["search_ms"], "walk_share_of_search": w["walk_share_of_search"],
+            "expansions": w["expansions"], "model_bytes": w["model_bytes"],
+            "model_gbs": round(w["model_bytes"] / (w["walk_ms"] * 1e-3) / 1e9, 2),
+            "profile": wsrc}
+    if hbm.get("bytes_per_launch") and run.get("expansions"):
+        per_exp = hbm["bytes_per_launch"] / run["expansions"]
+        measured = per_exp * w["expansions"]
+        gbs = measured / (w["walk_ms"] * 1e-3) / 1e9
+        walk.update({"measured_bytes": round(measured), "measured_bytes_per_expansion": round(per_exp, 2),
+                     "measured_gbs": round(gbs, 2), "measured_frac": round(gbs / HBM_PEAK_GBS, 5),
+                     "profile_walk_ns": (wprof.get("trace_last_avg_ns") or None),
+                     "stale": bool(wsrc and "STALE" in wsrc)})
+    walk["note"] = ("measured_frac = the walk-only kernel's PMC HBM bytes (per expansion, from the profile, times "
+                    "this run's expansions) over its own event time; model_gbs = SURVEY §8(d)'s 152 d + 96 model "
+                    "bytes over the same time (the model charges a root-to-leaf re-read per simulation that the "
+                    "kernel serves from LDS / L2, so it is not a rate and carries no frac)")
     return {"share": {k: round(v, 4) for k, v in share.items()},
             "ms_per_launch": {k: round(v * avg_kernel_s * 1e3, 3) for k, v in share.items()},
-            "walk_roofline": {"t_walk_ms": round(walk * avg_kernel_s * 1e3, 3),
-                              "model_gbs": round(bytes_launch / (walk * avg_kernel_s) / 1e9, 2),
-                              "model_frac": round(bytes_launch / (walk * avg_kernel_s) / 1e9 / HBM_PEAK_GBS, 5),
-                              "measured_frac": (round(traffic / (walk * avg_kernel_s) / 1e9 / HBM_PEAK_GBS, 5)
-                                                if traffic else None),
-                              "note": "SURVEY §8(d) roofline definition: model bytes / tree-walk time only "
-                                      "(phase shares from the stamped build: modelled, not a separate clock). "
-                                      "The model counts a root-to-leaf re-read per simulation that the kernel "
-                                      "serves from LDS / L2 (or never reads: the planned flush), so model_frac "
-                                      "can exceed 1 and is NOT a measured HBM rate; measured_frac = the whole "
-                                      "kernel's PMC HBM bytes over the walk time alone"}}
+            "walk_roofline": walk}
+
+
+def walk_measure(sp, reps: int = 5, check: bool = True) -> dict:
+    """Record / search / replay from one snapshot of pool `sp` (see the module docstring);
+    returns times (ms per launch, HIP events on the launch stream) and counts per launch."""
+    G, S, B = sp.G, sp.sims, sp.bs
+    dev = sp.dev
+    st = torch.cuda.current_stream(dev)
+    s = st.cuda_stream
+    nfl = (S + B - 1) // B
+    vals = torch.zeros((G, S), dtype=torch.int8, device=dev)
+    words = torch.zeros((G, nfl), dtype=torch.int32, device=dev)
+    rngbuf = torch.zeros(G * (4096 * 4 + 16), dtype=torch.uint8, device=dev)
+    roots = sp.roots.clone()
+
+    def outs():
+        return (torch.zeros(G, dtype=torch.int32, device=dev), torch.zeros((G, 7), dtype=torch.int32, device=dev),
+                torch.zeros((G, _native.STATS_FIELDS), dtype=torch.int64, device=dev))
+
+    sp.eng.rng_copy(0, G, rngbuf.data_ptr(), False, s)
+    rec = outs()
+    sp.eng.c4_walk_async(0, G, roots.data_ptr(), S, sp.c, B, 1, vals.data_ptr(), words.data_ptr(),
+                         rec[0].data_ptr(), rec[1].data_ptr(), rec[2].data_ptr(), s)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    sp.eng.rng_copy(0, G, rngbuf.data_ptr(), True, s)
+    ful = outs()
+    ev[0].record(st)
+    sp.eng.c4_search_async(roots.data_ptr(), G, S, sp.c, B, ful[0].data_ptr(), ful[1].data_ptr(), ful[2].data_ptr(),
+                           stream=s)
+    ev[1].record(st)
+    torch.cuda.synchronize(dev)
+    search_ms = ev[0].elapsed_time(ev[1])
+    walk = []
+    for _ in range(reps):
+        sp.eng.rng_copy(0, G, rngbuf.data_ptr(), True, s)
+        rep = outs()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(st)
+        sp.eng.c4_walk_async(0, G, roots.data_ptr(), S, sp.c, B, 2, vals.data_ptr(), words.data_ptr(),
+                             rep[0].data_ptr(), rep[1].data_ptr(), rep[2].data_ptr(), s)
+        e1.record(st)
+        torch.cuda.synchronize(dev)
+        walk.append(e0.elapsed_time(e1))
+        if check:
+            for a, b in ((rec, ful), (rec, rep)):
+                assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1]), "moves / root visits differ"
+                for k in (0, 1, 2, 4, 5):   # expansions, depth sum, leaves, words consumed, status
+                    assert torch.equal(a[2][:, k], b[2][:, k]), f"stats field {k} differs"
+    sp.eng.rng_copy(0, G, rngbuf.data_ptr(), True, s)   # leave the pool's streams as they were
+    tot = rec[2][:, :2].sum(0).tolist()
+    exp, dsum = int(tot[0]), int(tot[1])
+    walk_ms = sorted(walk)[len(walk) // 2]
+    return {"games": G, "sims": S, "batch": B, "expansions": exp, "depth_sum": dsum,
+            "model_bytes": bytes_per_expansion_model(exp, dsum), "search_ms": round(search_ms, 4),
+            "walk_ms": round(walk_ms, 4), "walk_ms_all": [round(x, 4) for x in walk],
+            "walk_share_of_search": round(walk_ms / search_ms, 4)}
 
 
 def tower_mode(dev, reps: int = 5) -> dict:

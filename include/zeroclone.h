@@ -629,6 +629,20 @@ int zc_debug_uct(zc_engine *eng, int32_t n, const double *logn, const int32_t *n
 int zc_debug_c4_rollout(zc_engine *eng, int32_t first_game, int32_t n, const zc_c4_state *states,
                         int32_t *out_value, int64_t *out_words);
 
+/* The tree walk alone (the walk-roofline measurement, tools/prof_walk.py): the lockstep
+ * Connect4 search of zc_c4_search_async with its rollouts recorded (mode 1: d_vals[g][sims]
+ * int8 the value of every simulation's leaf, d_words[g][ceil(sims/bs)] the words each flush's
+ * rollouts consumed; otherwise the normal search) or replayed (mode 2: the recorded values,
+ * the stream moved past the recorded words, no rollout run) — from the same roots and streams
+ * the replay builds the identical tree, so its time and HBM traffic are the walk's.
+ * zc_debug_rng_copy copies games first..first+n-1's streams (ring + positions) to d_buf
+ * (restore = 0) or back (restore = 1); d_buf holds n * (4096 * 4 + 16) bytes. */
+int zc_debug_c4_walk_async(zc_engine *eng, int32_t first_game, int32_t n_games, const zc_c4_state *d_roots,
+                           int32_t sims, double c, int32_t batch_size, int32_t mode, int8_t *d_vals, uint32_t *d_words,
+                           int32_t *d_out_move, int32_t *d_out_root_na, zc_game_stats *d_out_stats, void *hip_stream);
+int zc_debug_rng_copy(zc_engine *eng, int32_t first_game, int32_t n_games, void *d_buf, int32_t restore,
+                      void *hip_stream);
+
 /* A chess tree after a search (PUCT or UCT), copied to host buffers for the parity tests:
  * out_nodes = raw 96-byte node records (position, first slot, #moves, #untried, parent,
  * parent slot index, depth, material, in-check, evaluated), then per child slot the packed

@@ -50,6 +50,9 @@ def lib():
         L.zco_get_move_batch.argtypes = [ctypes.c_int, ctypes.c_char_p, P(ctypes.c_int), P(ctypes.c_uint64),
                                          ctypes.c_int, ctypes.c_double, ctypes.c_int, ctypes.c_int,
                                          P(ctypes.c_int), P(ctypes.c_int), P(ctypes.c_uint64)]
+        L.zco_selfplay_batch.argtypes = [ctypes.c_int, ctypes.c_char_p, P(ctypes.c_int), P(_MT), ctypes.c_int,
+                                         ctypes.c_int, ctypes.c_double, ctypes.c_int, ctypes.c_int,
+                                         P(ctypes.c_uint64)]
         L.zco_get_move_valued.argtypes = [ctypes.c_char_p, ctypes.c_int, P(_MT), ctypes.c_int, ctypes.c_double,
                                           ctypes.c_int, P(ctypes.c_int), P(ctypes.c_int), P(ctypes.c_int),
                                           VALUE_FN, ctypes.c_void_p]
@@ -163,6 +166,26 @@ def get_move_batch(boards: list[str], turns, seeds, sims: int, c: float = 1.4, b
                              sims, c, bs, threads, mv.ctypes.data_as(P(ctypes.c_int)),
                              na.ctypes.data_as(P(ctypes.c_int)), cons.ctypes.data_as(P(ctypes.c_uint64)))
     return mv, na, cons
+
+
+def selfplay_batch(boards: list[str], turns, mts: list["MT"], moves: int, sims: int, c: float = 1.4, bs: int = 32,
+                   threads: int = 1):
+    """zco_selfplay_batch: each game plays `moves` moves (search, play, evaluate, refill) from
+    its board and MT state (the MT objects are advanced); returns expansions per game."""
+    import numpy as np
+    n = len(boards)
+    b = "".join(boards).encode()
+    t = np.asarray(turns, np.int32)
+    arr = (_MT * max(n, 1))()
+    for i, m in enumerate(mts):
+        arr[i] = m.s
+    exp = np.zeros(n, np.uint64)
+    P = ctypes.POINTER
+    lib().zco_selfplay_batch(n, b, t.ctypes.data_as(P(ctypes.c_int)), arr, moves, sims, c, bs, threads,
+                             exp.ctypes.data_as(P(ctypes.c_uint64)))
+    for i, m in enumerate(mts):
+        m.s = arr[i]
+    return exp
 
 
 # ---------------------------------------------------------------- chess (chess_oracle.c)

@@ -303,6 +303,9 @@ static void backprop(onode *P, int node, double v) {   /* mcts.cpp:80-100 */
 
 /* mcts.cpp:102-160.  vfn == NULL: Value('random_rollout') on the same stream; otherwise
  * vfn(ctx, n, boards, turns, out) is Value.batch over the flush's pending leaves. */
+/* per thread: nodes of the last search (expansions = nodes - 1) */
+static __thread int t_last_nodes;
+
 static int get_move_impl(const char *board, int turn, zco_mt *r, int sims, double c, int bs,
                          int *root_na, int *order, int *n_moves, zco_value_fn vfn, void *ctx) {
     pthread_once(&g_order_once, order_init);
@@ -344,6 +347,7 @@ static int get_move_impl(const char *board, int turn, zco_mt *r, int sims, doubl
         if (order) order[i] = P[0].mv[i];
     }
     const int col = best >= 0 ? P[0].mv[best] : -1;
+    t_last_nodes = np;
     free(lt);
     free(lb);
     free(vals);
@@ -404,6 +408,62 @@ int zco_get_move_batch(int n, const char *boards, const int *turns, const uint64
         pthread_create(&th[t], NULL, worker, &J[t]);
     }
     for (int t = 0; t < n_threads; t++) pthread_join(th[t], NULL);
+    free(J);
+    free(th);
+    return 0;
+}
+
+/* ---------------------------------------------------- steady-state self-play baseline */
+/* The CPU side of bench.py's like-for-like baseline: n games from given positions and
+ * MT19937 states (a burned-in GPU pool's snapshot), each playing `moves` consecutive moves —
+ * get_move (mcts.cpp:102-160), play_move + _evaluate (engine.py:98-108, 148-153) and the
+ * refill of a finished game with the empty board (scripts/train.py:151-170) — spread over
+ * n_threads pthreads.  out_expansions[g] = nodes created by game g's searches. */
+typedef struct {
+    int lo, hi, moves, sims, bs;
+    double c;
+    const char *boards;
+    const int *turns;
+    zco_mt *mts;
+    uint64_t *out_exp;
+} sp_job;
+
+static void *sp_worker(void *arg) {
+    sp_job *J = (sp_job *)arg;
+    for (int g = J->lo; g < J->hi; g++) {
+        char b[43];
+        memcpy(b, J->boards + 42 * (size_t)g, 42);
+        b[42] = 0;
+        int t = J->turns[g];
+        uint64_t exp = 0;
+        for (int k = 0; k < J->moves; k++) {
+            const int col = zco_get_move(b, t, &J->mts[g], J->sims, J->c, J->bs, NULL, NULL, NULL);
+            exp += (uint64_t)(t_last_nodes - 1);
+            if (col < 0) break;
+            play(b, &t, col);
+            if (zco_check_win(b, t) || zco_check_draw(b)) {
+                memset(b, '.', 42);
+                t = 0;
+            }
+        }
+        J->out_exp[g] = exp;
+    }
+    return NULL;
+}
+
+int zco_selfplay_batch(int n, const char *boards, const int *turns, zco_mt *mts, int moves, int sims, double c,
+                       int bs, int n_threads, uint64_t *out_expansions) {
+    pthread_once(&g_order_once, order_init);
+    if (n_threads < 1) n_threads = 1;
+    if (n_threads > n) n_threads = n > 0 ? n : 1;
+    pthread_t *th = (pthread_t *)malloc(sizeof(pthread_t) * (size_t)n_threads);
+    sp_job *J = (sp_job *)malloc(sizeof(sp_job) * (size_t)n_threads);
+    for (int q = 0; q < n_threads; q++) {
+        J[q] = (sp_job){(int)((long)n * q / n_threads), (int)((long)n * (q + 1) / n_threads), moves, sims, bs, c,
+                        boards, turns, mts, out_expansions};
+        pthread_create(&th[q], NULL, sp_worker, &J[q]);
+    }
+    for (int q = 0; q < n_threads; q++) pthread_join(th[q], NULL);
     free(J);
     free(th);
     return 0;

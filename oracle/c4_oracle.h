@@ -56,6 +56,13 @@ int  zco_get_move_batch(int n, const char *boards, const int *turns, const uint6
                         int sims, double c, int bs, int n_threads,
                         int *out_move, int *out_root_na /* n*7 */, uint64_t *out_consumed);
 
+/* Steady-state self-play (bench.py's CPU baseline on a burned-in pool's snapshot): game g
+ * from boards[g] / turns[g] and MT state mts[g] (advanced in place) plays `moves` moves —
+ * get_move, play, _evaluate, the refill of a finished game with the empty board — on
+ * n_threads pthreads; out_expansions[g] = the nodes its searches created.  Returns 0. */
+int  zco_selfplay_batch(int n, const char *boards, const int *turns, zco_mt *mts, int moves, int sims, double c,
+                        int bs, int n_threads, uint64_t *out_expansions);
+
 #ifdef __cplusplus
 }
 #endif

@@ -329,3 +329,23 @@ def test_c2iii_connect4_value_net_pool_matches_oracle(c4_pool):
             assert _board(roots_after[g]) == (b, t), (g, k)
         assert same_mt(pool.eng, g, mt), g
     pool.close()
+
+
+def test_captured_step_graph_pins_the_trajectory_pool():
+    """A step graph has the trajectory pool's buffers baked into its record kernel: once one
+    is captured, a start(quota) that would need a larger pool is refused, and a
+    quota that fits keeps the graph valid."""
+    from zeroclone_amd.selfplay import C4SelfPlay
+    sp = C4SelfPlay(64, 16, batch_size=8, seed=1, games_cap=256)
+    g = sp.capture_step()
+    for _ in range(3):
+        g.replay()
+    torch.cuda.synchronize()
+    with pytest.raises(RuntimeError):
+        sp.start(100_000)
+    sp.start(128)   # fits the pool sized at construction
+    for _ in range(60):
+        g.replay()
+    torch.cuda.synchronize()
+    assert sp.traj.finished() > 0
+    sp.close()

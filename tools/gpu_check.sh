@@ -2,7 +2,7 @@
 # Runs ON THE GPU BOX (via gpurun): stages given as arguments, in order, each under its own
 # time limit; stops at the first stage that faults / aborts / times out (pytest failures,
 # rc=1, still let later stages run so a bench line is recorded).
-#   stages: pytest smoke bench bench8 prof pmc
+#   stages: pytest smoke bench bench8 prof pmc sel walk wprof whbm wpmc ...
 set -u
 cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
@@ -47,6 +47,16 @@ for st in "$@"; do
                 --pmc FETCH_SIZE -- python3 tools/prof_search.py --steps 60 || exit $?
             run shbm_write 600 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/shbm -o write \
                 --pmc WRITE_SIZE -- python3 tools/prof_search.py --steps 60 || exit $? ;;
+    walk)   run walk 300 python3 tools/prof_walk.py --reps 5 || exit $? ;;
+    wprof)  run wprof 400 rocprofv3 --kernel-trace --stats -d gpurun_out/wprof -o run --output-format csv \
+                -- python3 tools/prof_walk.py --reps 3 || exit $? ;;
+    whbm)   run whbm_fetch 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/whbm -o fetch \
+                --pmc FETCH_SIZE -- python3 tools/prof_walk.py --reps 3 || exit $?
+            run whbm_write 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/whbm -o write \
+                --pmc WRITE_SIZE -- python3 tools/prof_walk.py --reps 3 || exit $? ;;
+    wpmc)   run wpmc 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/wpmc -o pmc \
+                --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE \
+                -- python3 tools/prof_walk.py --reps 3 || exit $? ;;
     ab)     run ab 900 env AB_ROOTS=mixed AB_ROUNDS=${AB_ROUNDS:-3} python tools/ab_search.py ${AB_LIBS} || exit $? ;;
     *) echo "unknown stage $st"; exit 2 ;;
   esac

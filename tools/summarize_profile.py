@@ -25,7 +25,9 @@ kernel are used (the driver's burn-in steps come first).
 import argparse
 import collections
 import csv
+import hashlib
 import json
+import os
 
 KERNEL = "c4_selfplay_kernel<false>"  # the product kernel (K self-play moves per launch)
 N_CU, N_SIMD, N_XCD = 256, 1024, 8
@@ -59,9 +61,21 @@ def main():
     ap.add_argument("--last", type=int, default=1, help="launches to average (0 = all)")
     ap.add_argument("--moves", type=int, default=1, help="moves per launch: bytes and times are reported per move")
     ap.add_argument("--note", default="")
+    ap.add_argument("--lib", default=os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "zeroclone_amd",
+                                                  "libzeroclone_amd.so"),
+                    help="the library the profiled run loaded: its sha256 stamps the summary (bench.py marks "
+                         "the summary stale when the loaded library differs)")
+    ap.add_argument("--extra-json", default=None, help="a JSON line (e.g. tools/prof_walk.py's output) to embed")
     ap.add_argument("--out", required=True)
     a = ap.parse_args()
     out = {"kernel": a.kernel, "launches_used": a.last or "all", "moves_per_launch": a.moves}
+    if a.lib and os.path.exists(a.lib):
+        out["lib_sha256"] = hashlib.sha256(open(a.lib, "rb").read()).hexdigest()
+        out["lib_mtime"] = os.path.getmtime(a.lib)
+    if a.extra_json:
+        with open(a.extra_json) as fh:
+            lines = [ln for ln in fh.read().splitlines() if ln.startswith("{")]
+        out["run"] = json.loads(lines[-1])
     if a.note:
         out["note"] = a.note
     if a.stats:

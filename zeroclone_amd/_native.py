@@ -259,6 +259,12 @@ SIGNATURES = [
     ("zc_debug_chess_tree", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
                                            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    ("zc_debug_c4_walk_async", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p,
+                                              ctypes.c_int32, ctypes.c_double, ctypes.c_int32, ctypes.c_int32,
+                                              ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                              ctypes.c_void_p, ctypes.c_void_p]),
+    ("zc_debug_rng_copy", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p,
+                                         ctypes.c_int32, ctypes.c_void_p]),
     ("zc_debug_phase_cycles", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, P(ctypes.c_int64)]),
     ("zc_debug_phase_cycles_games", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, P(ctypes.c_int64)]),
     ("zc_debug_c4_rollout", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p,
@@ -592,6 +598,18 @@ class NativeEngine:
     def chess_ext_end(self, first_game: int, n: int, d_move: int, d_na: int, d_stats: int, stream: int = 0):
         check(lib().zc_chess_ext_end(self._h, first_game, n, ctypes.c_void_p(d_move), ctypes.c_void_p(d_na),
                                      ctypes.c_void_p(d_stats), ctypes.c_void_p(stream or None)))
+
+    # ---- the walk diagnostic (device pointers; tools/prof_walk.py)
+    def c4_walk_async(self, first_game: int, n: int, d_roots: int, sims: int, c: float, batch_size: int, mode: int,
+                      d_vals: int, d_words: int, d_move: int, d_na: int, d_stats: int, stream: int = 0):
+        check(lib().zc_debug_c4_walk_async(self._h, first_game, n, ctypes.c_void_p(d_roots), int(sims), float(c),
+                                           int(batch_size), int(mode), ctypes.c_void_p(d_vals),
+                                           ctypes.c_void_p(d_words), ctypes.c_void_p(d_move), ctypes.c_void_p(d_na),
+                                           ctypes.c_void_p(d_stats), ctypes.c_void_p(stream or None)))
+
+    def rng_copy(self, first_game: int, n: int, d_buf: int, restore: bool, stream: int = 0):
+        check(lib().zc_debug_rng_copy(self._h, first_game, n, ctypes.c_void_p(d_buf), 1 if restore else 0,
+                                      ctypes.c_void_p(stream or None)))
 
     # ---- Value('random_rollout') on chess (device pointers)
     def chess_rollouts_async(self, game: int, n: int, d_states: int, d_hist: int, d_hist_len: int, hist_cap: int,

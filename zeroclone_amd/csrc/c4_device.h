@@ -356,6 +356,13 @@ __device__ __forceinline__ void rng_advance(LRng &r) {
     lrng_prefetch(r);
 }
 
+// Consume w words without reading them (the walk-replay diagnostic: a flush's recorded
+// rollout words), window by window.
+__device__ __forceinline__ void lrng_skip(LRng &r, uint32_t w) {
+    r.off += w;
+    while (r.off >= (uint32_t)kWin) rng_advance(r);
+}
+
 // Write the stream back to the game's HBM ring and rngpos (see above).
 __device__ __forceinline__ void lrng_close(const LRng &r, uint32_t *ring, uint64_t use0, uint64_t *rngpos) {
     const uint32_t lane = lane_id();

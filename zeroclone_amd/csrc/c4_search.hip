@@ -723,7 +723,10 @@ __device__ __forceinline__ SearchLds search_lds(uint8_t *s_dyn, int bs) {
 // STAMP = diagnostic build: lane 0 adds s_memtime deltas per phase into p.a.phase[g][0..7] =
 // {-, first walk of a flush, resumed walks, expansion + leaf bookkeeping, rollouts, backup,
 //  publish, rollout sub-region}.
-template <bool STAMP, bool PHILOX>
+// WALK (diagnostic, zc_debug_c4_walk_async): 1 = record every leaf's rollout value and every
+// flush's rollout words (p.walk_vals / p.walk_words); 2 = replay them instead of running the
+// rollouts — the tree walk, expansion, backup and publish alone on the identical tree.
+template <bool STAMP, bool PHILOX, int WALK = 0>
 __device__ __forceinline__ void search_move(const SearchParams &p, const SearchLds &L, int gl, int g, const Tree &t,
                                             LRng &rng, uint32_t tag, Counters &cn, int &status) {
     const uint32_t lane = lane_id();
@@ -766,12 +769,24 @@ __device__ __forceinline__ void search_move(const SearchParams &p, const SearchL
         const int f0 = fs.f0, d0 = fs.d0;
 
         // ---- value.batch: random rollouts in pending order (mcts.cpp:112-124) ---------------
-        if (PHILOX)
+        const size_t wlog = (size_t)g * p.sims + done;
+        const size_t wfl = (size_t)g * ((p.sims + p.bs - 1) / p.bs) + done / p.bs;
+        if (WALK == 2) {   // replay: the recorded values, the stream moved past the recorded words
+            for (int jj = (int)lane; jj < nb; jj += kBlock) leaves[jj].val = p.walk_vals[wlog + jj];
+            lrng_skip(rng, uni(p.walk_words[wfl]));
+        } else if (PHILOX) {
             c4_rollouts_philox(leaves, nb, sel_table(s_order),
                                make_uint2((uint32_t)p.philox_seed, (uint32_t)(p.philox_seed >> 32)), (uint32_t)done,
                                tag, (uint32_t)g, cn);
-        else
+        } else {
+            const int32_t u0 = rng.use();
             c4_rollouts(leaves, nb, rng, s_order, cn, STAMP ? &stamp.ph[7] : nullptr);
+            if (WALK == 1) {
+                wave_mem_order();
+                for (int jj = (int)lane; jj < nb; jj += kBlock) p.walk_vals[wlog + jj] = (int8_t)leaves[jj].val;
+                if (lane == 0) p.walk_words[wfl] = (uint32_t)(rng.use() - u0);
+            }
+        }
         wave_mem_order();
         stamp.mark(4);
 
@@ -888,9 +903,8 @@ __device__ __forceinline__ int best_column(const Tree &t, int &na_col) {
     return (int)((ow >> (3 * best)) & 7u);
 }
 
-template <bool STAMP, bool PHILOX>
-__global__ __launch_bounds__(kSearchWaves * kBlock) void c4_search_kernel(SearchParams p) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t s_dyn[];
+template <bool STAMP, bool PHILOX, int WALK>
+__device__ __forceinline__ void search_games(const SearchParams &p, uint8_t *s_dyn) {
     const SearchLds L = search_lds(s_dyn, p.bs);
     load_tables(L.s_order);
     __syncthreads();
@@ -921,7 +935,7 @@ __global__ __launch_bounds__(kSearchWaves * kBlock) void c4_search_kernel(Search
     lrng_open(rng, L.ring, a.ring + (size_t)g * kRingWords, use0, uni64(a.rngpos[2 * (size_t)g + 1]));
     Counters cn;
     int status = 0;
-    search_move<STAMP, PHILOX>(p, L, gl, g, t, rng, uni((uint32_t)use0), cn, status);
+    search_move<STAMP, PHILOX, WALK>(p, L, gl, g, t, rng, uni((uint32_t)use0), cn, status);
     int na_col;
     const int col = best_column(t, na_col);
     if (lane < 7) p.out_na[(size_t)gl * 7 + lane] = na_col;
@@ -938,6 +952,20 @@ __global__ __launch_bounds__(kSearchWaves * kBlock) void c4_search_kernel(Search
         p.out_stats[gl] = st;
     }
     lrng_close(rng, a.ring + (size_t)g * kRingWords, use0, a.rngpos + 2 * (size_t)g);
+}
+
+template <bool STAMP, bool PHILOX>
+__global__ __launch_bounds__(kSearchWaves * kBlock) void c4_search_kernel(SearchParams p) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t s_dyn[];
+    search_games<STAMP, PHILOX, 0>(p, s_dyn);
+}
+
+// Diagnostic: the lockstep search with its rollouts recorded (WALK 1) or replayed (WALK 2):
+// the tree-walk-only kernel whose time and HBM traffic measure the walk (tools/prof_walk.py).
+template <int WALK>
+__global__ __launch_bounds__(kSearchWaves * kBlock) void c4_walk_kernel(SearchParams p) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t s_dyn[];
+    search_games<false, false, WALK>(p, s_dyn);
 }
 
 // Self-play without a global step: each wave plays `p.moves` consecutive moves of its game —
@@ -1151,6 +1179,16 @@ void launch_c4_search(const SearchParams &p, hipStream_t s) {
         else
             hipLaunchKernelGGL((c4_search_kernel<false, false>), grid, block, lds, s, p);
     }
+}
+
+void launch_c4_walk(const SearchParams &p, int mode, hipStream_t s) {
+    const int wpg = c4_search_wpg(p.bs);
+    const size_t lds = c4_search_lds_bytes(p.bs);
+    const dim3 grid((p.n_games + wpg - 1) / wpg), block(wpg * kBlock);
+    if (mode == 1)
+        hipLaunchKernelGGL((c4_walk_kernel<1>), grid, block, lds, s, p);
+    else
+        hipLaunchKernelGGL((c4_walk_kernel<2>), grid, block, lds, s, p);
 }
 
 void launch_c4_selfplay(const SearchParams &p, hipStream_t s) {

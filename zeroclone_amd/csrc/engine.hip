@@ -1605,6 +1605,42 @@ int zc_debug_c4_rollout(zc_engine *eng, int32_t first, int32_t n, const zc_c4_st
     return ZC_OK;
 }
 
+int zc_debug_c4_walk_async(zc_engine *eng, int32_t first, int32_t n, const zc_c4_state *d_roots, int32_t sims,
+                           double c, int32_t bs, int32_t mode, int8_t *d_vals, uint32_t *d_words, int32_t *d_move,
+                           int32_t *d_na, zc_game_stats *d_stats, void *hip_stream) {
+    if (!eng || (n && (!d_roots || !d_vals || !d_words || !d_move || !d_na || !d_stats)))
+        return fail(ZC_EINVAL, "null argument");
+    if (mode != 1 && mode != 2) return fail(ZC_EINVAL, "mode must be 1 (record) or 2 (replay)");
+    if (int r = check_search(eng, first, n, sims, c, bs)) return r;
+    if (!n) return ZC_OK;
+    std::lock_guard<std::mutex> lk(eng->mu);
+    ZC_HIP(hipSetDevice(eng->cfg.device));
+    zc::SearchParams p = make_params(eng, first, n, d_roots, sims, c, bs, d_move, d_na, d_stats);
+    if (p.philox || p.stamp) return fail(ZC_EINVAL, "the walk diagnostic runs the exact, unstamped search");
+    // the logs are indexed by engine game (g * sims, g * flushes): shift so game `first` is row 0
+    p.walk_vals = d_vals - (size_t)first * sims;
+    p.walk_words = d_words - (size_t)first * ((sims + bs - 1) / bs);
+    zc::launch_c4_walk(p, mode, (hipStream_t)hip_stream);
+    ZC_HIP(hipGetLastError());
+    return ZC_OK;
+}
+
+int zc_debug_rng_copy(zc_engine *eng, int32_t first, int32_t n, void *d_buf, int32_t restore, void *hip_stream) {
+    if (!eng || (n && !d_buf)) return fail(ZC_EINVAL, "null argument");
+    if (int r = check_games(eng, first, n)) return r;
+    if (!n) return ZC_OK;
+    std::lock_guard<std::mutex> lk(eng->mu);
+    ZC_HIP(hipSetDevice(eng->cfg.device));
+    hipStream_t s = (hipStream_t)hip_stream;
+    uint8_t *ring = (uint8_t *)(eng->a.ring + (size_t)first * zc::kRingWords);
+    uint8_t *pos = (uint8_t *)(eng->a.rngpos + 2 * (size_t)first);
+    uint8_t *b = (uint8_t *)d_buf;
+    const size_t rb = (size_t)n * zc::kRingWords * sizeof(uint32_t), pb = (size_t)n * 2 * sizeof(uint64_t);
+    ZC_HIP(hipMemcpyAsync(restore ? ring : b, restore ? b : ring, rb, hipMemcpyDeviceToDevice, s));
+    ZC_HIP(hipMemcpyAsync(restore ? pos : b + rb, restore ? b + rb : pos, pb, hipMemcpyDeviceToDevice, s));
+    return ZC_OK;
+}
+
 int zc_debug_phase_cycles_games(zc_engine *eng, int32_t n_games, int64_t *out) {
     if (!eng || !out) return fail(ZC_EINVAL, "null argument");
     if (n_games < 0 || n_games > eng->cfg.max_games) return fail(ZC_EINVAL, "n_games outside the engine");

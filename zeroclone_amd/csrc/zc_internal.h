@@ -101,6 +101,10 @@ struct SearchParams {
     // ticket[1] = the most moves any game played
     int32_t *ticket;
     int32_t budget;
+    // walk diagnostic (c4_walk_kernel): per game the rollout value of every simulation
+    // [G][sims] and the rollout words of every flush [G][ceil(sims / bs)]
+    int8_t *walk_vals;
+    uint32_t *walk_words;
 };
 
 struct ExtParams {
@@ -350,6 +354,7 @@ void launch_c4_ext_end(const ExtParams &p, hipStream_t s);
 void launch_c4_hp_walk(const ExtParams &p, hipStream_t s);
 void launch_c4_hp_expand(const ExtParams &p, hipStream_t s);
 void launch_c4_search(const SearchParams &p, hipStream_t s);
+void launch_c4_walk(const SearchParams &p, int mode, hipStream_t s);   // diagnostic: 1 record, 2 replay
 void launch_c4_selfplay(const SearchParams &p, hipStream_t s);
 int c4_selfplay_resident_games(int bs, int philox, int *out);  // games the self-play grid keeps resident
 void launch_c4_rollout_debug(const Arena &a, int M, int first_game, int n, const zc_c4_state *states,

@@ -100,6 +100,12 @@ class Trajectories:
         self.start(None)
 
     def _alloc_pool(self, games_cap: int, pool_cap: int):
+        if getattr(self, "pinned", False):
+            # a captured step graph has this pool's pointers baked into its record kernel:
+            # replacing the buffers would leave the graph writing into freed memory
+            raise RuntimeError(f"the trajectory pool ({self.games_cap} games, {self.pool_cap} positions) is held by "
+                               f"a captured step graph and cannot grow to ({games_cap}, {pool_cap}); construct the "
+                               "self-play pool with a larger games_cap before capture_step()")
         self.games_cap, self.pool_cap = int(games_cap), int(pool_cap)
         self.pool = torch.zeros((self.pool_cap, self.W), dtype=torch.int64, device=self.dev)
         self.labels = torch.zeros(self.pool_cap, dtype=torch.int32, device=self.dev)
@@ -347,6 +353,8 @@ class C4SelfPlay:
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
             self.step()
+        if self.traj is not None:
+            self.traj.pinned = True   # the graph holds the pool's buffers from now on
         return g
 
     def step_finish(self, stream: int | None = None) -> torch.Tensor:
@@ -517,6 +525,8 @@ class ChessSelfPlay:
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
             self.step()
+        if self.traj is not None:
+            self.traj.pinned = True   # the graph holds the pool's buffers from now on
         return g
 
     def _run_buffers(self, moves: int):
