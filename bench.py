@@ -98,10 +98,10 @@ def c4_row_board(row) -> tuple[str, int]:
     return "".join(cells), t & 1
 
 
-def pool_snapshot(sp, n: int = 1024) -> dict:
+def pool_snapshot(sp, n: int = 1 << 30) -> dict:
     """The burned-in pool's state at the timed window's start, for the like-for-like CPU
-    baseline: n games spread over the pool (every G/n-th slot), their positions and their
-    MT19937 states."""
+    baseline: up to n games spread over the pool (every G/n-th slot; default all), their
+    positions and their MT19937 states."""
     import oracle
     step = max(1, sp.G // n)
     idx = list(range(0, sp.G, step))[:n]
@@ -119,40 +119,42 @@ def pool_snapshot(sp, n: int = 1024) -> dict:
     return {"boards": boards, "turns": turns, "mts": mts, "slots": idx}
 
 
-def cpu_baseline(sims: int, bs: int, c: float, snap: dict, budget_s: float = 15.0):
+def cpu_baseline(sims: int, bs: int, c: float, snap: dict, moves: int, budget_s: float = 20.0):
     """The oracle port (oracle/c4_oracle.c, bit-exact to the reference's get_move on the
-    committed fixtures) on the SAME workload as the GPU window: games taken from the
-    burned-in pool's snapshot (mixed ages, their own MT19937 states), each playing
-    consecutive self-play moves (search, play, evaluate, refill) — one game per pthread task
-    across the host's CPU share.  Expansions are counted as the GPU counts them (nodes
-    created)."""
+    committed fixtures) on the SAME workload as the GPU window: the burned-in pool's games
+    from the snapshot taken before the timed steps (mixed ages, their own MT19937 states),
+    each playing the window's `moves` consecutive self-play moves (search, play, evaluate,
+    refill) — the lockstep schedule of the same window, one game per pthread task across the
+    host's CPU share.  A calibration round sizes the sample to about `budget_s` of CPU work:
+    every game while that fits, else an evenly spread subset.  Expansions are counted as the
+    GPU counts them (nodes created)."""
     import copy
     import oracle
     hc = host_cpus()
     threads = hc["threads"]
     boards, turns, mts = snap["boards"], snap["turns"], snap["mts"]
-    n0 = min(len(boards), threads)
+    G = len(boards)
+    probe = list(range(0, G, max(1, G // (4 * threads))))[: 4 * threads]
     t = time.perf_counter()
-    e0 = oracle.selfplay_batch(boards[:n0], turns[:n0], [copy.deepcopy(m) for m in mts[:n0]], 1, sims, c, bs,
-                               threads=threads)
-    rate0 = float(e0.sum()) / max(time.perf_counter() - t, 1e-6)
-    per_move = float(e0.sum()) / n0
-    moves = 4
-    n = int(min(len(boards), max(threads, rate0 * budget_s / (per_move * moves))))
-    n = max(min(threads, len(boards)), (n // threads) * threads)
-    ms = [copy.deepcopy(m) for m in mts[:n]]
+    e0 = oracle.selfplay_batch([boards[i] for i in probe], [turns[i] for i in probe],
+                               [copy.deepcopy(mts[i]) for i in probe], 1, sims, c, bs, threads=threads)
+    per_game_move_s = (time.perf_counter() - t) / len(probe) * threads
+    n = int(min(G, max(threads, budget_s * threads / (per_game_move_s * moves))))
+    idx = list(range(G)) if n >= G else [int(i * G / n) for i in range(n)]
     t = time.perf_counter()
-    exp = oracle.selfplay_batch(boards[:n], turns[:n], ms, moves, sims, c, bs, threads=threads)
+    exp = oracle.selfplay_batch([boards[i] for i in idx], [turns[i] for i in idx], [copy.deepcopy(mts[i]) for i in idx],
+                                moves, sims, c, bs, threads=threads)
     dt = time.perf_counter() - t
-    ages = [sum(ch != "." for ch in b) for b in boards[:n]]
+    ages = [sum(ch != "." for ch in boards[i]) for i in idx]
     return {"value": round(float(exp.sum()) / dt, 1), "unit": "expansions/s", "cores": threads, "kind": "port",
             "nproc": hc["nproc"], "cpu_model": hc["cpu_model"], "threads_why": hc["why"],
             "port": "oracle/c4_oracle.c: C restatement pinned bit-exact to the reference's own get_move outputs "
                     "(tests/golden/c4_get_move.json, 150 cases incl. 800 sims) and rollouts",
-            "sample": f"{n} games of the burned-in GPU pool's snapshot (the timed window's mixed-age roots, plies "
-                      f"{min(ages)}-{max(ages)}, and their own MT19937 states) x {moves} consecutive self-play moves "
-                      f"each (search, play, evaluate, refill), {sims} sims, batch {bs}; expansions counted as nodes "
-                      f"created; {threads} pthreads, {dt:.1f}s"}
+            "sample": f"{len(idx)} of the {G} games of the burned-in GPU pool's snapshot before the timed window "
+                      f"(mixed ages: {min(ages)}-{max(ages)} stones, their own MT19937 states) x the window's {moves} "
+                      f"consecutive self-play moves each (search, play, evaluate, refill: the lockstep schedule), "
+                      f"{sims} sims, batch {bs}; {int(exp.sum())} expansions counted as nodes created; {threads} "
+                      f"pthreads, {dt:.1f}s (calibration: {len(probe)} games x 1 move, {e0.sum()} expansions)"}
 
 
 def cpu_baseline_chess(sims: int = 400, bs: int = 32, c: float = 1.4, budget_s: float = 10.0):
@@ -684,7 +686,7 @@ def run_rank(args, rank: int, world: int, local: int):
             crude_pool.close()
             out["extra"]["net_tower"] = tower_mode(dev)
         if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(S, B, args.c, snap)
+            out["cpu_baseline"] = cpu_baseline(S, B, args.c, snap, args.steps)
             if args.net_steps > 0:
                 out["extra"]["c4_chess"]["crude"]["cpu_baseline"] = cpu_baseline_chess()
                 out["extra"]["c2_value_net"]["cpu_baseline"] = cpu_baseline_c4_net(S, B, args.c)

@@ -31,4 +31,7 @@ r = bench.run_steps(sp, a.steps, warmup=0, launch=a.launch)
 print(f"steps {a.steps}: {r['expansions'] / r['dt'] / 1e9:.4f} G expansions/s, "
       f"launch ms {r['launch_ms']:.3f} ({r['launch_ms'] / a.steps:.3f} per move), "
       f"depth {r['depth_sum'] / max(r['expansions'], 1):.3f}", flush=True)
+import json  # noqa: E402
+print(json.dumps({"expansions": r["expansions"], "depth_sum": r["depth_sum"], "moves": r["moves"],
+                  "launch_ms": r["launch_ms"], "lib_sha256": bench.lib_sha()}), flush=True)
 sp.close()

@@ -41,6 +41,7 @@ def main():
     burn = bench.burn_in(sp)
     out = bench.walk_measure(sp, a.reps)
     out["burn_in_steps"] = burn
+    out["lib_sha256"] = bench.lib_sha()   # the library this run loaded (stamps the profile summary)
     print(json.dumps(out), flush=True)
     sp.close()
 

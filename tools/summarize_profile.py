@@ -76,6 +76,8 @@ def main():
         with open(a.extra_json) as fh:
             lines = [ln for ln in fh.read().splitlines() if ln.startswith("{")]
         out["run"] = json.loads(lines[-1])
+        if out["run"].get("lib_sha256"):   # the GPU run's own stamp wins over the local file's
+            out["lib_sha256"] = out["run"]["lib_sha256"]
     if a.note:
         out["note"] = a.note
     if a.stats:

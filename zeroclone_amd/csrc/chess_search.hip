@@ -452,7 +452,7 @@ __device__ __forceinline__ void chess_play_errors(const ChessPlayParams &q, int 
         if (err & 1) atomicOr(q.err + 0, 1);
         if (err & 2) atomicOr(q.err + 1, 1);
         if (err & 4) atomicOr(q.err + 2, 1);
-        if (err & 8) atomicOr(q.err + 1, 1);
+        if (err & 8) atomicOr(q.err + 1, 2);   // a position's legal-move list overflowed (bit 1)
     }
 }
 

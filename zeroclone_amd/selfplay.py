@@ -579,6 +579,9 @@ class ChessSelfPlay:
         e = self.err.cpu().tolist()
         if e[0]:
             raise RuntimeError(f"a game exceeded {self.hist_cap} moves per side")
+        if e[1] & 2:
+            raise RuntimeError(f"a played position's legal-move list overflowed {_native.CHESS_MAX_MOVES} moves "
+                               "(the game was not judged)")
         if e[1]:
             raise RuntimeError("chess search exceeded the tree's child-slot pool or depth limit")
         if e[2]:
