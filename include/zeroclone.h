@@ -137,7 +137,11 @@ int zc_c4_selfplay_pooled_async(zc_engine *eng, int32_t first_game, int32_t n_ga
 
 /* The most games zc_c4_selfplay_pooled_async accepts at this batch size: the games the
  * self-play grid keeps resident on the device at once (occupancy x compute units).  A pooled
- * launch hands out its budget only to resident waves, so larger launches are refused. */
+ * launch hands out its budget only to resident waves, so larger launches are refused.  The
+ * count assumes the launch has the device to itself: beside other resident kernels (another
+ * process on the GPU, concurrent streams) some workgroups may start only after the budget is
+ * spent, and their games then play no move in that launch (each game's moves stay exact;
+ * only the share of moves per game changes). */
 int zc_c4_pooled_max_games(zc_engine *eng, int32_t batch_size, int32_t *out);
 
 /* Random source of the Connect4 search's rollouts (all zc_c4_search* calls that follow):

@@ -655,68 +655,6 @@ __device__ __forceinline__ void tower_mfma(const _Float16 *lds, int src, const _
     }
 }
 
-#ifndef ZC_TOWER_AHEAD
-#define ZC_TOWER_AHEAD 1   // weight fragments streamed 1 or 2 taps ahead of their MFMAs
-#endif
-// tower_mfma with the weights two taps ahead: a[p][kc] holds tap t's fragment kc for t of
-// parity p; on entry a[0] = tap 0, a[1] = tap 1; on exit (KCN == KC) a[1] = the next layer's
-// tap 0 and a[0] its tap 1 (the caller swaps), otherwise both reloaded after the loop.
-template <int H, int W, int NT, int KC, int KCN>
-__device__ __forceinline__ void tower_mfma2(const _Float16 *lds, int src, const _Float16 *wa, const _Float16 *wn,
-                                            h8 (&a)[2][8], const int (&prow)[NT], const int (&pyx)[NT], int hh,
-                                            f16x (&acc)[NT]) {
-    auto rows = [&](int tap, const _Float16 *(&xb)[NT]) {
-        const int dy = tap / 3 - 1, dx = tap % 3 - 1;
-#pragma unroll
-        for (int t = 0; t < NT; ++t) {
-            const int sy = (pyx[t] >> 8) + dy, sx = (pyx[t] & 255) + dx;
-            const bool sv = (unsigned)sy < (unsigned)H && (unsigned)sx < (unsigned)W;
-            const int row = prow[t] + dy * W + dx;
-            xb[t] = lds + (sv ? src + row : tower_zero<NT>() + (row & 15)) * kTowerLD + hh * 8;
-        }
-    };
-    const _Float16 *xb[NT];
-    rows(0, xb);
-    h8 x[NT], xn[NT];
-#pragma unroll
-    for (int t = 0; t < NT; ++t) x[t] = *(const h8 *)(xb[t]);
-#pragma unroll
-    for (int tap = 0; tap < 9; ++tap) {
-        const _Float16 *xbn[NT];
-        if (tap + 1 < 9) rows(tap + 1, xbn);
-#pragma unroll
-        for (int kc = 0; kc < KC; ++kc) {
-            if (kc + 1 < KC) {
-#pragma unroll
-                for (int t = 0; t < NT; ++t) xn[t] = *(const h8 *)(xb[t] + (kc + 1) * 16);
-            } else if (tap + 1 < 9) {
-#pragma unroll
-                for (int t = 0; t < NT; ++t) xn[t] = *(const h8 *)(xbn[t]);
-            }
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int t = 0; t < NT; ++t)
-                acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[tap & 1][kc], x[t], acc[t], 0, 0, 0);
-            __builtin_amdgcn_sched_barrier(0);
-            if (tap + 2 < 9) a[tap & 1][kc] = *(const h8 *)(wa + (size_t)((tap + 2) * KC + kc) * 2048);
-            else if (KCN == KC && wn) a[tap & 1][kc] = *(const h8 *)(wn + (size_t)((tap - 7) * KC + kc) * 2048);
-#pragma unroll
-            for (int t = 0; t < NT; ++t) x[t] = xn[t];
-        }
-        if (tap + 1 < 9) {
-#pragma unroll
-            for (int t = 0; t < NT; ++t) xb[t] = xbn[t];
-        }
-    }
-    if (KCN != KC && wn) {
-#pragma unroll
-        for (int kc = 0; kc < KCN; ++kc) {
-            a[0][kc] = *(const h8 *)(wn + (size_t)kc * 2048);
-            a[1][kc] = *(const h8 *)(wn + (size_t)(KCN + kc) * 2048);
-        }
-    }
-}
-
 // acc + bias (+ the residual already in dst), ReLU, fp16 -> dst rows (the stream form's
 // epilogue arithmetic, per lane: 4 channels x one pixel per store)
 template <int NT>
@@ -762,18 +700,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
     const h8 zero = {0, 0, 0, 0, 0, 0, 0, 0};
     const int r = lane & 31, hh = lane >> 5;
     const _Float16 *const wl0 = wall + (size_t)wave * 512 + lane * 8;  // this wave's fragments, layer 0
-#if ZC_TOWER_AHEAD == 2
-    h8 a2[2][8];
-#pragma unroll
-    for (int kc = 0; kc < KC0; ++kc) {
-        a2[0][kc] = *(const h8 *)(wl0 + (size_t)kc * 2048);
-        a2[1][kc] = *(const h8 *)(wl0 + (size_t)(KC0 + kc) * 2048);
-    }
-#else
     h8 a[8];
 #pragma unroll
     for (int kc = 0; kc < KC0; ++kc) a[kc] = *(const h8 *)(wl0 + (size_t)kc * 2048);
-#endif
     {
         constexpr int C8 = CIN0 / 8;
         const _Float16 *src = in + (size_t)b0 * HW * CIN0;
@@ -819,19 +748,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
         float4 bv[4];  // this wave's bias slice, in flight during the MFMA loop
 #pragma unroll
         for (int g = 0; g < 4; ++g) bv[g] = *(const float4 *)(ball + (size_t)l * kCout + wave * 32 + 8 * g + 4 * hh);
-#if ZC_TOWER_AHEAD == 2
-        tower_mfma2<H, W, NT, KC, 8>(lds, src, wa, wn, a2, pr, py, hh, acc);
-        if (KC == 8) {   // the next layer's tap 0 arrived in a2[1], its tap 1 in a2[0]
-#pragma unroll
-            for (int kc = 0; kc < 8; ++kc) {
-                const h8 tmp = a2[0][kc];
-                a2[0][kc] = a2[1][kc];
-                a2[1][kc] = tmp;
-            }
-        }
-#else
         tower_mfma<H, W, NT, KC, 8>(lds, src, wa, wn, a, pr, py, hh, acc);
-#endif
         tower_epilogue(lds + dst * kTowerLD, bv, l >= 2 && !(l & 1), npix, wave, r, hh, acc);
         __syncthreads();
     };
