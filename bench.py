@@ -134,6 +134,7 @@ def cpu_baseline(sims: int, bs: int, c: float, snap: dict, moves: int, budget_s:
     threads = hc["threads"]
     boards, turns, mts = snap["boards"], snap["turns"], snap["mts"]
     G = len(boards)
+    window = moves
     probe = list(range(0, G, max(1, G // (4 * threads))))[: 4 * threads]
     t = time.perf_counter()
     e0 = oracle.selfplay_batch([boards[i] for i in probe], [turns[i] for i in probe],
@@ -141,6 +142,8 @@ def cpu_baseline(sims: int, bs: int, c: float, snap: dict, moves: int, budget_s:
     per_game_move_s = (time.perf_counter() - t) / len(probe) * threads
     n = int(min(G, max(threads, budget_s * threads / (per_game_move_s * moves))))
     idx = list(range(G)) if n >= G else [int(i * G / n) for i in range(n)]
+    if n >= G:   # the whole window fits the budget: play on past it (more of the same steady state)
+        moves = int(min(4 * moves, max(moves, budget_s * threads / (per_game_move_s * G))))
     t = time.perf_counter()
     exp = oracle.selfplay_batch([boards[i] for i in idx], [turns[i] for i in idx], [copy.deepcopy(mts[i]) for i in idx],
                                 moves, sims, c, bs, threads=threads)
@@ -151,8 +154,9 @@ def cpu_baseline(sims: int, bs: int, c: float, snap: dict, moves: int, budget_s:
             "port": "oracle/c4_oracle.c: C restatement pinned bit-exact to the reference's own get_move outputs "
                     "(tests/golden/c4_get_move.json, 150 cases incl. 800 sims) and rollouts",
             "sample": f"{len(idx)} of the {G} games of the burned-in GPU pool's snapshot before the timed window "
-                      f"(mixed ages: {min(ages)}-{max(ages)} stones, their own MT19937 states) x the window's {moves} "
-                      f"consecutive self-play moves each (search, play, evaluate, refill: the lockstep schedule), "
+                      f"(mixed ages: {min(ages)}-{max(ages)} stones, their own MT19937 states) x {moves} consecutive "
+                      f"self-play moves each (the window's {window} and on; search, play, evaluate, refill: the lockstep "
+                      f"schedule), "
                       f"{sims} sims, batch {bs}; {int(exp.sum())} expansions counted as nodes created; {threads} "
                       f"pthreads, {dt:.1f}s (calibration: {len(probe)} games x 1 move, {e0.sum()} expansions)"}
 
