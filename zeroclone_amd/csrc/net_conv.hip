@@ -592,16 +592,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
 // operations in the same order as the layer-by-layer packed form: bit-identical outputs
 // (tests/test_gpu_net.py).
 constexpr int kTowerLD = kCout + 8;
-// NT pixel MFMA tiles (32 pixels each) per wave and workgroup: buffer rows TP = 32 NT
-template <int NT> constexpr int tower_zero() { return 32 * NT; }             // first zero row
-template <int NT> constexpr int tower_buf1() { return 32 * NT + 16; }        // buf1's first row
-template <int NT> constexpr size_t tower_lds() { return (size_t)(64 * NT + 16) * kTowerLD * sizeof(_Float16); }
+// NT pixel MFMA tiles (32 pixels each) per wave; PG pixel groups of 4 waves per workgroup
+// (the 4 waves of a group split the 128 output channels; the groups split the pixels): buffer
+// rows TP = 32 NT PG.  With PG = 2 the two waves that own the same output channels load the
+// same weight fragments at about the same time, so the second load is served by the CU's
+// vector L1 instead of L2.
+template <int NT, int PG = 1> constexpr int tower_zero() { return 32 * NT * PG; }       // first zero row
+template <int NT, int PG = 1> constexpr int tower_buf1() { return 32 * NT * PG + 16; }  // buf1's first row
+template <int NT, int PG = 1> constexpr size_t tower_lds() {
+    return (size_t)(64 * NT * PG + 16) * kTowerLD * sizeof(_Float16);
+}
 
 // One layer's MFMA loop: acc[t] += sum over taps and k of W * X (X from the LDS buffer at
 // row `src`).  a[0..KC) holds the layer's tap-0 fragments on entry; on exit it holds the
 // next layer's (KCN fragments from wn, when wn != nullptr and KCN == KC: in the ring at the
 // last tap; otherwise loaded after the loop).
-template <int H, int W, int NT, int KC, int KCN>
+template <int H, int W, int NT, int KC, int KCN, int PG = 1>
 __device__ __forceinline__ void tower_mfma(const _Float16 *lds, int src, const _Float16 *wa, const _Float16 *wn,
                                            h8 (&a)[8], const int (&prow)[NT], const int (&pyx)[NT], int hh,
                                            f16x (&acc)[NT]) {
@@ -613,7 +619,7 @@ __device__ __forceinline__ void tower_mfma(const _Float16 *lds, int src, const _
             const int sy = (pyx[t] >> 8) + dy, sx = (pyx[t] & 255) + dx;
             const bool sv = (unsigned)sy < (unsigned)H && (unsigned)sx < (unsigned)W;
             const int row = prow[t] + dy * W + dx;
-            xb[t] = lds + (sv ? src + row : tower_zero<NT>() + (row & 15)) * kTowerLD + hh * 8;
+            xb[t] = lds + (sv ? src + row : tower_zero<NT, PG>() + (row & 15)) * kTowerLD + hh * 8;
         }
     };
     const _Float16 *xb[NT];
@@ -659,10 +665,10 @@ __device__ __forceinline__ void tower_mfma(const _Float16 *lds, int src, const _
 // epilogue arithmetic, per lane: 4 channels x one pixel per store)
 template <int NT>
 __device__ __forceinline__ void tower_epilogue(_Float16 *dst, const float4 (&bv)[4], bool res, int npix, int wave,
-                                               int r, int hh, const f16x (&acc)[NT]) {
+                                               int r, int hh, const f16x (&acc)[NT], int pbase = 0) {
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
-        const int P = t * 32 + r;
+        const int P = pbase + t * 32 + r;
         if (P >= npix) continue;
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
@@ -683,18 +689,20 @@ __device__ __forceinline__ void tower_epilogue(_Float16 *dst, const float4 (&bv)
     }
 }
 
-template <int H, int W, int BPH, int CIN0, int NT, int WPE>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE))) void tower_kernel(
+template <int H, int W, int BPH, int CIN0, int NT, int WPE, int PG = 1>
+__global__ __launch_bounds__(256 * PG) __attribute__((amdgpu_waves_per_eu(WPE, WPE))) void tower_kernel(
     int nboards, int nconv, const _Float16 *__restrict__ in, const _Float16 *__restrict__ wall,
     const float *__restrict__ ball, _Float16 *__restrict__ out, const float *__restrict__ fcw, float fcb,
     double *__restrict__ values) {
     constexpr int HW = H * W;
-    static_assert(BPH * HW <= 32 * NT, "tile too large");
-    constexpr int TP = 32 * NT;
+    static_assert(BPH * HW <= 32 * NT * PG, "tile too large");
+    constexpr int TP = 32 * NT * PG;
+    constexpr int NTH = 256 * PG;   // threads
     constexpr int KC0 = CIN0 / 16;
     constexpr size_t kW0 = (size_t)9 * CIN0 * kCout, kW = (size_t)9 * kCout * kCout;  // halfs per layer
     extern __shared__ __attribute__((aligned(16))) _Float16 lds[];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63, wave = (tid >> 6) & 3, pg = tid >> 8;
+    const int pbase = pg * 32 * NT;   // this wave's first pixel of the tile
     const int b0 = blockIdx.x * BPH;
     const int npix = min(BPH, nboards - b0) * HW;
     const h8 zero = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -707,18 +715,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
         constexpr int C8 = CIN0 / 8;
         const _Float16 *src = in + (size_t)b0 * HW * CIN0;
 #pragma unroll
-        for (int q = 0; q < (TP * C8 + 255) / 256; ++q) {
-            const int i = tid + q * 256, row = i / C8, c8 = i - row * C8;
+        for (int q = 0; q < (TP * C8 + NTH - 1) / NTH; ++q) {
+            const int i = tid + q * NTH, row = i / C8, c8 = i - row * C8;
             if (row >= TP) break;
             const h8 t = *(const h8 *)(src + min(row, npix - 1) * CIN0 + c8 * 8);
-            *(h8 *)(lds + (tower_buf1<NT>() + row) * kTowerLD + c8 * 8) = row < npix ? t : zero;
+            *(h8 *)(lds + (tower_buf1<NT, PG>() + row) * kTowerLD + c8 * 8) = row < npix ? t : zero;
         }
-        for (int z = tid; z < 16 * kTowerLD / 8; z += 256) *(h8 *)(lds + tower_zero<NT>() * kTowerLD + z * 8) = zero;
+        for (int z = tid; z < 16 * kTowerLD / 8; z += NTH)
+            *(h8 *)(lds + tower_zero<NT, PG>() * kTowerLD + z * 8) = zero;
     }
     int prow[NT], pyx[NT];
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
-        const int P = t * 32 + r;
+        const int P = pbase + t * 32 + r;
         const int pb = P / HW, rem = P - pb * HW, py = rem / W;
         prow[t] = P;
         pyx[t] = (P < npix ? py << 8 : 64 << 8) | (rem - py * W);
@@ -742,14 +751,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
         for (int t = 0; t < NT; ++t)
 #pragma unroll
             for (int k = 0; k < 16; ++k) acc[t][k] = 0.0f;
-        const int src = (l & 1) ? 0 : tower_buf1<NT>(), dst = (l & 1) ? tower_buf1<NT>() : 0;
+        const int src = (l & 1) ? 0 : tower_buf1<NT, PG>(), dst = (l & 1) ? tower_buf1<NT, PG>() : 0;
         const _Float16 *const wa = l == 0 ? wl0 : wl0 + kW0 + (size_t)(l - 1) * kW;
         const _Float16 *const wn = l + 1 < nconv ? wl0 + kW0 + (size_t)l * kW : nullptr;  // layer l+1's
         float4 bv[4];  // this wave's bias slice, in flight during the MFMA loop
 #pragma unroll
         for (int g = 0; g < 4; ++g) bv[g] = *(const float4 *)(ball + (size_t)l * kCout + wave * 32 + 8 * g + 4 * hh);
-        tower_mfma<H, W, NT, KC, 8>(lds, src, wa, wn, a, pr, py, hh, acc);
-        tower_epilogue(lds + dst * kTowerLD, bv, l >= 2 && !(l & 1), npix, wave, r, hh, acc);
+        tower_mfma<H, W, NT, KC, 8, PG>(lds, src, wa, wn, a, pr, py, hh, acc);
+        tower_epilogue(lds + dst * kTowerLD, bv, l >= 2 && !(l & 1), npix, wave, r, hh, acc, pbase);
         __syncthreads();
     };
     layer(0, std::integral_constant<int, KC0>{});
@@ -759,7 +768,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
         // the value head on it, one wave per board: value_head_kernel's arithmetic in its
         // order (lane l sums channels 8 (l & 15) .. +8 over pixels l / 16, +4, ...), from LDS
         const int c0 = (lane & 15) * 8;
-        for (int bi = wave; bi < npix / HW; bi += 4) {
+        for (int bi = wave + 4 * pg; bi < npix / HW; bi += 4 * PG) {
             const _Float16 *act = lds + bi * HW * kTowerLD + c0;
             float sum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
             for (int p = lane >> 4; p < HW; p += 4) {
@@ -781,18 +790,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
     }
     if (out) {  // -> HBM, whole 256-byte rows
 #pragma unroll
-        for (int q = 0; q < TP * (kCout / 8) / 256; ++q) {
-            const int i = tid + q * 256, P = i >> 4, c0 = (i & 15) * 8;
+        for (int q = 0; q < TP * (kCout / 8) / NTH; ++q) {
+            const int i = tid + q * NTH, P = i >> 4, c0 = (i & 15) * 8;
             if (P < npix) *(h8 *)(out + ((size_t)b0 * HW + P) * kCout + c0) = *(const h8 *)(lds + P * kTowerLD + c0);
         }
     }
 }
 
-template <int H, int W, int BPH, int NT, int WPE>
+template <int H, int W, int BPH, int NT, int WPE, int PG = 1>
 void launch_tower(int n, int nconv, const void *in, const void *wall, const float *ball, void *out, const float *fcw,
                   float fcb, double *values, hipStream_t s) {
-    hipLaunchKernelGGL((tower_kernel<H, W, BPH, 32, NT, WPE>), dim3((n + BPH - 1) / BPH), dim3(256), tower_lds<NT>(), s,
-                       n, nconv, (const _Float16 *)in, (const _Float16 *)wall, ball, (_Float16 *)out, fcw, fcb, values);
+    hipLaunchKernelGGL((tower_kernel<H, W, BPH, 32, NT, WPE, PG>), dim3((n + BPH - 1) / BPH), dim3(256 * PG),
+                       (tower_lds<NT, PG>()), s, n, nconv, (const _Float16 *)in, (const _Float16 *)wall, ball,
+                       (_Float16 *)out, fcw, fcb, values);
 }
 
 // [9][kCout][cin] -> the stream form's fragments: packed[((tap * KC + kc) * 4 + mb) * 512 +
@@ -928,8 +938,16 @@ bool launch_net_tower(int n, int h, int w, int cin0, int nconv, const void *in, 
     if (cin0 != 32 || nconv < 1 || !(nconv & 1)) return false;
     // 128-pixel tiles at two workgroups per CU; 64-pixel tiles (one chess board) at 3 or 4
     // workgroups per CU measured 10 % slower (tools/ab_tower.py)
+#ifndef ZC_TOWER_PG
+#define ZC_TOWER_PG 1
+#endif
+#if ZC_TOWER_PG == 2
+    if (h == 8 && w == 8) launch_tower<8, 8, 4, 4, 2, 2>(n, nconv, in, wall, ball, out, fcw, fcb, values, s);
+    else if (h == 6 && w == 7) launch_tower<6, 7, 6, 4, 2, 2>(n, nconv, in, wall, ball, out, fcw, fcb, values, s);
+#else
     if (h == 8 && w == 8) launch_tower<8, 8, 2, 4, 2>(n, nconv, in, wall, ball, out, fcw, fcb, values, s);
     else if (h == 6 && w == 7) launch_tower<6, 7, 3, 4, 2>(n, nconv, in, wall, ball, out, fcw, fcb, values, s);
+#endif
     else return false;
     return true;
 }
