@@ -276,6 +276,16 @@ def chess_draw(s: ZccState) -> bool:
     return bool(_chess_lib().zcc_check_draw(ctypes.byref(s)))
 
 
+def chess_rollout(s: ZccState, mt: "MT"):
+    """Value('random_rollout') on the chess rules from s on the stream mt (advanced):
+    (value, plies); value 2 = a history outgrew the restatement's ZCC_HIST."""
+    L = _chess_lib()
+    L.zcc_rollout.argtypes = [ctypes.POINTER(ZccState), ctypes.c_void_p, ctypes.POINTER(ctypes.c_int)]
+    q = ctypes.c_int(0)
+    v = L.zcc_rollout(ctypes.byref(s), ctypes.cast(ctypes.byref(mt.s), ctypes.c_void_p), ctypes.byref(q))
+    return v, q.value
+
+
 def chess_tensor(s: ZccState):
     import numpy as np
     out = np.zeros(17 * 64, np.float32)

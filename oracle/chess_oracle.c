@@ -531,3 +531,38 @@ int zcc_get_move(const zcc_light *root, void *rv, int sims, double c, int bs, in
     free(P);
     return best;
 }
+
+/* Value('random_rollout') (value_functions.py:35-45) with the chess backend, on the CPython
+ * MT19937 stream r (a zco_mt*): while not check_win and not check_draw, play
+ * random.choice(list(get_legal_moves(state))).  Returns -1 when the side to move at the end
+ * (checkmated) is the start's side to move, +1 for the other side's checkmate, 0 for a draw;
+ * 2 when a history outgrew ZCC_HIST (the restatement's limit).  *plies = moves played. */
+int zcc_rollout(const zcc_state *start, void *rv, int *plies) {
+    zco_mt *r = (zco_mt *)rv;
+    zcc_state *s = (zcc_state *)malloc(sizeof(zcc_state));
+    memcpy(s, start, sizeof *s);
+    const int t0 = s->turn;
+    zcc_move m[ZCC_MAX_MOVES];
+    int q = 0, out;
+    for (;;) {
+        if (zcc_check_win(s)) {
+            out = s->turn == t0 ? -1 : 1;
+            break;
+        }
+        if (zcc_check_draw(s)) {
+            out = 0;
+            break;
+        }
+        const int n = zcc_legal_moves(s, m);
+        const zcc_move mv = m[zco_randbelow(r, (uint32_t)n)];
+        zcc_play(s, &mv, s);
+        ++q;
+        if (s->overflow) {
+            out = 2;
+            break;
+        }
+    }
+    if (plies) *plies = q;
+    free(s);
+    return out;
+}

@@ -53,6 +53,10 @@ typedef void (*zcc_value_fn)(void *ctx, int n, const zcc_light *leaves, double *
 int      zcc_get_move(const zcc_light *root, void *r, int sims, double c, int bs, int policy, double freedom,
                       zcc_value_fn vfn, void *ctx, int *root_na, zcc_move *root_moves, int *n_root);
 
+/* Value('random_rollout') (value_functions.py:35-45) on the chess rules, stream r (zco_mt*):
+ * -1 / +1 / 0 for the start's side to move, 2 if a history outgrew ZCC_HIST; *plies played. */
+int      zcc_rollout(const zcc_state *s, void *r, int *plies);
+
 #ifdef __cplusplus
 }
 #endif

@@ -113,3 +113,20 @@ def test_oracle_selfplay_batch_is_get_move_play_refill():
             if oracle.check_win(bb, tt) or oracle.check_draw(bb):
                 bb, tt = "." * 42, 0
         assert m.state() == mts[g].state()
+
+
+def test_oracle_chess_rollout_is_pinned_to_the_reference():
+    """oracle.chess_rollout (chess_oracle.c: zcc_rollout) reproduces every rollout value and
+    ply count of the reference's Value('random_rollout') on its chess backend
+    (tests/golden/fallback_get_move.json, chess_rollouts) and the stream afterwards."""
+    import json
+    import os
+    fx = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "fallback_get_move.json")))
+    n = 0
+    for case in fx["chess_rollouts"]:
+        mt = oracle.MT(case["seed"])
+        for e, v, q in zip(case["states"], case["values"], case["plies"]):
+            assert oracle.chess_rollout(oracle.chess_from_json(e), mt) == (v, q)
+            n += 1
+        assert mt.u32() == case["next_word"]
+    assert n >= 30

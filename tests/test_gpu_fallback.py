@@ -167,3 +167,32 @@ def test_chess_rollouts_fill_history_capacity_loudly():
     st.hist_white = [((6, 0, 5, 0), 0.0)] * (_native.CHESS_ROLL_CAP + 1)
     with pytest.raises((RuntimeError, ValueError)):
         Value("random_rollout").batch([st], backend=cb)
+
+
+@pytest.mark.parametrize("game", ["connect4", "chess"])
+def test_engine_per_game_streams_with_random_drawing_values(game):
+    """Engine's per-game streams (seed + idx): a host value that draws from
+    `random` is handed game i's own stream inside the batched search, so game i's move equals
+    get_move's with Python's random seeded seed + i — and Python's global stream is left
+    where it was."""
+    from zeroclone_amd.engine import Engine
+    backend = c4 if game == "connect4" else cb
+    value = FV.NoisyValue() if game == "connect4" else FV.HistoryValue()
+    cfg = {"game": game, "backend": "c4_backend" if game == "connect4" else "chess_backend",
+           "value_function": "random_rollout", "threads": 3, "seed": 500, "mcts": {"simulations": 48, "c_puct": 1.4}}
+    eng = Engine(cfg, value_functions=[value, value])
+    if game == "chess":   # distinct roots with histories
+        for i, line in enumerate([[0], [0, 5], [3, 1, 2]]):
+            for k in line:
+                eng.play_move(eng.legal_moves(i)[k], i)
+    roots = [eng.get_state(i) for i in range(3)]
+    random.seed(99)
+    ref = random.Random(99)
+    eng.play_mcts_parallel([0, 1, 2], 48, 1.4, batch_size=8)
+    assert random.random() == ref.random()   # the global stream untouched
+    for i in range(3):
+        random.seed(500 + i)
+        mv = mcts.get_move(roots[i], value, Policy("random"), backend, 48, 1.4, 8)
+        exp = backend.play_move(roots[i], mv)
+        got = eng.get_state(i)
+        assert list(got.board) == list(exp.board) and got.turn == exp.turn, (game, i)
