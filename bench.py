@@ -446,6 +446,43 @@ def puct_mode(src, steps: int, dev) -> dict:
             "net_tflops_lower": round(fl / dt / 1e12, 1), "mfma_frac_lower": round(fl / dt / 1e12 / MFMA_F16_PEAK_TFLOPS, 4)}
 
 
+def c1_mode(dev, sims: int = 100, games: int = 4) -> dict:
+    """BASELINE configs[0] (C1, plumbing): configs/connect4.yaml through the reference's own
+    API — Engine(config).play_mcts(0, 100 sims) move after move until the game ends, 1 game —
+    on the GPU (the package runs no search on the CPU), beside the C port playing the same
+    games on one host thread.  Expansions per move = the sims (every simulation from a
+    non-terminal position expands until the tree holds the whole game)."""
+    import oracle
+    from zeroclone_amd.engine import Engine
+    cfg = os.path.join(HERE, "configs", "connect4.yaml")
+    moves = 0
+    t = time.perf_counter()
+    for g in range(games):
+        e = Engine(cfg)
+        e.seed = 1000 + g
+        while e.play_mcts(0, sims) is None:
+            moves += 1
+        moves += 1
+    dt = time.perf_counter() - t
+    tc = time.perf_counter()
+    cmoves = 0
+    for g in range(games):
+        b, turn, mt = "." * 42, 0, oracle.MT(1000 + g)
+        while True:
+            col, _, _ = oracle.get_move_mt(b, turn, mt, sims, 1.4, 32)
+            b, turn = oracle.play(b, turn, col)
+            cmoves += 1
+            if oracle.check_win(b, turn) or oracle.check_draw(b):
+                break
+    dtc = time.perf_counter() - tc
+    return {"value": round(moves * sims / dt, 1), "unit": "simulations/s", "moves": moves, "games": games,
+            "ms_per_move": round(dt / moves * 1e3, 2),
+            "config": f"configs/connect4.yaml via Engine.play_mcts, 1 game at a time, {sims} sims/move, random_rollout, "
+                      "whole games (host round trip per move: the reference's API, not a batched launch)",
+            "cpu_baseline": {"value": round(cmoves * sims / dtc, 1), "unit": "simulations/s", "cores": 1, "kind": "port",
+                             "sample": f"the same {games} games' moves on oracle/c4_oracle.c, one thread, {dtc:.2f}s"}}
+
+
 def philox_mode(sp, args) -> dict:
     """C2(ii): the same self-play steps with ZC_ROLLOUT_PHILOX (leaf-parallel rollouts on
     per-leaf Philox-seeded streams; statistical parity, tests/test_gpu_philox.py)."""
@@ -689,6 +726,7 @@ def run_rank(args, rank: int, world: int, local: int):
             out["extra"]["c5_chess_puct"] = puct_mode(crude_pool, args.net_steps, dev)
             crude_pool.close()
             out["extra"]["net_tower"] = tower_mode(dev)
+            out["extra"]["c1_engine"] = c1_mode(dev)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(S, B, args.c, snap, args.steps)
             if args.net_steps > 0:

@@ -517,6 +517,16 @@ int zc_net_conv3x3_packed_async(int32_t n_boards, int32_t h, int32_t w, int32_t 
 int zc_net_tower_async(int32_t n_boards, int32_t h, int32_t w, int32_t cin0, int32_t nconv, const void *d_in,
                        const void *d_packed_weights, const float *d_biases, void *d_out, const float *d_fc_w,
                        float fc_b, double *d_values, void *hip_stream);
+/* zc_net_tower_policy_async: zc_net_tower_async with the policy head's 1x1 convolution (128 -> 32
+ *   channels, BN folded, ReLU) folded into the same launch as an MFMA epilogue on the on-chip
+ *   tower output (the PUCT network of SURVEY §8 a21 / config C5, which has no reference
+ *   counterpart): d_pw = the 1x1 weights packed as MFMA A fragments
+ *   [8][64][8] fp16 (nets.pack_policy_1x1), d_pb = [32] f32, d_pout = [n][h*w][32] fp16 (8-byte
+ *   aligned) — the policy head's flatten + linear is then one GEMM over d_pout.  The value head
+ *   (d_fc_w, fc_b, d_values) is required; no tower activation is written. */
+int zc_net_tower_policy_async(int32_t n_boards, int32_t h, int32_t w, int32_t cin0, int32_t nconv, const void *d_in,
+                              const void *d_packed_weights, const float *d_biases, const float *d_fc_w, float fc_b,
+                              double *d_values, const void *d_pw, const float *d_pb, void *d_pout, void *hip_stream);
 int zc_net_planes_to_nhwc_async(int32_t n, int32_t cin, int32_t hw, int32_t cpad, const void *d_planes, void *d_out,
                                 void *hip_stream);
 int zc_net_value_head_async(int32_t n, int32_t hw, const void *d_act, const float *d_fc_w, float fc_b, double *d_values,

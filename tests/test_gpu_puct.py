@@ -105,6 +105,37 @@ def test_policy_value_network_mfma_matches_torch():
     np.testing.assert_allclose(l.float().cpu().numpy(), l_ref.numpy(), atol=5e-2, rtol=2e-2)
 
 
+@pytest.mark.parametrize("shape", [(37, 17, 8, 8, 4096), (53, 2, 6, 7, 7)])
+def test_fused_policy_conv_matches_fp32(shape):
+    """The policy 1x1 conv fused into the tower launch (zc_net_tower_policy_async) against a
+    torch fp32 1x1 conv + bias + ReLU of the SAME tower activation (written by the unfused
+    launch): within fp16 output rounding (tolerance 1e-2 abs + 1e-2 rel; the fp32 MFMA sums
+    128 products in another order); values bit-identical to the unfused launch; logits of
+    both paths within 2e-2.  Ragged last tiles (37 / 53 boards)."""
+    from zeroclone_amd.nets import MfmaPolicyValueNetwork, PolicyValueNetwork, _fold
+    n, cin, h, w, nl = shape
+    torch.manual_seed(5)
+    net = PolicyValueNetwork(in_planes=cin, board=(h, w), n_logits=nl).eval()
+    for m in net.modules():
+        if isinstance(m, torch.nn.BatchNorm2d):
+            m.running_mean.uniform_(-0.1, 0.1)
+            m.running_var.uniform_(0.5, 1.5)
+    mnet = MfmaPolicyValueNetwork(net)
+    assert mnet.fused
+    x = ((torch.rand(n, cin, h, w) < 0.3).half()).cuda()
+    v_f, l_f = mnet(x)
+    p_f = mnet._pout[(n, h * w)].float().clone()
+    v_u, l_u = mnet(x, fused=False)
+    a, _ = mnet.tower.tower(x, head=False)
+    folded = _fold(net.policy[0], net.policy[1])
+    wf = folded.weight.detach().float().reshape(32, -1).cuda()
+    p_ref = torch.relu(a.float() @ wf.t() + folded.bias.detach().float().cuda())
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(p_f.cpu().numpy(), p_ref.cpu().numpy(), atol=1e-2, rtol=1e-2)
+    assert torch.equal(v_f, v_u)
+    np.testing.assert_allclose(l_f.float().cpu().numpy(), l_u.float().cpu().numpy(), atol=2e-2, rtol=1e-2)
+
+
 def test_puct_with_the_network_end_to_end(eng):
     from zeroclone_amd.nets import MfmaPolicyValueNetwork, PolicyValueNetwork
     from zeroclone_amd.valued import ChessPuctSearch

@@ -106,6 +106,9 @@ __device__ __forceinline__ uint32_t ff1(uint64_t m) {
 // Work is placed for the scalar unit's sake: the boards are uniform values kept in VGPRs,
 // lane conditions are single compares whose ballots are used as v_cndmask masks, and the
 // scalar unit only handles the masks, the block's end and the loop control.
+#ifndef ZC_RV
+#define ZC_RV 0  // experiment switches (tools/rv_libs.sh); 0 = the product kernel
+#endif
 #ifndef ZC_RSTAMP
 #define ZC_RSTAMP 0  // diagnostic build: 1..6 = accumulate one rollout region's cycles into *sub
 #endif
@@ -223,6 +226,7 @@ __device__ void c4_rollouts(Leaf *L, int nb, R &rng, const uint32_t *s_order, Co
                 const uint64_t G = A & F & __ballot(qk < cap_r);
                 // the first fill, with room for more plies: re-draw the words after it under
                 // the new legal set
+#if !(ZC_RV & 1)
                 uint32_t lf = 64u;  // lane of the absorbed fill (64: none)
                 uint32_t cf = 0;
                 RMARK(3);
@@ -266,6 +270,67 @@ __device__ void c4_rollouts(Leaf *L, int nb, R &rng, const uint32_t *s_order, Co
                 // back to word order: the accepted lane of ply qk won if its compacted lane did
                 const uint32_t W32 = (uint32_t)W | (uint32_t)(W >> 32);
                 const uint64_t Ew = A & __ballot(((W32 >> (c & 31u)) & 1u) != 0u);
+#else
+                uint32_t lf = 64u;  // lane of the absorbed fill (64: none)
+                uint32_t cf = 0;
+                // compact EVERY accepted word's ply by parity: ply q < 32 to lane (q & 1)*16 + q/2
+                // (a forward lane permute; the other lanes, and plies >= 32, land in lanes 32..63),
+                // then copy lanes 0..31 up over lanes 32..63.  No ply past the block's last one (at
+                // lane l0) needs masking: each row's plies ascend along its lanes, so a later ply's
+                // stones only reach its own prefix, and its win can only show up in a word lane
+                // beyond l0 (the end is min(first win, l0) below).  Returns the accepted word lanes
+                // whose ply completed four; mine_ = each row's stones so far.
+                auto win_test = [&](uint64_t A_, uint32_t qk_, uint32_t col_, uint32_t row_, uint64_t &mine_) {
+                    const uint32_t c = ((qk_ & 1u) << 4) | ((qk_ >> 1) & 15u) | (qk_ & 32u);
+                    const uint32_t b = __umul24(col_, 7u) + row_;  // the ply's cell (a 24-bit mad, not a 64-bit one)
+                    const uint32_t pl = (uint32_t)__builtin_amdgcn_ds_permute((int)(mask_sel(A_, 63u, c) << 2), (int)b);
+                    const uint32_t pb = __builtin_amdgcn_permlane32_swap(pl, pl, false, false)[0];
+                    const uint64_t bit = 1ull << (pb & 63u);
+                    uint32_t blo = (uint32_t)bit, bhi = (uint32_t)(bit >> 32);
+                    scan_or16x2(blo, bhi);
+                    mine_ = ((uint64_t)bhi << 32) | blo;  // this row's stones so far
+                    const uint64_t bd = (first_row ? me : op) | mine_;
+                    const uint64_t m1 = bd & (bd >> d1), m2 = bd & (bd >> d2);
+                    const uint64_t f4 = (m1 & (m1 >> (2 * d1))) | (m2 & (m2 >> (2 * d2)));
+                    const uint64_t W = __ballot(f4 != 0ull);
+                    // back to word order: the accepted lane of ply qk won if its compacted lane did
+                    const uint32_t W32 = (uint32_t)W | (uint32_t)(W >> 32);
+                    return A_ & __ballot(((W32 >> (c & 31u)) & 1u) != 0u);
+                };
+                // ZC_RV & 1 (experiment): an absorbed fill's first segment (plies through the fill,
+                // the same before and after the re-draw) is win-tested on the pre-re-draw plies,
+                // independent of the re-draw, so the two chains can overlap; a win there ends the
+                // block without the second test
+                uint64_t Ew1 = 0, mine1 = 0;
+                RMARK(3);
+                if (ff1(G) == l0) {  // a fill with room for more plies
+                    lf = l0;
+                    cf = (uint32_t)__builtin_amdgcn_readlane((int)col, (int)lf);
+                    const uint32_t ow2 = (uint32_t)__builtin_amdgcn_readlane((int)owp, (int)(8u * cf));
+                    const uint32_t n2 = (ow2 >> 24) & 15u;
+                    const uint32_t v2 = wv >> __clz(n2);
+                    const uint64_t low = (2ull << lf) - 1ull;  // lanes 0..lf
+                    if (ZC_RV & 1) Ew1 = win_test(A, qk, col, row, mine1) & low;
+                    A = (A & low) | (__ballot(v2 < n2) & ~low);
+                    qk = mbcnt(A);
+                    col = mask_sel(low, (ow2 >> (3 * v2)) & 7u, col);  // lanes after lf: the new order
+                    one = mask_sel0(A, 1u << (4 * col));
+                    sc = scan_add32(one);
+                    row = ((sc - one + hp) >> (4 * col)) & 15u;
+                    nacc = (uint32_t)__popcll(A);
+                    F = __ballot(row == 5u) & ~low;  // the absorbed fill no longer ends the block
+                    E0 = A & (F | __ballot(qk >= min(cap_r, nacc - 1u)));
+                    l0 = (uint32_t)__builtin_ctzll(E0);
+                }
+                RMARK(4);
+                uint64_t mine, Ew;
+                if ((ZC_RV & 1) && Ew1 != 0ull) {  // the win precedes the fill (l0 >= lf after the re-draw)
+                    Ew = Ew1;
+                    mine = mine1;
+                } else {
+                    Ew = win_test(A, qk, col, row, mine);
+                }
+#endif
                 const uint32_t ew = ff1(Ew);
                 const uint32_t endlane = min(ew, l0);
                 const bool win = ew <= l0;  // (ff1 of an empty mask is 0xFFFFFFFF)

@@ -1451,7 +1451,22 @@ int zc_net_tower_async(int32_t n, int32_t h, int32_t w, int32_t cin0, int32_t nc
         return fail(ZC_EINVAL, "bad argument");
     if (!n) return ZC_OK;
     if (!zc::launch_net_tower(n, h, w, cin0, nconv, d_in, d_packed, d_bias, d_out, d_values ? d_fc_w : nullptr, fc_b,
-                              d_values, (hipStream_t)hip_stream))
+                              d_values, nullptr, nullptr, nullptr, (hipStream_t)hip_stream))
+        return fail(ZC_EINVAL, "tower shape (h %d, w %d, cin0 %d, %d convs) not supported", h, w, cin0, nconv);
+    ZC_HIP(hipGetLastError());
+    return ZC_OK;
+}
+
+int zc_net_tower_policy_async(int32_t n, int32_t h, int32_t w, int32_t cin0, int32_t nconv, const void *d_in,
+                              const void *d_packed, const float *d_bias, const float *d_fc_w, float fc_b,
+                              double *d_values, const void *d_pw, const float *d_pb, void *d_pout, void *hip_stream) {
+    if (n < 0 || (n && (!d_in || !d_packed || !d_bias || !d_fc_w || !d_values || !d_pw || !d_pb || !d_pout)) ||
+        ((uintptr_t)d_packed & 15) || ((uintptr_t)d_in & 15) || ((uintptr_t)d_bias & 15) || ((uintptr_t)d_pw & 15) ||
+        ((uintptr_t)d_pout & 7))
+        return fail(ZC_EINVAL, "bad argument");
+    if (!n) return ZC_OK;
+    if (!zc::launch_net_tower(n, h, w, cin0, nconv, d_in, d_packed, d_bias, nullptr, d_fc_w, fc_b, d_values, d_pw,
+                              d_pb, d_pout, (hipStream_t)hip_stream))
         return fail(ZC_EINVAL, "tower shape (h %d, w %d, cin0 %d, %d convs) not supported", h, w, cin0, nconv);
     ZC_HIP(hipGetLastError());
     return ZC_OK;

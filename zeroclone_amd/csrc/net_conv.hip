@@ -689,11 +689,21 @@ __device__ __forceinline__ void tower_epilogue(_Float16 *dst, const float4 (&bv)
     }
 }
 
+// The policy head's 1x1 conv (PolicyValueNetwork.policy[0..2]: 128 -> 32 channels, BN folded,
+// ReLU) on the tower's output while it is still in LDS (tower_policy): pw = the folded
+// weights as 32x32x16 MFMA A fragments [8 k-steps][64 lanes][8] (lane = output channel
+// lane % 32, k = 16 kc + 8 (lane / 32) + e), pb [32] fp32 bias; out [n * H * W][32] fp16.
+struct TowerPolicy {
+    const _Float16 *pw;
+    const float *pb;
+    _Float16 *out;
+};
+
 template <int H, int W, int BPH, int CIN0, int NT, int WPE, int PG = 1>
 __global__ __launch_bounds__(256 * PG) __attribute__((amdgpu_waves_per_eu(WPE, WPE))) void tower_kernel(
     int nboards, int nconv, const _Float16 *__restrict__ in, const _Float16 *__restrict__ wall,
     const float *__restrict__ ball, _Float16 *__restrict__ out, const float *__restrict__ fcw, float fcb,
-    double *__restrict__ values) {
+    double *__restrict__ values, TowerPolicy pol) {
     constexpr int HW = H * W;
     static_assert(BPH * HW <= 32 * NT * PG, "tile too large");
     constexpr int TP = 32 * NT * PG;
@@ -788,6 +798,37 @@ __global__ __launch_bounds__(256 * PG) __attribute__((amdgpu_waves_per_eu(WPE, W
             if (lane == 0) values[b0 + bi] = (double)tanhf(d + fcb);
         }
     }
+    if (pol.out) {
+        // the 1x1 conv: wave (pg, wave) takes pixel tiles wave, wave + 4, ... of its group (32
+        // pixels each), 8 MFMAs over the 128 channels, + bias, ReLU, fp16 -> [pixel][32]
+        h8 pa[8];
+#pragma unroll
+        for (int kc = 0; kc < 8; ++kc) pa[kc] = *(const h8 *)(pol.pw + ((size_t)kc * 64 + lane) * 8);
+        float4 pbv[4];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) pbv[g] = *(const float4 *)(pol.pb + 8 * g + 4 * hh);
+        for (int t = wave; t < NT; t += 4) {
+            const int P = pbase + t * 32 + r;
+            f16x acc;
+#pragma unroll
+            for (int k = 0; k < 16; ++k) acc[k] = 0.0f;
+#pragma unroll
+            for (int kc = 0; kc < 8; ++kc) {
+                const h8 x = *(const h8 *)(lds + (size_t)P * kTowerLD + kc * 16 + hh * 8);
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(pa[kc], x, acc, 0, 0, 0);
+            }
+            if (P < npix) {
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    const float bb[4] = {pbv[g].x, pbv[g].y, pbv[g].z, pbv[g].w};
+                    h4 ov;
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) ov[e] = (_Float16)fmaxf(acc[4 * g + e] + bb[e], 0.0f);
+                    *(h4 *)(pol.out + ((size_t)b0 * HW + P) * 32 + 8 * g + 4 * hh) = ov;
+                }
+            }
+        }
+    }
     if (out) {  // -> HBM, whole 256-byte rows
 #pragma unroll
         for (int q = 0; q < TP * (kCout / 8) / NTH; ++q) {
@@ -799,10 +840,10 @@ __global__ __launch_bounds__(256 * PG) __attribute__((amdgpu_waves_per_eu(WPE, W
 
 template <int H, int W, int BPH, int NT, int WPE, int PG = 1>
 void launch_tower(int n, int nconv, const void *in, const void *wall, const float *ball, void *out, const float *fcw,
-                  float fcb, double *values, hipStream_t s) {
+                  float fcb, double *values, TowerPolicy pol, hipStream_t s) {
     hipLaunchKernelGGL((tower_kernel<H, W, BPH, 32, NT, WPE, PG>), dim3((n + BPH - 1) / BPH), dim3(256 * PG),
                        (tower_lds<NT, PG>()), s, n, nconv, (const _Float16 *)in, (const _Float16 *)wall, ball,
-                       (_Float16 *)out, fcw, fcb, values);
+                       (_Float16 *)out, fcw, fcb, values, pol);
 }
 
 // [9][kCout][cin] -> the stream form's fragments: packed[((tap * KC + kc) * 4 + mb) * 512 +
@@ -934,19 +975,21 @@ bool launch_net_conv3x3_packed(int n, int h, int w, int cin, const void *in, con
 }
 
 bool launch_net_tower(int n, int h, int w, int cin0, int nconv, const void *in, const void *wall, const float *ball,
-                      void *out, const float *fcw, float fcb, double *values, hipStream_t s) {
+                      void *out, const float *fcw, float fcb, double *values, const void *pw, const float *pb,
+                      void *pout, hipStream_t s) {
     if (cin0 != 32 || nconv < 1 || !(nconv & 1)) return false;
+    const TowerPolicy pol{(const _Float16 *)pw, pb, (_Float16 *)pout};
     // 128-pixel tiles at two workgroups per CU; 64-pixel tiles (one chess board) at 3 or 4
     // workgroups per CU measured 10 % slower (tools/ab_tower.py)
 #ifndef ZC_TOWER_PG
 #define ZC_TOWER_PG 1
 #endif
 #if ZC_TOWER_PG == 2
-    if (h == 8 && w == 8) launch_tower<8, 8, 4, 4, 2, 2>(n, nconv, in, wall, ball, out, fcw, fcb, values, s);
-    else if (h == 6 && w == 7) launch_tower<6, 7, 6, 4, 2, 2>(n, nconv, in, wall, ball, out, fcw, fcb, values, s);
+    if (h == 8 && w == 8) launch_tower<8, 8, 4, 4, 2, 2>(n, nconv, in, wall, ball, out, fcw, fcb, values, pol, s);
+    else if (h == 6 && w == 7) launch_tower<6, 7, 6, 4, 2, 2>(n, nconv, in, wall, ball, out, fcw, fcb, values, pol, s);
 #else
-    if (h == 8 && w == 8) launch_tower<8, 8, 2, 4, 2>(n, nconv, in, wall, ball, out, fcw, fcb, values, s);
-    else if (h == 6 && w == 7) launch_tower<6, 7, 3, 4, 2>(n, nconv, in, wall, ball, out, fcw, fcb, values, s);
+    if (h == 8 && w == 8) launch_tower<8, 8, 2, 4, 2>(n, nconv, in, wall, ball, out, fcw, fcb, values, pol, s);
+    else if (h == 6 && w == 7) launch_tower<6, 7, 3, 4, 2>(n, nconv, in, wall, ball, out, fcw, fcb, values, pol, s);
 #endif
     else return false;
     return true;

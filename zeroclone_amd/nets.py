@@ -206,6 +206,28 @@ class MfmaValueNetwork:
             a, b = b, a
         return a, vals
 
+    def tower_policy(self, planes, pw, pb, pout):
+        """The tower, the value head and a 128 -> 32 policy 1x1 conv (pw: pack_policy_1x1's
+        fragments, pb fp32 [32]) in ONE launch (zc_net_tower_policy_async): fp64 values [n];
+        pout [n, h*w, 32] fp16 receives ReLU(conv1x1 + pb).  No tower activation is written."""
+        import torch
+        from . import _native
+        n, c, h, w = planes.shape
+        if c != self.in_planes or planes.dtype != torch.float16:
+            raise ValueError("planes must be fp16 [n, in_planes, h, w]")
+        if pout.shape != (n, h * w, 32) or pout.dtype != torch.float16 or not pout.is_contiguous():
+            raise ValueError("pout must be contiguous fp16 [n, h*w, 32]")
+        planes = planes.contiguous()
+        x0, _, _, _, vals = self._buffers(n, h * w)
+        s = ctypes_stream(self.dev)
+        L = _native.lib()
+        _native.check(L.zc_net_planes_to_nhwc_async(n, c, h * w, self.cpad, planes.data_ptr(), x0.data_ptr(), s))
+        _native.check(L.zc_net_tower_policy_async(n, h, w, self.cpad, len(self.wp), x0.data_ptr(),
+                                                  self.wall.data_ptr(), self.ball.data_ptr(), self.fcw.data_ptr(),
+                                                  self.fcb, vals.data_ptr(), pw.data_ptr(), pb.data_ptr(),
+                                                  pout.data_ptr(), s))
+        return vals
+
     def __call__(self, planes, fused: bool = True):
         """fp64 values [n]: the tower and the value head in one launch (fused), or the layered
         tower + zc_net_value_head_async — bit-identical."""
@@ -223,6 +245,16 @@ def ctypes_stream(dev):
     import ctypes
     import torch
     return ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream or None)
+
+
+def pack_policy_1x1(weight):
+    """A [32, 128] (out, in) 1x1 conv weight as the tower kernel's v_mfma_f32_32x32x16_f16 A
+    fragments, fp16 [8 k-steps][64 lanes][8]: lane l of k-step kc holds
+    weight[l % 32, 16 kc + 8 (l // 32) + e] (csrc/net_conv.hip TowerPolicy)."""
+    co, ci = weight.shape
+    if (co, ci) != (32, 128):
+        raise ValueError("the fused policy conv is 128 -> 32 channels")
+    return weight.reshape(32, 8, 2, 8).permute(1, 2, 0, 3).reshape(8, 64, 8).contiguous()
 
 
 class PolicyValueNetwork(nn.Module):
@@ -256,10 +288,13 @@ class PolicyValueNetwork(nn.Module):
 
 
 class MfmaPolicyValueNetwork:
-    """PolicyValueNetwork for inference: the tower and value head on the MFMA kernels, the
-    policy head (BN folded; a 128->P channel matmul and one Linear) as two fp16 GEMMs on
-    PyTorch-ROCm reading the tower's NHWC activation in place.  Returns (fp64 values [n],
-    fp16 logits [n, 4096])."""
+    """PolicyValueNetwork for inference, ONE kernel launch up to the policy logits' GEMM: the
+    tower, the value head and the policy head's 1x1 conv (BN folded, ReLU) run in the fused
+    tower kernel (zc_net_tower_policy_async; the conv as an MFMA epilogue on the on-chip
+    activation, so the 128-channel activation never reaches HBM); the flatten + Linear to
+    the 4096 logits is one fp16 GEMM on PyTorch-ROCm over its [n, h*w*32] output.  Returns
+    (fp64 values [n], fp16 logits [n, 4096]).  fused=False: the tower's activation written
+    out and the 1x1 conv as a GEMM (the pre-round-4 path, kept for the A/B)."""
 
     def __init__(self, net: PolicyValueNetwork, device="cuda"):
         import torch
@@ -267,18 +302,32 @@ class MfmaPolicyValueNetwork:
         conv, bn, lin = net.policy[0], net.policy[1], net.policy[4]
         folded = _fold(conv, bn)
         P = conv.out_channels
-        self.w1 = folded.weight.detach().float().reshape(P, -1).t().contiguous().to(device, torch.float16)  # [C, P]
+        wf = folded.weight.detach().float().reshape(P, -1)                      # [P, C]
+        self.w1 = wf.t().contiguous().to(device, torch.float16)  # [C, P]
         self.b1 = folded.bias.detach().float().to(device, torch.float16)
+        self.fused = P == 32 and wf.shape[1] == 128
+        if self.fused:
+            self.pw = pack_policy_1x1(wf).to(device, torch.float16)
+            self.pb = folded.bias.detach().float().contiguous().to(device)
         hw = lin.in_features // P
         # torch flattens [P, h, w] channel-major; the NHWC activation is pixel-major
         wl = lin.weight.detach().float().reshape(lin.out_features, P, hw).permute(0, 2, 1).reshape(lin.out_features, -1)
         self.w2 = wl.t().contiguous().to(device, torch.float16)  # [hw*P, n_logits]
         self.b2 = lin.bias.detach().float().to(device, torch.float16)
+        self._pout = {}
 
-    def __call__(self, planes):
+    def __call__(self, planes, fused: bool = True):
         import torch
+        n, _, h, w = planes.shape
+        if fused and self.fused:
+            key = (n, h * w)
+            if key not in self._pout:
+                self._pout[key] = torch.empty((n, h * w, 32), dtype=torch.float16, device=self.tower.dev)
+            p = self._pout[key]
+            vals = self.tower.tower_policy(planes, self.pw, self.pb, p)
+            return vals, torch.addmm(self.b2, p.view(n, -1), self.w2)
         a, vals = self.tower.tower(planes, head=True)  # the activation and the values, one launch
-        n, hw = a.shape[0], a.shape[1]
+        hw = a.shape[1]
         p = torch.relu(torch.addmm(self.b1, a.reshape(n * hw, -1), self.w1)).reshape(n, -1)
         logits = torch.addmm(self.b2, p, self.w2)
         return vals, logits
