@@ -37,10 +37,13 @@ def test_mfma_network_matches_torch(shape, n):
     np.testing.assert_allclose(got.cpu().numpy(), want.cpu().numpy(), rtol=0, atol=2e-2)
 
 
-def test_single_conv_layer_exactness():
+@pytest.mark.parametrize("mf", ["32", "16"])
+def test_single_conv_layer_exactness(mf, monkeypatch):
     """One conv layer with small-integer data is exact in fp32 accumulation: checks the
-    MFMA operand/accumulator layouts, the tap shifts and the board edges bit for bit."""
+    MFMA operand/accumulator layouts, the tap shifts and the board edges bit for bit (the
+    packed form in both MFMA forms)."""
     from zeroclone_amd import _native
+    monkeypatch.setenv("ZC_TOWER_MF", mf)
     L = _native.lib()
     for (h, w, cin) in [(8, 8, 128), (6, 7, 32), (8, 8, 32), (6, 7, 128)]:
         n = 13
@@ -92,13 +95,15 @@ def test_packed_conv_is_bit_identical_to_the_staged_form():
             assert torch.equal(a.view(torch.int16), b.view(torch.int16)), (h, w, cin, n, use_res, relu)
 
 
+@pytest.mark.parametrize("mf", ["32", "16"])
 @pytest.mark.parametrize("shape", [(17, 8, 8), (2, 6, 7)])
 @pytest.mark.parametrize("n", [1, 7, 301, 4099])
-def test_fused_tower_is_bit_identical_to_layered(shape, n):
+def test_fused_tower_is_bit_identical_to_layered(shape, n, mf, monkeypatch):
     """zc_net_tower_async (the whole tower in one launch, activations on chip) against the
     layer-by-layer packed launches: the tower's output activation bit for bit, ragged last
-    tiles included."""
+    tiles included — in both MFMA forms (ZC_TOWER_MF selects the form of both launches)."""
     from zeroclone_amd.nets import MfmaValueNetwork
+    monkeypatch.setenv("ZC_TOWER_MF", mf)
     c, h, w = shape
     net = MfmaValueNetwork(_net(c, seed=100 + n))
     x = (torch.rand(n, c, h, w, device="cuda") < 0.3).half()
@@ -110,6 +115,48 @@ def test_fused_tower_is_bit_identical_to_layered(shape, n):
     assert got.shape == (n, h * w, 128)
     assert torch.equal(got, want)
     assert want.abs().sum().item() > 0
+
+
+def _integer_net(c, blocks, seed, density=0.002):
+    """A ValueNetwork whose folded convs are sparse small integers and whose BN is the identity
+    (eps 0): every activation of the tower is a small integer, so any fp32 summation order gives
+    the exact result — the MFMA forms' operand / accumulator layouts, tap shifts, board edges,
+    residual adds and ragged tiles are checked bit for bit against float64."""
+    from zeroclone_amd.nets import ValueNetwork
+    g = torch.Generator().manual_seed(seed)
+    net = ValueNetwork(128, blocks, in_planes=c).eval()
+    for m in net.modules():
+        if isinstance(m, torch.nn.Conv2d):
+            keep = torch.rand(m.weight.shape, generator=g) < (density if m.in_channels == 128 else 0.02)
+            m.weight.data = torch.randint(-2, 3, m.weight.shape, generator=g).float() * keep
+        elif isinstance(m, torch.nn.BatchNorm2d):
+            m.eps = 0.0
+            m.running_mean.zero_()
+            m.running_var.fill_(1.0)
+            m.weight.data.fill_(1.0)
+            m.bias.data = torch.randint(-1, 3, m.bias.shape, generator=g).float()
+    return net
+
+
+@pytest.mark.parametrize("mf", ["32", "16"])
+@pytest.mark.parametrize("shape", [(17, 8, 8), (2, 6, 7)])
+def test_tower_forms_exact_on_integers(mf, shape, monkeypatch):
+    """Both MFMA forms of the fused tower (ZC_TOWER_MF: 32x32x16, 16x16x32) on an integer
+    network, 2 residual blocks, ragged board counts: equal to float64 exactly."""
+    from zeroclone_amd.nets import FoldedValueNetwork, MfmaValueNetwork
+    monkeypatch.setenv("ZC_TOWER_MF", mf)
+    c, h, w = shape
+    vnet = _integer_net(c, 2, seed=h * 10 + int(mf))
+    net = MfmaValueNetwork(vnet)
+    f = FoldedValueNetwork(vnet).double()
+    for n in (1, 5, 131):
+        x = (torch.rand(n, c, h, w) < 0.3).half()
+        got, _ = net.tower(x.cuda(), fused=True)
+        torch.cuda.synchronize()
+        with torch.no_grad():
+            want = f.res(torch.relu(f.stem(x.double()))).permute(0, 2, 3, 1).reshape(n, h * w, 128)
+        assert want.abs().max().item() < 2048 and want.abs().sum().item() > 0
+        assert torch.equal(got.double().cpu(), want), (mf, shape, n)
 
 
 def test_fused_tower_rejects_unsupported_shapes():

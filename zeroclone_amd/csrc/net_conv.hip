@@ -47,6 +47,7 @@ namespace {
 typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 typedef _Float16 h4 __attribute__((ext_vector_type(4)));
 typedef float f16x __attribute__((ext_vector_type(16)));
+typedef float f4x __attribute__((ext_vector_type(4)));
 
 constexpr int kCout = 128;
 constexpr int kTilePix = 256;
@@ -412,6 +413,72 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 }
 
 
+// One layer's MFMA loop in the 16x16x32 form: each wave its 32 output channels (two 16-row
+// M tiles) x the tile's pixels as NN 16-pixel N tiles, k-steps of 32 channels.  Lane l takes
+// pixel l & 15 of each N tile and k-chunk q = l >> 4; the weight fragments come from the same
+// packed stream as tower_mfma's (lane l of M tile m reads the 8 halfs of fragment row
+// 16 m + (l & 15), k 8 q .. 8 q + 7: wa already holds the lane's offset), one tap ahead.
+template <int H, int W, int NN, int KC, int KCN, int LD, int ZERO, int ZR, int NA>
+__device__ __forceinline__ void tower_mfma16(const _Float16 *lds, int src, const _Float16 *wa, const _Float16 *wn,
+                                             h8 (&a)[NA], int l16, const int (&pyx)[NN], int q,
+                                             f4x (&acc)[2][NN]) {
+    constexpr int J = KC / 2, JN = KCN / 2;
+    auto rows = [&](int tap, const _Float16 *(&xb)[NN]) {
+        const int dy = tap / 3 - 1, dx = tap % 3 - 1;
+#pragma unroll
+        for (int n = 0; n < NN; ++n) {
+            const int sy = (pyx[n] >> 8) + dy, sx = (pyx[n] & 255) + dx;
+            const bool sv = (unsigned)sy < (unsigned)H && (unsigned)sx < (unsigned)W;
+            const int row = l16 + (n * 16 + dy * W + dx);  // pixel n * 16 + l16, shifted by the tap
+            xb[n] = lds + (sv ? src + row : ZERO + (row & (ZR - 1))) * LD + q * 8;
+        }
+    };
+    const _Float16 *xb[NN];
+    rows(0, xb);
+    h8 x[NN], xn[NN];
+#pragma unroll
+    for (int n = 0; n < NN; ++n) x[n] = *(const h8 *)(xb[n]);
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) {
+        const _Float16 *xbn[NN];
+        if (tap + 1 < 9) rows(tap + 1, xbn);
+#pragma unroll
+        for (int j = 0; j < J; ++j) {
+            if (j + 1 < J) {
+#pragma unroll
+                for (int n = 0; n < NN; ++n) xn[n] = *(const h8 *)(xb[n] + (j + 1) * 32);
+            } else if (tap + 1 < 9) {
+#pragma unroll
+                for (int n = 0; n < NN; ++n) xn[n] = *(const h8 *)(xbn[n]);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int n = 0; n < NN; ++n)
+#pragma unroll
+                for (int m = 0; m < 2; ++m)
+                    acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[2 * j + m], x[n], acc[m][n], 0, 0, 0);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int m = 0; m < 2; ++m) {
+                if (tap + 1 < 9) a[2 * j + m] = *(const h8 *)(wa + (size_t)((tap + 1) * KC + 2 * j) * 2048 + m * 128);
+                else if (JN == J && wn) a[2 * j + m] = *(const h8 *)(wn + (size_t)(2 * j) * 2048 + m * 128);
+            }
+#pragma unroll
+            for (int n = 0; n < NN; ++n) x[n] = xn[n];
+        }
+        if (tap + 1 < 9) {
+#pragma unroll
+            for (int n = 0; n < NN; ++n) xb[n] = xbn[n];
+        }
+    }
+    if (JN != J && wn) {
+#pragma unroll
+        for (int j = 0; j < JN; ++j)
+#pragma unroll
+            for (int m = 0; m < 2; ++m) a[2 * j + m] = *(const h8 *)(wn + (size_t)(2 * j) * 2048 + m * 128);
+    }
+}
+
 // Streamed-weight form (zc_net_conv3x3_packed_async): wave w owns output channels
 // [32 w, +32) x all 128 pixels of the tile (4 MFMA tiles).  The weights are pre-packed so
 // that every A fragment (32 channels x 16 k of one tap) is one contiguous 1-KB piece, 16 B
@@ -420,14 +487,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 // tile and the main loop has no barrier and no weight restaging.  WPE = waves per SIMD:
 // at 3 the fp32 epilogue tile goes through LDS in two 64-pixel halves, so three
 // workgroups fit a CU.  Same accumulation order as the other forms (bit-identical).
-template <int H, int W, int BPH, int CIN, int WPE>
+template <int H, int W, int BPH, int CIN, int WPE, int MF = 32>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE))) void conv3x3_stream_kernel(
     int nboards, const _Float16 *__restrict__ in, const _Float16 *__restrict__ wp, const float *__restrict__ bias,
     const _Float16 *__restrict__ res, _Float16 *__restrict__ out, int relu) {
     constexpr int HW = H * W;
     constexpr int PIX = BPH * HW;
     static_assert(PIX <= kHalfPix, "tile too large");
-    constexpr int LD = CIN + 8;
+    // MF = 16: the 16x16x32 MFMA form (tower_mfma16; rows of CIN + 16 halfs, 8 (mod 64) dwords x
+    // an odd number, keep its operand reads conflict-free)
+    constexpr int LD = MF == 16 ? CIN + 16 : CIN + 8;
     constexpr int C8 = CIN / 8;
     constexpr int KC = CIN / 16;
     constexpr int NI = kHalfPix * C8 / 256;
@@ -443,11 +512,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
     const int npix = min(BPH, nboards - b0) * HW;
     const h8 zero = {0, 0, 0, 0, 0, 0, 0, 0};
     const int r = lane & 31, hh = lane >> 5;
-    // fragment (tap, kc) of this wave: wp + ((tap * KC + kc) * 4 + wave) * 512 + lane * 8
-    const _Float16 *const wa = wp + (size_t)wave * 512 + lane * 8;
+    const int l16 = lane & 15, q4 = lane >> 4;
+    // fragment (tap, kc) of this wave: wp + ((tap * KC + kc) * 4 + wave) * 512 + lane * 8 (MF = 16:
+    // lane l reads row 16 m + (l & 15), k-chunk l >> 4 of the same stream)
+    const _Float16 *const wa =
+        MF == 16 ? wp + (size_t)wave * 512 + (size_t)((q4 & 1) * 32 + l16) * 8 + (size_t)(q4 >> 1) * 2048
+                 : wp + (size_t)wave * 512 + lane * 8;
     h8 a[KC];
+    if constexpr (MF == 16) {
 #pragma unroll
-    for (int kc = 0; kc < KC; ++kc) a[kc] = *(const h8 *)(wa + (size_t)kc * 2048);
+        for (int j = 0; j < KC / 2; ++j)
+#pragma unroll
+            for (int m = 0; m < 2; ++m) a[2 * j + m] = *(const h8 *)(wa + (size_t)(2 * j) * 2048 + m * 128);
+    } else {
+#pragma unroll
+        for (int kc = 0; kc < KC; ++kc) a[kc] = *(const h8 *)(wa + (size_t)kc * 2048);
+    }
     {
         h8 v[NI];
         const _Float16 *src = in + (size_t)b0 * HW * CIN;
@@ -464,6 +544,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
         }
         for (int z = tid; z < 16 * C8; z += 256) *(h8 *)(sin + (kHalfPix + z / C8) * LD + (z % C8) * 8) = zero;
     }
+    f16x acc[MF == 16 ? 1 : 4];
+    f4x acc16[2][MF == 16 ? 8 : 1];
+    if constexpr (MF == 16) {
+        int pyx16[8];
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+            const int P = t * 16 + l16;
+            const int pb = P / HW, rem = P - pb * HW, py = rem / W;
+            pyx16[t] = (P < npix ? py << 8 : 64 << 8) | (rem - py * W);
+#pragma unroll
+            for (int m = 0; m < 2; ++m) acc16[m][t] = f4x{0.0f, 0.0f, 0.0f, 0.0f};
+        }
+        __syncthreads();  // the input tile is in LDS
+        tower_mfma16<H, W, 8, KC, KC, LD, kHalfPix, 16>(lds, 0, wa, nullptr, a, l16, pyx16, q4, acc16);
+    }
+    if constexpr (MF != 16) {
     // per MFMA pixel tile t: the pixel's LDS row and its (y, x) packed as y << 8 | x (a pixel
     // beyond the tile gets y = 64: every shifted view of it is off the board)
     int prow[4], pyx[4];
@@ -474,7 +570,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
         prow[t] = P;
         pyx[t] = (P < npix ? py << 8 : 64 << 8) | (rem - py * W);
     }
-    f16x acc[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t)
 #pragma unroll
@@ -518,6 +613,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
         }
     }
 
+    }
     // epilogue through LDS (as in the half form): fp32 [pixel][cout] rows, then bias,
     // residual, ReLU and the fp16 store on whole 256-byte output rows; NP pixels per pass
     constexpr int SL = kCout + 4;
@@ -527,14 +623,27 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
 #pragma unroll
     for (int h0 = 0; h0 < kHalfPix; h0 += NP) {
         __syncthreads();  // the input tile / the previous pass is no longer read
+        if constexpr (MF == 16) {
 #pragma unroll
-        for (int t = 0; t < 4; ++t) {
-            if (t * 32 < h0 || t * 32 >= h0 + NP) continue;
+            for (int t = 0; t < 8; ++t) {
+                if (t * 16 < h0 || t * 16 >= h0 + NP) continue;
 #pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                const int P = t * 32 + r - h0, co = wave * 32 + 8 * g + 4 * hh;
-                *(float4 *)(sacc + P * SL + co) =
-                    make_float4(acc[t][4 * g + 0], acc[t][4 * g + 1], acc[t][4 * g + 2], acc[t][4 * g + 3]);
+                for (int m = 0; m < 2; ++m) {
+                    const int P = t * 16 + l16 - h0, co = wave * 32 + 16 * m + 4 * q4;
+                    *(float4 *)(sacc + P * SL + co) = make_float4(acc16[m][t][0], acc16[m][t][1], acc16[m][t][2],
+                                                                  acc16[m][t][3]);
+                }
+            }
+        } else {
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                if (t * 32 < h0 || t * 32 >= h0 + NP) continue;
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    const int P = t * 32 + r - h0, co = wave * 32 + 8 * g + 4 * hh;
+                    *(float4 *)(sacc + P * SL + co) =
+                        make_float4(acc[t][4 * g + 0], acc[t][4 * g + 1], acc[t][4 * g + 2], acc[t][4 * g + 3]);
+                }
             }
         }
         __syncthreads();
@@ -597,10 +706,17 @@ constexpr int kTowerLD = kCout + 8;
 // rows TP = 32 NT PG.  With PG = 2 the two waves that own the same output channels load the
 // same weight fragments at about the same time, so the second load is served by the CU's
 // vector L1 instead of L2.
+// MF = 16 (the 16x16x32 MFMA form, tower_mfma16): rows of 144 halfs (72 dwords: the operand's
+// four 16-byte k-chunks per pixel row land on distinct banks in every ds_read_b128 lane group)
+// and 8 zero rows (the bank class of a row is its index mod 8)
+template <int MF> constexpr int tower_ld() { return MF == 16 ? kCout + 16 : kTowerLD; }
+template <int MF> constexpr int tower_zr() { return MF == 16 ? 8 : 16; }
 template <int NT, int PG = 1> constexpr int tower_zero() { return 32 * NT * PG; }       // first zero row
-template <int NT, int PG = 1> constexpr int tower_buf1() { return 32 * NT * PG + 16; }  // buf1's first row
-template <int NT, int PG = 1> constexpr size_t tower_lds() {
-    return (size_t)(64 * NT * PG + 16) * kTowerLD * sizeof(_Float16);
+template <int NT, int PG = 1, int MF = 32> constexpr int tower_buf1() {                 // buf1's first row
+    return 32 * NT * PG + tower_zr<MF>();
+}
+template <int NT, int PG = 1, int MF = 32> constexpr size_t tower_lds() {
+    return (size_t)(64 * NT * PG + tower_zr<MF>()) * tower_ld<MF>() * sizeof(_Float16);
 }
 
 // One layer's MFMA loop: acc[t] += sum over taps and k of W * X (X from the LDS buffer at
@@ -689,6 +805,34 @@ __device__ __forceinline__ void tower_epilogue(_Float16 *dst, const float4 (&bv)
     }
 }
 
+// tower_epilogue for the 16x16x32 form: lane (pixel l & 15 of N tile n, q = l >> 4) holds
+// channels wave * 32 + 16 m + 4 q .. + 3; the same per-element arithmetic
+template <int NN>
+__device__ __forceinline__ void tower_epilogue16(_Float16 *dst, const float4 (&bv)[2], bool res, int npix, int wave,
+                                                 int l16, int q, const f4x (&acc)[2][NN]) {
+    constexpr int LD = tower_ld<16>();
+#pragma unroll
+    for (int n = 0; n < NN; ++n) {
+        const int P = n * 16 + l16;
+        if (P >= npix) continue;
+#pragma unroll
+        for (int m = 0; m < 2; ++m) {
+            h4 *const o = (h4 *)(dst + P * LD + wave * 32 + 16 * m + 4 * q);
+            float v[4] = {acc[m][n][0] + bv[m].x, acc[m][n][1] + bv[m].y, acc[m][n][2] + bv[m].z,
+                          acc[m][n][3] + bv[m].w};
+            if (res) {
+                const h4 rv = *o;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) v[e] += (float)rv[e];
+            }
+            h4 ov;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) ov[e] = (_Float16)fmaxf(v[e], 0.0f);
+            *o = ov;
+        }
+    }
+}
+
 // The policy head's 1x1 conv (PolicyValueNetwork.policy[0..2]: 128 -> 32 channels, BN folded,
 // ReLU) on the tower's output while it is still in LDS (tower_policy): pw = the folded
 // weights as 32x32x16 MFMA A fragments [8 k-steps][64 lanes][8] (lane = output channel
@@ -699,16 +843,19 @@ struct TowerPolicy {
     _Float16 *out;
 };
 
-template <int H, int W, int BPH, int CIN0, int NT, int WPE, int PG = 1>
+template <int H, int W, int BPH, int CIN0, int NT, int WPE, int PG = 1, int MF = 32>
 __global__ __launch_bounds__(256 * PG) __attribute__((amdgpu_waves_per_eu(WPE, WPE))) void tower_kernel(
     int nboards, int nconv, const _Float16 *__restrict__ in, const _Float16 *__restrict__ wall,
     const float *__restrict__ ball, _Float16 *__restrict__ out, const float *__restrict__ fcw, float fcb,
     double *__restrict__ values, TowerPolicy pol) {
     constexpr int HW = H * W;
     static_assert(BPH * HW <= 32 * NT * PG, "tile too large");
+    static_assert(MF == 32 || (MF == 16 && PG == 1), "the 16x16x32 form has one pixel group");
     constexpr int TP = 32 * NT * PG;
     constexpr int NTH = 256 * PG;   // threads
     constexpr int KC0 = CIN0 / 16;
+    constexpr int LD = tower_ld<MF>(), ZR = tower_zr<MF>(), BUF1 = tower_buf1<NT, PG, MF>();
+    constexpr int NP = MF == 16 ? 2 * NT : NT;  // pixel tiles per wave (16 or 32 pixels)
     constexpr size_t kW0 = (size_t)9 * CIN0 * kCout, kW = (size_t)9 * kCout * kCout;  // halfs per layer
     extern __shared__ __attribute__((aligned(16))) _Float16 lds[];
     const int tid = threadIdx.x, lane = tid & 63, wave = (tid >> 6) & 3, pg = tid >> 8;
@@ -717,10 +864,22 @@ __global__ __launch_bounds__(256 * PG) __attribute__((amdgpu_waves_per_eu(WPE, W
     const int npix = min(BPH, nboards - b0) * HW;
     const h8 zero = {0, 0, 0, 0, 0, 0, 0, 0};
     const int r = lane & 31, hh = lane >> 5;
-    const _Float16 *const wl0 = wall + (size_t)wave * 512 + lane * 8;  // this wave's fragments, layer 0
+    const int l16 = lane & 15, q4 = lane >> 4;  // the 16x16x32 form's pixel / k-chunk
+    // this wave's fragments, layer 0 (MF = 16: lane l reads row 16 m + (l & 15), k-chunk l >> 4
+    // of the same packed stream)
+    const _Float16 *const wl0 =
+        MF == 16 ? wall + (size_t)wave * 512 + (size_t)((q4 & 1) * 32 + l16) * 8 + (size_t)(q4 >> 1) * 2048
+                 : wall + (size_t)wave * 512 + lane * 8;
     h8 a[8];
+    if constexpr (MF == 16) {
 #pragma unroll
-    for (int kc = 0; kc < KC0; ++kc) a[kc] = *(const h8 *)(wl0 + (size_t)kc * 2048);
+        for (int j = 0; j < KC0 / 2; ++j)
+#pragma unroll
+            for (int m = 0; m < 2; ++m) a[2 * j + m] = *(const h8 *)(wl0 + (size_t)(2 * j) * 2048 + m * 128);
+    } else {
+#pragma unroll
+        for (int kc = 0; kc < KC0; ++kc) a[kc] = *(const h8 *)(wl0 + (size_t)kc * 2048);
+    }
     {
         constexpr int C8 = CIN0 / 8;
         const _Float16 *src = in + (size_t)b0 * HW * CIN0;
@@ -729,15 +888,15 @@ __global__ __launch_bounds__(256 * PG) __attribute__((amdgpu_waves_per_eu(WPE, W
             const int i = tid + q * NTH, row = i / C8, c8 = i - row * C8;
             if (row >= TP) break;
             const h8 t = *(const h8 *)(src + min(row, npix - 1) * CIN0 + c8 * 8);
-            *(h8 *)(lds + (tower_buf1<NT, PG>() + row) * kTowerLD + c8 * 8) = row < npix ? t : zero;
+            *(h8 *)(lds + (BUF1 + row) * LD + c8 * 8) = row < npix ? t : zero;
         }
-        for (int z = tid; z < 16 * kTowerLD / 8; z += NTH)
-            *(h8 *)(lds + tower_zero<NT, PG>() * kTowerLD + z * 8) = zero;
+        for (int z = tid; z < ZR * LD / 8; z += NTH)
+            *(h8 *)(lds + tower_zero<NT, PG>() * LD + z * 8) = zero;
     }
-    int prow[NT], pyx[NT];
+    int prow[NP], pyx[NP];
 #pragma unroll
-    for (int t = 0; t < NT; ++t) {
-        const int P = pbase + t * 32 + r;
+    for (int t = 0; t < NP; ++t) {
+        const int P = MF == 16 ? t * 16 + l16 : pbase + t * 32 + r;
         const int pb = P / HW, rem = P - pb * HW, py = rem / W;
         prow[t] = P;
         pyx[t] = (P < npix ? py << 8 : 64 << 8) | (rem - py * W);
@@ -749,26 +908,45 @@ __global__ __launch_bounds__(256 * PG) __attribute__((amdgpu_waves_per_eu(WPE, W
         constexpr int KC = decltype(kc_tag)::value;
         // per-lane pixel coordinates re-derived inside the layer (opaque to the compiler), so
         // that the 36 tap addresses are not hoisted out of the layer loop into registers
-        int pr[NT], py[NT];
-#pragma unroll
-        for (int t = 0; t < NT; ++t) {
-            pr[t] = prow[t];
-            py[t] = pyx[t];
-            __asm__ volatile("" : "+v"(pr[t]), "+v"(py[t]));
-        }
-        f16x acc[NT];
-#pragma unroll
-        for (int t = 0; t < NT; ++t)
-#pragma unroll
-            for (int k = 0; k < 16; ++k) acc[t][k] = 0.0f;
-        const int src = (l & 1) ? 0 : tower_buf1<NT, PG>(), dst = (l & 1) ? tower_buf1<NT, PG>() : 0;
+        const int src = (l & 1) ? 0 : BUF1, dst = (l & 1) ? BUF1 : 0;
         const _Float16 *const wa = l == 0 ? wl0 : wl0 + kW0 + (size_t)(l - 1) * kW;
         const _Float16 *const wn = l + 1 < nconv ? wl0 + kW0 + (size_t)l * kW : nullptr;  // layer l+1's
-        float4 bv[4];  // this wave's bias slice, in flight during the MFMA loop
+        if constexpr (MF == 16) {
+            int py16[NP];  // (the pixel rows are l16 + 16 t: nothing to carry)
 #pragma unroll
-        for (int g = 0; g < 4; ++g) bv[g] = *(const float4 *)(ball + (size_t)l * kCout + wave * 32 + 8 * g + 4 * hh);
-        tower_mfma<H, W, NT, KC, 8, PG>(lds, src, wa, wn, a, pr, py, hh, acc);
-        tower_epilogue(lds + dst * kTowerLD, bv, l >= 2 && !(l & 1), npix, wave, r, hh, acc, pbase);
+            for (int t = 0; t < NP; ++t) {
+                py16[t] = pyx[t];
+                __asm__ volatile("" : "+v"(py16[t]));
+            }
+            f4x acc[2][NP];
+#pragma unroll
+            for (int m = 0; m < 2; ++m)
+#pragma unroll
+                for (int t = 0; t < NP; ++t) acc[m][t] = f4x{0.0f, 0.0f, 0.0f, 0.0f};
+            float4 bv[2];
+#pragma unroll
+            for (int m = 0; m < 2; ++m) bv[m] = *(const float4 *)(ball + (size_t)l * kCout + wave * 32 + 16 * m + 4 * q4);
+            tower_mfma16<H, W, NP, KC, 8, LD, tower_zero<NT>(), ZR>(lds, src, wa, wn, a, l16, py16, q4, acc);
+            tower_epilogue16<NP>(lds + dst * LD, bv, l >= 2 && !(l & 1), npix, wave, l16, q4, acc);
+        } else {
+            int pr[NT], py[NT];
+#pragma unroll
+            for (int t = 0; t < NT; ++t) {
+                pr[t] = prow[t];
+                py[t] = pyx[t];
+                __asm__ volatile("" : "+v"(pr[t]), "+v"(py[t]));
+            }
+            f16x acc[NT];
+#pragma unroll
+            for (int t = 0; t < NT; ++t)
+#pragma unroll
+                for (int k = 0; k < 16; ++k) acc[t][k] = 0.0f;
+            float4 bv[4];  // this wave's bias slice, in flight during the MFMA loop
+#pragma unroll
+            for (int g = 0; g < 4; ++g) bv[g] = *(const float4 *)(ball + (size_t)l * kCout + wave * 32 + 8 * g + 4 * hh);
+            tower_mfma<H, W, NT, KC, 8, PG>(lds, src, wa, wn, a, pr, py, hh, acc);
+            tower_epilogue(lds + dst * LD, bv, l >= 2 && !(l & 1), npix, wave, r, hh, acc, pbase);
+        }
         __syncthreads();
     };
     layer(0, std::integral_constant<int, KC0>{});
@@ -779,10 +957,10 @@ __global__ __launch_bounds__(256 * PG) __attribute__((amdgpu_waves_per_eu(WPE, W
         // order (lane l sums channels 8 (l & 15) .. +8 over pixels l / 16, +4, ...), from LDS
         const int c0 = (lane & 15) * 8;
         for (int bi = wave + 4 * pg; bi < npix / HW; bi += 4 * PG) {
-            const _Float16 *act = lds + bi * HW * kTowerLD + c0;
+            const _Float16 *act = lds + bi * HW * LD + c0;
             float sum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
             for (int p = lane >> 4; p < HW; p += 4) {
-                const h8 v = *(const h8 *)(act + p * kTowerLD);
+                const h8 v = *(const h8 *)(act + p * LD);
 #pragma unroll
                 for (int e = 0; e < 8; ++e) sum[e] += (float)v[e];
             }
@@ -814,7 +992,7 @@ __global__ __launch_bounds__(256 * PG) __attribute__((amdgpu_waves_per_eu(WPE, W
             for (int k = 0; k < 16; ++k) acc[k] = 0.0f;
 #pragma unroll
             for (int kc = 0; kc < 8; ++kc) {
-                const h8 x = *(const h8 *)(lds + (size_t)P * kTowerLD + kc * 16 + hh * 8);
+                const h8 x = *(const h8 *)(lds + (size_t)P * LD + kc * 16 + hh * 8);
                 acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(pa[kc], x, acc, 0, 0, 0);
             }
             if (P < npix) {
@@ -833,18 +1011,19 @@ __global__ __launch_bounds__(256 * PG) __attribute__((amdgpu_waves_per_eu(WPE, W
 #pragma unroll
         for (int q = 0; q < TP * (kCout / 8) / NTH; ++q) {
             const int i = tid + q * NTH, P = i >> 4, c0 = (i & 15) * 8;
-            if (P < npix) *(h8 *)(out + ((size_t)b0 * HW + P) * kCout + c0) = *(const h8 *)(lds + P * kTowerLD + c0);
+            if (P < npix) *(h8 *)(out + ((size_t)b0 * HW + P) * kCout + c0) = *(const h8 *)(lds + P * LD + c0);
         }
     }
 }
 
-template <int H, int W, int BPH, int NT, int WPE, int PG = 1>
+template <int H, int W, int BPH, int NT, int WPE, int PG = 1, int MF = 32>
 void launch_tower(int n, int nconv, const void *in, const void *wall, const float *ball, void *out, const float *fcw,
                   float fcb, double *values, TowerPolicy pol, hipStream_t s) {
-    hipLaunchKernelGGL((tower_kernel<H, W, BPH, 32, NT, WPE, PG>), dim3((n + BPH - 1) / BPH), dim3(256 * PG),
-                       (tower_lds<NT, PG>()), s, n, nconv, (const _Float16 *)in, (const _Float16 *)wall, ball,
+    hipLaunchKernelGGL((tower_kernel<H, W, BPH, 32, NT, WPE, PG, MF>), dim3((n + BPH - 1) / BPH), dim3(256 * PG),
+                       (tower_lds<NT, PG, MF>()), s, n, nconv, (const _Float16 *)in, (const _Float16 *)wall, ball,
                        (_Float16 *)out, fcw, fcb, values, pol);
 }
+
 
 // [9][kCout][cin] -> the stream form's fragments: packed[((tap * KC + kc) * 4 + mb) * 512 +
 // lane * 8 + e] = w[tap][mb * 32 + lane % 32][kc * 16 + 8 * (lane / 32) + e].
@@ -914,6 +1093,11 @@ int conv_impl() {  // ZC_CONV_IMPL=tile: 256-pixel tiles for every layer; defaul
     return v;
 }
 
+int tower_mf() {  // ZC_TOWER_MF=16: the 16x16x32 MFMA form of the fused tower (A/B switch, read per launch)
+    const char *e = getenv("ZC_TOWER_MF");
+    return e && !strcmp(e, "16") ? 16 : 32;
+}
+
 int stream_wpe() {  // ZC_CONV_WPE=2: the packed form at two workgroups per CU (default 3)
     static const int v = [] {
         const char *e = getenv("ZC_CONV_WPE");
@@ -926,7 +1110,12 @@ template <int H, int W, int BPH, int CIN>
 void launch_stream(int n, const void *in, const void *wp, const float *bias, const void *res, void *out, int relu,
                    hipStream_t s) {
     const size_t tile = (size_t)(kHalfPix + 16) * (CIN + 8) * sizeof(_Float16);
-    if (stream_wpe() == 2)
+    if (tower_mf() == 16) {
+        const size_t tile16 = (size_t)(kHalfPix + 16) * (CIN + 16) * sizeof(_Float16);
+        hipLaunchKernelGGL((conv3x3_stream_kernel<H, W, BPH, CIN, 2, 16>), dim3((n + BPH - 1) / BPH), dim3(256),
+                           std::max(tile16, kHalfEpiBytes), s, n, (const _Float16 *)in, (const _Float16 *)wp, bias,
+                           (const _Float16 *)res, (_Float16 *)out, relu);
+    } else if (stream_wpe() == 2)
         hipLaunchKernelGGL((conv3x3_stream_kernel<H, W, BPH, CIN, 2>), dim3((n + BPH - 1) / BPH), dim3(256),
                            std::max(tile, kHalfEpiBytes), s, n, (const _Float16 *)in, (const _Float16 *)wp, bias,
                            (const _Float16 *)res, (_Float16 *)out, relu);
@@ -988,7 +1177,11 @@ bool launch_net_tower(int n, int h, int w, int cin0, int nconv, const void *in, 
     if (h == 8 && w == 8) launch_tower<8, 8, 4, 4, 2, 2>(n, nconv, in, wall, ball, out, fcw, fcb, values, pol, s);
     else if (h == 6 && w == 7) launch_tower<6, 7, 6, 4, 2, 2>(n, nconv, in, wall, ball, out, fcw, fcb, values, pol, s);
 #else
-    if (h == 8 && w == 8) launch_tower<8, 8, 2, 4, 2>(n, nconv, in, wall, ball, out, fcw, fcb, values, pol, s);
+    if (tower_mf() == 16) {
+        if (h == 8 && w == 8) launch_tower<8, 8, 2, 4, 2, 1, 16>(n, nconv, in, wall, ball, out, fcw, fcb, values, pol, s);
+        else if (h == 6 && w == 7) launch_tower<6, 7, 3, 4, 2, 1, 16>(n, nconv, in, wall, ball, out, fcw, fcb, values, pol, s);
+        else return false;
+    } else if (h == 8 && w == 8) launch_tower<8, 8, 2, 4, 2>(n, nconv, in, wall, ball, out, fcw, fcb, values, pol, s);
     else if (h == 6 && w == 7) launch_tower<6, 7, 3, 4, 2>(n, nconv, in, wall, ball, out, fcw, fcb, values, pol, s);
 #endif
     else return false;
