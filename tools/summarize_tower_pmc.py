@@ -30,6 +30,13 @@ def load(root, tag):
     return per, dur
 
 
+def lib_sha():
+    import hashlib
+    lib = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "zeroclone_amd", "libzeroclone_amd.so")
+    with open(lib, "rb") as fh:
+        return hashlib.sha256(fh.read()).hexdigest()
+
+
 def main():
     root, out = sys.argv[1], sys.argv[2]
     c, durs = {}, []
@@ -46,7 +53,9 @@ def main():
     tf = FLOPS / (ms * 1e-3) / 1e12
     res = {"shape": "fused tower (zc_net_tower_async): stem 32 -> 128 + 8 residual blocks (16 conv3x3 128 -> 128), "
                     "8x8 boards, 32768 boards (tools/one_tower.py)",
-           "kernel": "tower_kernel<8, 8, 2, 32>", "flops_per_launch": FLOPS, "rocprof_avg_ms": round(ms, 4),
+           "kernel": f"tower_kernel<8, 8, 2, 32, 4, 2, 1, {os.environ.get('ZC_TOWER_MF', '16')}> "
+                     f"({'16x16x32' if os.environ.get('ZC_TOWER_MF', '16') == '16' else '32x32x16'} MFMA form)",
+           "lib_sha256": lib_sha(), "flops_per_launch": FLOPS, "rocprof_avg_ms": round(ms, 4),
            "calls": len(durs), "tflops": round(tf, 1),
            "per_128ch_layer_equivalent_ms": round(ms * LAYER_FLOPS / FLOPS, 4),
            "clock_ghz_grbm": round(clock, 3), "mfma_busy_frac": round(busy, 3),

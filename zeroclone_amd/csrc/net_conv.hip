@@ -1093,7 +1093,15 @@ int conv_impl() {  // ZC_CONV_IMPL=tile: 256-pixel tiles for every layer; defaul
     return v;
 }
 
-int tower_mf() {  // ZC_TOWER_MF=16: the 16x16x32 MFMA form of the fused tower (A/B switch, read per launch)
+// The MFMA form (read per launch, so an A/B can alternate in one process): the fused tower
+// runs the 16x16x32 form (+9 % over 32x32x16 at the power-held clock, outputs bit-identical:
+// profiles/r04_ab_tower_mf.log) unless ZC_TOWER_MF=32; the packed per-layer conv keeps the
+// 32x32x16 form at three workgroups per CU unless ZC_TOWER_MF=16
+int tower_mf() {
+    const char *e = getenv("ZC_TOWER_MF");
+    return e && !strcmp(e, "32") ? 32 : 16;
+}
+int stream_mf() {
     const char *e = getenv("ZC_TOWER_MF");
     return e && !strcmp(e, "16") ? 16 : 32;
 }
@@ -1110,7 +1118,7 @@ template <int H, int W, int BPH, int CIN>
 void launch_stream(int n, const void *in, const void *wp, const float *bias, const void *res, void *out, int relu,
                    hipStream_t s) {
     const size_t tile = (size_t)(kHalfPix + 16) * (CIN + 8) * sizeof(_Float16);
-    if (tower_mf() == 16) {
+    if (stream_mf() == 16) {
         const size_t tile16 = (size_t)(kHalfPix + 16) * (CIN + 16) * sizeof(_Float16);
         hipLaunchKernelGGL((conv3x3_stream_kernel<H, W, BPH, CIN, 2, 16>), dim3((n + BPH - 1) / BPH), dim3(256),
                            std::max(tile16, kHalfEpiBytes), s, n, (const _Float16 *)in, (const _Float16 *)wp, bias,
