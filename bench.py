@@ -849,8 +849,12 @@ def tower_mode(dev, reps: int = 5) -> dict:
     n = 32768
     x = (torch.rand(n, 17, 8, 8, device=dev) < 0.3).half()
     flop = flops_per_position(128, 8, 32, 8, 8) * n
-    out = {"boards": n, "board": "8x8", "net": "ValueNetwork(128, 8), fp16, BN folded"}
-    for fused in (True, False):
+    out = {"boards": n, "board": "8x8", "net": "ValueNetwork(128, 8), fp16, BN folded",
+           "form": "fused: 16x16x32 MFMA form (the default); fused_32x32x16: the round-3 form (ZC_TOWER_MF=32)"}
+    saved = os.environ.pop("ZC_TOWER_MF", None)
+    for key, fused, mf in (("fused", True, None), ("fused_32x32x16", True, "32"), ("layered", False, None)):
+        if mf:
+            os.environ["ZC_TOWER_MF"] = mf
         net.tower(x, fused=fused)
         ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
         torch.cuda.synchronize(dev)
@@ -859,11 +863,13 @@ def tower_mode(dev, reps: int = 5) -> dict:
             net.tower(x, fused=fused)
         ev[1].record()
         torch.cuda.synchronize(dev)
+        os.environ.pop("ZC_TOWER_MF", None)
         ms = ev[0].elapsed_time(ev[1]) / reps
-        key = "fused" if fused else "layered"
         out[key] = {"ms": round(ms, 3), "tflops": round(flop / ms / 1e9, 1),
                     "frac_of_2p5PF": round(flop / ms / 1e9 / MFMA_F16_PEAK_TFLOPS, 4)}
-    out["pmc"] = "profiles/r03_tower_pmc.json (MFMA busy, held clock)"
+    if saved is not None:
+        os.environ["ZC_TOWER_MF"] = saved
+    out["pmc"] = "profiles/r04_tower_pmc.json (MFMA busy, held clock)"
     return out
 
 
