@@ -359,6 +359,10 @@ int zc_c4_selfplay_pooled_async(zc_engine *eng, int32_t first, int32_t n, zc_c4_
     ZC_HIP(hipSetDevice(eng->cfg.device));
     // A wave takes its tickets only once resident: with more games than the chip holds at
     // once, the first waves could spend the whole budget and the rest never move.  Refused.
+    // The check assumes the device runs nothing else: ranks sharing one GPU (bench.py
+    // --share-device, a rehearsal mode) or concurrent kernels can still delay some
+    // workgroups past the budget, and those games then make no move in that launch (their
+    // rows report ZC_SLOT_IDLE; nothing is lost, only the moves' spread over games shifts).
     int resident = 0;
     if (zc::c4_selfplay_resident_games(bs, eng->rollout_mode == ZC_ROLLOUT_PHILOX, &resident))
         return fail(ZC_EHIP, "occupancy query failed");
