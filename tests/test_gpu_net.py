@@ -138,15 +138,17 @@ def _integer_net(c, blocks, seed, density=0.002):
     return net
 
 
-@pytest.mark.parametrize("mf", ["32", "16"])
+@pytest.mark.parametrize("mf", ["32", "16", "16e"])
 @pytest.mark.parametrize("shape", [(17, 8, 8), (2, 6, 7)])
 def test_tower_forms_exact_on_integers(mf, shape, monkeypatch):
-    """Both MFMA forms of the fused tower (ZC_TOWER_MF: 32x32x16, 16x16x32) on an integer
-    network, 2 residual blocks, ragged board counts: equal to float64 exactly."""
+    """Both MFMA forms of the fused tower (ZC_TOWER_MF: 32x32x16, 16x16x32; "16e": the
+    16x16x32 form with the swap epilogue, ZC_TOWER_EPI=1) on an integer network, 2 residual
+    blocks, ragged board counts: equal to float64 exactly."""
     from zeroclone_amd.nets import FoldedValueNetwork, MfmaValueNetwork
-    monkeypatch.setenv("ZC_TOWER_MF", mf)
+    monkeypatch.setenv("ZC_TOWER_MF", mf[:2])
+    monkeypatch.setenv("ZC_TOWER_EPI", "1" if mf.endswith("e") else "0")
     c, h, w = shape
-    vnet = _integer_net(c, 2, seed=h * 10 + int(mf))
+    vnet = _integer_net(c, 2, seed=h * 10 + int(mf[:2]))
     net = MfmaValueNetwork(vnet)
     f = FoldedValueNetwork(vnet).double()
     for n in (1, 5, 131):

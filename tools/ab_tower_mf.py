@@ -29,11 +29,12 @@ def main():
         net = MfmaValueNetwork(vnet, "cuda")
         g = torch.Generator(device="cuda").manual_seed(1)
         x = (torch.rand(n, planes, h, w, device="cuda", generator=g) < 0.3).half()
-        res = {"32": [], "16": []}
+        res = {"32": [], "16": [], "16e": []}
         outs = {}
         for _ in range(rounds):
-            for mf in ("32", "16"):
-                os.environ["ZC_TOWER_MF"] = mf
+            for mf in ("32", "16", "16e"):
+                os.environ["ZC_TOWER_MF"] = mf[:2]
+                os.environ["ZC_TOWER_EPI"] = "1" if mf.endswith("e") else "0"
                 a, _ = net.tower(x)
                 torch.cuda.synchronize()
                 outs[mf] = a.clone()
@@ -51,6 +52,7 @@ def main():
             torch.cuda.synchronize()
             same[mf] = bool(torch.equal(outs[mf], layered))
         os.environ.pop("ZC_TOWER_MF", None)
+        os.environ.pop("ZC_TOWER_EPI", None)
         # torch fp32 reference on 2048 boards (the folded network, NHWC-compared)
         k = 2048
         f = FoldedValueNetwork(vnet).float().cuda()
@@ -63,6 +65,9 @@ def main():
             "mf32_ms": statistics.median(res["32"]), "mf16_ms": statistics.median(res["16"]),
             "mf32_tflops": round(flop / statistics.median(res["32"]) / 1e9, 1),
             "mf16_tflops": round(flop / statistics.median(res["16"]) / 1e9, 1),
+            "mf16e_ms": statistics.median(res["16e"]),
+            "mf16e_tflops": round(flop / statistics.median(res["16e"]) / 1e9, 1),
+            "mf16e_equals_mf16": bool(torch.equal(outs["16e"], outs["16"])),
             "all_ms": res,
             "fused_equals_layered": same,
             "max_abs_mf16_vs_mf32": float((outs["16"].float() - outs["32"].float()).abs().max()),

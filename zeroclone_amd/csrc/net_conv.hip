@@ -833,6 +833,41 @@ __device__ __forceinline__ void tower_epilogue16(_Float16 *dst, const float4 (&b
     }
 }
 
+// tower_epilogue16 with whole 16-byte stores: the per-element arithmetic in the MFMA layout
+// (residual read per 4 channels, as there), then one v_permlane16_swap per dword hands lane
+// (pixel, q) the 8 consecutive channels wave * 32 + 16 (q & 1) + 8 (q >> 1) .. + 7 of its
+// pixel (rows 0 / 2 keep M tile 0 and take the next row's, rows 1 / 3 the M tile 1 halves):
+// 8 ds_write_b128 per layer and wave instead of 16 ds_write_b64, 2-way instead of 4-way on
+// the 72-dword rows.  Every lane takes part in the swaps; only the store is predicated.
+template <int NN>
+__device__ __forceinline__ void tower_epilogue16_swap(_Float16 *dst, const float4 (&bv)[2], bool res, int npix,
+                                                      int wave, int l16, int q, const f4x (&acc)[2][NN]) {
+    constexpr int LD = tower_ld<16>();
+    const int co8 = wave * 32 + 16 * (q & 1) + 8 * (q >> 1);
+#pragma unroll
+    for (int n = 0; n < NN; ++n) {
+        const int P = n * 16 + l16;
+        uint32_t pk[2][2];
+#pragma unroll
+        for (int m = 0; m < 2; ++m) {
+            float v[4] = {acc[m][n][0] + bv[m].x, acc[m][n][1] + bv[m].y, acc[m][n][2] + bv[m].z,
+                          acc[m][n][3] + bv[m].w};
+            if (res) {
+                const h4 rv = *(const h4 *)(dst + P * LD + wave * 32 + 16 * m + 4 * q);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) v[e] += (float)rv[e];
+            }
+            h4 ov;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) ov[e] = (_Float16)fmaxf(v[e], 0.0f);
+            __builtin_memcpy(pk[m], &ov, 8);
+        }
+        const auto s0 = __builtin_amdgcn_permlane16_swap(pk[0][0], pk[1][0], false, false);
+        const auto s1 = __builtin_amdgcn_permlane16_swap(pk[0][1], pk[1][1], false, false);
+        if (P < npix) *(uint4 *)(dst + P * LD + co8) = make_uint4(s0[0], s1[0], s0[1], s1[1]);
+    }
+}
+
 // The policy head's 1x1 conv (PolicyValueNetwork.policy[0..2]: 128 -> 32 channels, BN folded,
 // ReLU) on the tower's output while it is still in LDS (tower_policy): pw = the folded
 // weights as 32x32x16 MFMA A fragments [8 k-steps][64 lanes][8] (lane = output channel
@@ -843,7 +878,7 @@ struct TowerPolicy {
     _Float16 *out;
 };
 
-template <int H, int W, int BPH, int CIN0, int NT, int WPE, int PG = 1, int MF = 32>
+template <int H, int W, int BPH, int CIN0, int NT, int WPE, int PG = 1, int MF = 32, int EPI = 0>
 __global__ __launch_bounds__(256 * PG) __attribute__((amdgpu_waves_per_eu(WPE, WPE))) void tower_kernel(
     int nboards, int nconv, const _Float16 *__restrict__ in, const _Float16 *__restrict__ wall,
     const float *__restrict__ ball, _Float16 *__restrict__ out, const float *__restrict__ fcw, float fcb,
@@ -927,7 +962,10 @@ __global__ __launch_bounds__(256 * PG) __attribute__((amdgpu_waves_per_eu(WPE, W
 #pragma unroll
             for (int m = 0; m < 2; ++m) bv[m] = *(const float4 *)(ball + (size_t)l * kCout + wave * 32 + 16 * m + 4 * q4);
             tower_mfma16<H, W, NP, KC, 8, LD, tower_zero<NT>(), ZR>(lds, src, wa, wn, a, l16, py16, q4, acc);
-            tower_epilogue16<NP>(lds + dst * LD, bv, l >= 2 && !(l & 1), npix, wave, l16, q4, acc);
+            if constexpr (EPI == 1)
+                tower_epilogue16_swap<NP>(lds + dst * LD, bv, l >= 2 && !(l & 1), npix, wave, l16, q4, acc);
+            else
+                tower_epilogue16<NP>(lds + dst * LD, bv, l >= 2 && !(l & 1), npix, wave, l16, q4, acc);
         } else {
             int pr[NT], py[NT];
 #pragma unroll
@@ -1016,12 +1054,25 @@ __global__ __launch_bounds__(256 * PG) __attribute__((amdgpu_waves_per_eu(WPE, W
     }
 }
 
+int tower_epi() {  // ZC_TOWER_EPI=1: the 16x16x32 form's epilogue with 16-byte stores (A/B switch)
+    const char *e = getenv("ZC_TOWER_EPI");
+    return e && !strcmp(e, "1") ? 1 : 0;
+}
+
 template <int H, int W, int BPH, int NT, int WPE, int PG = 1, int MF = 32>
 void launch_tower(int n, int nconv, const void *in, const void *wall, const float *ball, void *out, const float *fcw,
                   float fcb, double *values, TowerPolicy pol, hipStream_t s) {
-    hipLaunchKernelGGL((tower_kernel<H, W, BPH, 32, NT, WPE, PG, MF>), dim3((n + BPH - 1) / BPH), dim3(256 * PG),
-                       (tower_lds<NT, PG, MF>()), s, n, nconv, (const _Float16 *)in, (const _Float16 *)wall, ball,
-                       (_Float16 *)out, fcw, fcb, values, pol);
+    if constexpr (MF == 16) {
+        if (tower_epi() == 1) {
+            hipLaunchKernelGGL((tower_kernel<H, W, BPH, 32, NT, WPE, PG, MF, 1>), dim3((n + BPH - 1) / BPH),
+                               dim3(256 * PG), (tower_lds<NT, PG, MF>()), s, n, nconv, (const _Float16 *)in,
+                               (const _Float16 *)wall, ball, (_Float16 *)out, fcw, fcb, values, pol);
+            return;
+        }
+    }
+    hipLaunchKernelGGL((tower_kernel<H, W, BPH, 32, NT, WPE, PG, MF>), dim3((n + BPH - 1) / BPH),
+                           dim3(256 * PG), (tower_lds<NT, PG, MF>()), s, n, nconv, (const _Float16 *)in,
+                           (const _Float16 *)wall, ball, (_Float16 *)out, fcw, fcb, values, pol);
 }
 
 
