@@ -501,7 +501,8 @@ int zc_debug_c4_puct_tree(zc_engine *eng, int32_t game, int32_t max_nodes, void 
  *     [nconv][128] f32, d_out = [n][h*w][128] fp16 or NULL; all 16-byte aligned.  With
  *     d_values (fp64 [n]) the value head runs in the same launch on the on-chip activation
  *     (d_fc_w [128] f32, fc_b; bit-identical to zc_net_value_head_async), so a value-only
- *     network needs no d_out.  cin0 = 32, nconv odd, (h, w) in {(8, 8), (6, 7)}.
+ *     network needs no d_out.  cin0 = 32, nconv odd, (h, w) in {(8, 8), (6, 7)}.  Runs the
+ *     16x16x32 MFMA form (environment ZC_TOWER_MF=32: the 32x32x16 form; same outputs).
  *   zc_net_planes_to_nhwc_async: state_to_tensor planes [n][cin][h*w] fp16 -> [n][h*w][cpad],
  *     zero padded; cpad a multiple of 8 (16-byte rows), d_out 16-byte aligned.
  *   zc_net_value_head_async: mean over pixels -> dot(fc_w[128]) + fc_b -> tanh, as fp64
