@@ -22,6 +22,11 @@
 
 #include "../../include/zeroclone.h"
 
+#ifndef CDEV_T  // diagnostic phase stamps (chess_tree.h under ZC_CHESS_STAMP); no-ops otherwise
+#define CDEV_T(v)
+#define CDEV_ADD(k, t0)
+#endif
+
 namespace zc {
 namespace chessdev {
 namespace {
@@ -105,6 +110,11 @@ struct BitView {
     __device__ __forceinline__ uint32_t piece_at(int s) const {  // only "is it the mover's king" is asked
         return ((kings >> s) & 1ull) ? (t == 0 ? 'K' : 'k') : 0u;
     }
+    // the capture value of a move to `to` (0 when nothing capturable stands there)
+    __device__ __forceinline__ uint32_t capval(int to) const {
+        if (!((cap >> to) & 1ull)) return 0u;
+        return ((tP >> to) & 1ull) ? 1u : ((tNB >> to) & 1ull) ? 3u : ((tR >> to) & 1ull) ? 5u : 9u;
+    }
     // king_attacked (:85-144) for the mover's king on square k (0..63) after the piece on
     // `from` moved to `to` (-1, -1: the position as it stands): the moved piece is the
     // mover's, so it only blocks; the enemy piece it captured, if any, no longer attacks.
@@ -145,7 +155,9 @@ struct BitView {
 };
 
 // Pseudo-legal moves of the piece `pc` on square s from the BitView's masks, in the
-// reference's order (piece_moves below is the square-by-square statement of it): target
+// reference's order (piece_moves below is the square-by-square statement of it), emitted
+// WITHOUT their capture values (0): legal_moves_view adds BitView::capval in its lane-per-move
+// legality pass, off the serial emission loops.  Target
 // sets come from shifts and masked bit scans, then each set is emitted in its order — a
 // knight's eight offsets (-17 ... +17) are in index order, a king's are tested one by one
 // in kAll8 order, and a slider's rays run away from s (descending indices for the
@@ -155,22 +167,18 @@ __device__ __forceinline__ void bit_piece_moves(const BitView &v, int s, uint32_
     const int r = s >> 3, c = s & 7;
     const uint32_t up = upper(pc);
     const uint64_t empty = ~v.occ, ok = ~v.occ | v.cap;
-    auto val = [&](int to) -> uint32_t {
-        if (!((v.cap >> to) & 1ull)) return 0u;
-        return ((v.tP >> to) & 1ull) ? 1u : ((v.tNB >> to) & 1ull) ? 3u : ((v.tR >> to) & 1ull) ? 5u : 9u;
-    };
     auto asc = [&](uint64_t T) {
         while (T) {
             const int to = __builtin_ctzll(T);
             T &= T - 1ull;
-            emit(s, to, val(to));
+            emit(s, to, 0u);
         }
     };
     auto desc = [&](uint64_t T) {
         while (T) {
             const int to = 63 - __builtin_clzll(T);
             T &= ~(1ull << to);
-            emit(s, to, val(to));
+            emit(s, to, 0u);
         }
     };
     const uint64_t kb = 1ull << s;
@@ -184,8 +192,8 @@ __device__ __forceinline__ void bit_piece_moves(const BitView &v, int s, uint32_
                 const int t2 = t1 + (white ? -8 : 8);
                 if (r == (white ? 6 : 1) && ((empty >> t2) & 1ull)) emit(s, t2, 0u);
             }
-            if (c > 0 && ((v.cap >> (t1 - 1)) & 1ull)) emit(s, t1 - 1, val(t1 - 1));
-            if (c < 7 && ((v.cap >> (t1 + 1)) & 1ull)) emit(s, t1 + 1, val(t1 + 1));
+            if (c > 0 && ((v.cap >> (t1 - 1)) & 1ull)) emit(s, t1 - 1, 0u);
+            if (c < 7 && ((v.cap >> (t1 + 1)) & 1ull)) emit(s, t1 + 1, 0u);
         }
     } else if (up == 'N') {
         asc(ok & (((kb << 17) & kNotA) | ((kb << 15) & kNotH) | ((kb << 10) & kNotAB) | ((kb << 6) & kNotGH) |
@@ -197,7 +205,7 @@ __device__ __forceinline__ void bit_piece_moves(const BitView &v, int s, uint32_
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
             const int to = s + off[i];
-            if ((unsigned)to < 64u && ((T >> to) & 1ull)) emit(s, to, val(to));
+            if ((unsigned)to < 64u && ((T >> to) & 1ull)) emit(s, to, 0u);
         }
     } else if (up == 'B' || up == 'R' || up == 'Q') {
         const uint64_t low = kb - 1ull, high = ~low & ~kb;
@@ -228,13 +236,13 @@ __device__ __forceinline__ void bit_piece_moves(const BitView &v, int s, uint32_
     }
 }
 
-__device__ __forceinline__ bool known_piece(uint32_t x) {
-    switch (x) {
-        case 0: case ' ':
-        case 'P': case 'N': case 'B': case 'R': case 'Q': case 'K':
-        case 'p': case 'n': case 'b': case 'r': case 'q': case 'k': return true;
-        default: return false;
-    }
+__device__ __forceinline__ bool known_piece(uint32_t x) {  // 0, ' ', PNBRQK, pnbrqk
+    constexpr uint64_t kLo = (1ull << 0) | (1ull << ' ');
+    constexpr uint64_t kHi = (1ull << ('P' - 64)) | (1ull << ('N' - 64)) | (1ull << ('B' - 64)) |
+                             (1ull << ('R' - 64)) | (1ull << ('Q' - 64)) | (1ull << ('K' - 64)) |
+                             (1ull << ('p' - 64)) | (1ull << ('n' - 64)) | (1ull << ('b' - 64)) |
+                             (1ull << ('r' - 64)) | (1ull << ('q' - 64)) | (1ull << ('k' - 64));
+    return x < 64u ? ((kLo >> x) & 1ull) != 0ull : x < 128u ? ((kHi >> (x - 64u)) & 1ull) != 0ull : false;
 }
 
 // The BitView of the board for side t to move, built from x = this lane's square.  Returns
@@ -392,16 +400,21 @@ __device__ __forceinline__ int legal_moves_view(const V &v, int t, uint32_t pc, 
     uint16_t *const own = reg + s * kRegion;
     uint32_t cnt = 0;
     auto put = [&](int f, int to, uint32_t val) { own[cnt++] = (uint16_t)pack_move(f, to, val); };
+    CDEV_T(cd11);
     if (mine) {
         if constexpr (V::kCheapProbe) bit_piece_moves(v, (int)s, pc, put);
         else piece_moves(v, (int)s, pc, put);
     }
+    CDEV_ADD(11, cd11);
+    CDEV_T(cd12);
     uint32_t total;
     const uint32_t off = wave_excl_sum(cnt, total);
     if (total > (uint32_t)kMaxPseudo) return -1;
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     for (uint32_t k = 0; k < cnt; ++k) ps[off + k] = own[k];
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    CDEV_ADD(12, cd12);
+    CDEV_T(cd13);
     const uint32_t kch = t == 0 ? 'K' : 'k';
     int n = 0;
     for (uint32_t base = 0; base < total; base += 64) {
@@ -411,6 +424,7 @@ __device__ __forceinline__ int legal_moves_view(const V &v, int t, uint32_t pc, 
         if (i < total) {
             m = ps[i];
             const int from = (int)(m & 63u), to = (int)((m >> 6) & 63u);
+            if constexpr (V::kCheapProbe) m |= v.capval(to) << 12;
             const uint32_t mp = v.piece_at(from);
             // find_king on the board after the move: first square holding the mover's king
             const uint64_t km = (kings & ~(1ull << from)) | (mp == kch ? (1ull << to) : 0ull);
@@ -423,6 +437,7 @@ __device__ __forceinline__ int legal_moves_view(const V &v, int t, uint32_t pc, 
         n += __popcll(L);
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    CDEV_ADD(13, cd13);
     return n > kMaxLegal ? -1 : n;
 }
 
@@ -443,28 +458,36 @@ __device__ __forceinline__ int legal_moves(const uint8_t *b, int t, uint16_t *ou
     return legal_moves_view(ByteView{b, t}, t, pc, king_mask(b, t), out, ps, reg);
 }
 
-// get_legal_moves and king_attacked of the side to move (check_win, crude_chess_score) on
-// one board view.
+// get_legal_moves and, for a position without legal moves, king_attacked of the side to
+// move (check_win, crude_chess_score's mate score) on one board view; `check` is false when
+// the position has moves.
 __device__ __forceinline__ int legal_moves_check(const uint8_t *b, int t, uint16_t *out, uint16_t *ps, uint16_t *reg,
                                                  bool &check) {
+    CDEV_T(cd14);
     const uint32_t pc = b[lane()];
     BitView bv;
     const bool fast = make_bitview(pc, t, bv);
-    uint64_t kings;
-    if (fast) {
-        kings = bv.kings;
-        check = bv.attacked(__builtin_ctzll(kings), -1, -1, 0);
-    } else {
-        kings = king_mask(b, t);
-        const int ks = kings ? __builtin_ctzll(kings) : -1;
-        check = attacked_after(b, t, ks >= 0 ? ks >> 3 : -1, ks >= 0 ? ks & 7 : -1, -1, -1, 0);
-    }
+    const uint64_t kings = fast ? bv.kings : king_mask(b, t);
+    CDEV_ADD(14, cd14);
     const uint32_t up = upper(pc);
     const uint64_t heavy = __ballot(up == 'P' || up == 'R' || up == 'Q');
     const int minor = __popcll(__ballot(up == 'B' || up == 'N'));
-    if (!heavy && minor <= 1) return 0;  // insufficient material (:188-198)
-    return fast ? legal_moves_view(bv, t, pc, kings, out, ps, reg)
-                : legal_moves_view(ByteView{b, t}, t, pc, kings, out, ps, reg);
+    int n = 0;
+    if (heavy || minor > 1)  // else insufficient material (:188-198): no moves
+        n = fast ? legal_moves_view(bv, t, pc, kings, out, ps, reg)
+                 : legal_moves_view(ByteView{b, t}, t, pc, kings, out, ps, reg);
+    // every caller asks "in check?" only of a position without moves (checkmate against
+    // stalemate): the king test runs only then, and `check` is false otherwise
+    check = false;
+    if (n == 0) {
+        if (fast) {
+            check = bv.attacked(__builtin_ctzll(kings), -1, -1, 0);
+        } else {
+            const int ks = kings ? __builtin_ctzll(kings) : -1;
+            check = attacked_after(b, t, ks >= 0 ? ks >> 3 : -1, ks >= 0 ? ks & 7 : -1, -1, -1, 0);
+        }
+    }
+    return n;
 }
 
 // Sum of piece values, white positive (crude_chess_score's material), by ballots.
@@ -497,6 +520,43 @@ __device__ __forceinline__ void apply_move(zc_chess_state &o, uint32_t m) {
     b[from] = ' ';
     if (tr == 0 && pc == 'P') b[to] = 'Q';
     if (tr == 7 && pc == 'p') b[to] = 'q';
+}
+
+// apply_move with one square per lane (all lanes call it; the position in `o` is complete
+// and visible to the wave): lane l computes square l of the position after the move from
+// the writes apply_move makes, in their order — a castling rook's two squares, then
+// b[to] = pc, b[from] = ' ', then the promotion on `to` — and lane 0 the counters.  The
+// caller fences before the result is read.
+__device__ __forceinline__ void apply_move_wave(zc_chess_state &o, uint32_t m) {
+    const uint32_t l = lane();
+    const int from = (int)(m & 63u), to = (int)((m >> 6) & 63u);
+    const int fc = from & 7, tc = to & 7, tr = to >> 3;
+    uint8_t *b = o.board;
+    const uint32_t pc = b[from], trg = b[to], x0 = b[l];
+    const int turn = o.turn;
+    uint32_t x = x0;
+    const int dcol = tc - fc;
+    if (pc == 'K' && dcol == 2) x = l == 61 ? 'R' : l == 63 ? ' ' : x;
+    if (pc == 'k' && dcol == 2) x = l == 5 ? 'r' : l == 7 ? ' ' : x;
+    if (pc == 'K' && dcol == -2) x = l == 59 ? 'R' : l == 56 ? ' ' : x;
+    if (pc == 'k' && dcol == -2) x = l == 3 ? 'r' : l == 0 ? ' ' : x;
+    if ((int)l == to) x = pc;
+    if ((int)l == from) x = ' ';
+    if ((int)l == to && tr == 0 && pc == 'P') x = 'Q';
+    if ((int)l == to && tr == 7 && pc == 'p') x = 'q';
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // every lane has read the old board
+    if (x != x0) b[l] = (uint8_t)x;
+    if (l == 0) {
+        uint32_t fifty = (uint32_t)o.fifty + 1u, castle = o.castle;
+        if (pc == 'P' || pc == 'p' || !(trg == ' ' || trg == 0)) fifty = 0;
+        if (pc == 'K' || (pc == 'R' && fc == 7)) castle &= ~1u;
+        if (pc == 'K' || (pc == 'R' && fc == 0)) castle &= ~2u;
+        if (pc == 'k' || (pc == 'r' && fc == 7)) castle &= ~4u;
+        if (pc == 'k' || (pc == 'r' && fc == 0)) castle &= ~8u;
+        o.turn = (uint8_t)(1 - turn);
+        o.fifty = (uint8_t)fifty;
+        o.castle = (uint8_t)castle;
+    }
 }
 
 // has_repeated_prefix (chess_backend.cpp:148-180; min_pattern_len 2, min_repeats 3) of the

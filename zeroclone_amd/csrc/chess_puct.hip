@@ -88,7 +88,7 @@ __device__ int puct_walk(const ChessParams &p, const CTree &t, CLds &L, int &nno
         const uint32_t m = uni((uint32_t)t.mv[s]);
         if (lane < 18) ((uint32_t *)&L.st)[lane] = ((const uint32_t *)&N->st)[lane];
         wave_sync_mem();
-        if (lane == 0) chessdev::apply_move(L.st, m);
+        chessdev::apply_move_wave(L.st, m);
         wave_sync_mem();
         const int id = nnodes++;
         if (id >= p.M) {

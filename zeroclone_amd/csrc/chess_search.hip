@@ -118,7 +118,10 @@ __device__ int simulate(const ChessParams &p, const CTree &t, CLds &L, ConstDoub
         nN = rs.nN;
         pathv = rs.pathv;
     }
+    CSTAMP_T(cs0);
     if (!rs.cached) chess_walk(p, t, logtab, node, depth, nN, pathv, status);
+    CSTAMP_ADD(0, cs0);
+    CSTAMP_T(cs1);
     ChessNode *N = &t.nodes[node];
     const bool hit = rs.cached;
     const int nu = hit ? rs.nu : uni((int)N->nu);
@@ -152,8 +155,19 @@ __device__ int simulate(const ChessParams &p, const CTree &t, CLds &L, ConstDoub
         if (p.policy == 1) {
             // Policy('immediate_value') (policy_functions.py:14-17): random.choice over the
             // untried moves whose capture value >= max - policy_freedom
-            int v = lane < (uint32_t)nu ? (int)(mvv >> 12) : -1;
-            for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o));
+            // the maximum capture value (4 bits) of the untried moves, bit by bit from the top
+            // with ballots instead of a cross-lane shuffle reduction (nu >= 1 here)
+            const uint32_t cv = mvv >> 12;
+            uint64_t cand = __ballot(lane < (uint32_t)nu);
+            int v = 0;
+#pragma unroll
+            for (int bit = 3; bit >= 0; --bit) {
+                const uint64_t B = __ballot(((cand >> lane) & 1ull) && ((cv >> bit) & 1u));
+                if (B) {
+                    v |= 1 << bit;
+                    cand = B;
+                }
+            }
             const double thr = (double)v - p.freedom;
             const uint64_t cm = __ballot(lane < (uint32_t)nu && (double)(mvv >> 12) >= thr);
             const uint32_t r = rng_below(rng, (uint32_t)__popcll(cm));
@@ -210,16 +224,21 @@ __device__ int simulate(const ChessParams &p, const CTree &t, CLds &L, ConstDoub
         m = uni((uint32_t)t.mv[base + midx]);
     }
     if (lane == 0) N->nu = (uint16_t)(nu - 1);
+    CSTAMP_ADD(1, cs1);
+    CSTAMP_T(cs2);
     if (lane < 18) ((uint32_t *)&L.st)[lane] = stw;
     wave_sync_mem();
-    if (lane == 0) chessdev::apply_move(L.st, m);
+    chessdev::apply_move_wave(L.st, m);
     wave_sync_mem();
+    CSTAMP_ADD(2, cs2);
     const int child = nnodes++;
     if (child >= p.M) {
         status = ZC_STATUS_INTERNAL;
         return node;
     }
+    CSTAMP_T(cs3);
     create_node(t, L, child, node, midx, depth + 1, slots, status);
+    CSTAMP_ADD(3, cs3);
     if (lane == 0) t.ch[base + midx] = (uint16_t)child;
     ++depth;
     if (lane == (uint32_t)depth) pathv = base + (uint32_t)midx;
@@ -364,10 +383,14 @@ __device__ void chess_backup_flush(const ChessParams &p, const CTree &t, int g, 
 __device__ void crude_search(const ChessParams &p, const CTree &t, CLds &L, double *s_vals, int gl, int g,
                              int32_t *ctl) {
     ConstDouble *logtab = (ConstDouble *)p.a.logtab;
+    CSTAMP_T(cs7);
     root_init(p, t, L, gl, g, ctl);
     const uint32_t *meta = p.ca.meta + (size_t)g * p.max_batch;
     for (int done = 0; done < p.sims && !uni(ctl[cStatus]);) {
+        CSTAMP_T(cs6);
         const int nb = chess_select_flush(p, t, L, logtab, g, ctl, done, min(p.bs, p.sims - done));
+        CSTAMP_ADD(6, cs6);
+        CSTAMP_T(cs4);
         // value.batch: crude_chess_score of every pending leaf (mcts.cpp:116-118)
         for (int j = (int)lane_id(); j < nb; j += 64) {
             const ChessNode *N = &t.nodes[meta[j] & 0xFFFFu];
@@ -375,9 +398,13 @@ __device__ void crude_search(const ChessParams &p, const CTree &t, CLds &L, doub
             s_vals[j] = (nm == 0 && chk) ? 1000.0 : (double)((turn * -2 + 1) * mat);
         }
         wave_sync_mem();
+        CSTAMP_ADD(4, cs4);
+        CSTAMP_T(cs5);
         chess_backup_flush(p, t, g, ctl, s_vals, nb);
+        CSTAMP_ADD(5, cs5);
         done += nb;
     }
+    CSTAMP_ADD(7, cs7);
 }
 
 __global__ __launch_bounds__(64) void chess_search_kernel(ChessParams p) {
@@ -388,7 +415,9 @@ __global__ __launch_bounds__(64) void chess_search_kernel(ChessParams p) {
     const int g = p.first_game + gl;
     const CTree t = ctree(p, g);
     int32_t *ctl = p.ca.ctl + (size_t)g * kCtlWords;
+    CSTAMP_INIT();
     crude_search(p, t, L, s_vals, gl, g, ctl);
+    CSTAMP_FLUSH();
     finish(p, t, gl, g, ctl);
 }
 
@@ -403,7 +432,7 @@ __device__ int chess_play_judge(const ChessPlayParams &q, int gl, CLds &L, uint1
     if (lane < 18) ((uint32_t *)&L.st)[lane] = ((const uint32_t *)&q.roots[gl])[lane];
     wave_sync_mem();
     const int mover = uni((int)L.st.turn);
-    if (lane == 0) chessdev::apply_move(L.st, m);
+    chessdev::apply_move_wave(L.st, m);
     wave_sync_mem();
     L.s.board[lane] = L.st.board[lane];
     wave_sync_mem();
@@ -689,7 +718,7 @@ __global__ __launch_bounds__(64) void chess_hp_expand_kernel(ChessParams p) {
         if (lane == 0) N->nu = (uint16_t)(nu - 1);
         if (lane < 18) ((uint32_t *)&L.st)[lane] = ((const uint32_t *)&N->st)[lane];
         wave_sync_mem();
-        if (lane == 0) chessdev::apply_move(L.st, m);
+        chessdev::apply_move_wave(L.st, m);
         wave_sync_mem();
         const int child = nnodes++;
         create_node(t, L, child, node, midx, depth + 1, slots, status);
@@ -811,7 +840,7 @@ __device__ int chess_rollout(CLds &L, RollSide &w, RollSide &k, R &rng, int &sta
         }
         if (turn) roll_side_push(k, m);
         else roll_side_push(w, m);
-        if (lane == 0) chessdev::apply_move(L.st, m);
+        chessdev::apply_move_wave(L.st, m);
         wave_sync_mem();
     }
 }
@@ -953,3 +982,16 @@ void launch_chess_leaf_moves(const ChessParams &p, hipStream_t s) {
 }
 
 }  // namespace zc
+
+#if ZC_CHESS_STAMP
+// diagnostic build only (not in include/zeroclone.h): copy / clear the phase stamps
+extern "C" int zc_debug_chess_stamps(uint64_t *host, int n, int clear) {
+    if (n > 4096 * 16) n = 4096 * 16;
+    if (hipMemcpyFromSymbol(host, HIP_SYMBOL(zc::g_chess_stamp), (size_t)n * 8) != hipSuccess) return 1;
+    if (clear) {
+        static uint64_t zeros[4096 * 16];
+        if (hipMemcpyToSymbol(HIP_SYMBOL(zc::g_chess_stamp), zeros, sizeof(zeros)) != hipSuccess) return 1;
+    }
+    return 0;
+}
+#endif

@@ -2,6 +2,50 @@
 // slots) and the wave-level helpers shared by the UCT search (chess_search.hip) and the
 // PUCT search (chess_puct.hip).  Included by exactly those translation units.
 #pragma once
+#include <hip/hip_runtime.h>
+
+#ifndef ZC_CHESS_STAMP
+#define ZC_CHESS_STAMP 0  // diagnostic build: per-game s_memtime cycles per phase (tools/chess_stamps.py)
+#endif
+#if ZC_CHESS_STAMP
+// [game of the launch][16]: walk, policy + erase, apply_move, create_node, values, backup,
+// select flush (whole), whole search, legal_moves_check, material, node writes,
+// and inside legal_moves_check: emission, copy, legality, bit view + check.  A region adds
+// its cycles to the workgroup's LDS copy with a no-return LDS atomic (no wait on the chain);
+// the kernel folds the LDS copy into the global table once at its end (CSTAMP_FLUSH).
+namespace zc {
+namespace {
+__device__ uint64_t g_chess_stamp[4096 * 16];
+__shared__ uint64_t s_chess_stamp[16];
+}  // namespace
+}  // namespace zc
+#define CSTAMP_T(v) const uint64_t v = __builtin_amdgcn_s_memtime()
+#define CSTAMP_ADD(k, t0)                                                                          \
+    do {                                                                                           \
+        const uint64_t now_ = __builtin_amdgcn_s_memtime();                                        \
+        if (__lane_id() == 0)                                                                      \
+            __hip_atomic_fetch_add(&::zc::s_chess_stamp[(k)], now_ - (t0), __ATOMIC_RELAXED,       \
+                                   __HIP_MEMORY_SCOPE_WORKGROUP);                                  \
+    } while (0)
+#define CSTAMP_INIT()                                                                              \
+    do {                                                                                           \
+        if (__lane_id() < 16) ::zc::s_chess_stamp[__lane_id()] = 0;                                \
+    } while (0)
+#define CSTAMP_FLUSH()                                                                             \
+    do {                                                                                           \
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");                                     \
+        if (__lane_id() < 16 && blockIdx.x < 4096)                                                 \
+            ::zc::g_chess_stamp[blockIdx.x * 16 + __lane_id()] += ::zc::s_chess_stamp[__lane_id()]; \
+    } while (0)
+#else
+#define CSTAMP_T(v)
+#define CSTAMP_ADD(k, t0)
+#define CSTAMP_INIT()
+#define CSTAMP_FLUSH()
+#endif
+#define CDEV_T(v) CSTAMP_T(v)
+#define CDEV_ADD(k, t0) CSTAMP_ADD(k, t0)
+
 #include "c4_device.h"
 #include "chess_device.h"
 
@@ -46,12 +90,17 @@ __device__ void create_node(const CTree &t, CLds &L, int id, int parent, int pac
     wave_sync_mem();
     const int turn = uni((int)L.st.turn);
     bool check;
+    CSTAMP_T(cs8);
     int n = chessdev::legal_moves_check(L.s.board, turn, L.s.legal, L.s.pseudo, L.s.region, check);
+    CSTAMP_ADD(8, cs8);
     if (n < 0) {
         status = ZC_STATUS_CAPACITY;
         n = 0;
     }
+    CSTAMP_T(cs9);
     const int32_t mat = chessdev::material(sq);
+    CSTAMP_ADD(9, cs9);
+    CSTAMP_T(cs10);
     const int base = slots;
     if ((int64_t)base + n > t.S) {
         status = ZC_STATUS_CAPACITY;
@@ -79,6 +128,7 @@ __device__ void create_node(const CTree &t, CLds &L, int id, int parent, int pac
         N->evaluated = 0;
     }
     wave_sync_mem();
+    CSTAMP_ADD(10, cs10);
 }
 
 __device__ __forceinline__ void argmax64(double &v, int &i) {

@@ -140,7 +140,7 @@ struct ChessNode {
     uint16_t pact;       // slot index in the parent's move list (parent_action_idx)
     uint16_t depth;
     int16_t material;    // sum of piece values, white positive (crude_chess_score)
-    uint8_t check;       // side to move in check
+    uint8_t check;       // side to move in check, computed for a node without legal moves (0 otherwise)
     uint8_t evaluated;   // PUCT search: the network's priors are in the slots
     uint8_t pad[6];
 };
