@@ -390,29 +390,157 @@ __device__ __forceinline__ uint64_t king_mask(const uint8_t *b, int side) {
     return __ballot(b[lane()] == (side == 0 ? 'K' : 'k'));
 }
 
+// The BitView generator with one lane per (piece, direction) run instead of one lane per
+// piece.  A piece's moves are up to eight runs in the reference's order — a slider's rays in
+// kAll8 order (each away from s: descending indices for the directions that lower it), a
+// knight's targets as one ascending run, a king's eight kAll8 targets as eight one-square
+// runs, a pawn's push / double push / captures as four — so each square lane builds its
+// runs' target masks, two exclusive scans over the squares place the runs (records in `rec`,
+// 4 u32 each) and their moves (in `ps`), and then every lane emits ONE run: the serial loop
+// is as long as the longest run (<= 8) instead of a piece's whole move list.  Capture values
+// are added by the caller, as for bit_piece_moves.  Returns false, leaving nothing written,
+// when the position has more than 128 runs (never in reachable chess: <= 16 pieces).
+__device__ __forceinline__ bool bit_runs(const BitView &v, int s, uint32_t pc, bool mine, uint16_t *ps, uint32_t *rec,
+                                         uint32_t &total) {
+    const int r = s >> 3, c = s & 7;
+    const uint32_t up = upper(pc);
+    const uint64_t empty = ~v.occ, ok = ~v.occ | v.cap;
+    const uint64_t kb = 1ull << s;
+    uint64_t M[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint32_t desc = 0;  // bit k: run k is emitted from the highest index down
+    if (mine) {
+        if (up == 'P') {
+            const bool white = pc == 'P';
+            const int nr = r + (white ? -1 : 1);
+            if ((unsigned)nr < 8u) {
+                const int t1 = nr * 8 + c;
+                if ((empty >> t1) & 1ull) {
+                    M[0] = 1ull << t1;
+                    const int t2 = t1 + (white ? -8 : 8);
+                    if (r == (white ? 6 : 1) && ((empty >> t2) & 1ull)) M[1] = 1ull << t2;
+                }
+                if (c > 0) M[2] = v.cap & (1ull << (t1 - 1));
+                if (c < 7) M[3] = v.cap & (1ull << (t1 + 1));
+            }
+        } else if (up == 'N') {
+            M[0] = ok & (((kb << 17) & kNotA) | ((kb << 15) & kNotH) | ((kb << 10) & kNotAB) | ((kb << 6) & kNotGH) |
+                         ((kb >> 17) & kNotH) | ((kb >> 15) & kNotA) | ((kb >> 10) & kNotGH) | ((kb >> 6) & kNotAB));
+        } else if (up == 'K') {
+            const uint64_t T = ok & (((kb << 1) & kNotA) | ((kb >> 1) & kNotH) | (kb << 8) | (kb >> 8) |
+                                     ((kb << 9) & kNotA) | ((kb << 7) & kNotH) | ((kb >> 7) & kNotA) | ((kb >> 9) & kNotH));
+            constexpr int off[8] = {-9, -7, 7, 9, -8, 8, -1, 1};  // kAll8 order
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const int to = s + off[i];
+                M[i] = (unsigned)to < 64u ? T & (1ull << (to & 63)) : 0ull;
+            }
+        } else if (up == 'B' || up == 'R' || up == 'Q') {
+            const uint64_t low = kb - 1ull, high = ~low & ~kb;
+            const uint64_t file = kFileA << c, rank = 0xFFull << (8 * r);
+            const int dd = r - c, da = r + c - 7;
+            const uint64_t diag = dd >= 0 ? kDiag << (8 * dd) : kDiag >> (-8 * dd);
+            const uint64_t anti = da >= 0 ? kAnti << (8 * da) : kAnti >> (-8 * da);
+            auto up_ray = [&](uint64_t ray) {  // towards higher indices: through the nearest blocker
+                const uint64_t bl = ray & v.occ, first = bl & (0ull - bl);
+                return ok & (first ? ray & ((first << 1) - 1ull) : ray);
+            };
+            auto down_ray = [&](uint64_t ray) {  // towards lower indices
+                const uint64_t bl = ray & v.occ;
+                return ok & (bl ? ray & ~((1ull << (63 - __builtin_clzll(bl))) - 1ull) : ray);
+            };
+            if (up != 'R') {  // kAll8[0..4): (-1,-1) (-1,1) (1,-1) (1,1)
+                M[0] = down_ray(diag & low);
+                M[1] = down_ray(anti & low);
+                M[2] = up_ray(anti & high);
+                M[3] = up_ray(diag & high);
+            }
+            if (up != 'B') {  // kAll8[4..8): (-1,0) (1,0) (0,-1) (0,1)
+                M[4] = down_ray(file & low);
+                M[5] = up_ray(file & high);
+                M[6] = down_ray(rank & low);
+                M[7] = up_ray(rank & high);
+            }
+            desc = 0x53u;  // runs 0, 1, 4, 6
+        }
+    }
+    uint32_t nruns = 0, nmoves = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        nruns += M[k] != 0ull ? 1u : 0u;
+        nmoves += (uint32_t)__popcll(M[k]);
+    }
+    uint32_t runs_total;
+    const uint32_t rbase = wave_excl_sum(nruns, runs_total);
+    const uint32_t mbase = wave_excl_sum(nmoves, total);
+    if (runs_total > 128u || total > (uint32_t)kMaxPseudo) return false;
+    uint32_t ri = rbase, mo = mbase;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        if (M[k] != 0ull) {
+            uint32_t *const q = rec + 4 * ri;
+            q[0] = (uint32_t)M[k];
+            q[1] = (uint32_t)(M[k] >> 32);
+            q[2] = mo;
+            q[3] = (uint32_t)s | (((desc >> k) & 1u) << 6);
+            ++ri;
+            mo += (uint32_t)__popcll(M[k]);
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    for (uint32_t base = 0; base < runs_total; base += 64) {
+        const uint32_t j = base + lane();
+        if (j < runs_total) {
+            const uint32_t *const q = rec + 4 * j;
+            uint64_t T = (uint64_t)q[0] | ((uint64_t)q[1] << 32);
+            uint16_t *dst = ps + q[2];
+            const uint32_t meta = q[3];
+            const int from = (int)(meta & 63u);
+            if (meta & 64u) {
+                while (T) {
+                    const int to = 63 - __builtin_clzll(T);
+                    T &= ~(1ull << to);
+                    *dst++ = (uint16_t)pack_move(from, to, 0u);
+                }
+            } else {
+                while (T) {
+                    const int to = __builtin_ctzll(T);
+                    T &= T - 1ull;
+                    *dst++ = (uint16_t)pack_move(from, to, 0u);
+                }
+            }
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    return true;
+}
+
 template <class V>
 __device__ __forceinline__ int legal_moves_view(const V &v, int t, uint32_t pc, uint64_t kings, uint16_t *out,
                                                 uint16_t *ps, uint16_t *reg) {
     const uint32_t s = lane();
     const bool mine = !empty_sq(pc) && ((t == 0) == is_white(pc));
-    // one generation pass into this lane's own region (a piece has at most 27 pseudo-legal
-    // moves), then each lane copies its run to its place in board-scan order
-    uint16_t *const own = reg + s * kRegion;
-    uint32_t cnt = 0;
-    auto put = [&](int f, int to, uint32_t val) { own[cnt++] = (uint16_t)pack_move(f, to, val); };
+    uint32_t total = 0;
     CDEV_T(cd11);
-    if (mine) {
-        if constexpr (V::kCheapProbe) bit_piece_moves(v, (int)s, pc, put);
-        else piece_moves(v, (int)s, pc, put);
+    bool runs = false;  // the bit view's run-parallel generator (bit_runs) when it applies
+    if constexpr (V::kCheapProbe) runs = bit_runs(v, (int)s, pc, mine, ps, (uint32_t *)reg, total);
+    if (!runs) {
+        // one generation pass into this lane's own region (a piece has at most 27
+        // pseudo-legal moves), then each lane copies its run to its place in board-scan order
+        uint16_t *const own = reg + s * kRegion;
+        uint32_t cnt = 0;
+        auto put = [&](int f, int to, uint32_t val) { own[cnt++] = (uint16_t)pack_move(f, to, val); };
+        if (mine) {
+            if constexpr (V::kCheapProbe) bit_piece_moves(v, (int)s, pc, put);
+            else piece_moves(v, (int)s, pc, put);
+        }
+        const uint32_t off = wave_excl_sum(cnt, total);
+        if (total > (uint32_t)kMaxPseudo) return -1;
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        for (uint32_t k = 0; k < cnt; ++k) ps[off + k] = own[k];
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     }
     CDEV_ADD(11, cd11);
     CDEV_T(cd12);
-    uint32_t total;
-    const uint32_t off = wave_excl_sum(cnt, total);
-    if (total > (uint32_t)kMaxPseudo) return -1;
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    for (uint32_t k = 0; k < cnt; ++k) ps[off + k] = own[k];
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     CDEV_ADD(12, cd12);
     CDEV_T(cd13);
     const uint32_t kch = t == 0 ? 'K' : 'k';
