@@ -251,3 +251,93 @@ def test_repetition_matches_has_repeated_prefix():
         hits += want
         assert bool((got[k // 2] >> (k % 2)) & 1) == want, (k, s.tolist())
     assert hits > 100   # the cases exercise both answers
+
+
+def _dense_boards(n=400, seed=23):
+    """Boards no game reaches, crowded so that the mover has more than 128 (piece, direction)
+    runs, where chess_device.h's run-parallel generator gives up and the per-piece generator
+    takes over: the mover's queens and king fill most of every other rank (or file), the
+    ranks between hold enemy pieces or nothing, so each queen keeps up to six directions open.
+    The odd-numbered boards are thinned out, with rooks, bishops and knights among the queens
+    (at most 128 runs: the run-parallel generator on the same kind of board).  Returns the
+    boards and (runs, pseudo-legal moves) of each, as the device generator counts them."""
+    rng = np.random.default_rng(seed)
+    out, stats = [], []
+    for i in range(n):
+        t = int(rng.integers(2))
+        fill = rng.uniform(0.8, 1.0) if i % 2 == 0 else rng.uniform(0.3, 0.6)
+        par, foe_p = int(rng.integers(2)), rng.uniform(0.0, 0.5)
+        b = [" "] * 64
+        own_sq = [s for s in range(64) if (s // 8) % 2 == par and rng.random() < fill]
+        other = [s for s in range(64) if (s // 8) % 2 != par]
+        for s in own_sq:
+            b[s] = "Q" if i % 2 == 0 else str(rng.choice(list("QQQQRBN")))
+        b[int(rng.choice(own_sq))] = "K"
+        ek = int(rng.choice(other))
+        b[ek] = "K" if t == 1 else "k"
+        for s in other:
+            if s != ek and rng.random() < foe_p:
+                b[s] = str(rng.choice(list("NBRQ")))
+        if t == 0:   # the mover is white: own pieces upper case, the enemy's lower
+            b = [x.lower() if s in set(other) else x for s, x in enumerate(b)]
+        else:
+            b = [x if s in set(other) else x.lower() for s, x in enumerate(b)]
+        if i % 4 == 3:   # files instead of ranks
+            b = [b[(s % 8) * 8 + s // 8] for s in range(64)]
+        out.append(("".join(b).encode("latin-1"), t, int(rng.integers(40)), 0))
+        stats.append(_count_runs(b, t))
+    return out, stats
+
+
+def _count_runs(b, t):
+    """(non-empty runs, pseudo-legal moves) of side t's queens, rooks, bishops, knights and
+    kings on board b: a knight's targets are one run, a slider or a king one per direction."""
+    mine = (lambda x: x.isupper()) if t == 0 else (lambda x: x.islower())
+
+    def target(r, c):
+        x = b[r * 8 + c]
+        return x == " " or (not mine(x) and x.upper() != "K")
+    runs = moves = 0
+    dirs = {"B": [(-1, -1), (-1, 1), (1, -1), (1, 1)], "R": [(-1, 0), (1, 0), (0, -1), (0, 1)]}
+    dirs["Q"] = dirs["K"] = dirs["B"] + dirs["R"]
+    for s in range(64):
+        x = b[s]
+        if x == " " or not mine(x):
+            continue
+        r, c, u = s // 8, s % 8, x.upper()
+        if u == "N":
+            k = sum(0 <= r + dr < 8 and 0 <= c + dc < 8 and target(r + dr, c + dc)
+                    for dr, dc in ((-2, -1), (-2, 1), (-1, -2), (-1, 2), (1, -2), (1, 2), (2, -1), (2, 1)))
+            runs, moves = runs + (k > 0), moves + k
+            continue
+        for dr, dc in dirs[u]:
+            rr, cc, k = r + dr, c + dc, 0
+            while 0 <= rr < 8 and 0 <= cc < 8 and target(rr, cc):
+                k += 1
+                if b[rr * 8 + cc] != " " or u == "K":
+                    break
+                rr, cc = rr + dr, cc + dc
+            runs, moves = runs + (k > 0), moves + k
+    return runs, moves
+
+
+def test_crowded_boards_match_oracle(eng):
+    """The generator's fallback above 128 runs on crowded boards (and the run-parallel
+    generator on their thinned-out twins): move lists vs the oracle."""
+    import oracle
+    from zeroclone_amd._native import CHESS_STATE_DTYPE
+    pos, stats = _dense_boards()
+    assert sum(r > 128 for r, _ in stats) >= 100 and sum(r <= 128 for r, _ in stats) >= 100
+    assert max(m for _, m in stats) <= 512
+    a = np.zeros(len(pos), CHESS_STATE_DTYPE)
+    for i, (b, t, f, c) in enumerate(pos):
+        a[i]["board"] = np.frombuffer(b, np.uint8)
+        a[i]["turn"], a[i]["fifty"], a[i]["castle"] = t, f, c
+    moves, counts = legal(eng, dev(a))
+    for i, (b, t, fifty, c) in enumerate(pos):
+        want = [list(m) for m in oracle.chess_moves(oracle.chess_state(b.decode("latin-1"), t, fifty, c))]
+        if len(want) > MAXM:
+            assert counts[i] == -1, (i, b)
+            continue
+        assert counts[i] == len(want), (i, b, stats[i])
+        assert [decode(m) for m in moves[i, :counts[i]]] == want, (i, b, stats[i])
