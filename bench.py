@@ -149,8 +149,24 @@ def cpu_baseline(sims: int, bs: int, c: float, snap: dict, moves: int, budget_s:
                                 moves, sims, c, bs, threads=threads)
     dt = time.perf_counter() - t
     ages = [sum(ch != "." for ch in boards[i]) for i in idx]
-    return {"value": round(float(exp.sum()) / dt, 1), "unit": "expansions/s", "cores": threads, "kind": "port",
-            "nproc": hc["nproc"], "cpu_model": hc["cpu_model"], "threads_why": hc["why"],
+    value = float(exp.sum()) / dt
+    # one thread on an evenly spread subset (~budget/6 s): the per-core rate, the scaling over
+    # the CPU share, and what the whole affinity mask would give at that efficiency
+    n1 = max(1, min(G, int(budget_s / 6 / (per_game_move_s / threads * moves))))
+    i1 = [int(i * G / n1) for i in range(n1)]
+    t = time.perf_counter()
+    e1 = oracle.selfplay_batch([boards[i] for i in i1], [turns[i] for i in i1], [copy.deepcopy(mts[i]) for i in i1],
+                               moves, sims, c, bs, threads=1)
+    r1 = float(e1.sum()) / (time.perf_counter() - t)
+    eff = value / (r1 * threads)
+    scaling = {"one_thread": round(r1, 1), "one_thread_sample": f"{n1} games x {moves} moves",
+               "efficiency_at_threads": round(eff, 3),
+               "extrapolated_affinity_mask": round(r1 * hc["affinity"] * min(eff, 1.0), 1),
+               "extrapolation_note": f"NOT measured: the port on all {hc['affinity']} CPUs of the affinity mask at "
+                                     f"the {threads}-thread efficiency; the harness gives this process a "
+                                     f"{threads}-CPU share (OMP_NUM_THREADS), so the pool is sized to it"}
+    return {"value": round(value, 1), "unit": "expansions/s", "cores": threads, "kind": "port",
+            "nproc": hc["nproc"], "cpu_model": hc["cpu_model"], "threads_why": hc["why"], "thread_scaling": scaling,
             "port": "oracle/c4_oracle.c: C restatement pinned bit-exact to the reference's own get_move outputs "
                     "(tests/golden/c4_get_move.json, 150 cases incl. 800 sims) and rollouts",
             "sample": f"{len(idx)} of the {G} games of the burned-in GPU pool's snapshot before the timed window "
@@ -161,31 +177,54 @@ def cpu_baseline(sims: int, bs: int, c: float, snap: dict, moves: int, budget_s:
                       f"pthreads, {dt:.1f}s (calibration: {len(probe)} games x 1 move, {e0.sum()} expansions)"}
 
 
-def cpu_baseline_chess(sims: int = 400, bs: int = 32, c: float = 1.4, budget_s: float = 10.0):
-    """Same-run CPU baseline of the chess crude mode (configs/crude_chess.yaml, C4 shape):
-    the oracle's chess get_move (oracle/chess_oracle.c, bit-exact to the reference's on the
-    26 committed get_move goldens), one opening search per task on a thread pool (ctypes
-    releases the GIL)."""
-    from concurrent.futures import ThreadPoolExecutor
+def chess_pool_snapshot(pool) -> dict:
+    """The burned-in crude chess pool's games at the timed window's start: positions
+    (zc_chess_state rows) and MT19937 states, for the like-for-like chess CPU baseline."""
     import oracle
-    threads = host_cpus()["threads"]
-    root = oracle.chess_init()
+    rows = pool.roots.cpu().numpy().copy()
+    mts = []
+    for g in range(pool.G):
+        mt, k = pool.eng.get_rng_state(g)
+        o = oracle.MT(0)
+        o.s.mt[:] = [int(x) for x in mt]
+        o.s.index = k
+        mts.append(o)
+    return {"rows": rows, "mts": mts}
 
-    def one(seed):
-        mt = oracle.MT(seed)
-        oracle.chess_get_move(root, mt, sims, c, bs, policy="immediate_value", freedom=3.0)
 
-    with ThreadPoolExecutor(threads) as ex:
-        t = time.perf_counter()
-        list(ex.map(one, range(threads)))
-        rate0 = threads / max(time.perf_counter() - t, 1e-6)
-        n = max(threads, int(rate0 * budget_s) // threads * threads)
-        t = time.perf_counter()
-        list(ex.map(one, range(100, 100 + n)))
-        dt = time.perf_counter() - t
-    return {"value": round(n * sims / dt, 1), "unit": "expansions/s", "cores": threads, "kind": "port",
-            "sample": f"{n} chess openings x {sims} sims, crude_chess_score, immediate_value(3), {threads} threads, "
-                      f"{dt:.1f}s (expansions ~= sims from the opening)"}
+def cpu_baseline_chess(snap: dict, moves: int, sims: int = 400, bs: int = 32, c: float = 1.4, budget_s: float = 10.0):
+    """Same-run CPU baseline of the chess crude mode (configs/crude_chess.yaml, C4 shape) on
+    the SAME workload as the GPU window: the burned-in pool's games from the snapshot taken
+    before the timed launch (mixed ages, their own MT19937 states), each playing consecutive
+    crude-score self-play moves (search, play, judge, refill: oracle/chess_oracle.c
+    zcc_selfplay_batch, whose search is bit-exact to the reference's get_move on the 26
+    committed goldens) on the host's CPU share, sized by a calibration round to ~budget_s.
+    Expansions are counted as nodes created, as the GPU counts them.  The positions carry no
+    move histories (the pool's are on the device): a repetition draw can only come from moves
+    played after the snapshot."""
+    import copy
+    import oracle
+    hc = host_cpus()
+    threads = hc["threads"]
+    rows, mts = snap["rows"], snap["mts"]
+    G = len(mts)
+    probe = list(range(0, G, max(1, G // (2 * threads))))[: 2 * threads]
+    t = time.perf_counter()
+    oracle.chess_selfplay_batch(rows[probe], [copy.deepcopy(mts[i]) for i in probe], 1, sims, c, bs, threads=threads)
+    per_game_move_s = (time.perf_counter() - t) / len(probe) * threads
+    n = int(min(G, max(threads, budget_s * threads / (per_game_move_s * moves))))
+    idx = list(range(G)) if n >= G else [int(i * G / n) for i in range(n)]
+    if n >= G:
+        moves = int(min(4 * moves, max(moves, budget_s * threads / (per_game_move_s * G))))
+    t = time.perf_counter()
+    exp = oracle.chess_selfplay_batch(rows[idx], [copy.deepcopy(mts[i]) for i in idx], moves, sims, c, bs,
+                                      threads=threads)
+    dt = time.perf_counter() - t
+    return {"value": round(float(exp.sum()) / dt, 1), "unit": "expansions/s", "cores": threads, "kind": "port",
+            "sample": f"{len(idx)} of the {G} games of the burned-in GPU pool's snapshot before the timed launch "
+                      f"(mixed ages, their own MT19937 states) x {moves} consecutive crude-score self-play moves each "
+                      f"(search, play, judge, refill; lockstep), {sims} sims, batch {bs}, immediate_value(3); "
+                      f"{int(exp.sum())} expansions counted as nodes created; {threads} pthreads, {dt:.1f}s"}
 
 
 def _cpu_net(planes: int, policy: bool = False):
@@ -321,6 +360,20 @@ def _timed_pool_steps(pool, steps: int, warm: int = 1):
 MIXED = "steady-state self-play: the pool adopts a burned-in pool's games in progress (mixed ages), "
 
 
+def net_rates(fl_pos: int, games: int, sims: int, bs: int, nfl: int, steps: int, dt: float) -> dict:
+    """Network FLOP rates of a network-mode step.  Useful FLOPs count the leaves the search
+    evaluates (`sims` per move: every simulation's leaf, the PUCT root included); executed
+    FLOPs count every slot the tower computes (`nfl` flushes x `bs` slots per move: the last
+    flush's unused slots are padding).  Both over the whole step time (search, play and record
+    included), so each is a lower bound on the tower's own rate at that work."""
+    useful = fl_pos * games * sims * steps
+    executed = fl_pos * games * bs * nfl * steps
+    return {"net_tflops_lower": round(useful / dt / 1e12, 1),
+            "mfma_frac_lower": round(useful / dt / 1e12 / MFMA_F16_PEAK_TFLOPS, 4),
+            "net_tflops_executed": round(executed / dt / 1e12, 1),
+            "net_slots_per_move": bs * nfl, "net_leaves_per_move": sims}
+
+
 def net_mode(src, games: int, sims: int, bs: int, c: float, steps: int, dev) -> dict:
     """C2(iii): Connect4 self-play whose search takes its leaf values from a random-init
     value network (stepwise search zc_c4_ext_*, fp16 ValueNetwork(128, 8, in_planes=2) on
@@ -334,14 +387,14 @@ def net_mode(src, games: int, sims: int, bs: int, c: float, steps: int, dev) -> 
     pool.adopt(src)
     exp, dt = _timed_pool_steps(pool, steps)
     pool.close()
-    fl = flops_per_position(128, 8, 2, 6, 7) * games * bs * ((sims + bs - 1) // bs) * steps
+    rates = net_rates(flops_per_position(128, 8, 2, 6, 7), games, sims, bs, (sims + bs - 1) // bs, steps, dt)
     return {"value": round(exp / dt, 1), "unit": "expansions/s", "ms_per_move": round(dt / steps * 1e3, 1),
             "steps": steps, "config": MIXED + f"{games} games x {sims} sims, batch {bs}",
             "net": "ValueNetwork(128, 8, in_planes=2) random init, fp16, BN folded, this package's MFMA conv kernels",
-            "net_tflops_lower": round(fl / dt / 1e12, 1),
-            "mfma_frac_lower": round(fl / dt / 1e12 / MFMA_F16_PEAK_TFLOPS, 4),
-            "note": "TFLOP/s = network FLOPs / whole step time (search, play and record included), so a lower "
-                    "bound on the network's own rate; one HIP graph per step"}
+            **rates,
+            "note": "net_tflops_lower = network FLOPs of the evaluated leaves / whole step time (search, play and "
+                    "record included), a lower bound on the network's own rate; net_tflops_executed counts the "
+                    "padded flush slots the tower also computes; one HIP graph per step"}
 
 
 def c4_puct_mode(src, games: int, sims: int, bs: int, steps: int, dev) -> dict:
@@ -358,12 +411,11 @@ def c4_puct_mode(src, games: int, sims: int, bs: int, steps: int, dev) -> dict:
     exp, dt = _timed_pool_steps(pool, steps)
     pool.close()
     nfl = _native.check(_native.lib().zc_chess_puct_flushes(sims, bs))
-    fl = flops_per_position(128, 8, 2, 6, 7) * games * bs * nfl * steps
     return {"value": round(exp / dt, 1), "unit": "expansions/s", "ms_per_move": round(dt / steps * 1e3, 1),
             "steps": steps,
             "config": MIXED + f"C2 + PUCT: {games} games x {sims} sims, c_puct 1.5, Dirichlet(0.3, 0.25), policy "
                               "(7 logits) + value ResNet 128x8 random init fp16 (MFMA tower), temperature 1",
-            "net_tflops_lower": round(fl / dt / 1e12, 1), "mfma_frac_lower": round(fl / dt / 1e12 / MFMA_F16_PEAK_TFLOPS, 4)}
+            **net_rates(flops_per_position(128, 8, 2, 6, 7), games, sims, bs, nfl, steps, dt)}
 
 
 def chess_burned_pool(dev, games: int = 1024, sims: int = 400, bs: int = 32, max_moves: int = 600):
@@ -391,6 +443,7 @@ def chess_modes(steps: int, dev) -> dict:
     from zeroclone_amd.selfplay import ChessSelfPlay
     G, S, B = 1024, 400, 32
     crude, burn = chess_burned_pool(dev, G, S, B)
+    snap = chess_pool_snapshot(crude)
     K = max(steps, 20)
     ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
     torch.cuda.synchronize(dev)
@@ -413,14 +466,13 @@ def chess_modes(steps: int, dev) -> dict:
     pool.adopt(crude)
     exp, dt = _timed_pool_steps(pool, steps)
     pool.close()
-    fl = flops_per_position(128, 8, 17, 8, 8) * G * B * ((S + B - 1) // B) * steps
     out["value_net"] = {"value": round(exp / dt, 1), "unit": "expansions/s", "ms_per_move": round(dt / steps * 1e3, 1),
                         "steps": steps,
                         "config": MIXED + f"{G} games x {S} sims, ValueNetwork(128, 8) random init fp16 (MFMA "
                                           "kernels), random policy",
-                        "net_tflops_lower": round(fl / dt / 1e12, 1),
-                        "mfma_frac_lower": round(fl / dt / 1e12 / MFMA_F16_PEAK_TFLOPS, 4)}
+                        **net_rates(flops_per_position(128, 8, 17, 8, 8), G, S, B, (S + B - 1) // B, steps, dt)}
     out["_pool"] = crude
+    out["_snap"] = snap
     return out
 
 
@@ -438,12 +490,11 @@ def puct_mode(src, steps: int, dev) -> dict:
     exp, dt = _timed_pool_steps(pool, steps)
     pool.close()
     nfl = _native.check(_native.lib().zc_chess_puct_flushes(S, B))
-    fl = flops_per_position(128, 8, 17, 8, 8) * G * B * nfl * steps
     return {"value": round(exp / dt, 1), "unit": "expansions/s", "ms_per_move": round(dt / steps * 1e3, 1),
             "steps": steps,
             "config": MIXED + "C5 per GPU: 1024 games x 1600 sims, PUCT c 1.5, Dirichlet(0.3, 0.25), policy+value "
                               "ResNet 128x8 random init fp16 (MFMA tower), temperature 1",
-            "net_tflops_lower": round(fl / dt / 1e12, 1), "mfma_frac_lower": round(fl / dt / 1e12 / MFMA_F16_PEAK_TFLOPS, 4)}
+            **net_rates(flops_per_position(128, 8, 17, 8, 8), G, S, B, nfl, steps, dt)}
 
 
 def c1_mode(dev, sims: int = 100, games: int = 4) -> dict:
@@ -722,6 +773,7 @@ def run_rank(args, rank: int, world: int, local: int):
             sp = None
             chess = chess_modes(args.net_steps, dev)
             crude_pool = chess.pop("_pool")
+            chess_snap = chess.pop("_snap")
             out["extra"]["c4_chess"] = chess
             out["extra"]["c5_chess_puct"] = puct_mode(crude_pool, args.net_steps, dev)
             crude_pool.close()
@@ -730,7 +782,8 @@ def run_rank(args, rank: int, world: int, local: int):
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(S, B, args.c, snap, args.steps)
             if args.net_steps > 0:
-                out["extra"]["c4_chess"]["crude"]["cpu_baseline"] = cpu_baseline_chess()
+                out["extra"]["c4_chess"]["crude"]["cpu_baseline"] = cpu_baseline_chess(
+                    chess_snap, out["extra"]["c4_chess"]["crude"]["steps"])
                 out["extra"]["c2_value_net"]["cpu_baseline"] = cpu_baseline_c4_net(S, B, args.c)
                 out["extra"]["c4_chess"]["value_net"]["cpu_baseline"] = cpu_baseline_chess_net()
                 out["extra"]["c5_chess_puct"]["cpu_baseline"] = cpu_baseline_chess_puct()

@@ -338,3 +338,31 @@ def chess_get_move(s: ZccState, mt: MT, sims: int, c: float, bs: int, policy: st
                           mv, ctypes.byref(n))
     moves = [(m.fr, m.fc, m.tr, m.tc, m.value) for m in mv[:n.value]]
     return best, moves, list(na[:n.value])
+
+
+def chess_selfplay_batch(rows, mts: list["MT"], moves: int, sims: int, c: float = 1.4, bs: int = 32,
+                         policy: str = "immediate_value", freedom: float = 3.0, threads: int = 1):
+    """zcc_selfplay_batch: crude-score self-play, each game `moves` moves (search, play, judge,
+    refill) from its position — rows: [n, >= 67] uint8 zc_chess_state rows (board, turn, fifty,
+    castle) — and MT state (advanced); returns expansions (nodes created) per game."""
+    import numpy as np
+    rows = np.ascontiguousarray(rows, np.uint8)
+    n = rows.shape[0]
+    light = (ZccLight * max(n, 1))()
+    for i in range(n):
+        light[i].board[:] = [int(x) for x in rows[i, :64]]
+        light[i].turn, light[i].fifty, light[i].castle = int(rows[i, 64]), int(rows[i, 65]), int(rows[i, 66])
+    arr = (_MT * max(n, 1))()
+    for i, m in enumerate(mts):
+        arr[i] = m.s
+    exp = np.zeros(n, np.uint64)
+    L = _chess_lib()
+    L.zcc_selfplay_batch.argtypes = [ctypes.c_int, ctypes.POINTER(ZccLight), ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                     ctypes.c_double, ctypes.c_int, ctypes.c_int, ctypes.c_double, ctypes.c_int,
+                                     ctypes.POINTER(ctypes.c_uint64)]
+    L.zcc_selfplay_batch(n, light, ctypes.cast(arr, ctypes.c_void_p), moves, sims, c, bs,
+                         1 if policy == "immediate_value" else 0, float(freedom), threads,
+                         exp.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)))
+    for i, m in enumerate(mts):
+        m.s = arr[i]
+    return exp

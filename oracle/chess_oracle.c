@@ -481,6 +481,8 @@ static void cbackprop(cnode *P, int node, double v) {   /* mcts.cpp:80-100 */
     }
 }
 
+static __thread int t_chess_nodes;   /* nodes the calling thread's last zcc_get_move created */
+
 int zcc_get_move(const zcc_light *root, void *rv, int sims, double c, int bs, int policy, double freedom,
                  zcc_value_fn vfn, void *ctx, int *root_na, zcc_move *root_moves, int *n_root) {
     zco_mt *r = (zco_mt *)rv;
@@ -517,6 +519,7 @@ int zcc_get_move(const zcc_light *root, void *rv, int sims, double c, int bs, in
         if (root_na) root_na[i] = P[0].Na[i];
         if (root_moves) root_moves[i] = P[0].mv[i];
     }
+    t_chess_nodes = np;
     for (int i = 0; i < np; i++) {
         free(P[i].mv);
         free(P[i].untried);
@@ -565,4 +568,65 @@ int zcc_rollout(const zcc_state *start, void *rv, int *plies) {
     if (plies) *plies = q;
     free(s);
     return out;
+}
+
+/* Steady-state crude-score self-play from given positions and streams (bench.py's chess CPU
+ * baseline on the GPU pool's snapshot; the caller of get_move is Engine.play_mcts +
+ * scripts/train.py:151-170): per game, `moves` times: get_move (crude_chess_score, the
+ * policy), play the best root move, and refill from the initial position when the game is
+ * over (no legal move — check_win or stalemate — or check_draw: fifty moves, repetition over
+ * the histories played since the snapshot).  out_expansions[g] = nodes created (the root
+ * excluded), as the GPU counts them.  One pthread per slice of games. */
+#include <pthread.h>
+
+typedef struct {
+    int lo, hi, moves, sims, bs, policy;
+    double c, freedom;
+    const zcc_light *roots;
+    zco_mt *mts;
+    uint64_t *out;
+} csp_job;
+
+static void *csp_worker(void *arg) {
+    csp_job *J = (csp_job *)arg;
+    zcc_state *s = (zcc_state *)malloc(sizeof(zcc_state));
+    zcc_move mv[ZCC_MAX_MOVES];
+    for (int g = J->lo; g < J->hi; g++) {
+        light_to_state(&J->roots[g], s);
+        uint64_t exp = 0;
+        for (int k = 0; k < J->moves; k++) {
+            zcc_light l;
+            memcpy(l.board, s->board, 64);
+            l.turn = s->turn;
+            l.fifty = s->fifty;
+            l.castle = s->castle;
+            int n = 0;
+            const int best = zcc_get_move(&l, &J->mts[g], J->sims, J->c, J->bs, J->policy, J->freedom, NULL, NULL,
+                                          NULL, mv, &n);
+            exp += (uint64_t)(t_chess_nodes - 1);
+            if (best >= 0) zcc_play(s, &mv[best], s);
+            if (best < 0 || s->overflow || zcc_legal_moves(s, mv) == 0 || zcc_check_draw(s)) zcc_init(s);
+        }
+        J->out[g] = exp;
+    }
+    free(s);
+    return NULL;
+}
+
+int zcc_selfplay_batch(int n, const zcc_light *roots, void *mtv, int moves, int sims, double c, int bs, int policy,
+                       double freedom, int n_threads, uint64_t *out_expansions) {
+    zco_mt *mts = (zco_mt *)mtv;
+    if (n_threads < 1) n_threads = 1;
+    if (n_threads > n) n_threads = n > 0 ? n : 1;
+    pthread_t *th = (pthread_t *)malloc(sizeof(pthread_t) * (size_t)n_threads);
+    csp_job *J = (csp_job *)malloc(sizeof(csp_job) * (size_t)n_threads);
+    for (int q = 0; q < n_threads; q++) {
+        J[q] = (csp_job){(int)((long)n * q / n_threads), (int)((long)n * (q + 1) / n_threads), moves, sims, bs,
+                         policy, c, freedom, roots, mts, out_expansions};
+        pthread_create(&th[q], NULL, csp_worker, &J[q]);
+    }
+    for (int q = 0; q < n_threads; q++) pthread_join(th[q], NULL);
+    free(J);
+    free(th);
+    return 0;
 }

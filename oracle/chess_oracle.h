@@ -52,6 +52,9 @@ double   zcc_crude_score(const zcc_light *l);
 typedef void (*zcc_value_fn)(void *ctx, int n, const zcc_light *leaves, double *out);
 int      zcc_get_move(const zcc_light *root, void *r, int sims, double c, int bs, int policy, double freedom,
                       zcc_value_fn vfn, void *ctx, int *root_na, zcc_move *root_moves, int *n_root);
+/* crude-score self-play of n games from roots on their streams (bench.py's CPU baseline) */
+int      zcc_selfplay_batch(int n, const zcc_light *roots, void *mts, int moves, int sims, double c, int bs, int policy,
+                            double freedom, int n_threads, uint64_t *out_expansions);
 
 /* Value('random_rollout') (value_functions.py:35-45) on the chess rules, stream r (zco_mt*):
  * -1 / +1 / 0 for the start's side to move, 2 if a history outgrew ZCC_HIST; *plies played. */

@@ -70,3 +70,39 @@ def test_chess_search_matches_reference(golden):
         assert list(moves[best]) == case["move"]
         assert mt.drawn == case["consumed"]
         assert mt.u32() == case["next_word"]
+
+
+def test_chess_selfplay_batch_equals_get_move_play_judge():
+    """zcc_selfplay_batch (bench.py's chess CPU baseline) = per game, per move: get_move
+    (crude_chess_score, immediate_value(3)), play the best move, refill at a finished game —
+    the same stream consumption as the step-by-step oracle calls, from mixed positions."""
+    import copy
+    import numpy as np
+    rng = np.random.default_rng(3)
+    states = []
+    for _ in range(6):
+        s = oracle.chess_init()
+        for _ in range(int(rng.integers(0, 30))):
+            ms = oracle.chess_moves(s)
+            if not ms or oracle.chess_draw(s):
+                break
+            s = oracle.chess_play(s, ms[int(rng.integers(len(ms)))])
+        states.append(s)
+    rows = np.zeros((len(states), 72), np.uint8)
+    for i, s in enumerate(states):
+        rows[i, :64] = list(s.board)
+        rows[i, 64:67] = (s.turn, s.fifty, s.castle)
+    mts = [oracle.MT(40 + i) for i in range(len(states))]
+    ref = [copy.deepcopy(m) for m in mts]
+    K, S = 5, 60
+    exp = oracle.chess_selfplay_batch(rows, mts, K, S, 1.4, 16, threads=3)
+    assert (exp > 0).all() and (exp <= K * S).all()
+    for i, s in enumerate(states):
+        s = oracle.chess_state(bytes(rows[i, :64]).decode("latin-1"), int(rows[i, 64]), int(rows[i, 65]),
+                               int(rows[i, 66]))
+        for _ in range(K):
+            best, ms, _ = oracle.chess_get_move(s, ref[i], S, 1.4, 16, "immediate_value", 3.0)
+            s = oracle.chess_play(s, ms[best])
+            if not oracle.chess_moves(s) or oracle.chess_draw(s):
+                s = oracle.chess_init()
+        assert ref[i].state() == mts[i].state(), i

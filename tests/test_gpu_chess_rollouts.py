@@ -81,3 +81,30 @@ def test_chess_rollouts_match_the_oracle_at_scale():
     assert [int(x) for x in m] == list(mt.s.mt) and idx == mt.s.index
     assert plies > 20000 and {-1.0, 0.0, 1.0} <= set(exp)
     eng.close()
+
+
+def test_chess_rollouts_refuse_a_history_longer_than_its_buffer():
+    """A history length above hist_cap: the kernel reports ZC_STATUS_CAPACITY
+    instead of rolling out on a truncated history (which would drop the most recent moves, the
+    ones the repetition draw reads); a consistent length on the same buffers runs."""
+    rng = random.Random(5)
+    states = positions(2, rng)
+    rows, hist, hlen = device_rows(states)
+    eng = _native.NativeEngine(max_games=1, max_sims=1, max_batch=1)
+    eng.seed(0, [7])
+    dev = torch.device("cuda", 0)
+    d_rows = torch.from_numpy(rows.view(np.uint8).reshape(len(states), 72).copy()).to(dev)
+    d_hist = torch.from_numpy(hist).to(dev)
+    s = torch.cuda.current_stream(dev)
+    for over, want in ((True, _native.ZC_STATUS_CAPACITY), (False, 0)):
+        bad = hlen.copy()
+        if over:
+            bad[1, 0] = hist.shape[2] + 1
+        d_hlen = torch.from_numpy(bad).to(dev)
+        vals = torch.zeros(len(states), dtype=torch.float64, device=dev)
+        status = torch.zeros(1, dtype=torch.int32, device=dev)
+        eng.chess_rollouts_async(0, len(states), d_rows.data_ptr(), d_hist.data_ptr(), d_hlen.data_ptr(),
+                                 hist.shape[2], vals.data_ptr(), status.data_ptr(), s.cuda_stream)
+        s.synchronize()
+        assert int(status.item()) == want, over
+    eng.close()

@@ -141,3 +141,24 @@ def test_chess_pooled_launch_refuses_more_games_than_resident():
     with pytest.raises(ValueError):
         sp.run_pooled(2 * (cap + 64), 4)
     sp.close()
+
+
+def test_simulate_games_grows_the_trajectory_pool_on_demand():
+    """simulate_games with a quota on a chess pool whose trajectory pool starts small: the
+    positions grow on demand before each step (the worst case of one step is known: every
+    active slot's history + 1), nothing is dropped, every game is recorded whole, and the
+    pool ends far below round 4's up-front quota x max_len reservation."""
+    from zeroclone_amd.selfplay import ChessSelfPlay, simulate_games
+    G, S, B, total = 8, 24, 8, 48
+    sp = ChessSelfPlay(G, S, batch_size=B, seed=31, init_fen=KQK, hist_cap=256, games_cap=8)
+    sp.traj._alloc_pool(8, 64)   # start tiny: 64 positions
+    cap0 = sp.traj.pool_cap
+    res = simulate_games(sp, total, max_steps=3000)
+    assert len(res) == total
+    b = sp.last_batch
+    lens = b.games[:, 4].cpu().numpy()
+    assert int(lens.sum()) == b.rows.shape[0] and (lens >= 2).all()
+    assert sp.traj.pool_cap >= int(lens.sum())
+    assert sp.traj.pool_cap < total * sp.traj.max_len
+    assert int(lens.sum()) > cap0 and sp.traj.pool_cap > cap0   # it had to grow
+    sp.close()

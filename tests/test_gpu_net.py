@@ -21,20 +21,44 @@ def _net(in_planes, seed, channels=128, blocks=8):
     return net.eval()
 
 
+def _features32(ref, x):
+    """Pooled tower features of a FoldedValueNetwork (fp32 on the GPU)."""
+    with torch.no_grad():
+        a = torch.relu(ref.stem(x.contiguous(memory_format=torch.channels_last)))
+        return ref.res(a).mean(dim=(2, 3))
+
+
 @pytest.mark.parametrize("shape", [(17, 8, 8), (2, 6, 7)])
 @pytest.mark.parametrize("n", [1, 7, 301])
 def test_mfma_network_matches_torch(shape, n):
+    """The fp16 MFMA network against the same folded network in fp32 (torch on the GPU), with
+    two heads: the network's own (outputs std ~0.01): atol 5e-4; and a wide head along the
+    top principal direction of 64 calibration boards' fp32 features (outputs std ~0.65,
+    most of tanh's range): atol 6e-3.  The CPU restatement of the fp16 storage points
+    (tests/nn_check.py) predicts max errors <= 1.1e-4 / 3.5e-3 on these networks, whose
+    non-trivial BN scales the activations' fp16 rounding.  Pearson >= 0.999 (n > 2)."""
+    from nn_check import assert_tracks, wide_head
     from zeroclone_amd.nets import FoldedValueNetwork, MfmaValueNetwork
     c, h, w = shape
     net = _net(c, seed=n)
-    ref = FoldedValueNetwork(net).cuda().float().eval()
-    x = (torch.rand(n, c, h, w, device="cuda") < 0.3).half()
-    with torch.no_grad():
-        want = ref(x.float()).reshape(-1).double()
-    got = MfmaValueNetwork(net)(x).clone()
-    torch.cuda.synchronize()
-    assert got.dtype == torch.float64 and got.shape == (n,)
-    np.testing.assert_allclose(got.cpu().numpy(), want.cpu().numpy(), rtol=0, atol=2e-2)
+    g = torch.Generator(device="cuda").manual_seed(1000 + n)
+    x = (torch.rand(n, c, h, w, device="cuda", generator=g) < 0.3).half()
+    cal = (torch.rand(64, c, h, w, device="cuda", generator=g) < 0.3).float()
+    for head, atol in (("own", 5e-4), ("wide", 6e-3)):
+        if head == "wide":
+            wv, bv = wide_head(_features32(FoldedValueNetwork(net).cuda().float().eval(), cal).cpu())
+            with torch.no_grad():
+                net.head[2].weight.copy_(wv.reshape(1, -1))
+                net.head[2].bias.fill_(bv)
+        ref = FoldedValueNetwork(net).cuda().float().eval()
+        with torch.no_grad():
+            want = ref(x.float()).reshape(-1).double()
+        got = MfmaValueNetwork(net)(x).clone()
+        torch.cuda.synchronize()
+        assert got.dtype == torch.float64 and got.shape == (n,)
+        assert_tracks(got.cpu().numpy(), want.cpu().numpy(), atol, min_r=0.999, what=f"{head} head {shape} n={n}")
+        if head == "wide" and n > 2:
+            assert want.std().item() > 0.3
 
 
 @pytest.mark.parametrize("mf", ["32", "16"])
@@ -95,15 +119,20 @@ def test_packed_conv_is_bit_identical_to_the_staged_form():
             assert torch.equal(a.view(torch.int16), b.view(torch.int16)), (h, w, cin, n, use_res, relu)
 
 
-@pytest.mark.parametrize("mf", ["32", "16"])
+@pytest.mark.parametrize("mf", ["32", "16", "default"])
 @pytest.mark.parametrize("shape", [(17, 8, 8), (2, 6, 7)])
 @pytest.mark.parametrize("n", [1, 7, 301, 4099])
 def test_fused_tower_is_bit_identical_to_layered(shape, n, mf, monkeypatch):
     """zc_net_tower_async (the whole tower in one launch, activations on chip) against the
     layer-by-layer packed launches: the tower's output activation bit for bit, ragged last
-    tiles included — in both MFMA forms (ZC_TOWER_MF selects the form of both launches)."""
+    tiles included — in both MFMA forms (ZC_TOWER_MF selects the form of both launches), and
+    in the default pairing (ZC_TOWER_MF unset: the fused tower on 16x16x32, the layered
+    launches on 32x32x16)."""
     from zeroclone_amd.nets import MfmaValueNetwork
-    monkeypatch.setenv("ZC_TOWER_MF", mf)
+    if mf == "default":
+        monkeypatch.delenv("ZC_TOWER_MF", raising=False)
+    else:
+        monkeypatch.setenv("ZC_TOWER_MF", mf)
     c, h, w = shape
     net = MfmaValueNetwork(_net(c, seed=100 + n))
     x = (torch.rand(n, c, h, w, device="cuda") < 0.3).half()
@@ -186,3 +215,116 @@ def test_fused_value_head_is_bit_identical(shape, n):
     torch.cuda.synchronize()
     assert torch.equal(got, want)
     assert want.abs().sum().item() > 0
+
+
+def _integer_head(vnet, hw, seed):
+    """Integer value head on an integer tower: Linear weights k_c * hw / 64 (k_c in {-1, 0, 1},
+    sparse) and a bias that is a multiple of 1/64.  The kernels' head sums each lane's
+    channels (exact integers times hw / 64), divides by hw (exact: the quotient k / 64 is
+    representable) and adds the lanes (multiples of 1/64), so the pre-tanh sum is exact:
+    sum_c k_c * S_c / 64 + bias, S_c the channel's pixel sum."""
+    g = torch.Generator().manual_seed(seed)
+    k = torch.randint(-1, 2, (128,), generator=g).float() * (torch.rand(128, generator=g) < 0.25)
+    with torch.no_grad():
+        vnet.head[2].weight.copy_((k * hw / 64.0).reshape(1, -1))
+        vnet.head[2].bias.fill_(-3.0 + 5.0 / 64.0)
+    return vnet
+
+
+@pytest.mark.parametrize("mf", ["32", "16"])
+@pytest.mark.parametrize("shape", [(17, 8, 8), (2, 6, 7)])
+def test_value_head_exact_on_integers(mf, shape, monkeypatch):
+    """The value head (avg-pool, Linear(128, 1), + bias) on an integer network: its pre-tanh
+    sum (ZC_HEAD_RAW=1) equals float64 exactly on 8x8 boards (the pool's 1/64 is exact), in the
+    fused tower launch and in the layered value_head_kernel, ragged tiles included; on 6x7 the
+    division by 42 rounds in fp32, so there the bound is 8 fp32 ulps of the sums.  With the
+    tanh (the product path) the values equal float64 tanh of that sum within tanhf's precision.
+    A head without its bias or without its Linear would fail every one of these."""
+    from zeroclone_amd.nets import FoldedValueNetwork, MfmaValueNetwork
+    monkeypatch.setenv("ZC_TOWER_MF", mf)
+    c, h, w = shape
+    vnet = _integer_head(_integer_net(c, 2, seed=h * 7 + int(mf)), h * w, seed=int(mf) + h)
+    xs = [(torch.rand(n, c, h, w) < 0.3).half() for n in (1, 5, 131)]
+
+    def pre_tanh(x):
+        f = FoldedValueNetwork(vnet).double()
+        with torch.no_grad():
+            act = f.res(torch.relu(f.stem(x.double())))
+            return act.mean(dim=(2, 3)) @ f.fc.weight.detach().double().reshape(-1) + f.fc.bias.detach().double()
+    with torch.no_grad():   # centre the sums on tanh's active range (a multiple of 1/64)
+        vnet.head[2].bias.fill_(0.0)
+        vnet.head[2].bias.fill_(-float(torch.round(pre_tanh(xs[-1]).median() * 64)) / 64)
+    net = MfmaValueNetwork(vnet)
+    for x in xs:
+        n = x.shape[0]
+        pre = pre_tanh(x)
+        assert pre.abs().max().item() < 2 ** 16
+        if n > 1:
+            assert pre.std().item() > 0
+        monkeypatch.setenv("ZC_HEAD_RAW", "1")
+        for fused in (True, False):
+            got = net(x.cuda(), fused=fused).clone()
+            torch.cuda.synchronize()
+            if h * w == 64:
+                assert torch.equal(got.cpu(), pre), (mf, shape, n, fused)
+            else:   # the pool's 1/42 is rounded in fp32: a few ulps of the lane sums
+                np.testing.assert_allclose(got.cpu().numpy(), pre.numpy(), rtol=0,
+                                           atol=8 * 2.0 ** -23 * max(1.0, float(pre.abs().max())))
+        monkeypatch.setenv("ZC_HEAD_RAW", "0")
+        got = net(x.cuda()).clone()
+        torch.cuda.synchronize()
+        np.testing.assert_allclose(got.cpu().numpy(), np.tanh(pre.numpy()), rtol=0, atol=1e-6)
+
+
+def _integer_pv_net(c, h, w, nl, seed):
+    """PolicyValueNetwork with an integer tower (as _integer_net), an integer 1x1 policy conv,
+    identity BN with integer biases and a sparse integer Linear: every policy value is a small
+    integer, exact in fp16 and in any fp32 summation order."""
+    from zeroclone_amd.nets import PolicyValueNetwork
+    g = torch.Generator().manual_seed(seed)
+    net = PolicyValueNetwork(in_planes=c, board=(h, w), n_logits=nl).eval()
+    for m in net.modules():
+        if isinstance(m, torch.nn.Conv2d):
+            dens = 0.002 if m.in_channels == 128 and m.kernel_size == (3, 3) else 0.02
+            keep = torch.rand(m.weight.shape, generator=g) < dens
+            m.weight.data = torch.randint(-2, 3, m.weight.shape, generator=g).float() * keep
+        elif isinstance(m, torch.nn.BatchNorm2d):
+            m.eps = 0.0
+            m.running_mean.zero_()
+            m.running_var.fill_(1.0)
+            m.weight.data.fill_(1.0)
+            m.bias.data = torch.randint(-1, 3, m.bias.shape, generator=g).float()
+        elif isinstance(m, torch.nn.Linear) and m.out_features == nl:
+            keep = torch.rand(m.weight.shape, generator=g) < 0.004
+            m.weight.data = torch.randint(-1, 2, m.weight.shape, generator=g).float() * keep
+            m.bias.data = torch.randint(-4, 5, m.bias.shape, generator=g).float()
+    net.res = net.res[:2]
+    return net
+
+
+@pytest.mark.parametrize("shape", [(37, 17, 8, 8, 4096), (53, 2, 6, 7, 7)])
+def test_policy_head_exact_on_integers(shape):
+    """TowerPolicy (the 1x1 policy conv fused into the tower launch, zc_net_tower_policy_async)
+    and the policy Linear on an integer PolicyValueNetwork: the conv's ReLU output and the
+    logits equal float64 exactly (2 residual blocks, ragged last tiles)."""
+    from zeroclone_amd.nets import MfmaPolicyValueNetwork
+    n, c, h, w, nl = shape
+    net = _integer_pv_net(c, h, w, nl, seed=n)
+    mnet = MfmaPolicyValueNetwork(net)
+    assert mnet.fused
+    x = (torch.rand(n, c, h, w) < 0.3).half()
+    _, logits = mnet(x.cuda())
+    pout = mnet._pout[(n, h * w)].double().cpu()
+    torch.cuda.synchronize()
+    from zeroclone_amd.nets import FoldedValueNetwork
+    fv = FoldedValueNetwork(net.value_network()).double()
+    conv, bn, lin = net.policy[0], net.policy[1], net.policy[4]
+    with torch.no_grad():   # identity BN (eps 0): the folded form is the module's own algebra
+        t = fv.res(torch.relu(fv.stem(x.double())))
+        p = torch.relu(torch.nn.functional.conv2d(t, conv.weight.double()) + bn.bias.double().reshape(1, -1, 1, 1))
+        want_logits = p.flatten(1) @ lin.weight.double().t() + lin.bias.double()
+    want_p = p.permute(0, 2, 3, 1).reshape(n, h * w, 32)
+    assert want_p.abs().max().item() < 2048 and want_p.abs().sum().item() > 0
+    assert want_logits.abs().max().item() < 2048 and (want_logits != lin.bias.double()).any()
+    assert torch.equal(pout, want_p)
+    assert torch.equal(logits.double().cpu(), want_logits)

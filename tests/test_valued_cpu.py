@@ -73,3 +73,48 @@ def test_folded_network_matches_unfolded_fp32():
         ref = net(x)
         got = for_inference(net, "cpu", torch.float32)(x)
     torch.testing.assert_close(got, ref, rtol=1e-5, atol=1e-5)
+
+
+def _seeded_net(g, wide):
+    from zeroclone_amd.nets import ValueNetwork
+    torch.manual_seed(g["seed"])
+    net = ValueNetwork().eval()
+    if wide:
+        with torch.no_grad():
+            net.head[2].weight.copy_(torch.tensor(g["head_weight_wide"]).reshape(1, -1))
+            net.head[2].bias.fill_(g["head_bias_wide"])
+    return net
+
+
+def test_wide_head_golden_matches_this_package_in_fp32(golden):
+    """The wide head (the pooled features' top principal direction, tests/golden/gen_golden_nn.py)
+    loaded into this package's ValueNetwork reproduces the reference's fp32 outputs, and those
+    outputs span most of tanh's range (a tolerance of 3e-3 is < 1 % of their spread)."""
+    g = golden("value_network.json")
+    y = np.array(g["outputs_wide"])
+    assert y.std() > 0.5 and y.min() < -0.9 and y.max() > 0.9
+    with torch.no_grad():
+        got = _seeded_net(g, True)(_inputs(g)).reshape(-1).double().numpy()
+    np.testing.assert_allclose(got, y, rtol=0, atol=1e-5)
+
+
+@pytest.mark.parametrize("wide,atol", [(False, 2e-4), (True, 3e-3)])
+def test_fp16_storage_error_fits_the_gpu_tolerance(golden, wide, atol):
+    """The GPU test's tolerances are not guesses: the fp16 storage points of the MFMA path
+    (fp16 weights, fp16 activations after every layer) restated in float64 stay inside them
+    against the reference's fp32 outputs, with a margin; a head missing its bias, or a
+    constant head, does not."""
+    from nn_check import assert_tracks, fails_tracking, fp16_emulation_features
+    from zeroclone_amd.nets import FoldedValueNetwork
+    g = golden("value_network.json")
+    want = np.array(g["outputs_wide" if wide else "outputs"])
+    net = _seeded_net(g, wide)
+    f = FoldedValueNetwork(net)
+    feat = fp16_emulation_features(f, _inputs(g))
+    w = f.fc.weight.detach().double().reshape(-1)
+    b = f.fc.bias.detach().double().item()
+    emu = torch.tanh(feat @ w + b).numpy()
+    err = assert_tracks(emu, want, atol, what="fp16 emulation")
+    assert err < atol / 2, err
+    assert fails_tracking(torch.tanh(feat @ w).numpy(), want, atol)          # bias dropped
+    assert fails_tracking(np.full_like(want, want.mean()), want, atol)       # constant head

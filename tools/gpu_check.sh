@@ -20,6 +20,8 @@ for st in "$@"; do
   case $st in
     pytest) run pytest_gpu 1200 python -m pytest tests -m gpu -x -q -p no:cacheprovider; rc=$?
             if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi ;;
+    pyall)  run pytest_all 1200 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread -p no:cacheprovider -rf; rc=$?
+            if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi ;;
     sel)    run pytest_sel 1100 python -u -m pytest ${PYSEL} -x -v --timeout 400 --timeout-method thread -p no:cacheprovider; rc=$?
             if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi ;;
     smoke)  run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit $? ;;

@@ -449,7 +449,10 @@ __device__ int chess_play_judge(const ChessPlayParams &q, int gl, CLds &L, uint1
     }
     wave_sync_mem();
     const int rep = chessdev::repetitions(h, hl, q.cap, Lh);
-    if (k < 0) err |= 8;
+    if (k < 0) {   // the legal-move list overflowed: the position cannot be judged.  The game
+        err |= 8;  // ends here (refilled, recorded as a draw) instead of playing on from an
+        return 0;  // unjudged position; err bit 8 makes check() / take() raise before any use
+    }
     if (k == 0 && check) return turn * 2 - 1;
     if ((k == 0 && !check) || uni((int)L.st.fifty) >= 50 || rep == 3) return 0;
     return ZC_C4_ONGOING;
@@ -873,9 +876,15 @@ __global__ __launch_bounds__(64) void chess_rollouts_kernel(ChessParams p, int f
     for (int j = 0; j < nb && !status; ++j) {
         const int hi = from_tree ? gl : j;   // whose histories
         const uint16_t *hs = p.rhist + (size_t)hi * 2 * p.rhcap;
-        RollSide w{s_roll, s_roll + 2 * kRollCap, min(uni(p.rhlen[2 * hi]), p.rhcap), 0, false};
-        RollSide k{s_roll + kRollCap, s_roll + 2 * kRollCap + kRollCap + 1, min(uni(p.rhlen[2 * hi + 1]), p.rhcap), 0,
-                   false};
+        const int nw = uni(p.rhlen[2 * hi]), nk = uni(p.rhlen[2 * hi + 1]);
+        if (nw > p.rhcap || nk > p.rhcap || nw < 0 || nk < 0) {
+            // a history longer than its buffer: its most recent moves (what the repetition
+            // draw reads) are missing, so refuse rather than roll out on a truncated history
+            status = ZC_STATUS_CAPACITY;
+            break;
+        }
+        RollSide w{s_roll, s_roll + 2 * kRollCap, nw, 0, false};
+        RollSide k{s_roll + kRollCap, s_roll + 2 * kRollCap + kRollCap + 1, nk, 0, false};
         int d = 0;
         const uint32_t *pw = nullptr;
         if (from_tree) {

@@ -876,6 +876,7 @@ struct TowerPolicy {
     const _Float16 *pw;
     const float *pb;
     _Float16 *out;
+    int head_raw;  // test switch (ZC_HEAD_RAW=1): the value head writes its pre-tanh sum
 };
 
 template <int H, int W, int BPH, int CIN0, int NT, int WPE, int PG = 1, int MF = 32, int EPI = 0>
@@ -1011,7 +1012,7 @@ __global__ __launch_bounds__(256 * PG) __attribute__((amdgpu_waves_per_eu(WPE, W
             }
             d /= (float)HW;
             for (int o = 8; o > 0; o >>= 1) d += __shfl_xor(d, o);
-            if (lane == 0) values[b0 + bi] = (double)tanhf(d + fcb);
+            if (lane == 0) values[b0 + bi] = pol.head_raw ? (double)(d + fcb) : (double)tanhf(d + fcb);
         }
     }
     if (pol.out) {
@@ -1112,7 +1113,7 @@ __global__ void planes_to_nhwc_kernel(int n, int cin, int hw, int cpad, const _F
 // pixel groups are then summed across lanes.  Writes the fp64 value the backup takes.
 __global__ __launch_bounds__(256) void value_head_kernel(int n, int hw, const _Float16 *__restrict__ act,
                                                          const float *__restrict__ fcw, float fcb,
-                                                         double *__restrict__ values) {
+                                                         double *__restrict__ values, int raw) {
     const int i = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
     const int lane = threadIdx.x & 63;
     if (i >= n) return;
@@ -1133,7 +1134,14 @@ __global__ __launch_bounds__(256) void value_head_kernel(int n, int hw, const _F
     }
     d /= (float)hw;
     for (int o = 8; o > 0; o >>= 1) d += __shfl_xor(d, o);
-    if (lane == 0) values[i] = (double)tanhf(d + fcb);
+    if (lane == 0) values[i] = raw ? (double)(d + fcb) : (double)tanhf(d + fcb);
+}
+
+// ZC_HEAD_RAW=1 (tests only): the value head returns its pre-tanh sum, so the pooled Linear
+// can be checked exactly against float64 on integer networks
+int head_raw() {
+    const char *e = getenv("ZC_HEAD_RAW");
+    return e && !strcmp(e, "1") ? 1 : 0;
 }
 
 int conv_impl() {  // ZC_CONV_IMPL=tile: 256-pixel tiles for every layer; default: half tiles for 128 planes
@@ -1226,7 +1234,7 @@ bool launch_net_tower(int n, int h, int w, int cin0, int nconv, const void *in, 
                       void *out, const float *fcw, float fcb, double *values, const void *pw, const float *pb,
                       void *pout, hipStream_t s) {
     if (cin0 != 32 || nconv < 1 || !(nconv & 1)) return false;
-    const TowerPolicy pol{(const _Float16 *)pw, pb, (_Float16 *)pout};
+    const TowerPolicy pol{(const _Float16 *)pw, pb, (_Float16 *)pout, head_raw()};
     // 128-pixel tiles at two workgroups per CU; 64-pixel tiles (one chess board) at 3 or 4
     // workgroups per CU measured 10 % slower (tools/ab_tower.py)
 #ifndef ZC_TOWER_PG
@@ -1263,7 +1271,7 @@ void launch_net_planes_to_nhwc(int n, int cin, int hw, int cpad, const void *pla
 
 void launch_net_value_head(int n, int hw, const void *act, const float *fcw, float fcb, double *values, hipStream_t s) {
     hipLaunchKernelGGL(value_head_kernel, dim3((unsigned)(((int64_t)n * 64 + 255) / 256)), dim3(256), 0, s, n, hw,
-                       (const _Float16 *)act, fcw, fcb, values);
+                       (const _Float16 *)act, fcw, fcb, values, head_raw());
 }
 
 }  // namespace zc

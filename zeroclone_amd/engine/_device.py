@@ -45,14 +45,18 @@ class GrowingEngine:
             return self.eng
 
 
-def scratch(sims: int, batch: int, device: int = 0) -> GrowingEngine:
-    """One-game engine for calls that consume Python's global `random` (get_move, Value)."""
+def scratch(sims: int, batch: int, device: int = 0, depth: int = 0) -> GrowingEngine:
+    """One-game engine for calls that consume Python's global `random` (get_move, Value).
+    `depth` is the caller's get_move nesting level on its thread: a host plugin (policy,
+    value, backend) that itself calls get_move in the middle of a search gets the engine of
+    the next level, so the outer search's tree — and its engine's capacity — stay untouched.
+    Do not call `ensure` on another level's engine while a search runs on it."""
+    key = device if depth == 0 else (device, "nested", depth)
     with _lock:
-        ge = _scratch.get(device)
+        ge = _scratch.get(key)
         if ge is None:
-            ge = _scratch[device] = GrowingEngine(1, sims, batch, device)
-        ge.ensure(1, sims, batch)
-        return ge
+            ge = _scratch[key] = GrowingEngine(1, sims, batch, device)
+    return ge
 
 
 def value_engine(device: int = 0) -> GrowingEngine:

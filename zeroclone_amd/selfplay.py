@@ -119,16 +119,41 @@ class Trajectories:
             setattr(b, f, t.data_ptr())
         self._buf = b
 
+    def _grow_pool(self, games_cap: int, pool_cap: int):
+        """A larger pool holding the positions and game records reserved so far."""
+        ctl = self.ctl.cpu().tolist()
+        npos, ngames = int(ctl[_native.ZC_TRAJ_POSITIONS]), int(ctl[_native.ZC_TRAJ_GAMES])
+        old = (self.pool, self.labels, self.pool_moves, self.games)
+        self._alloc_pool(games_cap, pool_cap)
+        self.pool[:npos] = old[0][:npos]
+        self.labels[:npos] = old[1][:npos]
+        self.pool_moves[:npos] = old[2][:npos]
+        self.games[:ngames] = old[3][:ngames]
+
+    def ensure_room(self):
+        """Grow the pool (on demand, keeping its contents) so that the next step cannot
+        overflow it: a slot's game that finishes at that step has at most its current
+        history length + 1 positions, so the worst case is known before the step — far less
+        than quota x max_len.  One small device read; simulate_games calls it per step."""
+        act = self.slot[:, 1] >= 0
+        need = torch.stack([(self.slot[:, 0].to(torch.int64) + 1)[act].sum(), act.sum().to(torch.int64)])
+        ctl = self.ctl[[_native.ZC_TRAJ_POSITIONS, _native.ZC_TRAJ_GAMES]]
+        npos, ngames = (int(x) for x in (ctl + need).tolist())
+        if npos > self.pool_cap or ngames > self.games_cap:
+            self._grow_pool(max(ngames, self.games_cap, 2 * self.games_cap if ngames > self.games_cap else 0),
+                            max(npos, self.pool_cap, 2 * self.pool_cap if npos > self.pool_cap else 0))
+
     def start(self, quota: int | None, games_cap: int | None = None):
         """Slot g plays game g (g < quota) or idles; the pool is emptied.  quota None = no
-        limit (every finished game's slot starts another).  With a quota the pool is sized for
-        its worst case (quota games of max_len positions), so simulate_games never drops one."""
+        limit (every finished game's slot starts another).  With a quota the game records are
+        sized for it and the positions grow on demand (`ensure_room` before each step), so
+        simulate_games never drops a game (round 4 reserved quota x max_len positions up
+        front: 2,049 rows per chess game)."""
         q = _UNLIMITED if quota is None else int(quota)
         self.quota = q
         need_g = max(int(games_cap or 0), q if quota is not None else 0)
-        need_p = need_g * self.max_len if quota is not None else 0
-        if need_g > self.games_cap or need_p > self.pool_cap:
-            self._alloc_pool(max(need_g, self.games_cap), max(need_p, self.pool_cap))
+        if need_g > self.games_cap:
+            self._alloc_pool(need_g, self.pool_cap)
         ids = torch.arange(self.n, dtype=torch.int32, device=self.dev)
         self.slot.zero_()
         self.slot[:, 0] = 1
@@ -194,6 +219,14 @@ class Trajectories:
         return out
 
 
+def _room(traj):
+    """Before a step under a game quota: grow the trajectory pool so the step cannot overflow
+    it (not while a step is being captured into a graph: the unlimited quota is the graphs'
+    case, and their pool is pinned)."""
+    if traj is not None and traj.quota != _UNLIMITED and not torch.cuda.is_current_stream_capturing():
+        traj.ensure_room()
+
+
 class C4SelfPlay:
     """Connect4 self-play pool on one GPU: search (zc_c4_search_async) + play/evaluate
     (zc_c4_play_async) + trajectory recording (zc_traj_record_async), all stream-ordered,
@@ -248,6 +281,7 @@ class C4SelfPlay:
         """One move for every game (on torch's current stream unless given); returns the
         per-game results tensor (ONGOING = 2, IDLE = 3).  Finished games restart from the
         opening."""
+        _room(self.traj)
         self.step_search(stream)
         return self.step_finish(stream)
 
@@ -476,6 +510,7 @@ class ChessSelfPlay:
     def step(self, stream: int | None = None) -> torch.Tensor:
         """One move for every game; returns the per-game results tensor (ONGOING = 2,
         IDLE = 3).  Finished games restart from the initial position."""
+        _room(self.traj)
         s = self._stream(stream)
         if self.ps is not None:
             mv, _, st = self.ps.enqueue(self.roots, self.sims, self.net_fn, temperature=self.temperature)
@@ -614,7 +649,7 @@ def simulate_games(pool, total_games: int, max_steps: int | None = None, check_e
     while total_games and (steps % check_every or pool.traj.finished() < total_games):
         if max_steps is not None and steps >= max_steps:
             raise RuntimeError(f"{pool.traj.finished()} of {total_games} games finished in {max_steps} steps")
-        pool.step()
+        pool.step()   # with a quota, step() grows the trajectory pool first (ensure_room)
         steps += 1
     pool.last_batch = pool.take()
     res = pool.last_batch.results()
