@@ -227,7 +227,7 @@ def cpu_baseline_chess(snap: dict, moves: int, sims: int = 400, bs: int = 32, c:
                       f"{int(exp.sum())} expansions counted as nodes created; {threads} pthreads, {dt:.1f}s"}
 
 
-def _cpu_net(planes: int, policy: bool = False):
+def _cpu_net(planes: int, policy: bool = False, head: str = "conv"):
     """The network the reference evaluates on a host without a GPU (value_functions.py:61-99:
     DEVICE "cpu", DTYPE float32; models/chess_value/network.py:24-45), random init, with the
     process's CPU share as torch's intra-op threads."""
@@ -236,7 +236,7 @@ def _cpu_net(planes: int, policy: bool = False):
     torch.set_num_threads(threads)
     torch.manual_seed(0)
     if policy:
-        return PolicyValueNetwork().eval(), threads
+        return PolicyValueNetwork(head=head).eval(), threads
     return ValueNetwork(128, 8, in_planes=planes).eval(), threads
 
 
@@ -331,7 +331,7 @@ def cpu_baseline_chess_puct(sims: int = 1600, bs: int = 32, c: float = 1.5, budg
 
     n, dt = _timed_moves(one, budget_s)
     return {"value": round(n * (sims - 1) / dt, 1), "unit": "expansions/s", "cores": threads, "kind": "port",
-            "sample": f"{n} chess openings x {sims} sims, batch {bs}, PUCT specification oracle/puct_ref.py + fp32 "
+            "sample": f"{n} chess openings x {sims} sims, batch {bs}, PUCT specification oracle/puct_ref.py + fp32 conv-head "
                       f"PolicyValueNetwork (128 x 8) on {threads} torch threads, {dt:.1f}s"}
 
 
@@ -476,7 +476,7 @@ def chess_modes(steps: int, dev) -> dict:
     return out
 
 
-def puct_mode(src, steps: int, dev) -> dict:
+def puct_mode(src, steps: int, dev, head: str = "conv", streams: int = 1) -> dict:
     """BASELINE configs[4] (C5) per GPU: chess PUCT self-play, 1024 games x 1600 sims, policy
     + value ResNet (128 x 8, random init, fp16; tower on the MFMA kernels), Dirichlet root
     noise, temperature 1, from the burned-in crude pool's positions; one graph per step."""
@@ -484,8 +484,9 @@ def puct_mode(src, steps: int, dev) -> dict:
     from zeroclone_amd.selfplay import ChessSelfPlay
     G, S, B = 1024, 1600, 32
     torch.manual_seed(0)
-    net = MfmaPolicyValueNetwork(PolicyValueNetwork().eval(), dev)
-    pool = ChessSelfPlay(G, S, batch_size=B, seed=6, device=dev.index, puct_net=net, temperature=1.0)
+    net = MfmaPolicyValueNetwork(PolicyValueNetwork(head=head).eval(), dev)
+    pool = ChessSelfPlay(G, S, batch_size=B, seed=6, device=dev.index, puct_net=net, temperature=1.0,
+                         puct_streams=streams)
     pool.adopt(src)
     exp, dt = _timed_pool_steps(pool, steps)
     pool.close()
@@ -494,6 +495,10 @@ def puct_mode(src, steps: int, dev) -> dict:
             "steps": steps,
             "config": MIXED + "C5 per GPU: 1024 games x 1600 sims, PUCT c 1.5, Dirichlet(0.3, 0.25), policy+value "
                               "ResNet 128x8 random init fp16 (MFMA tower), temperature 1",
+            "policy_head": ("convolutional (AlphaZero: 1x1 conv 128 -> 64, logit(from, to) = channel to at pixel "
+                            "from; an epilogue of the tower launch, no GEMM)" if head == "conv" else
+                            "linear (1x1 conv 128 -> 32 in the tower launch + Linear 2048 -> 4096 as a GEMM)"),
+            "search_streams": streams,
             **net_rates(flops_per_position(128, 8, 17, 8, 8), G, S, B, nfl, steps, dt)}
 
 
@@ -776,6 +781,7 @@ def run_rank(args, rank: int, world: int, local: int):
             chess_snap = chess.pop("_snap")
             out["extra"]["c4_chess"] = chess
             out["extra"]["c5_chess_puct"] = puct_mode(crude_pool, args.net_steps, dev)
+            out["extra"]["c5_chess_puct_linear_head"] = puct_mode(crude_pool, args.net_steps, dev, head="linear")
             crude_pool.close()
             out["extra"]["net_tower"] = tower_mode(dev)
             out["extra"]["c1_engine"] = c1_mode(dev)

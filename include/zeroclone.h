@@ -528,6 +528,16 @@ int zc_net_tower_async(int32_t n_boards, int32_t h, int32_t w, int32_t cin0, int
 int zc_net_tower_policy_async(int32_t n_boards, int32_t h, int32_t w, int32_t cin0, int32_t nconv, const void *d_in,
                               const void *d_packed_weights, const float *d_biases, const float *d_fc_w, float fc_b,
                               double *d_values, const void *d_pw, const float *d_pb, void *d_pout, void *hip_stream);
+/* zc_net_tower_policy_ex_async: zc_net_tower_policy_async with policy_channels = 32 or 64 output
+ *   channels (d_pw [policy_channels / 32][8][64][8], d_pb [policy_channels] f32, d_pout
+ *   [n][h*w][policy_channels]) and the ReLU on (relu != 0) or off.  policy_channels 64, relu 0
+ *   on an 8x8 board is the CONVOLUTIONAL policy head (nets.PolicyValueNetwork(head="conv"),
+ *   AlphaZero's design): logit(from, to) = channel `to` at pixel `from`, so d_pout viewed as
+ *   [n][4096] is the logits in the from*64 + to order zc_chess_puct_backup reads — no GEMM. */
+int zc_net_tower_policy_ex_async(int32_t n_boards, int32_t h, int32_t w, int32_t cin0, int32_t nconv,
+                                 const void *d_in, const void *d_packed_weights, const float *d_biases,
+                                 const float *d_fc_w, float fc_b, double *d_values, const void *d_pw, const float *d_pb,
+                                 int32_t policy_channels, int32_t relu, void *d_pout, void *hip_stream);
 int zc_net_planes_to_nhwc_async(int32_t n, int32_t cin, int32_t hw, int32_t cpad, const void *d_planes, void *d_out,
                                 void *hip_stream);
 int zc_net_value_head_async(int32_t n, int32_t hw, const void *d_act, const float *d_fc_w, float fc_b, double *d_values,

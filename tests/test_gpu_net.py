@@ -235,9 +235,9 @@ def _integer_head(vnet, hw, seed):
 @pytest.mark.parametrize("shape", [(17, 8, 8), (2, 6, 7)])
 def test_value_head_exact_on_integers(mf, shape, monkeypatch):
     """The value head (avg-pool, Linear(128, 1), + bias) on an integer network: its pre-tanh
-    sum (ZC_HEAD_RAW=1) equals float64 exactly on 8x8 boards (the pool's 1/64 is exact), in the
-    fused tower launch and in the layered value_head_kernel, ragged tiles included; on 6x7 the
-    division by 42 rounds in fp32, so there the bound is 8 fp32 ulps of the sums.  With the
+    sum (ZC_HEAD_RAW=1) equals float64 exactly, in the fused tower launch and in the layered
+    value_head_kernel, ragged tiles included (on 6x7 too: each lane's sum is a multiple of
+    42/64, so the kernel's correctly rounded division by 42 is exact).  With the
     tanh (the product path) the values equal float64 tanh of that sum within tanhf's precision.
     A head without its bias or without its Linear would fail every one of these."""
     from zeroclone_amd.nets import FoldedValueNetwork, MfmaValueNetwork
@@ -247,10 +247,13 @@ def test_value_head_exact_on_integers(mf, shape, monkeypatch):
     xs = [(torch.rand(n, c, h, w) < 0.3).half() for n in (1, 5, 131)]
 
     def pre_tanh(x):
+        # exact in float64: the channel sums S_c (integers), k_c = fcw_c * 64 / hw (integers),
+        # sum_c S_c k_c / 64 + bias (a mean taken first would round S_c / 42)
         f = FoldedValueNetwork(vnet).double()
         with torch.no_grad():
             act = f.res(torch.relu(f.stem(x.double())))
-            return act.mean(dim=(2, 3)) @ f.fc.weight.detach().double().reshape(-1) + f.fc.bias.detach().double()
+            k = torch.round(f.fc.weight.detach().double().reshape(-1) * 64.0 / (h * w))
+            return (act.sum(dim=(2, 3)) @ k) / 64.0 + f.fc.bias.detach().double()
     with torch.no_grad():   # centre the sums on tanh's active range (a multiple of 1/64)
         vnet.head[2].bias.fill_(0.0)
         vnet.head[2].bias.fill_(-float(torch.round(pre_tanh(xs[-1]).median() * 64)) / 64)
@@ -265,24 +268,20 @@ def test_value_head_exact_on_integers(mf, shape, monkeypatch):
         for fused in (True, False):
             got = net(x.cuda(), fused=fused).clone()
             torch.cuda.synchronize()
-            if h * w == 64:
-                assert torch.equal(got.cpu(), pre), (mf, shape, n, fused)
-            else:   # the pool's 1/42 is rounded in fp32: a few ulps of the lane sums
-                np.testing.assert_allclose(got.cpu().numpy(), pre.numpy(), rtol=0,
-                                           atol=8 * 2.0 ** -23 * max(1.0, float(pre.abs().max())))
+            assert torch.equal(got.cpu(), pre), (mf, shape, n, fused)
         monkeypatch.setenv("ZC_HEAD_RAW", "0")
         got = net(x.cuda()).clone()
         torch.cuda.synchronize()
         np.testing.assert_allclose(got.cpu().numpy(), np.tanh(pre.numpy()), rtol=0, atol=1e-6)
 
 
-def _integer_pv_net(c, h, w, nl, seed):
+def _integer_pv_net(c, h, w, nl, seed, head="linear"):
     """PolicyValueNetwork with an integer tower (as _integer_net), an integer 1x1 policy conv,
     identity BN with integer biases and a sparse integer Linear: every policy value is a small
     integer, exact in fp16 and in any fp32 summation order."""
     from zeroclone_amd.nets import PolicyValueNetwork
     g = torch.Generator().manual_seed(seed)
-    net = PolicyValueNetwork(in_planes=c, board=(h, w), n_logits=nl).eval()
+    net = PolicyValueNetwork(in_planes=c, board=(h, w), n_logits=nl, head=head).eval()
     for m in net.modules():
         if isinstance(m, torch.nn.Conv2d):
             dens = 0.002 if m.in_channels == 128 and m.kernel_size == (3, 3) else 0.02
@@ -328,3 +327,25 @@ def test_policy_head_exact_on_integers(shape):
     assert want_logits.abs().max().item() < 2048 and (want_logits != lin.bias.double()).any()
     assert torch.equal(pout, want_p)
     assert torch.equal(logits.double().cpu(), want_logits)
+
+
+def test_convolutional_policy_head_exact_on_integers():
+    """PolicyValueNetwork(head="conv") on an integer network: the logits the tower launch
+    writes (1x1 conv 128 -> 64 + BN bias, no ReLU; pixel = from, channel = to) equal float64
+    exactly, in from*64 + to order (ragged last tile)."""
+    from zeroclone_amd.nets import FoldedValueNetwork, MfmaPolicyValueNetwork
+    n = 37
+    net = _integer_pv_net(17, 8, 8, 4096, seed=91, head="conv")
+    mnet = MfmaPolicyValueNetwork(net)
+    x = (torch.rand(n, 17, 8, 8) < 0.3).half()
+    _, logits = mnet(x.cuda())
+    logits = logits.double().cpu()
+    fv = FoldedValueNetwork(net.value_network()).double()
+    conv, bn = net.policy[0], net.policy[1]
+    with torch.no_grad():
+        t = fv.res(torch.relu(fv.stem(x.double())))
+        p = torch.nn.functional.conv2d(t, conv.weight.double()) + bn.bias.double().reshape(1, -1, 1, 1)
+        want = p.flatten(2).transpose(1, 2).reshape(n, 4096)       # [n, from, to]
+        assert torch.equal(want.float().double(), want)
+    assert want.abs().max().item() < 2048 and (want < 0).any() and (want > 0).any()
+    assert torch.equal(logits, want)

@@ -236,7 +236,7 @@ def test_c5_chess_puct_pool_matches_puct_ref(chess_pool):
     from zeroclone_amd.selfplay import ChessSelfPlay
     S = 1600
     torch.manual_seed(13)
-    net = MfmaPolicyValueNetwork(PolicyValueNetwork().eval())
+    net = MfmaPolicyValueNetwork(PolicyValueNetwork(head="conv").eval())   # the head bench.py times
     pool = ChessSelfPlay(CG, S, batch_size=CB, seed=6, puct_net=net, temperature=1.0)
     pool.adopt(chess_pool)
     pool.ps.leaves = torch.zeros((CG * CB, 72), dtype=torch.uint8, device=pool.dev)   # export leaves (test hook)

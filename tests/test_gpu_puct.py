@@ -105,6 +105,35 @@ def test_policy_value_network_mfma_matches_torch():
     np.testing.assert_allclose(l.float().cpu().numpy(), l_ref.numpy(), atol=5e-2, rtol=2e-2)
 
 
+def test_convolutional_policy_head_matches_fp32():
+    """PolicyValueNetwork(head="conv") (round 5): the 1x1 conv 128 -> 64 epilogue writes the
+    logits (pixel = from square, channel = to square) in the tower launch; against torch fp32
+    of the same network on the same tower activation (fp16 output rounding: 1e-2 abs + 1e-2
+    rel), values bit-identical to the value-only launch of the same tower, ragged tiles."""
+    from zeroclone_amd.nets import MfmaPolicyValueNetwork, PolicyValueNetwork, _fold
+    torch.manual_seed(6)
+    net = PolicyValueNetwork(head="conv").eval()
+    for m in net.modules():
+        if isinstance(m, torch.nn.BatchNorm2d):
+            m.running_mean.uniform_(-0.1, 0.1)
+            m.running_var.uniform_(0.5, 1.5)
+    mnet = MfmaPolicyValueNetwork(net)
+    assert mnet.conv_head and mnet.fused
+    n = 37
+    x = ((torch.rand(n, 17, 8, 8) < 0.3).half()).cuda()
+    v, logits = mnet(x)
+    logits = logits.float().clone()
+    a, vals = mnet.tower.tower(x, head=True)
+    folded = _fold(net.policy[0], net.policy[1])
+    wf = folded.weight.detach().float().reshape(64, -1).cuda()
+    ref = (a.float() @ wf.t() + folded.bias.detach().float().cuda()).reshape(n, 4096)   # [n, from, to]
+    torch.cuda.synchronize()
+    assert logits.shape == (n, 4096)
+    np.testing.assert_allclose(logits.cpu().numpy(), ref.cpu().numpy(), atol=1e-2, rtol=1e-2)
+    assert torch.equal(v, vals)
+    assert ref.abs().max().item() > 0.1 and (ref < 0).any()   # no ReLU on logits
+
+
 @pytest.mark.parametrize("shape", [(37, 17, 8, 8, 4096), (53, 2, 6, 7, 7)])
 def test_fused_policy_conv_matches_fp32(shape):
     """The policy 1x1 conv fused into the tower launch (zc_net_tower_policy_async) against a
@@ -166,3 +195,34 @@ def test_consecutive_searches_draw_fresh_noise(eng):
         pri.append(ps.prior.cpu().numpy()[:, :20].copy())
     assert ps.search_no.cpu().tolist() == [2] * n
     assert all(not np.array_equal(pri[0][i], pri[1][i]) for i in range(n))
+
+
+@pytest.mark.parametrize("k", [2, 3])
+def test_split_stream_search_equals_the_single_stream_search(eng, k):
+    """ChessPuctSearch with k network callables: the games in k contiguous parts on k streams
+    (one part's select / backup / policy GEMM beside another part's tower).  The parts share
+    nothing, so moves, root visits, root priors (noise included: the per-game search numbers
+    of a sub-range launch) and counters equal the one-stream search's — eagerly and replayed
+    from a captured graph."""
+    from zeroclone_amd.nets import MfmaPolicyValueNetwork, PolicyValueNetwork
+    from zeroclone_amd.valued import ChessPuctSearch
+    torch.manual_seed(3)
+    net = MfmaPolicyValueNetwork(PolicyValueNetwork().eval())
+    fens = (FENS * 8)[:37]
+    roots = roots_of(fens)
+    outs = []
+    for split in (False, True):
+        ps = ChessPuctSearch(eng, len(fens), 32, seed=9)
+        fn = [(lambda l, p, c, m=net.replica(): m(p)) for _ in range(k)] if split else (lambda l, p, c: net(p))
+        mv, na, st = ps.run(roots, 97, fn, temperature=1.0)
+        first = (mv.cpu().clone(), na.cpu().clone(), ps.prior.cpu().clone(), st[:, :3].cpu().clone())
+        g = ps.capture(roots, 97, fn, temperature=1.0)
+        g.replay()
+        torch.cuda.synchronize()
+        second = (ps.move.cpu().clone(), ps.na.cpu().clone(), ps.prior.cpu().clone())
+        assert ps.search_no.cpu().tolist() == [2] * len(fens)
+        outs.append((first, second))
+    (a1, a2), (b1, b2) = outs
+    for x, y in zip(a1 + a2, b1 + b2):
+        assert torch.equal(x, y)
+    assert (a1[1].sum(dim=1) == 96).all()

@@ -118,3 +118,21 @@ def test_fp16_storage_error_fits_the_gpu_tolerance(golden, wide, atol):
     assert err < atol / 2, err
     assert fails_tracking(torch.tanh(feat @ w).numpy(), want, atol)          # bias dropped
     assert fails_tracking(np.full_like(want, want.mean()), want, atol)       # constant head
+
+
+def test_convolutional_policy_head_orders_logits_from_to():
+    """PolicyValueNetwork(head="conv"): logit index from*64 + to = the 1x1 conv's channel `to`
+    at pixel `from` (the order zc_chess_puct_backup reads)."""
+    from zeroclone_amd.nets import PolicyValueNetwork
+    torch.manual_seed(2)
+    net = PolicyValueNetwork(head="conv").eval()
+    x = (torch.rand(2, 17, 8, 8) < 0.3).float()
+    with torch.no_grad():
+        _, lg = net(x)
+        t = net.res(net.stem(x))
+        p = net.policy(t)   # [n, 64 to, 8, 8]
+    for fr in (0, 9, 63):
+        for to in (0, 17, 63):
+            assert torch.equal(lg[:, fr * 64 + to], p[:, to, fr // 8, fr % 8])
+    with pytest.raises(ValueError):
+        PolicyValueNetwork(board=(6, 7), n_logits=7, in_planes=2, head="conv")

@@ -117,6 +117,7 @@ __device__ int c4_puct_walk(const C4PuctParams &p, C4PNode *T, int &nnodes, int 
         const int32_t na = valid ? N->na[k] : 0;
         const double wk = valid ? N->w[k] : 0.0;
         const float pk = valid ? N->pr[k] : 0.0f;
+        const uint32_t chk = valid ? (uint32_t)N->child[k] : 0xFFFFu;  // with the others: no dependent load after the argmax
         // sum_b N(b): lanes 0..7 (integers: exact in any order)
         int tot = (lane < 8u) ? na : 0;
         tot += dpp<0xB1>(tot);
@@ -134,7 +135,7 @@ __device__ int c4_puct_walk(const C4PuctParams &p, C4PNode *T, int &nnodes, int 
         }
         ++depth;
         if (lane == (uint32_t)depth) pathv = (uint32_t)node | ((uint32_t)best << 16);
-        const int child = uni((int)N->child[best]);
+        const int child = (int)(uint32_t)__builtin_amdgcn_readlane((int)chk, best);
         if (child != 0xFFFF) {
             node = child;
             continue;

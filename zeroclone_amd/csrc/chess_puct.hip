@@ -49,21 +49,45 @@ __device__ int puct_walk(const ChessParams &p, const CTree &t, CLds &L, int &nno
             break;
         }
         const uint32_t base = uni(N->base);
+        // ONE round of loads per level: every child slot's N, W, P and child id (up to four
+        // 64-slot chunks, registers), issued together; the sum of N, the scores and the child
+        // pointer then come from registers (round 4 read N twice and the child once more:
+        // three dependent global round trips per level).  Same arithmetic in the same order.
+        int32_t na_r[4];
+        double w_r[4];
+        float pr_r[4];
+        uint32_t ch_r[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int j = q * 64 + (int)lane;
+            na_r[q] = 0;
+            w_r[q] = 0.0;
+            pr_r[q] = 0.0f;
+            ch_r[q] = 0xFFFFu;
+            if (q * 64 < nm && j < nm) {
+                na_r[q] = t.na[base + j];
+                w_r[q] = t.w[base + j];
+                pr_r[q] = t.pr[base + j];
+                ch_r[q] = t.ch[base + j];
+            }
+        }
         double tot = 0.0;
-        for (int b = 0; b < nm; b += 64) {
-            const int j = b + (int)lane;
-            tot += j < nm ? (double)t.na[base + j] : 0.0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int j = q * 64 + (int)lane;
+            if (q * 64 < nm) tot += j < nm ? (double)na_r[q] : 0.0;
         }
         const double sq = sqrt(wave_sum_d(tot));
         double bv = -INFINITY;
         int bi = 0x7FFFFFFF;
-        for (int b = 0; b < nm; b += 64) {
-            const int j = b + (int)lane;
-            if (j < nm) {
-                const int32_t na = t.na[base + j];
-                const double q = na > 0 ? t.w[base + j] / (double)na : 0.0;
-                const double u = p.c * (double)t.pr[base + j] * sq / (double)(1 + na);
-                const double v = q + u;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int j = q * 64 + (int)lane;
+            if (q * 64 < nm && j < nm) {
+                const int32_t na = na_r[q];
+                const double qv = na > 0 ? w_r[q] / (double)na : 0.0;
+                const double u = p.c * (double)pr_r[q] * sq / (double)(1 + na);
+                const double v = qv + u;
                 if (v > bv) {
                     bv = v;
                     bi = j;
@@ -73,13 +97,15 @@ __device__ int puct_walk(const ChessParams &p, const CTree &t, CLds &L, int &nno
         argmax64(bv, bi);
         const int best = uni(bi);
         const uint32_t s = base + (uint32_t)best;
+        const int bq = best >> 6;
+        const uint32_t chv = bq == 0 ? ch_r[0] : bq == 1 ? ch_r[1] : bq == 2 ? ch_r[2] : ch_r[3];
+        const int child = (int)(uint32_t)__builtin_amdgcn_readlane((int)chv, best & 63);
         if (lane == 0) {  // virtual loss: one visit lost by this node's mover
             t.na[s] += 1;
             t.w[s] -= 1.0;
         }
         ++depth;
         if (lane == (uint32_t)depth) pathv = s;
-        const int child = uni((int)t.ch[s]);
         if (child != 0xFFFF) {
             node = child;
             continue;

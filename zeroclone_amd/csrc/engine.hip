@@ -1132,7 +1132,9 @@ zc::ChessParams puct_params(zc_engine *e, int32_t first, int32_t n) {
     p.dir_alpha = e->px_alpha;
     p.dir_eps = e->px_eps;
     p.seed = e->px_seed;
-    p.search_no = e->px_search_no;
+    // d_search_no is indexed by game - first_game of the begin call; a launch over a
+    // sub-range [first, first + n) indexes it from its own first game
+    p.search_no = e->px_search_no ? e->px_search_no + (first - e->px_first) : nullptr;
     return p;
 }
 int check_px(zc_engine *e, int32_t first, int32_t n, int32_t flush, bool need_flush) {
@@ -1270,7 +1272,7 @@ zc::C4PuctParams c4p_params(zc_engine *e, int32_t first, int32_t n) {
     p.dir_alpha = e->qx_alpha;
     p.dir_eps = e->qx_eps;
     p.seed = e->qx_seed;
-    p.search_no = e->qx_search_no;
+    p.search_no = e->qx_search_no ? e->qx_search_no + (first - e->qx_first) : nullptr;
     return p;
 }
 int check_qx(zc_engine *e, int32_t first, int32_t n, int32_t flush, bool need_flush) {
@@ -1471,6 +1473,22 @@ int zc_net_tower_policy_async(int32_t n, int32_t h, int32_t w, int32_t cin0, int
     if (!n) return ZC_OK;
     if (!zc::launch_net_tower(n, h, w, cin0, nconv, d_in, d_packed, d_bias, nullptr, d_fc_w, fc_b, d_values, d_pw,
                               d_pb, d_pout, (hipStream_t)hip_stream))
+        return fail(ZC_EINVAL, "tower shape (h %d, w %d, cin0 %d, %d convs) not supported", h, w, cin0, nconv);
+    ZC_HIP(hipGetLastError());
+    return ZC_OK;
+}
+
+int zc_net_tower_policy_ex_async(int32_t n, int32_t h, int32_t w, int32_t cin0, int32_t nconv, const void *d_in,
+                                 const void *d_packed, const float *d_bias, const float *d_fc_w, float fc_b,
+                                 double *d_values, const void *d_pw, const float *d_pb, int32_t policy_channels,
+                                 int32_t relu, void *d_pout, void *hip_stream) {
+    if (n < 0 || (n && (!d_in || !d_packed || !d_bias || !d_fc_w || !d_values || !d_pw || !d_pb || !d_pout)) ||
+        ((uintptr_t)d_packed & 15) || ((uintptr_t)d_in & 15) || ((uintptr_t)d_bias & 15) || ((uintptr_t)d_pw & 15) ||
+        ((uintptr_t)d_pb & 15) || ((uintptr_t)d_pout & 7) || (policy_channels != 32 && policy_channels != 64))
+        return fail(ZC_EINVAL, "bad argument");
+    if (!n) return ZC_OK;
+    if (!zc::launch_net_tower(n, h, w, cin0, nconv, d_in, d_packed, d_bias, nullptr, d_fc_w, fc_b, d_values, d_pw,
+                              d_pb, d_pout, (hipStream_t)hip_stream, policy_channels, relu))
         return fail(ZC_EINVAL, "tower shape (h %d, w %d, cin0 %d, %d convs) not supported", h, w, cin0, nconv);
     ZC_HIP(hipGetLastError());
     return ZC_OK;

@@ -873,10 +873,12 @@ __device__ __forceinline__ void tower_epilogue16_swap(_Float16 *dst, const float
 // weights as 32x32x16 MFMA A fragments [8 k-steps][64 lanes][8] (lane = output channel
 // lane % 32, k = 16 kc + 8 (lane / 32) + e), pb [32] fp32 bias; out [n * H * W][32] fp16.
 struct TowerPolicy {
-    const _Float16 *pw;
-    const float *pb;
-    _Float16 *out;
-    int head_raw;  // test switch (ZC_HEAD_RAW=1): the value head writes its pre-tanh sum
+    const _Float16 *pw;  // [mblocks][8 k-steps][64 lanes][8] fp16 A fragments
+    const float *pb;     // [32 * mblocks]
+    _Float16 *out;       // [n][hw][32 * mblocks]
+    int head_raw;        // test switch (ZC_HEAD_RAW=1): the value head writes its pre-tanh sum
+    int mblocks;         // output channels / 32 (1: the 128 -> 32 conv; 2: the 128 -> 64 logit conv)
+    int relu;            // ReLU on the outputs (the linear-head network's conv) or not (logits)
 };
 
 template <int H, int W, int BPH, int CIN0, int NT, int WPE, int PG = 1, int MF = 32, int EPI = 0>
@@ -1017,31 +1019,37 @@ __global__ __launch_bounds__(256 * PG) __attribute__((amdgpu_waves_per_eu(WPE, W
     }
     if (pol.out) {
         // the 1x1 conv: wave (pg, wave) takes pixel tiles wave, wave + 4, ... of its group (32
-        // pixels each), 8 MFMAs over the 128 channels, + bias, ReLU, fp16 -> [pixel][32]
-        h8 pa[8];
+        // pixels each); per block of 32 output channels 8 MFMAs over the 128 channels, + bias,
+        // ReLU (the linear head's conv) or not (the convolutional head's logits), fp16 ->
+        // [pixel][32 * mblocks]
+        const int nout = 32 * pol.mblocks;
+        for (int mb = 0; mb < pol.mblocks; ++mb) {
+            h8 pa[8];
 #pragma unroll
-        for (int kc = 0; kc < 8; ++kc) pa[kc] = *(const h8 *)(pol.pw + ((size_t)kc * 64 + lane) * 8);
-        float4 pbv[4];
+            for (int kc = 0; kc < 8; ++kc) pa[kc] = *(const h8 *)(pol.pw + (((size_t)mb * 8 + kc) * 64 + lane) * 8);
+            float4 pbv[4];
 #pragma unroll
-        for (int g = 0; g < 4; ++g) pbv[g] = *(const float4 *)(pol.pb + 8 * g + 4 * hh);
-        for (int t = wave; t < NT; t += 4) {
-            const int P = pbase + t * 32 + r;
-            f16x acc;
+            for (int g = 0; g < 4; ++g) pbv[g] = *(const float4 *)(pol.pb + 32 * mb + 8 * g + 4 * hh);
+            const float lo = pol.relu ? 0.0f : -INFINITY;
+            for (int t = wave; t < NT; t += 4) {
+                const int P = pbase + t * 32 + r;
+                f16x acc;
 #pragma unroll
-            for (int k = 0; k < 16; ++k) acc[k] = 0.0f;
+                for (int k = 0; k < 16; ++k) acc[k] = 0.0f;
 #pragma unroll
-            for (int kc = 0; kc < 8; ++kc) {
-                const h8 x = *(const h8 *)(lds + (size_t)P * LD + kc * 16 + hh * 8);
-                acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(pa[kc], x, acc, 0, 0, 0);
-            }
-            if (P < npix) {
+                for (int kc = 0; kc < 8; ++kc) {
+                    const h8 x = *(const h8 *)(lds + (size_t)P * LD + kc * 16 + hh * 8);
+                    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(pa[kc], x, acc, 0, 0, 0);
+                }
+                if (P < npix) {
 #pragma unroll
-                for (int g = 0; g < 4; ++g) {
-                    const float bb[4] = {pbv[g].x, pbv[g].y, pbv[g].z, pbv[g].w};
-                    h4 ov;
+                    for (int g = 0; g < 4; ++g) {
+                        const float bb[4] = {pbv[g].x, pbv[g].y, pbv[g].z, pbv[g].w};
+                        h4 ov;
 #pragma unroll
-                    for (int e = 0; e < 4; ++e) ov[e] = (_Float16)fmaxf(acc[4 * g + e] + bb[e], 0.0f);
-                    *(h4 *)(pol.out + ((size_t)b0 * HW + P) * 32 + 8 * g + 4 * hh) = ov;
+                        for (int e = 0; e < 4; ++e) ov[e] = (_Float16)fmaxf(acc[4 * g + e] + bb[e], lo);
+                        *(h4 *)(pol.out + ((size_t)b0 * HW + P) * nout + 32 * mb + 8 * g + 4 * hh) = ov;
+                    }
                 }
             }
         }
@@ -1232,9 +1240,10 @@ bool launch_net_conv3x3_packed(int n, int h, int w, int cin, const void *in, con
 
 bool launch_net_tower(int n, int h, int w, int cin0, int nconv, const void *in, const void *wall, const float *ball,
                       void *out, const float *fcw, float fcb, double *values, const void *pw, const float *pb,
-                      void *pout, hipStream_t s) {
+                      void *pout, hipStream_t s, int pol_channels, int pol_relu) {
     if (cin0 != 32 || nconv < 1 || !(nconv & 1)) return false;
-    const TowerPolicy pol{(const _Float16 *)pw, pb, (_Float16 *)pout, head_raw()};
+    if (pout && pol_channels != 32 && pol_channels != 64) return false;
+    const TowerPolicy pol{(const _Float16 *)pw, pb, (_Float16 *)pout, head_raw(), pol_channels / 32, pol_relu ? 1 : 0};
     // 128-pixel tiles at two workgroups per CU; 64-pixel tiles (one chess board) at 3 or 4
     // workgroups per CU measured 10 % slower (tools/ab_tower.py)
 #ifndef ZC_TOWER_PG

@@ -340,7 +340,7 @@ bool launch_net_conv3x3(int n, int h, int w, int cin, const void *in, const void
                         const void *res, void *out, int relu, hipStream_t s);
 bool launch_net_tower(int n, int h, int w, int cin0, int nconv, const void *in, const void *wall, const float *ball,
                       void *out, const float *fcw, float fcb, double *values, const void *pw, const float *pb,
-                      void *pout, hipStream_t s);
+                      void *pout, hipStream_t s, int pol_channels = 32, int pol_relu = 1);
 bool launch_net_conv3x3_packed(int n, int h, int w, int cin, const void *in, const void *wp, const float *bias,
                                const void *res, void *out, int relu, hipStream_t s);
 bool launch_net_pack_conv_weight(int cin, const void *w, void *packed, hipStream_t s);

@@ -160,6 +160,13 @@ class MfmaValueNetwork:
         self.fcb = float(f.fc.bias.detach().float().item())
         self._bufs = {}
 
+    def replica(self) -> "MfmaValueNetwork":
+        """The same network (weights shared) with buffers of its own: a second stream can
+        evaluate it concurrently (valued.ChessPuctSearch's split search)."""
+        r = copy.copy(self)
+        r._bufs = {}
+        return r
+
     def _buffers(self, n, hw):
         import torch
         key = (n, hw)
@@ -206,26 +213,28 @@ class MfmaValueNetwork:
             a, b = b, a
         return a, vals
 
-    def tower_policy(self, planes, pw, pb, pout):
-        """The tower, the value head and a 128 -> 32 policy 1x1 conv (pw: pack_policy_1x1's
-        fragments, pb fp32 [32]) in ONE launch (zc_net_tower_policy_async): fp64 values [n];
-        pout [n, h*w, 32] fp16 receives ReLU(conv1x1 + pb).  No tower activation is written."""
+    def tower_policy(self, planes, pw, pb, pout, relu: bool = True):
+        """The tower, the value head and a policy 1x1 conv 128 -> P (P = 32 or 64; pw:
+        pack_policy_1x1's fragments, pb fp32 [P]) in ONE launch (zc_net_tower_policy_ex_async):
+        fp64 values [n]; pout [n, h*w, P] fp16 receives conv1x1 + pb, ReLU'd when `relu`.  No
+        tower activation is written."""
         import torch
         from . import _native
         n, c, h, w = planes.shape
+        P = pout.shape[-1] if pout.dim() == 3 else 0
         if c != self.in_planes or planes.dtype != torch.float16:
             raise ValueError("planes must be fp16 [n, in_planes, h, w]")
-        if pout.shape != (n, h * w, 32) or pout.dtype != torch.float16 or not pout.is_contiguous():
-            raise ValueError("pout must be contiguous fp16 [n, h*w, 32]")
+        if P not in (32, 64) or pout.shape != (n, h * w, P) or pout.dtype != torch.float16 or not pout.is_contiguous():
+            raise ValueError("pout must be contiguous fp16 [n, h*w, 32 or 64]")
         planes = planes.contiguous()
         x0, _, _, _, vals = self._buffers(n, h * w)
         s = ctypes_stream(self.dev)
         L = _native.lib()
         _native.check(L.zc_net_planes_to_nhwc_async(n, c, h * w, self.cpad, planes.data_ptr(), x0.data_ptr(), s))
-        _native.check(L.zc_net_tower_policy_async(n, h, w, self.cpad, len(self.wp), x0.data_ptr(),
-                                                  self.wall.data_ptr(), self.ball.data_ptr(), self.fcw.data_ptr(),
-                                                  self.fcb, vals.data_ptr(), pw.data_ptr(), pb.data_ptr(),
-                                                  pout.data_ptr(), s))
+        _native.check(L.zc_net_tower_policy_ex_async(n, h, w, self.cpad, len(self.wp), x0.data_ptr(),
+                                                     self.wall.data_ptr(), self.ball.data_ptr(), self.fcw.data_ptr(),
+                                                     self.fcb, vals.data_ptr(), pw.data_ptr(), pb.data_ptr(), P,
+                                                     1 if relu else 0, pout.data_ptr(), s))
         return vals
 
     def __call__(self, planes, fused: bool = True):
@@ -248,13 +257,15 @@ def ctypes_stream(dev):
 
 
 def pack_policy_1x1(weight):
-    """A [32, 128] (out, in) 1x1 conv weight as the tower kernel's v_mfma_f32_32x32x16_f16 A
-    fragments, fp16 [8 k-steps][64 lanes][8]: lane l of k-step kc holds
-    weight[l % 32, 16 kc + 8 (l // 32) + e] (csrc/net_conv.hip TowerPolicy)."""
+    """A [P, 128] (out, in) 1x1 conv weight, P = 32 or 64, as the tower kernel's
+    v_mfma_f32_32x32x16_f16 A fragments, fp16 [P / 32 blocks][8 k-steps][64 lanes][8]: lane l of
+    k-step kc of block mb holds weight[32 mb + l % 32, 16 kc + 8 (l // 32) + e]
+    (csrc/net_conv.hip TowerPolicy)."""
     co, ci = weight.shape
-    if (co, ci) != (32, 128):
-        raise ValueError("the fused policy conv is 128 -> 32 channels")
-    return weight.reshape(32, 8, 2, 8).permute(1, 2, 0, 3).reshape(8, 64, 8).contiguous()
+    if co not in (32, 64) or ci != 128:
+        raise ValueError("the fused policy conv is 128 -> 32 or 64 channels")
+    mb = co // 32
+    return weight.reshape(mb, 32, 8, 2, 8).permute(0, 2, 3, 1, 4).reshape(mb, 8, 64, 8).contiguous()
 
 
 class PolicyValueNetwork(nn.Module):
@@ -264,27 +275,43 @@ class PolicyValueNetwork(nn.Module):
     rules promote to a queen only, so from/to identifies a move)."""
 
     def __init__(self, channels: int = 128, blocks: int = 8, in_planes: int = 17, board=(8, 8),
-                 policy_planes: int = 32, n_logits: int = 4096):
+                 policy_planes: int = 32, n_logits: int = 4096, head: str = "linear"):
         super().__init__()
         base = ValueNetwork(channels, blocks, in_planes)
         self.stem, self.res, self.head = base.stem, base.res, base.head
         h, w = board
-        self.policy = nn.Sequential(
-            nn.Conv2d(channels, policy_planes, 1, bias=False),
-            nn.BatchNorm2d(policy_planes),
-            nn.ReLU(inplace=True),
-            nn.Flatten(),
-            nn.Linear(policy_planes * h * w, n_logits),
-        )
+        self.head_kind = head
+        if head == "conv":
+            # AlphaZero's convolutional policy head: logit(from, to) = channel `to` of a 1x1 conv
+            # at pixel `from` — one logit per (from, to) square pair, index from*64 + to, with no
+            # fully connected layer (on the GPU it is an MFMA epilogue of the tower: no GEMM)
+            if h * w * h * w != n_logits:
+                raise ValueError("the convolutional head needs n_logits = (h*w)**2 (one per square pair)")
+            self.policy = nn.Sequential(nn.Conv2d(channels, h * w, 1, bias=False), nn.BatchNorm2d(h * w))
+        elif head == "linear":
+            self.policy = nn.Sequential(
+                nn.Conv2d(channels, policy_planes, 1, bias=False),
+                nn.BatchNorm2d(policy_planes),
+                nn.ReLU(inplace=True),
+                nn.Flatten(),
+                nn.Linear(policy_planes * h * w, n_logits),
+            )
+        else:
+            raise ValueError("head must be 'linear' or 'conv'")
 
     def value_network(self) -> ValueNetwork:
         v = ValueNetwork(self.stem[0].out_channels, len(self.res), self.stem[0].in_channels)
         v.stem, v.res, v.head = self.stem, self.res, self.head
         return v
 
+    def policy_logits(self, t):
+        if self.head_kind == "conv":   # [n, to, h, w] -> [n, from, to] -> [n, from*64 + to]
+            return self.policy(t).flatten(2).transpose(1, 2).reshape(t.shape[0], -1)
+        return self.policy(t)
+
     def forward(self, x):
         t = self.res(self.stem(x))
-        return self.head(t), self.policy(t)
+        return self.head(t), self.policy_logits(t)
 
 
 class MfmaPolicyValueNetwork:
@@ -294,11 +321,26 @@ class MfmaPolicyValueNetwork:
     activation, so the 128-channel activation never reaches HBM); the flatten + Linear to
     the 4096 logits is one fp16 GEMM on PyTorch-ROCm over its [n, h*w*32] output.  Returns
     (fp64 values [n], fp16 logits [n, 4096]).  fused=False: the tower's activation written
-    out and the 1x1 conv as a GEMM (the pre-round-4 path, kept for the A/B)."""
+    out and the 1x1 conv as a GEMM (the pre-round-4 path, kept for the A/B).
+
+    With the convolutional head (PolicyValueNetwork(head="conv"), round 5) the whole network
+    is ONE launch: the 1x1 conv 128 -> 64 epilogue (BN folded, no ReLU) writes [n, 64 from,
+    64 to] fp16 = the logits in from*64 + to order, and there is no GEMM."""
 
     def __init__(self, net: PolicyValueNetwork, device="cuda"):
         import torch
         self.tower = MfmaValueNetwork(net.value_network(), device)
+        self.conv_head = getattr(net, "head_kind", "linear") == "conv"
+        if self.conv_head:
+            folded = _fold(net.policy[0], net.policy[1])
+            wf = folded.weight.detach().float().reshape(folded.out_channels, -1)   # [h*w, C]
+            if wf.shape != (64, 128):
+                raise ValueError("the fused convolutional head is 128 -> 64 channels (an 8x8 board)")
+            self.fused = True
+            self.pw = pack_policy_1x1(wf).to(device, torch.float16)
+            self.pb = folded.bias.detach().float().contiguous().to(device)
+            self._pout = {}
+            return
         conv, bn, lin = net.policy[0], net.policy[1], net.policy[4]
         folded = _fold(conv, bn)
         P = conv.out_channels
@@ -316,9 +358,23 @@ class MfmaPolicyValueNetwork:
         self.b2 = lin.bias.detach().float().to(device, torch.float16)
         self._pout = {}
 
+    def replica(self) -> "MfmaPolicyValueNetwork":
+        """Weights shared, buffers (tower activations, policy conv output) of its own."""
+        r = copy.copy(self)
+        r.tower = self.tower.replica()
+        r._pout = {}
+        return r
+
     def __call__(self, planes, fused: bool = True):
         import torch
         n, _, h, w = planes.shape
+        if self.conv_head:   # the logits straight from the tower launch: [n, 64 from, 64 to]
+            key = (n, h * w)
+            if key not in self._pout:
+                self._pout[key] = torch.empty((n, h * w, 64), dtype=torch.float16, device=self.tower.dev)
+            p = self._pout[key]
+            vals = self.tower.tower_policy(planes, self.pw, self.pb, p, relu=False)
+            return vals, p.view(n, h * w * 64)
         if fused and self.fused:
             key = (n, h * w)
             if key not in self._pout:

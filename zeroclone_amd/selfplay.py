@@ -458,7 +458,8 @@ class ChessSelfPlay:
     def __init__(self, games: int, sims: int, c: float = 1.4, batch_size: int = 32, seed: int = 0,
                  rank: int = 0, device: int = 0, policy: int = _native.ZC_POLICY_IMMEDIATE_VALUE,
                  freedom: float = 3.0, net=None, init_fen: str | None = None, games_cap: int | None = None,
-                 hist_cap: int = 1024, puct_net=None, temperature: float = 1.0, puct_seed: int = 1):
+                 hist_cap: int = 1024, puct_net=None, temperature: float = 1.0, puct_seed: int = 1,
+                 puct_streams: int = 1):
         self.G, self.sims, self.c, self.bs = games, sims, c, batch_size
         self.policy, self.freedom = int(policy), float(freedom)
         self.dev = torch.device("cuda", device) if isinstance(device, int) else torch.device(device)
@@ -487,6 +488,9 @@ class ChessSelfPlay:
             from .valued import ChessPuctSearch
             self.ps = ChessPuctSearch(self.eng, games, batch_size, seed=puct_seed, leaves=False)
             self.net_fn = lambda leaves, planes, counts: puct_net(planes)
+            if puct_streams > 1:   # the games in parts on their own streams (ChessPuctSearch._enqueue_split)
+                self.net_fn = [(lambda leaves, planes, counts, m=puct_net.replica(): m(planes))
+                               for _ in range(puct_streams)]
         self.hist_cap = hist_cap  # moves per side
         self.hist = torch.zeros((games, 2, self.hist_cap), dtype=torch.int16, device=self.dev)
         self.hlen = torch.zeros((games, 2), dtype=torch.int32, device=self.dev)
@@ -553,7 +557,10 @@ class ChessSelfPlay:
         side.wait_stream(torch.cuda.current_stream(self.dev))
         with torch.cuda.stream(side):   # the network's kernels warmed outside the capture
             if self.ps is not None:
-                self.net_fn(None, self.ps.planes, self.ps.counts)
+                fns = self.net_fn if isinstance(self.net_fn, list) else [self.net_fn]
+                for q, fn in enumerate(fns):   # each part's network warmed on its own slice
+                    lo, hi = q * self.G // len(fns), (q + 1) * self.G // len(fns)
+                    fn(None, self.ps.planes[lo * self.bs:hi * self.bs], self.ps.counts[lo:hi])
             elif self.vs is not None:
                 self.value_fn(None, self.vs.planes, self.vs.counts)
         torch.cuda.current_stream(self.dev).wait_stream(side)

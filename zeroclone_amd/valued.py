@@ -219,11 +219,19 @@ class ChessPuctSearch:
         self.search_no = torch.zeros(n_games, dtype=torch.int32, device=self.dev)
 
     def enqueue(self, roots: torch.Tensor, sims: int, net_fn, temperature: float = 0.0, first_game: int = 0):
+        """net_fn: one callable, or a list of k callables — then the games are split into k
+        contiguous parts searched on k streams (`_enqueue_split`): one part's select, backup
+        and policy GEMM overlap another part's tower.  The results are the same."""
         e, n = self.eng, self.n
         p = lambda t: t.data_ptr() if t is not None else 0  # noqa: E731
         nfl = _native.check(_native.lib().zc_chess_puct_flushes(int(sims), int(self.bs)))
         e.chess_puct_begin(first_game, n, roots.data_ptr(), sims, self.c, self.bs, self.alpha, self.eps, self.seed,
                            self.search_no.data_ptr(), stream=_stream(self.dev))
+        if isinstance(net_fn, (list, tuple)):
+            self._enqueue_split(nfl, list(net_fn), first_game)
+            e.chess_puct_end(first_game, n, temperature, self.move.data_ptr(), self.na.data_ptr(),
+                             self.prior.data_ptr(), self.stats.data_ptr(), _stream(self.dev))
+            return self.move, self.na, self.stats
         for f in range(nfl):
             e.chess_puct_select(first_game, n, f, p(self.leaves), p(self.planes),
                                 self.planes.dtype == torch.float16, self.counts.data_ptr(), _stream(self.dev))
@@ -237,6 +245,42 @@ class ChessPuctSearch:
                          self.stats.data_ptr(), _stream(self.dev))
         return self.move, self.na, self.stats
 
+    def _enqueue_split(self, nfl: int, fns: list, first_game: int):
+        """The flushes of k contiguous game parts, part i on stream i (stream 0: the current
+        one; the others fork from it and join back).  The parts share no tree, buffer or
+        counter — select / backup of a part touch only its games, its slices of the leaf /
+        plane / value buffers, and net_fn i owns its network buffers — so the order of the
+        launches across parts does not matter, and the GPU runs one part's search kernels and
+        policy GEMM beside another part's tower."""
+        e, n, bs, k = self.eng, self.n, self.bs, len(fns)
+        main = torch.cuda.current_stream(self.dev)
+        if getattr(self, "_side", None) is None or len(self._side) < k - 1:
+            self._side = [torch.cuda.Stream(self.dev) for _ in range(k - 1)]
+        streams = [main] + self._side[:k - 1]
+        for st in streams[1:]:
+            st.wait_stream(main)
+        parts = [(i * n // k, (i + 1) * n // k) for i in range(k)]
+        views = []
+        for lo, hi in parts:
+            views.append((self.leaves[lo * bs:hi * bs] if self.leaves is not None else None,
+                          self.planes[lo * bs:hi * bs], self.counts[lo:hi], self.values[lo * bs:hi * bs]))
+        for f in range(nfl):
+            for (lo, hi), st, fn, (lv, pv, cv, vv) in zip(parts, streams, fns, views):
+                if hi == lo:
+                    continue
+                with torch.cuda.stream(st):
+                    s = st.cuda_stream
+                    e.chess_puct_select(first_game + lo, hi - lo, f, lv.data_ptr() if lv is not None else 0,
+                                        pv.data_ptr(), pv.dtype == torch.float16, cv.data_ptr(), s)
+                    v, logits = fn(lv, pv, cv)
+                    if v.data_ptr() != vv.data_ptr():
+                        vv.copy_(v.reshape(-1))
+                    logits = logits.contiguous()
+                    e.chess_puct_backup(first_game + lo, hi - lo, f, vv.data_ptr(), logits.data_ptr(),
+                                        logits.dtype == torch.float16, s)
+        for st in streams[1:]:
+            main.wait_stream(st)
+
     def run(self, roots, sims, net_fn, temperature: float = 0.0, first_game: int = 0):
         self.enqueue(roots, sims, net_fn, temperature, first_game)
         torch.cuda.current_stream(self.dev).synchronize()
@@ -246,7 +290,14 @@ class ChessPuctSearch:
         side = torch.cuda.Stream(self.dev)
         side.wait_stream(torch.cuda.current_stream(self.dev))
         with torch.cuda.stream(side):
-            net_fn(self.leaves, self.planes, self.counts)
+            if isinstance(net_fn, (list, tuple)):   # warm each part's network on its own slice
+                k, n, bs = len(net_fn), self.n, self.bs
+                for i, fn in enumerate(net_fn):
+                    lo, hi = i * n // k, (i + 1) * n // k
+                    fn(self.leaves[lo * bs:hi * bs] if self.leaves is not None else None,
+                       self.planes[lo * bs:hi * bs], self.counts[lo:hi])
+            else:
+                net_fn(self.leaves, self.planes, self.counts)
         torch.cuda.current_stream(self.dev).wait_stream(side)
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
