@@ -476,7 +476,7 @@ def chess_modes(steps: int, dev) -> dict:
     return out
 
 
-def puct_mode(src, steps: int, dev, head: str = "conv", streams: int = 1) -> dict:
+def puct_mode(src, steps: int, dev, head: str = "conv", streams: int = 2) -> dict:
     """BASELINE configs[4] (C5) per GPU: chess PUCT self-play, 1024 games x 1600 sims, policy
     + value ResNet (128 x 8, random init, fp16; tower on the MFMA kernels), Dirichlet root
     noise, temperature 1, from the burned-in crude pool's positions; one graph per step."""
@@ -781,7 +781,9 @@ def run_rank(args, rank: int, world: int, local: int):
             chess_snap = chess.pop("_snap")
             out["extra"]["c4_chess"] = chess
             out["extra"]["c5_chess_puct"] = puct_mode(crude_pool, args.net_steps, dev)
-            out["extra"]["c5_chess_puct_linear_head"] = puct_mode(crude_pool, args.net_steps, dev, head="linear")
+            # round 4's C5 network and schedule (linear policy head, one stream), for continuity
+            out["extra"]["c5_chess_puct_linear_head"] = puct_mode(crude_pool, args.net_steps, dev, head="linear",
+                                                                 streams=1)
             crude_pool.close()
             out["extra"]["net_tower"] = tower_mode(dev)
             out["extra"]["c1_engine"] = c1_mode(dev)

@@ -237,28 +237,36 @@ def test_c5_chess_puct_pool_matches_puct_ref(chess_pool):
     S = 1600
     torch.manual_seed(13)
     net = MfmaPolicyValueNetwork(PolicyValueNetwork(head="conv").eval())   # the head bench.py times
-    pool = ChessSelfPlay(CG, S, batch_size=CB, seed=6, puct_net=net, temperature=1.0)
+    # the schedule bench.py times: the games in two halves on two streams (ChessPuctSearch._enqueue_split)
+    pool = ChessSelfPlay(CG, S, batch_size=CB, seed=6, puct_net=net, temperature=1.0, puct_streams=2)
     pool.adopt(chess_pool)
     pool.ps.leaves = torch.zeros((CG * CB, 72), dtype=torch.uint8, device=pool.dev)   # export leaves (test hook)
     sampled = list(range(3, CG, 32)) + [68, 644]   # 32 spread games + two one move from the fifty-move draw
     inject_fifty(pool, [68, 644])
     snap, _ = snapshot(pool, sampled)
     assert len(snap) >= 32
-    rows_idx = torch.tensor([g * CB + j for g in sampled for j in range(CB)], device=pool.dev)
     logs = {g: {} for g in sampled}
 
-    def net_fn(leaves, planes, counts):
-        v, logits = net(planes)
-        lv = leaves[rows_idx].cpu().numpy()
-        vv = v.reshape(-1)[rows_idx].cpu().numpy()
-        ll = logits[rows_idx].float().cpu().numpy()
-        cnt = counts.cpu().numpy()
-        for a, g in enumerate(sampled):
-            for j in range(int(cnt[g])):
-                logs[g].setdefault(_key_row(lv[a * CB + j]), (float(vv[a * CB + j]), ll[a * CB + j]))
-        return v, logits
+    def part_fn(lo, hi):   # the logging network of the part holding games [lo, hi)
+        mine = [g for g in sampled if lo <= g < hi]
+        rows_idx = torch.tensor([(g - lo) * CB + j for g in mine for j in range(CB)], device=pool.dev,
+                                dtype=torch.long)
+        m = net.replica()
 
-    pool.net_fn = net_fn
+        def fn(leaves, planes, counts):
+            v, logits = m(planes)
+            if mine:
+                lv = leaves[rows_idx].cpu().numpy()
+                vv = v.reshape(-1)[rows_idx].cpu().numpy()
+                ll = logits[rows_idx].float().cpu().numpy()
+                cnt = counts.cpu().numpy()
+                for a, g in enumerate(mine):
+                    for j in range(int(cnt[g - lo])):
+                        logs[g].setdefault(_key_row(lv[a * CB + j]), (float(vv[a * CB + j]), ll[a * CB + j]))
+            return v, logits
+        return fn
+
+    pool.net_fn = [part_fn(0, CG // 2), part_fn(CG // 2, CG)]
     res = pool.step().cpu().numpy()
     mv, post = pool.moves.cpu().numpy(), pool.post.cpu().numpy()
     roots_after = pool.roots.cpu().numpy()
