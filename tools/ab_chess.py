@@ -65,8 +65,11 @@ def main():
     for rnd in range(int(os.environ.get("AB_ROUNDS", "3"))):
         for lib in libs:
             env = dict(os.environ, ZC_LIB=os.path.join(ROOT, lib))
-            out = subprocess.run([sys.executable, "-c", CHILD % ROOT], env=env, check=True, capture_output=True,
-                                 text=True, timeout=300).stdout
+            cp = subprocess.run([sys.executable, "-c", CHILD % ROOT], env=env, capture_output=True, text=True,
+                                timeout=300)
+            if cp.returncode:
+                sys.exit(f"{lib}: child failed ({cp.returncode})\n{cp.stderr[-3000:]}")
+            out = cp.stdout
             ms, h = out.strip().splitlines()[-1].split()
             res[lib].append(float(ms))
             hashes.setdefault(lib, set()).add(h)

@@ -104,14 +104,24 @@ __device__ __forceinline__ void chess_walk(const ChessParams &p, const CTree &t,
     }
 }
 
-// select + expand + record of ONE simulation (mcts.cpp:129-147).  Returns the leaf node;
-// its depth in `ldepth`; lane l of `pathv` holds the slot of the edge into level l.
-__device__ int simulate(const ChessParams &p, const CTree &t, CLds &L, ConstDouble *logtab, Rng &rng, int done,
-                        int &nnodes, int &slots, int &status, int &ldepth, uint32_t &pathv, Counters &cn,
-                        Resume &rs) {
+// One simulation's decision (mcts.cpp:129-147) before its child exists: the walk (or the
+// resumed one), and when the node it stops at has untried moves, the policy's pick among them
+// and the untried list's erase.  midx < 0: no expansion (the leaf is `node` itself).
+struct Expansion {
+    int node;        // the expanded node X (or the leaf, midx < 0)
+    int depth;       // its depth
+    uint32_t pathv;  // lane l: the slot of the edge into level l of X's path
+    int midx;        // the expanded slot of X, or -1
+    uint32_t m;      // its move
+    uint32_t stw;    // lanes 0..17: X's position (zc_chess_state words)
+    uint32_t base;   // X's first slot
+};
+
+__device__ Expansion sim_front(const ChessParams &p, const CTree &t, ConstDouble *logtab, Rng &rng, int done,
+                               int &status, Resume &rs) {
     const uint32_t lane = lane_id();
     int node = 0, depth = 0, nN = done;
-    pathv = 0;
+    uint32_t pathv = 0;
     if (rs.valid) {
         node = rs.node;
         depth = rs.depth;
@@ -125,14 +135,13 @@ __device__ int simulate(const ChessParams &p, const CTree &t, CLds &L, ConstDoub
     ChessNode *N = &t.nodes[node];
     const bool hit = rs.cached;
     const int nu = hit ? rs.nu : uni((int)N->nu);
-    ldepth = depth;
     rs.node = node;
     rs.depth = depth;
     rs.nN = nN;
     rs.pathv = pathv;
     rs.valid = true;
     rs.cached = false;
-    if (nu == 0 || status) return node;
+    if (nu == 0 || status) return Expansion{node, depth, pathv, -1, 0u, 0u, 0u};
 
     // expand (mcts.cpp:65-78): the policy picks among the untried moves, in untried order.
     // The node's position is fetched now, under the policy's memory traffic.
@@ -225,28 +234,54 @@ __device__ int simulate(const ChessParams &p, const CTree &t, CLds &L, ConstDoub
     }
     if (lane == 0) N->nu = (uint16_t)(nu - 1);
     CSTAMP_ADD(1, cs1);
-    CSTAMP_T(cs2);
-    if (lane < 18) ((uint32_t *)&L.st)[lane] = stw;
-    wave_sync_mem();
-    chessdev::apply_move_wave(L.st, m);
-    wave_sync_mem();
-    CSTAMP_ADD(2, cs2);
-    const int child = nnodes++;
-    if (child >= p.M) {
-        status = ZC_STATUS_INTERNAL;
-        return node;
+    return Expansion{node, depth, pathv, midx, m, stw, base};
+}
+
+// The hand-off between a search workgroup's leader wave and its helper wave (LDS): when two
+// consecutive simulations of a flush expand the same node (the cached case: no backup inside a
+// flush, so the second walk stops where the first did), the leader stages the second child's
+// position in `L.st` and the helper generates its legal moves while the leader generates the
+// first child's.  The leader then commits both children in simulation order (node ids, slots),
+// so the tree, the stream and every output are those of the one-wave search.
+struct Helper {
+    CLds L;
+    NodeGen gen;
+    int cmd;  // 1: generate L.st; 2: exit
+};
+
+__device__ void helper_loop(Helper &h) {
+    for (;;) {
+        __syncthreads();  // a command is posted
+        const int cmd = uni(*(volatile int *)&h.cmd);
+        if (cmd != 1) return;
+        const NodeGen gen = create_node_gen(h.L);
+        if (lane_id() == 0) h.gen = gen;
+        __syncthreads();  // the generated node is in h
     }
-    CSTAMP_T(cs3);
-    create_node(t, L, child, node, midx, depth + 1, slots, status);
-    CSTAMP_ADD(3, cs3);
-    if (lane == 0) t.ch[base + midx] = (uint16_t)child;
-    ++depth;
-    if (lane == (uint32_t)depth) pathv = base + (uint32_t)midx;
-    ldepth = depth;
+}
+
+__device__ __forceinline__ void helper_exit(Helper *h) {
+    if (!h) return;
+    if (lane_id() == 0) *(volatile int *)&h->cmd = 2;
+    __syncthreads();
+}
+
+// The child of expansion e in L (generated: gen), committed as node `child` (mcts.cpp:74-76).
+__device__ __forceinline__ void commit_child(const CTree &t, const CLds &L, NodeGen gen, const Expansion &e, int child,
+                                             int &slots, int &status, Counters &cn) {
+    create_node_commit(t, L, gen, child, e.node, e.midx, e.depth + 1, slots, status);
+    if (lane_id() == 0) t.ch[e.base + (uint32_t)e.midx] = (uint16_t)child;
     cn.add(cn.expansions, 1);
-    cn.add(cn.depth_sum, depth);
+    cn.add(cn.depth_sum, e.depth + 1);
     wave_sync_mem();
-    return child;
+}
+
+// X's position plus move m into the staging position st (the expansion's play_move)
+__device__ __forceinline__ void stage_child(zc_chess_state &st, const Expansion &e) {
+    if (lane_id() < 18) ((uint32_t *)&st)[lane_id()] = e.stw;
+    wave_sync_mem();
+    chessdev::apply_move_wave(st, e.m);
+    wave_sync_mem();
 }
 
 // backprop of leaf j (mcts.cpp:80-100): Na += 1, Wa -= (-1)^(d-l) v on the edge into level l.
@@ -333,8 +368,10 @@ __device__ void finish(const ChessParams &p, const CTree &t, int gl, int g, cons
 }
 
 // select + expand of one flush; leaf records to the arena (meta, paths).  Returns nb.
+// With a helper wave (h != nullptr), two consecutive expansions of the same node generate their
+// children's legal moves in parallel (Helper).
 __device__ int chess_select_flush(const ChessParams &p, const CTree &t, CLds &L, ConstDouble *logtab, int g, int32_t *ctl,
-                            int done, int nb) {
+                            int done, int nb, Helper *h = nullptr) {
     const uint32_t lane = lane_id();
     int nnodes = uni(ctl[cNodes]), slots = uni(ctl[cSlots]), status = uni(ctl[cStatus]);
     Rng rng;
@@ -345,13 +382,52 @@ __device__ int chess_select_flush(const ChessParams &p, const CTree &t, CLds &L,
     uint32_t *meta = p.ca.meta + (size_t)g * p.max_batch;
     int j = 0;
     Resume rs;
-    for (; j < nb && !status; ++j) {
-        int d = 0;
-        uint32_t pathv = 0;
-        const int leaf = simulate(p, t, L, logtab, rng, done, nnodes, slots, status, d, pathv, cn, rs);
+    auto record = [&](int leaf, int d, uint32_t pathv) {
         if (lane < (uint32_t)kChessPath) paths[(size_t)j * kChessPath + lane] = pathv;
         if (lane == 0) meta[j] = (uint32_t)leaf | ((uint32_t)d << 16);
+        ++j;
+    };
+    auto leaf_path = [&](const Expansion &e) { return lane == (uint32_t)(e.depth + 1) ? e.base + (uint32_t)e.midx : e.pathv; };
+    while (j < nb && !status) {
+        const Expansion a = sim_front(p, t, logtab, rng, done, status, rs);
+        if (a.midx < 0 || status) {  // no expansion: the walk's end is the leaf
+            record(a.node, a.depth, a.pathv);
+            continue;
+        }
+        // the next simulation expands the same node (its untried moves are still cached):
+        // take its pick now and let the helper generate its child
+        const bool pair = h != nullptr && rs.cached && j + 1 < nb;
+        Expansion b{};
+        const Rng rng_a = rng;  // the stream after a's draw: restored when a ends the flush
+        if (pair) {
+            b = sim_front(p, t, logtab, rng, done, status, rs);
+            stage_child(h->L.st, b);
+            if (lane == 0) *(volatile int *)&h->cmd = 1;
+            __syncthreads();  // the helper starts on b's child
+        }
+        CSTAMP_T(cs2);
+        stage_child(L.st, a);
+        CSTAMP_ADD(2, cs2);
+        const int ida = nnodes++;
+        if (ida >= p.M) status = ZC_STATUS_INTERNAL;
+        CSTAMP_T(cs3);
+        const NodeGen ga = create_node_gen(L);
+        if (!status) commit_child(t, L, ga, a, ida, slots, status, cn);
+        CSTAMP_ADD(3, cs3);
+        record(ida, a.depth + 1, leaf_path(a));
+        if (pair) {
+            __syncthreads();  // b's child is generated
+            if (status) {  // a ended the flush (capacity): b never ran, its draw is not consumed
+                rng = rng_a;
+                break;
+            }
+            const int idb = nnodes++;
+            if (idb >= p.M) status = ZC_STATUS_INTERNAL;
+            if (!status) commit_child(t, h->L, h->gen, b, idb, slots, status, cn);
+            record(idb, b.depth + 1, leaf_path(b));
+        }
     }
+    j = min(j, nb);
     wave_sync_mem();
     if (lane == 0) {
         ctl[cNodes] = nnodes;
@@ -381,14 +457,14 @@ __device__ void chess_backup_flush(const ChessParams &p, const CTree &t, int g, 
 // ---------------------------------------------------------------- fused: crude_chess_score
 // The whole search of one game from p.roots[gl] (root_init .. the last backup).
 __device__ void crude_search(const ChessParams &p, const CTree &t, CLds &L, double *s_vals, int gl, int g,
-                             int32_t *ctl) {
+                             int32_t *ctl, Helper *h = nullptr) {
     ConstDouble *logtab = (ConstDouble *)p.a.logtab;
     CSTAMP_T(cs7);
     root_init(p, t, L, gl, g, ctl);
     const uint32_t *meta = p.ca.meta + (size_t)g * p.max_batch;
     for (int done = 0; done < p.sims && !uni(ctl[cStatus]);) {
         CSTAMP_T(cs6);
-        const int nb = chess_select_flush(p, t, L, logtab, g, ctl, done, min(p.bs, p.sims - done));
+        const int nb = chess_select_flush(p, t, L, logtab, g, ctl, done, min(p.bs, p.sims - done), h);
         CSTAMP_ADD(6, cs6);
         CSTAMP_T(cs4);
         // value.batch: crude_chess_score of every pending leaf (mcts.cpp:116-118)
@@ -407,18 +483,26 @@ __device__ void crude_search(const ChessParams &p, const CTree &t, CLds &L, doub
     CSTAMP_ADD(7, cs7);
 }
 
-__global__ __launch_bounds__(64) void chess_search_kernel(ChessParams p) {
+// Two waves per game: the leader runs the search, the helper generates the second child of
+// each paired expansion (Helper).
+__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void chess_search_kernel(ChessParams p) {
     __shared__ CLds L;
     __shared__ double s_vals[256];
+    __shared__ Helper H;
     const int gl = blockIdx.x;
     if (gl >= p.n_games) return;
+    if (__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) != 0) {
+        helper_loop(H);
+        return;
+    }
     const int g = p.first_game + gl;
     const CTree t = ctree(p, g);
     int32_t *ctl = p.ca.ctl + (size_t)g * kCtlWords;
     CSTAMP_INIT();
-    crude_search(p, t, L, s_vals, gl, g, ctl);
+    crude_search(p, t, L, s_vals, gl, g, ctl, &H);
     CSTAMP_FLUSH();
     finish(p, t, gl, g, ctl);
+    helper_exit(&H);
 }
 
 // ---------------------------------------------------------------- chess self-play
@@ -427,7 +511,7 @@ __global__ __launch_bounds__(64) void chess_search_kernel(ChessParams p) {
 // chess_backend.cpp:364-400), check_win / check_draw of the new position (:404-441:
 // checkmate; stalemate, the fifty-move counter, both sides' histories repeating).  Returns
 // the result (turn*2-1 with the new side to move, 0, or ZC_C4_ONGOING).
-__device__ int chess_play_judge(const ChessPlayParams &q, int gl, CLds &L, uint16_t *Lh, uint32_t m, int &err) {
+__device__ __attribute__((noinline)) int chess_play_judge(const ChessPlayParams &q, int gl, CLds &L, uint16_t *Lh, uint32_t m, int &err) {
     const uint32_t lane = lane_id();
     if (lane < 18) ((uint32_t *)&L.st)[lane] = ((const uint32_t *)&q.roots[gl])[lane];
     wave_sync_mem();
@@ -516,12 +600,17 @@ __global__ __launch_bounds__(64) void chess_play_step_kernel(ChessPlayParams q, 
 // step above, the refill.  With q.ticket the games share q.budget moves (pooled); steps a
 // game did not reach are ZC_SLOT_SKIP / move 0xFFFF.  Outputs [moves][n]; q.stats[gl] sums
 // the moves' counters (reserved = games finished).
-__global__ __launch_bounds__(64) void chess_selfplay_kernel(ChessParams p, ChessPlayParams q) {
+__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void chess_selfplay_kernel(ChessParams p, ChessPlayParams q) {
     extern __shared__ uint16_t s_hist[];
     __shared__ CLds L;
     __shared__ double s_vals[256];
+    __shared__ Helper H;
     const int gl = blockIdx.x;
     if (gl >= p.n_games) return;
+    if (__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) != 0) {  // the helper wave (Helper)
+        helper_loop(H);
+        return;
+    }
     const uint32_t lane = lane_id();
     const int g = p.first_game + gl;
     const CTree t = ctree(p, g);
@@ -535,7 +624,7 @@ __global__ __launch_bounds__(64) void chess_selfplay_kernel(ChessParams p, Chess
             if (lane == 0) tk = atomicAdd(q.ticket, 1);
             if (uni(tk) >= q.budget) break;
         }
-        crude_search(p, t, L, s_vals, gl, g, ctl);
+        crude_search(p, t, L, s_vals, gl, g, ctl, &H);
         status = uni(ctl[cStatus]);
         exp += uni(ctl[cExp]);
         depth += uni(ctl[cDepth]);
@@ -572,6 +661,7 @@ __global__ __launch_bounds__(64) void chess_selfplay_kernel(ChessParams p, Chess
         st.reserved = finished;
         q.stats[gl] = st;
     }
+    helper_exit(&H);
 }
 
 // ---------------------------------------------------------------- stepwise (caller values)
@@ -952,17 +1042,17 @@ void launch_chess_hp_expand(const ChessParams &p, hipStream_t s) {
 }
 
 void launch_chess_search(const ChessParams &p, hipStream_t s) {
-    hipLaunchKernelGGL(chess_search_kernel, dim3(p.n_games), dim3(64), 0, s, p);
+    hipLaunchKernelGGL(chess_search_kernel, dim3(p.n_games), dim3(128), 0, s, p);
 }
 void launch_chess_play_step(const ChessPlayParams &q, int n, hipStream_t s) {
     hipLaunchKernelGGL(chess_play_step_kernel, dim3(n), dim3(64), (size_t)q.cap * sizeof(uint16_t), s, q, n);
 }
 void launch_chess_selfplay(const ChessParams &p, const ChessPlayParams &q, hipStream_t s) {
-    hipLaunchKernelGGL(chess_selfplay_kernel, dim3(p.n_games), dim3(64), (size_t)q.cap * sizeof(uint16_t), s, p, q);
+    hipLaunchKernelGGL(chess_selfplay_kernel, dim3(p.n_games), dim3(128), (size_t)q.cap * sizeof(uint16_t), s, p, q);
 }
 int chess_selfplay_resident_games(int cap, int *out) {
     int blocks = 0, dev = 0, cus = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, (const void *)chess_selfplay_kernel, 64,
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, (const void *)chess_selfplay_kernel, 128,
                                                      (size_t)cap * sizeof(uint16_t)) != hipSuccess)
         return -1;
     if (hipGetDevice(&dev) != hipSuccess) return -1;

@@ -82,8 +82,18 @@ struct CLds {
 __device__ __forceinline__ void wave_sync_mem() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); }
 
 // Node(state, get_legal_moves(state), parent, idx) (mcts.cpp:23-34) for the position in
-// L.st: moves in the reference order into fresh slots, all untried, no children.
-__device__ void create_node(const CTree &t, CLds &L, int id, int parent, int pact, int depth, int &slots, int &status) {
+// L.st, in two parts: create_node_gen generates the legal moves (into L.s.legal), the check flag
+// of a position without moves and the material; create_node_commit takes the next `n` slots
+// and writes the moves (all untried, no children) and the node record.  The generation is the
+// expensive part and touches nothing but L, so another wave can run it (chess_search.hip's
+// helper wave) while the leader generates another node.
+struct NodeGen {
+    int n;
+    int check;
+    int32_t mat;
+};
+
+__device__ __forceinline__ NodeGen create_node_gen(CLds &L) {
     const uint32_t lane = lane_id();
     const uint32_t sq = L.st.board[lane];
     L.s.board[lane] = (uint8_t)sq;
@@ -91,15 +101,22 @@ __device__ void create_node(const CTree &t, CLds &L, int id, int parent, int pac
     const int turn = uni((int)L.st.turn);
     bool check;
     CSTAMP_T(cs8);
-    int n = chessdev::legal_moves_check(L.s.board, turn, L.s.legal, L.s.pseudo, L.s.region, check);
+    const int n = chessdev::legal_moves_check(L.s.board, turn, L.s.legal, L.s.pseudo, L.s.region, check);
     CSTAMP_ADD(8, cs8);
+    CSTAMP_T(cs9);
+    const int32_t mat = chessdev::material(sq);
+    CSTAMP_ADD(9, cs9);
+    return NodeGen{n, check ? 1 : 0, mat};
+}
+
+__device__ __forceinline__ void create_node_commit(const CTree &t, const CLds &L, NodeGen gen, int id, int parent,
+                                                   int pact, int depth, int &slots, int &status) {
+    const uint32_t lane = lane_id();
+    int n = gen.n;
     if (n < 0) {
         status = ZC_STATUS_CAPACITY;
         n = 0;
     }
-    CSTAMP_T(cs9);
-    const int32_t mat = chessdev::material(sq);
-    CSTAMP_ADD(9, cs9);
     CSTAMP_T(cs10);
     const int base = slots;
     if ((int64_t)base + n > t.S) {
@@ -123,12 +140,17 @@ __device__ void create_node(const CTree &t, CLds &L, int id, int parent, int pac
         N->parent = (uint16_t)parent;
         N->pact = (uint16_t)pact;
         N->depth = (uint16_t)depth;
-        N->material = (int16_t)mat;
-        N->check = check ? 1 : 0;
+        N->material = (int16_t)gen.mat;
+        N->check = gen.check ? 1 : 0;
         N->evaluated = 0;
     }
     wave_sync_mem();
     CSTAMP_ADD(10, cs10);
+}
+
+__device__ void create_node(const CTree &t, CLds &L, int id, int parent, int pact, int depth, int &slots, int &status) {
+    const NodeGen gen = create_node_gen(L);
+    create_node_commit(t, L, gen, id, parent, pact, depth, slots, status);
 }
 
 __device__ __forceinline__ void argmax64(double &v, int &i) {
