@@ -80,6 +80,15 @@ __device__ __forceinline__ uint32_t mbcnt64(uint64_t m) {  // set bits of m in l
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
+// Wait for x's load here.  Stores and loads share gfx950's in-order vector-memory counter, so
+// a load still in flight where two paths join makes the compiler's wait at the join (vmcnt(0))
+// also drain every store issued since — on the path that never loaded anything.  Waiting on
+// the loading path itself keeps the other path free of it.
+template <class T>
+__device__ __forceinline__ void vmem_ready(T &x) {
+    asm volatile("" : "+v"(x));
+}
+
 __device__ __forceinline__ void wave_mem_order() {
     // Same-wave hand-offs through memory (one lane stores, another loads) are ordered by
     // program order on gfx950 (wavefront scope needs no cache action); this only stops the
@@ -214,6 +223,7 @@ __device__ __forceinline__ void rng_open(Rng &r, uint32_t *ring, uint64_t use0, 
     r.wt = temper(r.ring[r.slot(r.wrel + (int32_t)lane_id())]);
     r.wn = temper(r.ring[r.slot(r.wrel + kWin + (int32_t)lane_id())]);
     r.wx = r.ring[r.slot(r.wrel + 2 * kWin + (int32_t)lane_id())];
+    vmem_ready(r.wx);
 }
 
 // Move the windows on by 64 words (precondition: off >= 64).
@@ -224,6 +234,7 @@ __device__ __forceinline__ void rng_advance(Rng &r) {
     r.wn = temper(r.wx);
     if (r.grel < r.wrel + 3 * kWin) rng_fill(r, r.wrel + 3 * kWin);
     r.wx = r.ring[r.slot(r.wrel + 2 * kWin + (int32_t)lane_id())];
+    vmem_ready(r.wx);  // once per 64 words, instead of at every later join
 }
 
 // The 64 tempered words from the next unconsumed one on: lane l = word off + l of the

@@ -589,10 +589,10 @@ __device__ __forceinline__ int legal_moves(const uint8_t *b, int t, uint16_t *ou
 // get_legal_moves and, for a position without legal moves, king_attacked of the side to
 // move (check_win, crude_chess_score's mate score) on one board view; `check` is false when
 // the position has moves.
-__device__ __forceinline__ int legal_moves_check(const uint8_t *b, int t, uint16_t *out, uint16_t *ps, uint16_t *reg,
-                                                 bool &check) {
+// (pc: this lane's square b[lane], when the caller has it in a register)
+__device__ __forceinline__ int legal_moves_check(const uint8_t *b, uint32_t pc, int t, uint16_t *out, uint16_t *ps,
+                                                 uint16_t *reg, bool &check) {
     CDEV_T(cd14);
-    const uint32_t pc = b[lane()];
     BitView bv;
     const bool fast = make_bitview(pc, t, bv);
     const uint64_t kings = fast ? bv.kings : king_mask(b, t);
@@ -616,6 +616,11 @@ __device__ __forceinline__ int legal_moves_check(const uint8_t *b, int t, uint16
         }
     }
     return n;
+}
+
+__device__ __forceinline__ int legal_moves_check(const uint8_t *b, int t, uint16_t *out, uint16_t *ps, uint16_t *reg,
+                                                 bool &check) {
+    return legal_moves_check(b, (uint32_t)b[lane()], t, out, ps, reg, check);
 }
 
 // Sum of piece values, white positive (crude_chess_score's material), by ballots.
@@ -685,6 +690,38 @@ __device__ __forceinline__ void apply_move_wave(zc_chess_state &o, uint32_t m) {
         o.fifty = (uint8_t)fifty;
         o.castle = (uint8_t)castle;
     }
+}
+
+// apply_move with the position in registers instead of LDS: lanes 0..17 of `stw` hold the
+// zc_chess_state words of the position; returns this lane's square of the position after m
+// (apply_move_wave's per-square rule) and, in w16, the new state word 16 (turn | fifty << 8 |
+// castle << 16 | reserved[0] << 24).  Words 17.. are unchanged.
+__device__ __forceinline__ uint32_t apply_move_regs(uint32_t stw, uint32_t m, uint32_t &w16) {
+    const uint32_t l = lane();
+    const int from = (int)(m & 63u), to = (int)((m >> 6) & 63u);
+    const int fc = from & 7, tc = to & 7, tr = to >> 3;
+    const uint32_t x0 = ((uint32_t)__shfl((int)stw, (int)(l >> 2)) >> (8u * (l & 3u))) & 0xFFu;
+    const uint32_t pc = ((uint32_t)__builtin_amdgcn_readlane((int)stw, from >> 2) >> (8 * (from & 3))) & 0xFFu;
+    const uint32_t trg = ((uint32_t)__builtin_amdgcn_readlane((int)stw, to >> 2) >> (8 * (to & 3))) & 0xFFu;
+    const uint32_t w = (uint32_t)__builtin_amdgcn_readlane((int)stw, 16);
+    uint32_t x = x0;
+    const int dcol = tc - fc;
+    if (pc == 'K' && dcol == 2) x = l == 61 ? 'R' : l == 63 ? ' ' : x;
+    if (pc == 'k' && dcol == 2) x = l == 5 ? 'r' : l == 7 ? ' ' : x;
+    if (pc == 'K' && dcol == -2) x = l == 59 ? 'R' : l == 56 ? ' ' : x;
+    if (pc == 'k' && dcol == -2) x = l == 3 ? 'r' : l == 0 ? ' ' : x;
+    if ((int)l == to) x = pc;
+    if ((int)l == from) x = ' ';
+    if ((int)l == to && tr == 0 && pc == 'P') x = 'Q';
+    if ((int)l == to && tr == 7 && pc == 'p') x = 'q';
+    uint32_t fifty = ((w >> 8) & 0xFFu) + 1u, castle = (w >> 16) & 0xFFu;
+    if (pc == 'P' || pc == 'p' || !(trg == ' ' || trg == 0)) fifty = 0;
+    if (pc == 'K' || (pc == 'R' && fc == 7)) castle &= ~1u;
+    if (pc == 'K' || (pc == 'R' && fc == 0)) castle &= ~2u;
+    if (pc == 'k' || (pc == 'r' && fc == 7)) castle &= ~4u;
+    if (pc == 'k' || (pc == 'r' && fc == 0)) castle &= ~8u;
+    w16 = ((1u - (w & 0xFFu)) & 0xFFu) | ((fifty & 0xFFu) << 8) | (castle << 16) | (w & 0xFF000000u);
+    return x;
 }
 
 // has_repeated_prefix (chess_backend.cpp:148-180; min_pattern_len 2, min_repeats 3) of the

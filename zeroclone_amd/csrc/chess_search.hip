@@ -117,7 +117,7 @@ struct Expansion {
     uint32_t base;   // X's first slot
 };
 
-__device__ Expansion sim_front(const ChessParams &p, const CTree &t, ConstDouble *logtab, Rng &rng, int done,
+__device__ __forceinline__ Expansion sim_front(const ChessParams &p, const CTree &t, ConstDouble *logtab, Rng &rng, int done,
                                int &status, Resume &rs) {
     const uint32_t lane = lane_id();
     int node = 0, depth = 0, nN = done;
@@ -145,7 +145,11 @@ __device__ Expansion sim_front(const ChessParams &p, const CTree &t, ConstDouble
 
     // expand (mcts.cpp:65-78): the policy picks among the untried moves, in untried order.
     // The node's position is fetched now, under the policy's memory traffic.
-    const uint32_t stw = hit ? rs.stw : (lane < 18 ? ((const uint32_t *)&N->st)[lane] : 0u);
+    uint32_t stw = rs.stw;
+    if (!hit) {
+        stw = lane < 18 ? ((const uint32_t *)&N->st)[lane] : 0u;
+        vmem_ready(stw);
+    }
     const uint32_t base = hit ? rs.base : uni(N->base);
     int local, midx;
     uint32_t m;
@@ -160,25 +164,25 @@ __device__ Expansion sim_front(const ChessParams &p, const CTree &t, ConstDouble
         } else {
             utv = lane < (uint32_t)nu ? (int)t.ut[base + lane] : 0;
             mvv = lane < (uint32_t)nu ? (uint32_t)t.mv[base + utv] : 0u;
+            vmem_ready(mvv);
         }
         if (p.policy == 1) {
             // Policy('immediate_value') (policy_functions.py:14-17): random.choice over the
             // untried moves whose capture value >= max - policy_freedom
             // the maximum capture value (4 bits) of the untried moves, bit by bit from the top
             // with ballots instead of a cross-lane shuffle reduction (nu >= 1 here)
+            // A capture value is one of 0, 1, 3, 5, 9 (chess_device.h capval): one ballot per
+            // value, all independent, give the maximum and the candidates at once (ok: the
+            // classes that pass `value >= max - freedom` for each maximum, ChessParams::cls_ok)
             const uint32_t cv = mvv >> 12;
-            uint64_t cand = __ballot(lane < (uint32_t)nu);
-            int v = 0;
-#pragma unroll
-            for (int bit = 3; bit >= 0; --bit) {
-                const uint64_t B = __ballot(((cand >> lane) & 1ull) && ((cv >> bit) & 1u));
-                if (B) {
-                    v |= 1 << bit;
-                    cand = B;
-                }
-            }
-            const double thr = (double)v - p.freedom;
-            const uint64_t cm = __ballot(lane < (uint32_t)nu && (double)(mvv >> 12) >= thr);
+            const bool in = lane < (uint32_t)nu;
+            const uint64_t B1 = __ballot(in && cv == 1u), B3 = __ballot(in && cv == 3u);
+            const uint64_t B5 = __ballot(in && cv == 5u), B9 = __ballot(in && cv == 9u);
+            const uint64_t B0 = __ballot(in) & ~(B1 | B3 | B5 | B9);
+            const int top = B9 ? 4 : B5 ? 3 : B3 ? 2 : B1 ? 1 : 0;
+            const uint32_t ok = (p.cls_ok >> (5 * top)) & 31u;
+            const uint64_t cm = ((ok & 1u) ? B0 : 0ull) | ((ok & 2u) ? B1 : 0ull) | ((ok & 4u) ? B3 : 0ull) |
+                                ((ok & 8u) ? B5 : 0ull) | ((ok & 16u) ? B9 : 0ull);
             const uint32_t r = rng_below(rng, (uint32_t)__popcll(cm));
             const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(cm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)cm, 0u));
             local = __builtin_ctzll(__ballot(((cm >> lane) & 1ull) && rank == r));
@@ -188,8 +192,8 @@ __device__ Expansion sim_front(const ChessParams &p, const CTree &t, ConstDouble
         midx = __builtin_amdgcn_readlane(utv, local);
         m = (uint32_t)__builtin_amdgcn_readlane((int)mvv, local);
         // untried.erase(begin + local): entry i takes entry i + 1
-        const int nxt = __shfl(utv, (int)lane + 1);
-        const uint32_t nmv = (uint32_t)__shfl((int)mvv, (int)lane + 1);
+        const int nxt = dpp<0x130>(utv);  // wave_shl:1, lane l reads lane l + 1
+        const uint32_t nmv = (uint32_t)dpp<0x130>((int)mvv);
         const bool moved = (int)lane >= local;
         if (moved && (int)lane < nu - 1) t.ut[base + lane] = (uint8_t)nxt;
         rs.cached = nu > 1;  // the next walk stops here again
@@ -239,24 +243,29 @@ __device__ Expansion sim_front(const ChessParams &p, const CTree &t, ConstDouble
 
 // The hand-off between a search workgroup's leader wave and its helper wave (LDS): when two
 // consecutive simulations of a flush expand the same node (the cached case: no backup inside a
-// flush, so the second walk stops where the first did), the leader stages the second child's
-// position in `L.st` and the helper generates its legal moves while the leader generates the
-// first child's.  The leader then commits both children in simulation order (node ids, slots),
-// so the tree, the stream and every output are those of the one-wave search.
+// flush, so the second walk stops where the first did), the leader posts the second child's
+// parent position and move; the helper plays the move and generates the child's legal moves
+// while the leader does the same for the first child.  The leader then commits both children
+// in simulation order (node ids, slots), so the tree, the stream and every output are those of
+// the one-wave search.  (Letting the helper also write the second child, with a join before
+// every walk, measured 6 % slower: profiles/r05_ab_chess_variants.log.)
 struct Helper {
     CLds L;
     NodeGen gen;
-    int cmd;  // 1: generate L.st; 2: exit
+    int cmd;           // 1: generate; 2: exit
+    uint32_t stw[18];  // the parent's position (zc_chess_state words) ...
+    uint32_t m;        // ... and the move to play
 };
 
 __device__ void helper_loop(Helper &h) {
+    const uint32_t lane = lane_id();
     for (;;) {
         __syncthreads();  // a command is posted
-        const int cmd = uni(*(volatile int *)&h.cmd);
-        if (cmd != 1) return;
-        const NodeGen gen = create_node_gen(h.L);
-        if (lane_id() == 0) h.gen = gen;
-        __syncthreads();  // the generated node is in h
+        if (uni(*(volatile int *)&h.cmd) != 1) return;
+        const uint32_t stw = lane < 18 ? h.stw[lane] : 0u;
+        const NodeGen gen = create_child_gen(h.L, stw, uni(*(volatile uint32_t *)&h.m));
+        if (lane == 0) h.gen = gen;
+        __syncthreads();  // the generated child is in h
     }
 }
 
@@ -276,26 +285,7 @@ __device__ __forceinline__ void commit_child(const CTree &t, const CLds &L, Node
     wave_sync_mem();
 }
 
-// X's position plus move m into the staging position st (the expansion's play_move)
-__device__ __forceinline__ void stage_child(zc_chess_state &st, const Expansion &e) {
-    if (lane_id() < 18) ((uint32_t *)&st)[lane_id()] = e.stw;
-    wave_sync_mem();
-    chessdev::apply_move_wave(st, e.m);
-    wave_sync_mem();
-}
-
-// backprop of leaf j (mcts.cpp:80-100): Na += 1, Wa -= (-1)^(d-l) v on the edge into level l.
-__device__ __forceinline__ void backup_leaf(const CTree &t, const uint32_t *path, int d, double v) {
-    const uint32_t lane = lane_id();
-    if (lane >= 1 && lane <= (uint32_t)d) {
-        const uint32_t s = path[lane];
-        const double r = ((d - (int)lane) & 1) ? -v : v;
-        t.na[s] += 1;
-        t.w[s] -= r;
-    }
-}
-
-__device__ void root_init(const ChessParams &p, const CTree &t, CLds &L, int gl, int g, int32_t *ctl) {
+__device__ __forceinline__ void root_init(const ChessParams &p, const CTree &t, CLds &L, int gl, int g, int32_t *ctl) {
     const uint32_t lane = lane_id();
     if (lane < 18) {
         const uint32_t w = ((const uint32_t *)&p.roots[gl])[lane];
@@ -345,7 +335,7 @@ __device__ __forceinline__ int best_root_slot(const CTree &t, int nm, uint32_t b
     return uni(bi);
 }
 
-__device__ void finish(const ChessParams &p, const CTree &t, int gl, int g, const int32_t *ctl) {
+__device__ __forceinline__ void finish(const ChessParams &p, const CTree &t, int gl, int g, const int32_t *ctl) {
     const uint32_t lane = lane_id();
     const int status = uni(ctl[cStatus]);
     const ChessNode *R = &t.nodes[0];
@@ -370,7 +360,7 @@ __device__ void finish(const ChessParams &p, const CTree &t, int gl, int g, cons
 // select + expand of one flush; leaf records to the arena (meta, paths).  Returns nb.
 // With a helper wave (h != nullptr), two consecutive expansions of the same node generate their
 // children's legal moves in parallel (Helper).
-__device__ int chess_select_flush(const ChessParams &p, const CTree &t, CLds &L, ConstDouble *logtab, int g, int32_t *ctl,
+__device__ __forceinline__ int chess_select_flush(const ChessParams &p, const CTree &t, CLds &L, ConstDouble *logtab, int g, int32_t *ctl,
                             int done, int nb, Helper *h = nullptr) {
     const uint32_t lane = lane_id();
     int nnodes = uni(ctl[cNodes]), slots = uni(ctl[cSlots]), status = uni(ctl[cStatus]);
@@ -401,17 +391,17 @@ __device__ int chess_select_flush(const ChessParams &p, const CTree &t, CLds &L,
         const Rng rng_a = rng;  // the stream after a's draw: restored when a ends the flush
         if (pair) {
             b = sim_front(p, t, logtab, rng, done, status, rs);
-            stage_child(h->L.st, b);
-            if (lane == 0) *(volatile int *)&h->cmd = 1;
+            if (lane < 18) h->stw[lane] = b.stw;
+            if (lane == 0) {
+                h->m = b.m;
+                *(volatile int *)&h->cmd = 1;
+            }
             __syncthreads();  // the helper starts on b's child
         }
-        CSTAMP_T(cs2);
-        stage_child(L.st, a);
-        CSTAMP_ADD(2, cs2);
         const int ida = nnodes++;
         if (ida >= p.M) status = ZC_STATUS_INTERNAL;
         CSTAMP_T(cs3);
-        const NodeGen ga = create_node_gen(L);
+        const NodeGen ga = create_child_gen(L, a.stw, a.m);  // play_move + Node(...) (mcts.cpp:74-76)
         if (!status) commit_child(t, L, ga, a, ida, slots, status, cn);
         CSTAMP_ADD(3, cs3);
         record(ida, a.depth + 1, leaf_path(a));
@@ -442,21 +432,36 @@ __device__ int chess_select_flush(const ChessParams &p, const CTree &t, CLds &L,
     return status ? 0 : nb;
 }
 
-__device__ void chess_backup_flush(const ChessParams &p, const CTree &t, int g, const int32_t *ctl, const double *vals,
+__device__ __forceinline__ void chess_backup_flush(const ChessParams &p, const CTree &t, int g, const int32_t *ctl, const double *vals,
                              int nb) {
     const uint32_t *paths = p.ca.paths + (size_t)g * p.max_batch * kChessPath;
     const uint32_t *meta = p.ca.meta + (size_t)g * p.max_batch;
+    const uint32_t lane = lane_id();
+    if (nb <= 0) return;
+    // leaf j + 1's record is loaded while leaf j's edges are updated: the only dependent
+    // memory round trip left per leaf is its edges' read-modify-write
+    uint32_t mn = meta[0], sn = paths[lane];
     for (int j = 0; j < nb; ++j) {
-        const uint32_t m = uni(meta[j]);
+        const int d = (int)(uni(mn) >> 16);
+        const uint32_t s = sn;
+        if (j + 1 < nb) {
+            mn = meta[j + 1];
+            sn = paths[(size_t)(j + 1) * kChessPath + lane];
+        }
         const double v = __hiloint2double(uni(__double2hiint(vals[j])), uni(__double2loint(vals[j])));
-        backup_leaf(t, paths + (size_t)j * kChessPath, (int)(m >> 16), v);
+        // backprop (mcts.cpp:80-100): Na += 1, Wa -= (-1)^(d-l) v on the edge into level l
+        if (lane >= 1 && lane <= (uint32_t)d) {
+            const double r = ((d - (int)lane) & 1) ? -v : v;
+            t.na[s] += 1;
+            t.w[s] -= r;
+        }
         wave_sync_mem();
     }
 }
 
 // ---------------------------------------------------------------- fused: crude_chess_score
 // The whole search of one game from p.roots[gl] (root_init .. the last backup).
-__device__ void crude_search(const ChessParams &p, const CTree &t, CLds &L, double *s_vals, int gl, int g,
+__device__ __forceinline__ void crude_search(const ChessParams &p, const CTree &t, CLds &L, double *s_vals, int gl, int g,
                              int32_t *ctl, Helper *h = nullptr) {
     ConstDouble *logtab = (ConstDouble *)p.a.logtab;
     CSTAMP_T(cs7);
@@ -491,12 +496,12 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void c
     __shared__ Helper H;
     const int gl = blockIdx.x;
     if (gl >= p.n_games) return;
+    const int g = p.first_game + gl;
+    const CTree t = ctree(p, g);
     if (__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) != 0) {
         helper_loop(H);
         return;
     }
-    const int g = p.first_game + gl;
-    const CTree t = ctree(p, g);
     int32_t *ctl = p.ca.ctl + (size_t)g * kCtlWords;
     CSTAMP_INIT();
     crude_search(p, t, L, s_vals, gl, g, ctl, &H);
@@ -607,13 +612,13 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void c
     __shared__ Helper H;
     const int gl = blockIdx.x;
     if (gl >= p.n_games) return;
+    const int g = p.first_game + gl;
+    const CTree t = ctree(p, g);
     if (__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) != 0) {  // the helper wave (Helper)
         helper_loop(H);
         return;
     }
     const uint32_t lane = lane_id();
-    const int g = p.first_game + gl;
-    const CTree t = ctree(p, g);
     int32_t *ctl = p.ca.ctl + (size_t)g * kCtlWords;
     const uint64_t use_start = uni64(p.a.rngpos[2 * (size_t)g]);
     int64_t exp = 0, depth = 0;

@@ -93,6 +93,28 @@ struct NodeGen {
     int32_t mat;
 };
 
+// The child of the position in `stw` (lanes 0..17: its zc_chess_state words) by move m, into
+// L.st, and its generation, with the child's squares kept in registers (one LDS round trip
+// fewer than staging the parent in L.st and applying the move there).
+__device__ __forceinline__ NodeGen create_child_gen(CLds &L, uint32_t stw, uint32_t m) {
+    const uint32_t lane = lane_id();
+    uint32_t w16;
+    const uint32_t x = chessdev::apply_move_regs(stw, m, w16);
+    L.st.board[lane] = (uint8_t)x;
+    if (lane == 16) ((uint32_t *)&L.st)[16] = w16;
+    if (lane == 17) ((uint32_t *)&L.st)[17] = stw;
+    wave_sync_mem();
+    bool check;
+    CSTAMP_T(cs8);
+    const int n = chessdev::legal_moves_check(L.st.board, x, (int)(w16 & 0xFFu), L.s.legal, L.s.pseudo, L.s.region,
+                                              check);
+    CSTAMP_ADD(8, cs8);
+    CSTAMP_T(cs9);
+    const int32_t mat = chessdev::material(x);
+    CSTAMP_ADD(9, cs9);
+    return NodeGen{n, check ? 1 : 0, mat};
+}
+
 __device__ __forceinline__ NodeGen create_node_gen(CLds &L) {
     const uint32_t lane = lane_id();
     const uint32_t sq = L.st.board[lane];
@@ -109,21 +131,29 @@ __device__ __forceinline__ NodeGen create_node_gen(CLds &L) {
     return NodeGen{n, check ? 1 : 0, mat};
 }
 
-__device__ __forceinline__ void create_node_commit(const CTree &t, const CLds &L, NodeGen gen, int id, int parent,
-                                                   int pact, int depth, int &slots, int &status) {
-    const uint32_t lane = lane_id();
+// The slot range of a node of gen.n moves: its base (the next free slot) and the move count it
+// keeps (0 when the list overflowed or the slots ran out: ZC_STATUS_CAPACITY).
+__device__ __forceinline__ int create_node_take(const CTree &t, NodeGen gen, int &slots, int &status) {
     int n = gen.n;
     if (n < 0) {
         status = ZC_STATUS_CAPACITY;
         n = 0;
     }
-    CSTAMP_T(cs10);
     const int base = slots;
     if ((int64_t)base + n > t.S) {
         status = ZC_STATUS_CAPACITY;
         n = 0;
     }
     slots = base + n;
+    return n;
+}
+
+__device__ __forceinline__ void create_node_commit(const CTree &t, const CLds &L, NodeGen gen, int id, int parent,
+                                                   int pact, int depth, int &slots, int &status) {
+    const uint32_t lane = lane_id();
+    CSTAMP_T(cs10);
+    const int base = slots;
+    const int n = create_node_take(t, gen, slots, status);
     for (int j = (int)lane; j < n; j += 64) {
         t.mv[base + j] = L.s.legal[j];
         t.ut[base + j] = (uint8_t)j;

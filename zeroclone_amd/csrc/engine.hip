@@ -786,6 +786,10 @@ zc::ChessParams chess_params(zc_engine *e, int32_t first, int32_t n, int32_t sim
     p.c = c;
     p.policy = policy;
     p.freedom = freedom;
+    static const double kCapVal[5] = {0.0, 1.0, 3.0, 5.0, 9.0};
+    for (int i = 0; i < 5; ++i)
+        for (int k = 0; k < 5; ++k)
+            if (kCapVal[k] >= kCapVal[i] - freedom) p.cls_ok |= 1u << (5 * i + k);
     p.a = e->a;
     p.ca = e->ca;
     return p;

@@ -166,6 +166,9 @@ struct ChessParams {
     double c;
     int policy;        // 0 = Policy('random'), 1 = Policy('immediate_value')
     double freedom;    // policy_freedom
+    // immediate_value's candidate classes: bit 5 i + k set when capture value V[k] >= V[i] -
+    // freedom (V = 0, 1, 3, 5, 9: the maximum V[i] among the untried moves), chess_params_cls_ok
+    uint32_t cls_ok;
     Arena a;           // RNG ring / positions and the log table
     ChessArena ca;
     const zc_chess_state *roots;
