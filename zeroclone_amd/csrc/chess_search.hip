@@ -247,8 +247,10 @@ __device__ __forceinline__ Expansion sim_front(const ChessParams &p, const CTree
 // parent position and move; the helper plays the move and generates the child's legal moves
 // while the leader does the same for the first child.  The leader then commits both children
 // in simulation order (node ids, slots), so the tree, the stream and every output are those of
-// the one-wave search.  (Letting the helper also write the second child, with a join before
-// every walk, measured 6 % slower: profiles/r05_ab_chess_variants.log.)
+// the one-wave search.  The hand-offs are plain LDS accesses ordered by the barriers (a volatile
+// one is a flat store whose wait drains all the wave's global stores).  Letting the helper also
+// write the second child, with a join before every walk, measured within 1 % of this
+// (profiles/r05_ab_chess_variants.log): the two waves are about balanced.
 struct Helper {
     CLds L;
     NodeGen gen;
@@ -261,9 +263,9 @@ __device__ void helper_loop(Helper &h) {
     const uint32_t lane = lane_id();
     for (;;) {
         __syncthreads();  // a command is posted
-        if (uni(*(volatile int *)&h.cmd) != 1) return;
+        if (uni(h.cmd) != 1) return;  // plain LDS accesses: the barriers order them
         const uint32_t stw = lane < 18 ? h.stw[lane] : 0u;
-        const NodeGen gen = create_child_gen(h.L, stw, uni(*(volatile uint32_t *)&h.m));
+        const NodeGen gen = create_child_gen(h.L, stw, uni(h.m));
         if (lane == 0) h.gen = gen;
         __syncthreads();  // the generated child is in h
     }
@@ -271,7 +273,7 @@ __device__ void helper_loop(Helper &h) {
 
 __device__ __forceinline__ void helper_exit(Helper *h) {
     if (!h) return;
-    if (lane_id() == 0) *(volatile int *)&h->cmd = 2;
+    if (lane_id() == 0) h->cmd = 2;
     __syncthreads();
 }
 
@@ -394,7 +396,7 @@ __device__ __forceinline__ int chess_select_flush(const ChessParams &p, const CT
             if (lane < 18) h->stw[lane] = b.stw;
             if (lane == 0) {
                 h->m = b.m;
-                *(volatile int *)&h->cmd = 1;
+                h->cmd = 1;
             }
             __syncthreads();  // the helper starts on b's child
         }
