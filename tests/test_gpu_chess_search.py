@@ -187,3 +187,65 @@ def test_rng_state_after_chess_search_is_pythons(eng):
             want = r.getstate()[1]
             mt, idx = eng.get_rng_state(g)
             assert [int(x) for x in mt] == list(want[:624]) and idx == want[624], (sims, g)
+
+
+CROWDED = ["qqqqkqqq/8/8/8/8/8/8/QQQQKQQQ w - - 0 1",   # ~100 moves a side: the slot pool runs out
+           "qqqqkqqq/8/8/8/8/8/8/QQQQKQQQ b - - 0 1"]
+
+
+def _crude_value(rows):
+    """crude_chess_score (value_functions.py:48-55) of leaf rows on the host, as the fused
+    kernel scores them: 1000 for the side to move checkmated, else the material for it."""
+    vals = {"P": 1, "N": 3, "B": 3, "R": 5, "Q": 9}
+    out = []
+    for r in rows:
+        st = oracle.chess_state(bytes(r[:64]).decode("latin-1"), int(r[64]), int(r[65]), int(r[66]))
+        if oracle.chess_win(st):
+            out.append(1000.0)
+            continue
+        mat = sum(vals.get(chr(b).upper(), 0) * (1 if chr(b).isupper() else -1) for b in r[:64] if chr(b) != " ")
+        out.append(float(mat if st.turn == 0 else -mat))
+    return out
+
+
+@pytest.mark.parametrize("sims", [200, 400])
+def test_paired_crude_search_equals_the_stepwise_one(eng, sims):
+    """The fused crude search pairs consecutive expansions of one node across two waves
+    (chess_search.hip Helper); the stepwise search (zc_chess_ext_*, one wave) does not.  With
+    the crude score computed on the host for the stepwise one, both must build the same tree:
+    root visits, move, counters and MT words — also when the slot pool runs out mid-flush
+    (the crowded boards at 400 simulations: ZC_STATUS_CAPACITY, the failing simulation's pair
+    partner never drawn)."""
+    from zeroclone_amd._native import ZC_POLICY_IMMEDIATE_VALUE, ZC_STATUS_CAPACITY
+    from zeroclone_amd.valued import ChessValuedSearch
+    fens = FENS * 2 + CROWDED * 2
+    n, bs = len(fens), 32
+    seeds = [300 + i for i in range(n)]
+    roots = roots_of(fens)
+    eng.seed(0, seeds)
+    mv = torch.zeros(n, dtype=torch.int16, device="cuda")
+    na = torch.zeros((n, MAXM), dtype=torch.int32, device="cuda")
+    st = torch.zeros((n, 8), dtype=torch.int64, device="cuda")
+    eng.chess_search_async(0, n, roots.data_ptr(), sims, 1.4, bs, ZC_POLICY_IMMEDIATE_VALUE, 3.0, mv.data_ptr(),
+                           na.data_ptr(), st.data_ptr())
+    torch.cuda.synchronize()
+    fused = (mv.cpu().numpy(), na.cpu().numpy(), st.cpu().numpy())
+    eng.seed(0, seeds)
+
+    def fn(leaves, planes, counts):
+        return torch.tensor(_crude_value(leaves.cpu().numpy()), dtype=torch.float64).cuda()
+
+    vs = ChessValuedSearch(eng, n, bs, planes=False, policy=ZC_POLICY_IMMEDIATE_VALUE, freedom=3.0)
+    smv, sna, sst = (x.cpu().numpy() for x in vs.run(roots, sims, 1.4, fn))
+    fmv, fna, fst = fused
+    capacity = 0
+    for i, fen in enumerate(fens):
+        assert list(fst[i, [0, 1, 4, 5]]) == list(sst[i, [0, 1, 4, 5]]), (fen, fst[i], sst[i])
+        capacity += int(fst[i, 5] == ZC_STATUS_CAPACITY)
+        if fst[i, 5] == 0:
+            assert list(fna[i]) == list(sna[i]), fen
+            assert fmv[i] == smv[i], fen
+    if sims == 400:
+        assert capacity >= 2, [list(r) for r in fst]   # the crowded boards ran out of slots
+    else:
+        assert capacity == 0, [list(r) for r in fst]
