@@ -208,14 +208,14 @@ def _crude_value(rows):
     return out
 
 
-@pytest.mark.parametrize("sims", [200, 400])
+@pytest.mark.parametrize("sims", [200, 500])
 def test_paired_crude_search_equals_the_stepwise_one(eng, sims):
     """The fused crude search pairs consecutive expansions of one node across two waves
     (chess_search.hip Helper); the stepwise search (zc_chess_ext_*, one wave) does not.  With
     the crude score computed on the host for the stepwise one, both must build the same tree:
-    root visits, move, counters and MT words — also when the slot pool runs out mid-flush
-    (the crowded boards at 400 simulations: ZC_STATUS_CAPACITY, the failing simulation's pair
-    partner never drawn)."""
+    root visits, move, counters and MT words — also when the slot pool runs out mid-flush (the
+    crowded boards at 500 simulations: ~80 moves a node against 64 slots a node, so
+    ZC_STATUS_CAPACITY, and the failing simulation's pair partner never drawn)."""
     from zeroclone_amd._native import ZC_POLICY_IMMEDIATE_VALUE, ZC_STATUS_CAPACITY
     from zeroclone_amd.valued import ChessValuedSearch
     fens = FENS * 2 + CROWDED * 2
@@ -245,7 +245,7 @@ def test_paired_crude_search_equals_the_stepwise_one(eng, sims):
         if fst[i, 5] == 0:
             assert list(fna[i]) == list(sna[i]), fen
             assert fmv[i] == smv[i], fen
-    if sims == 400:
+    if sims == 500:
         assert capacity >= 2, [list(r) for r in fst]   # the crowded boards ran out of slots
     else:
         assert capacity == 0, [list(r) for r in fst]
