@@ -656,8 +656,8 @@ def exchange_positions(local, world: int, sync=lambda: None):
 # the committed rocprofv3 summaries (tools/summarize_profile.py, stamped with the sha256 of the
 # library they profiled): the self-play kernel (HBM bytes per launch from separate FETCH_SIZE /
 # WRITE_SIZE passes, SQ issue counters) and the walk-only replay kernel (tools/prof_walk.py)
-SEARCH_PROFILE = os.path.join("profiles", "r04_c4_search_summary.json")
-WALK_PROFILE = os.path.join("profiles", "r04_walk_summary.json")
+SEARCH_PROFILE = os.path.join("profiles", "r05_c4_search_summary.json")
+WALK_PROFILE = os.path.join("profiles", "r05_walk_summary.json")
 
 
 def lib_sha() -> str:
@@ -930,7 +930,7 @@ def tower_mode(dev, reps: int = 5) -> dict:
                     "frac_of_2p5PF": round(flop / ms / 1e9 / MFMA_F16_PEAK_TFLOPS, 4)}
     if saved is not None:
         os.environ["ZC_TOWER_MF"] = saved
-    out["pmc"] = "profiles/r04_tower_pmc.json (MFMA busy, held clock)"
+    out["pmc"] = "profiles/r05_tower_pmc.json (MFMA busy, held clock)"
     return out
 
 

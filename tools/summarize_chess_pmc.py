@@ -38,13 +38,19 @@ def main():
            "counter_pass_warm_ms": round(ms, 4), "clock_ghz": round(C / (ms * 1e-3) / 1e9, 3),
            "per_wave_per_move": {"SQ_INSTS_VALU": round(c["SQ_INSTS_VALU"] / w), "SQ_INSTS_SALU": round(c["SQ_INSTS_SALU"] / w),
                                  "SQ_INSTS_LDS": round(c["SQ_INSTS_LDS"] / w), "wave_cycles": round(c["SQ_WAVE_CYCLES"] / w * 4)},
-           "per_simulation": {"instructions": round((c["SQ_INSTS_VALU"] + c["SQ_INSTS_SALU"] + c["SQ_INSTS_LDS"]) / w / sims),
-                              "wave_cycles": round(c["SQ_WAVE_CYCLES"] / w * 4 / sims)},
+           "waves_per_game": round(w / 1024, 3),
+           "per_simulation": {"instructions_all_waves": round((c["SQ_INSTS_VALU"] + c["SQ_INSTS_SALU"] + c["SQ_INSTS_LDS"])
+                                                              / 1024 / sims),
+                              "wave_cycles_per_wave": round(c["SQ_WAVE_CYCLES"] / w * 4 / sims),
+                              "wall_cycles": round(C / sims)},
            "issue": {"valu_util": round(2 * c["SQ_INSTS_VALU"] / (1024 * C), 3), "salu_util": round(c["SQ_INSTS_SALU"] / (256 * C), 3),
                      "issue_any": round(c["SQ_ACTIVE_INST_ANY"] / c["SQ_WAVE_CYCLES"], 3),
                      "wait_any": round(c["SQ_WAIT_ANY"] / c["SQ_WAVE_CYCLES"], 3)},
-           "note": ("1024 games = 1 wave per SIMD: the chain's latency is fully exposed. SQ_WAVE_CYCLES counts "
-                    "quad-cycles (x4). Counter pass: tools/gpu_check.sh cpmc; stats: cprof.")}
+           "note": ("1024 games on 1024 SIMDs: round 5 runs each game as a workgroup of two waves (leader + helper, "
+                    "chess_search.hip Helper), so SQ_WAVES = 2048 and the per-wave figures average the two roles; "
+                    "per simulation: all instructions of a game's waves, a wave's own cycles, and the launch's wall "
+                    "cycles per simulation. SQ_WAVE_CYCLES counts quad-cycles (x4). Counter pass: tools/gpu_check.sh "
+                    "cpmc; stats: cprof.")}
     with open(out_path, "w") as fh:
         json.dump(out, fh, indent=1)
     print(json.dumps(out)[:600])
