@@ -845,7 +845,14 @@ __device__ __forceinline__ void search_move(const SearchParams &p, const SearchL
                                tag, (uint32_t)g, cn);
         } else {
             const int32_t u0 = rng.use();
+            // The rollouts issue at a raised wave priority: a CU's 16 games are each in the walk,
+            // the rollouts or the backup, and the arbiter then serves the compute-bound rollout
+            // chains (scalar-unit bound) first while the walk's and the backup's memory round
+            // trips are in flight.  Priority 1, 2 or 3: 1.62 ms against 1.73 per 4096 x 800
+            // lockstep search; the memory phases raised instead: 1.70 (profiles/r05_ab_c4_wave_priority.log).
+            __builtin_amdgcn_s_setprio(1);
             c4_rollouts(leaves, nb, rng, s_order, cn, STAMP ? &stamp.ph[7] : nullptr);
+            __builtin_amdgcn_s_setprio(0);
             if (WALK == 1) {
                 wave_mem_order();
                 for (int jj = (int)lane; jj < nb; jj += kBlock) p.walk_vals[wlog + jj] = (int8_t)leaves[jj].val;

@@ -504,6 +504,9 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void c
         helper_loop(H);
         return;
     }
+    // the leader carries the serial chain (draws, commits, backups): it issues first when both
+    // waves are ready (1.582 vs 1.691 ms per move, profiles/r05_ab_chess_variants.log)
+    __builtin_amdgcn_s_setprio(1);
     int32_t *ctl = p.ca.ctl + (size_t)g * kCtlWords;
     CSTAMP_INIT();
     crude_search(p, t, L, s_vals, gl, g, ctl, &H);
@@ -620,6 +623,7 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void c
         helper_loop(H);
         return;
     }
+    __builtin_amdgcn_s_setprio(1);  // the leader first (chess_search_kernel)
     const uint32_t lane = lane_id();
     int32_t *ctl = p.ca.ctl + (size_t)g * kCtlWords;
     const uint64_t use_start = uni64(p.a.rngpos[2 * (size_t)g]);
