@@ -360,18 +360,21 @@ def _timed_pool_steps(pool, steps: int, warm: int = 1):
 MIXED = "steady-state self-play: the pool adopts a burned-in pool's games in progress (mixed ages), "
 
 
-def net_rates(fl_pos: int, games: int, sims: int, bs: int, nfl: int, steps: int, dt: float) -> dict:
+def net_rates(fl_pos: int, games: int, sims: int, bs: int, nfl: int, steps: int, dt: float,
+              slots: int | None = None) -> dict:
     """Network FLOP rates of a network-mode step.  Useful FLOPs count the leaves the search
     evaluates (`sims` per move: every simulation's leaf, the PUCT root included); executed
-    FLOPs count every slot the tower computes (`nfl` flushes x `bs` slots per move: the last
-    flush's unused slots are padding).  Both over the whole step time (search, play and record
-    included), so each is a lower bound on the tower's own rate at that work."""
+    FLOPs count every slot the tower computes (`slots` per move; by default `nfl` flushes x
+    `bs`: a short last flush's or the PUCT root flush's unused slots are padding).  Both over
+    the whole step time (search, play and record included), so each is a lower bound on the
+    tower's own rate at that work."""
+    slots = bs * nfl if slots is None else slots
     useful = fl_pos * games * sims * steps
-    executed = fl_pos * games * bs * nfl * steps
+    executed = fl_pos * games * slots * steps
     return {"net_tflops_lower": round(useful / dt / 1e12, 1),
             "mfma_frac_lower": round(useful / dt / 1e12 / MFMA_F16_PEAK_TFLOPS, 4),
             "net_tflops_executed": round(executed / dt / 1e12, 1),
-            "net_slots_per_move": bs * nfl, "net_leaves_per_move": sims}
+            "net_slots_per_move": slots, "net_leaves_per_move": sims}
 
 
 def net_mode(src, games: int, sims: int, bs: int, c: float, steps: int, dev) -> dict:
@@ -470,7 +473,9 @@ def chess_modes(steps: int, dev) -> dict:
                         "steps": steps,
                         "config": MIXED + f"{G} games x {S} sims, ValueNetwork(128, 8) random init fp16 (MFMA "
                                           "kernels), random policy",
-                        **net_rates(flops_per_position(128, 8, 17, 8, 8), G, S, B, (S + B - 1) // B, steps, dt)}
+                        # the short last flush runs the network on its leaves only (NetValue.rows)
+                        **net_rates(flops_per_position(128, 8, 17, 8, 8), G, S, B, (S + B - 1) // B, steps, dt,
+                                    slots=S)}
     out["_pool"] = crude
     out["_snap"] = snap
     return out

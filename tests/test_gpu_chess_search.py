@@ -249,3 +249,31 @@ def test_paired_crude_search_equals_the_stepwise_one(eng, sims):
         assert capacity >= 2, [list(r) for r in fst]   # the crowded boards ran out of slots
     else:
         assert capacity == 0, [list(r) for r in fst]
+
+
+def test_short_last_flush_runs_the_network_on_its_leaves_only(eng):
+    """sims not a multiple of the batch: NetValue.rows evaluates the last flush's n*nb boards
+    only (valued.ChessValuedSearch); the search must equal the one that evaluates all n*bs
+    slots (the same network called through a plain function)."""
+    from zeroclone_amd.nets import MfmaValueNetwork, ValueNetwork
+    from zeroclone_amd.valued import ChessValuedSearch, NetValue
+    torch.manual_seed(3)
+    net = NetValue(MfmaValueNetwork(ValueNetwork(128, 2).eval(), "cuda"))
+    fens = FENS * 3
+    n, sims, bs = len(fens), 100, 32   # the last flush holds 4 leaves a game
+    seeds = [40 + i for i in range(n)]
+    calls = []
+
+    def full(leaves, planes, counts):
+        calls.append(planes.shape[0])
+        return net(leaves, planes, counts)
+
+    outs = []
+    for fn in (net, full):
+        eng.seed(0, seeds)
+        vs = ChessValuedSearch(eng, n, bs)
+        outs.append([x.cpu().numpy().copy() for x in vs.run(roots_of(fens), sims, 1.4, fn)])
+    assert calls == [n * bs] * 4
+    for a, b in zip(*outs):
+        assert (a == b).all()
+    assert (outs[0][2][:, 5] == 0).all() and (outs[0][2][:, 0] == sims).all()

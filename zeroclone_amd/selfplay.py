@@ -383,6 +383,9 @@ class C4SelfPlay:
                 self.net_fn(None, self.ps.planes, self.ps.counts)
             elif self.vs is not None:
                 self.value_fn(None, self.vs.planes, self.vs.counts)
+                nb = self.sims % self.bs   # the short last flush's network buffers, too
+                if nb and hasattr(self.value_fn, "rows"):
+                    self.value_fn.rows(self.vs.planes, self.G, self.bs, nb, self.vs.values)
         torch.cuda.current_stream(self.dev).wait_stream(side)
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
@@ -563,6 +566,9 @@ class ChessSelfPlay:
                     fn(None, self.ps.planes[lo * self.bs:hi * self.bs], self.ps.counts[lo:hi])
             elif self.vs is not None:
                 self.value_fn(None, self.vs.planes, self.vs.counts)
+                nb = self.sims % self.bs   # the short last flush's network buffers, too
+                if nb and hasattr(self.value_fn, "rows"):
+                    self.value_fn.rows(self.vs.planes, self.G, self.bs, nb, self.vs.values)
         torch.cuda.current_stream(self.dev).wait_stream(side)
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):

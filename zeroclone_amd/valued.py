@@ -65,7 +65,11 @@ class C4ValuedSearch:
         for f in range((sims + self.bs - 1) // self.bs):
             e.c4_ext_select(first_game, n, f, self._ptr(self.leaves), self._ptr(self.planes),
                             self.planes is None or self.planes.dtype == torch.float16, self.counts.data_ptr(), s)
-            v = value_fn(self.leaves, self.planes, self.counts)
+            nb = min(self.bs, sims - f * self.bs)   # every game's pending leaves (0 after an error)
+            if nb < self.bs and hasattr(value_fn, "rows") and self.planes is not None:
+                v = value_fn.rows(self.planes, n, self.bs, nb, self.values)   # a short last flush
+            else:
+                v = value_fn(self.leaves, self.planes, self.counts)
             if v is not self.values:
                 self.values.copy_(v.reshape(-1))
             e.c4_ext_backup(first_game, n, f, self.values.data_ptr(), _stream(self.dev))
@@ -103,6 +107,17 @@ class NetValue:
     @torch.no_grad()
     def __call__(self, leaves, planes, counts):
         return self.model(planes).reshape(-1).to(torch.float64)
+
+    @torch.no_grad()
+    def rows(self, planes, n: int, bs: int, nb: int, out):
+        """A flush whose games all hold nb < bs pending leaves (the last flush of a search
+        whose simulations are not a multiple of the batch): the network runs on those n*nb
+        boards only, and their values land in out's first nb slots of each game (the others
+        are never backed up).  Each board's value does not depend on its batch: the values
+        are those of the full call."""
+        sub = planes.view(n, bs, *planes.shape[1:])[:, :nb].reshape(n * nb, *planes.shape[1:])
+        out.view(n, bs)[:, :nb].copy_(self.model(sub).reshape(n, nb).to(torch.float64))
+        return out
 
 
 class HostValue:
@@ -170,8 +185,11 @@ class ChessValuedSearch:
             e.chess_ext_select(first_game, n, f, p(self.leaves), p(self.planes),
                                self.planes is None or self.planes.dtype == torch.float16, self.counts.data_ptr(),
                                _stream(self.dev))
+            nb = min(self.bs, sims - f * self.bs)   # every game's pending leaves (0 after an error)
             if hasattr(value_fn, "flush_values"):   # values computed on the device from the tree itself
                 v = value_fn.flush_values(first_game, n, f, _stream(self.dev))
+            elif nb < self.bs and hasattr(value_fn, "rows") and self.planes is not None:
+                v = value_fn.rows(self.planes, n, self.bs, nb, self.values)   # a short last flush
             else:
                 v = value_fn(self.leaves, self.planes, self.counts)
             if v is not self.values:
