@@ -386,13 +386,14 @@ def net_mode(src, games: int, sims: int, bs: int, c: float, steps: int, dev) -> 
     from zeroclone_amd.selfplay import C4SelfPlay
     torch.manual_seed(0)
     model = for_inference(ValueNetwork(128, 8, in_planes=2).eval(), dev, torch.float16)
-    pool = C4SelfPlay(games, sims, c=c, batch_size=bs, seed=7, device=dev.index, net=model)
+    streams = 1   # split streams measured no faster here (profiles/r05_ab_split_streams.log)
+    pool = C4SelfPlay(games, sims, c=c, batch_size=bs, seed=7, device=dev.index, net=model, streams=streams)
     pool.adopt(src)
     exp, dt = _timed_pool_steps(pool, steps)
     pool.close()
     rates = net_rates(flops_per_position(128, 8, 2, 6, 7), games, sims, bs, (sims + bs - 1) // bs, steps, dt)
     return {"value": round(exp / dt, 1), "unit": "expansions/s", "ms_per_move": round(dt / steps * 1e3, 1),
-            "steps": steps, "config": MIXED + f"{games} games x {sims} sims, batch {bs}",
+            "steps": steps, "config": MIXED + f"{games} games x {sims} sims, batch {bs}", "search_streams": streams,
             "net": "ValueNetwork(128, 8, in_planes=2) random init, fp16, BN folded, this package's MFMA conv kernels",
             **rates,
             "note": "net_tflops_lower = network FLOPs of the evaluated leaves / whole step time (search, play and "
@@ -409,13 +410,15 @@ def c4_puct_mode(src, games: int, sims: int, bs: int, steps: int, dev) -> dict:
     from zeroclone_amd.selfplay import C4SelfPlay
     torch.manual_seed(0)
     net = MfmaPolicyValueNetwork(PolicyValueNetwork(in_planes=2, board=(6, 7), n_logits=7).eval(), dev)
-    pool = C4SelfPlay(games, sims, batch_size=bs, seed=7, device=dev.index, puct_net=net, temperature=1.0)
+    streams = 4   # the games in four parts on four streams (valued._split_flushes)
+    pool = C4SelfPlay(games, sims, batch_size=bs, seed=7, device=dev.index, puct_net=net, temperature=1.0,
+                      streams=streams)
     pool.adopt(src)
     exp, dt = _timed_pool_steps(pool, steps)
     pool.close()
     nfl = _native.check(_native.lib().zc_chess_puct_flushes(sims, bs))
     return {"value": round(exp / dt, 1), "unit": "expansions/s", "ms_per_move": round(dt / steps * 1e3, 1),
-            "steps": steps,
+            "steps": steps, "search_streams": streams,
             "config": MIXED + f"C2 + PUCT: {games} games x {sims} sims, c_puct 1.5, Dirichlet(0.3, 0.25), policy "
                               "(7 logits) + value ResNet 128x8 random init fp16 (MFMA tower), temperature 1",
             **net_rates(flops_per_position(128, 8, 2, 6, 7), games, sims, bs, nfl, steps, dt)}
@@ -465,12 +468,12 @@ def chess_modes(steps: int, dev) -> dict:
     torch.manual_seed(0)
     model = for_inference(ValueNetwork(128, 8).eval(), dev, torch.float16)
     pool = ChessSelfPlay(G, S, batch_size=B, seed=4, device=dev.index, net=model,
-                         policy=_native.ZC_POLICY_RANDOM, freedom=0.0)
+                         policy=_native.ZC_POLICY_RANDOM, freedom=0.0, streams=4)
     pool.adopt(crude)
     exp, dt = _timed_pool_steps(pool, steps)
     pool.close()
     out["value_net"] = {"value": round(exp / dt, 1), "unit": "expansions/s", "ms_per_move": round(dt / steps * 1e3, 1),
-                        "steps": steps,
+                        "steps": steps, "search_streams": 4,
                         "config": MIXED + f"{G} games x {S} sims, ValueNetwork(128, 8) random init fp16 (MFMA "
                                           "kernels), random policy",
                         # the short last flush runs the network on its leaves only (NetValue.rows)
@@ -481,7 +484,7 @@ def chess_modes(steps: int, dev) -> dict:
     return out
 
 
-def puct_mode(src, steps: int, dev, head: str = "conv", streams: int = 2) -> dict:
+def puct_mode(src, steps: int, dev, head: str = "conv", streams: int = 4) -> dict:
     """BASELINE configs[4] (C5) per GPU: chess PUCT self-play, 1024 games x 1600 sims, policy
     + value ResNet (128 x 8, random init, fp16; tower on the MFMA kernels), Dirichlet root
     noise, temperature 1, from the burned-in crude pool's positions; one graph per step."""

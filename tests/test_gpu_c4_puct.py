@@ -229,3 +229,59 @@ def test_c4_consecutive_searches_draw_fresh_noise(eng):
     ps.search_no.zero_()
     mv, _, _ = ps.run(r, 33, _hash_net, temperature=1.0)
     assert np.array_equal(ps.prior.cpu().numpy(), out[0][0]) and np.array_equal(mv.cpu().numpy(), out[0][1])
+
+
+@pytest.mark.parametrize("k", [2, 4])
+def test_c4_split_stream_search_equals_the_single_stream_search(eng, k):
+    """C4PuctSearch with k network callables (valued._split_flushes): the games in k parts on
+    k streams; moves, root visits, priors and counters equal the one-stream search's."""
+    from zeroclone_amd.nets import MfmaPolicyValueNetwork
+    from zeroclone_amd.valued import C4PuctSearch
+    net = MfmaPolicyValueNetwork(_c4_net(seed=6))
+    pos = (POSITIONS * 8)[:37]
+    r = _roots(pos)
+    outs = []
+    for split in (False, True):
+        ps = C4PuctSearch(eng, len(pos), 16, seed=5)
+        fn = [(lambda l, p, c, m=net.replica(): m(p)) for _ in range(k)] if split else (lambda l, p, c: net(p))
+        mv, na, st = ps.run(r, 97, fn, temperature=1.0)
+        outs.append((mv.cpu().clone(), na.cpu().clone(), ps.prior.cpu().clone(), st[:, :3].cpu().clone()))
+    for x, y in zip(*outs):
+        assert torch.equal(x, y)
+
+
+def test_value_searches_split_over_streams_equal_the_single_stream_ones(eng):
+    """C4ValuedSearch and ChessValuedSearch with a list of network values (one per part and
+    stream, valued._split_flushes; 99 simulations, so the short last flush's rows path runs
+    in every part): the same moves, root visits and counters as one stream."""
+    from zeroclone_amd._native import NativeEngine, chess_from_fen, CHESS_STATE_DTYPE
+    from zeroclone_amd.nets import MfmaValueNetwork, ValueNetwork
+    from zeroclone_amd.valued import C4ValuedSearch, ChessValuedSearch, NetValue
+    torch.manual_seed(8)
+    c4net = MfmaValueNetwork(ValueNetwork(128, 2, in_planes=2).eval(), "cuda")
+    pos = (POSITIONS * 8)[:29]
+    r = _roots(pos)
+    for k in (2, 3):
+        outs = []
+        for split in (False, True):
+            eng.seed(0, list(range(100, 100 + len(pos))))
+            vs = C4ValuedSearch(eng, len(pos), 32)
+            fn = [NetValue(c4net.replica()) for _ in range(k)] if split else NetValue(c4net)
+            outs.append([x.cpu().clone() for x in vs.run(r, 99, 1.4, fn)])
+        for x, y in zip(*outs):
+            assert torch.equal(x, y)
+    ce = NativeEngine(max_games=24, max_sims=128, max_batch=32)
+    chnet = MfmaValueNetwork(ValueNetwork(128, 2).eval(), "cuda")
+    fens = ["rnbqkbnr/pppppppp/8/8/8/8/PPPPPPPP/RNBQKBNR w KQkq - 0 1",
+            "r3k2r/p1ppqpb1/bn2pnp1/3PN3/1p2P3/2N2Q1p/PPPBBPPP/R3K2R w KQkq - 0 1"] * 10
+    a = np.array([chess_from_fen(f) for f in fens], CHESS_STATE_DTYPE)
+    croots = torch.from_numpy(a.view(np.uint8).reshape(len(fens), 72).copy()).cuda()
+    outs = []
+    for split in (False, True):
+        ce.seed(0, list(range(200, 200 + len(fens))))
+        vs = ChessValuedSearch(ce, len(fens), 32)
+        fn = [NetValue(chnet.replica()) for _ in range(3)] if split else NetValue(chnet)
+        outs.append([x.cpu().clone() for x in vs.run(croots, 99, 1.4, fn)])
+    ce.close()
+    for x, y in zip(*outs):
+        assert torch.equal(x, y)

@@ -197,7 +197,7 @@ def test_consecutive_searches_draw_fresh_noise(eng):
     assert all(not np.array_equal(pri[0][i], pri[1][i]) for i in range(n))
 
 
-@pytest.mark.parametrize("k", [2, 3])
+@pytest.mark.parametrize("k", [2, 3, 4])
 def test_split_stream_search_equals_the_single_stream_search(eng, k):
     """ChessPuctSearch with k network callables: the games in k contiguous parts on k streams
     (one part's select / backup / policy GEMM beside another part's tower).  The parts share

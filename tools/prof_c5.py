@@ -7,6 +7,7 @@ search's select / backup, play, record) and for same-box A/Bs (tools/ab_c5.sh).
   chess   C4: chess value network, 1024 games x 400 sims, ValueNetwork(128, 8)
   c2net   C2(iii): Connect4 value network, 4096 games x 800 sims, ValueNetwork(128, 8, 2)
   c2puct  C2 + PUCT: Connect4, 4096 x 800, policy (7 logits) + value ResNet
+ZC_STREAMS=k (chess, c2net, c2puct) / ZC_PUCT_STREAMS=k (c5): the games in k parts on k streams.
 Prints ms per step."""
 import argparse
 import os
@@ -33,7 +34,8 @@ def make_pool(mode, dev):
         else:
             model = for_inference(ValueNetwork(128, 8).eval(), dev, torch.float16)
             pool = ChessSelfPlay(1024, 400, batch_size=32, seed=4, device=0, net=model,
-                                 policy=_native.ZC_POLICY_RANDOM, freedom=0.0)
+                                 policy=_native.ZC_POLICY_RANDOM, freedom=0.0,
+                                 streams=int(os.environ.get("ZC_STREAMS", "1")))
         pool.adopt(crude)
         crude.close()
         return pool, burn
@@ -41,10 +43,12 @@ def make_pool(mode, dev):
     burn = bench.burn_in(src)
     if mode == "c2net":
         model = for_inference(ValueNetwork(128, 8, in_planes=2).eval(), dev, torch.float16)
-        pool = C4SelfPlay(4096, 800, batch_size=32, seed=7, device=0, net=model)
+        pool = C4SelfPlay(4096, 800, batch_size=32, seed=7, device=0, net=model,
+                          streams=int(os.environ.get("ZC_STREAMS", "1")))
     else:
         net = MfmaPolicyValueNetwork(PolicyValueNetwork(in_planes=2, board=(6, 7), n_logits=7).eval(), dev)
-        pool = C4SelfPlay(4096, 800, batch_size=32, seed=7, device=0, puct_net=net, temperature=1.0)
+        pool = C4SelfPlay(4096, 800, batch_size=32, seed=7, device=0, puct_net=net, temperature=1.0,
+                          streams=int(os.environ.get("ZC_STREAMS", "1")))
     pool.adopt(src)
     src.close()
     return pool, burn

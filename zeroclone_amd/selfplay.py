@@ -227,6 +227,20 @@ def _room(traj):
         traj.ensure_room()
 
 
+def _warm(search, fn, sims: int):
+    """Each part's network once on its own slice of the search's buffers, and once at the
+    short last flush's shape (NetValue.rows) when the simulations are not a multiple of the
+    batch: kernels loaded and buffers allocated before a graph capture."""
+    from .valued import _warm_parts
+    fns = list(fn) if isinstance(fn, (list, tuple)) else [fn]
+    _warm_parts(search, fns)
+    nb, k, n, bs = sims % search.bs, len(fns), search.n, search.bs
+    for i, f in enumerate(fns):
+        if nb and hasattr(f, "rows"):
+            lo, hi = i * n // k, (i + 1) * n // k
+            f.rows(search.planes[lo * bs:hi * bs], hi - lo, bs, nb, search.values[lo * bs:hi * bs])
+
+
 class C4SelfPlay:
     """Connect4 self-play pool on one GPU: search (zc_c4_search_async) + play/evaluate
     (zc_c4_play_async) + trajectory recording (zc_traj_record_async), all stream-ordered,
@@ -239,7 +253,7 @@ class C4SelfPlay:
 
     def __init__(self, games: int, sims: int, c: float = 1.4, batch_size: int = 32, seed: int = 0,
                  rank: int = 0, device: int = 0, record: bool = True, games_cap: int | None = None,
-                 net=None, puct_net=None, temperature: float = 1.0, puct_seed: int = 1):
+                 net=None, puct_net=None, temperature: float = 1.0, puct_seed: int = 1, streams: int = 1):
         self.G, self.sims, self.c, self.bs = games, sims, c, batch_size
         self.dev = torch.device("cuda", device) if isinstance(device, int) else torch.device(device)
         self.eng = _native.NativeEngine(max_games=games, max_sims=sims, max_batch=batch_size,
@@ -265,10 +279,14 @@ class C4SelfPlay:
             from .valued import C4ValuedSearch, NetValue
             self.vs = C4ValuedSearch(self.eng, games, batch_size, leaves=False)
             self.value_fn = NetValue(net)
+            if streams > 1:   # the games in parts on their own streams (valued._split_flushes)
+                self.value_fn = [NetValue(net.replica() if hasattr(net, "replica") else net) for _ in range(streams)]
         if puct_net is not None:
             from .valued import C4PuctSearch
             self.ps = C4PuctSearch(self.eng, games, batch_size, seed=puct_seed, leaves=False)
             self.net_fn = lambda leaves, planes, counts: puct_net(planes)
+            if streams > 1:
+                self.net_fn = [(lambda leaves, planes, counts, m=puct_net.replica(): m(planes)) for _ in range(streams)]
 
     def start(self, quota: int | None = None):
         """Every slot back to the opening; with a quota, slots beyond it idle and finished
@@ -380,12 +398,9 @@ class C4SelfPlay:
         side.wait_stream(torch.cuda.current_stream(self.dev))
         with torch.cuda.stream(side):   # the network's kernels warmed outside the capture
             if self.ps is not None:
-                self.net_fn(None, self.ps.planes, self.ps.counts)
+                _warm(self.ps, self.net_fn, self.sims)
             elif self.vs is not None:
-                self.value_fn(None, self.vs.planes, self.vs.counts)
-                nb = self.sims % self.bs   # the short last flush's network buffers, too
-                if nb and hasattr(self.value_fn, "rows"):
-                    self.value_fn.rows(self.vs.planes, self.G, self.bs, nb, self.vs.values)
+                _warm(self.vs, self.value_fn, self.sims)
         torch.cuda.current_stream(self.dev).wait_stream(side)
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
@@ -462,7 +477,7 @@ class ChessSelfPlay:
                  rank: int = 0, device: int = 0, policy: int = _native.ZC_POLICY_IMMEDIATE_VALUE,
                  freedom: float = 3.0, net=None, init_fen: str | None = None, games_cap: int | None = None,
                  hist_cap: int = 1024, puct_net=None, temperature: float = 1.0, puct_seed: int = 1,
-                 puct_streams: int = 1):
+                 puct_streams: int = 1, streams: int = 1):
         self.G, self.sims, self.c, self.bs = games, sims, c, batch_size
         self.policy, self.freedom = int(policy), float(freedom)
         self.dev = torch.device("cuda", device) if isinstance(device, int) else torch.device(device)
@@ -487,6 +502,8 @@ class ChessSelfPlay:
             self.vs = ChessValuedSearch(self.eng, games, batch_size, leaves=False, policy=self.policy,
                                         freedom=self.freedom)
             self.value_fn = NetValue(net)
+            if streams > 1:   # the games in parts on their own streams (valued._split_flushes)
+                self.value_fn = [NetValue(net.replica() if hasattr(net, "replica") else net) for _ in range(streams)]
         if puct_net is not None:
             from .valued import ChessPuctSearch
             self.ps = ChessPuctSearch(self.eng, games, batch_size, seed=puct_seed, leaves=False)
@@ -560,15 +577,9 @@ class ChessSelfPlay:
         side.wait_stream(torch.cuda.current_stream(self.dev))
         with torch.cuda.stream(side):   # the network's kernels warmed outside the capture
             if self.ps is not None:
-                fns = self.net_fn if isinstance(self.net_fn, list) else [self.net_fn]
-                for q, fn in enumerate(fns):   # each part's network warmed on its own slice
-                    lo, hi = q * self.G // len(fns), (q + 1) * self.G // len(fns)
-                    fn(None, self.ps.planes[lo * self.bs:hi * self.bs], self.ps.counts[lo:hi])
+                _warm(self.ps, self.net_fn, self.sims)
             elif self.vs is not None:
-                self.value_fn(None, self.vs.planes, self.vs.counts)
-                nb = self.sims % self.bs   # the short last flush's network buffers, too
-                if nb and hasattr(self.value_fn, "rows"):
-                    self.value_fn.rows(self.vs.planes, self.G, self.bs, nb, self.vs.values)
+                _warm(self.vs, self.value_fn, self.sims)
         torch.cuda.current_stream(self.dev).wait_stream(side)
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):

@@ -29,6 +29,64 @@ def _stream(dev) -> int:
     return torch.cuda.current_stream(dev).cuda_stream
 
 
+def _split_flushes(search, nfl: int, fns: list, first_game: int, select, evaluate_backup):
+    """The flushes of k contiguous game parts, part i on stream i (stream 0: the current one;
+    the others fork from it and join back), fns[i] the part's value / network function.  The
+    parts share no tree, buffer or counter — select and backup of a part touch only its games
+    and its slices of the leaf / plane / count / value buffers, and each fns[i] owns its
+    network buffers — so the order of the launches across parts does not matter, and the GPU
+    runs one part's search kernels beside another part's network.  select(first, n, f, leaves,
+    planes, counts, stream); evaluate_backup(first, n, f, fn, leaves, planes, counts, values,
+    stream) calls fn and backs its output up."""
+    n, bs, k = search.n, search.bs, len(fns)
+    main = torch.cuda.current_stream(search.dev)
+    if getattr(search, "_side", None) is None or len(search._side) < k - 1:
+        search._side = [torch.cuda.Stream(search.dev) for _ in range(k - 1)]
+    streams = [main] + search._side[:k - 1]
+    for st in streams[1:]:
+        st.wait_stream(main)
+    parts = []
+    for i in range(k):
+        lo, hi = i * n // k, (i + 1) * n // k
+        if hi > lo:
+            sl = slice(lo * bs, hi * bs)
+            parts.append((lo, hi, streams[i], fns[i], search.leaves[sl] if search.leaves is not None else None,
+                          search.planes[sl] if search.planes is not None else None, search.counts[lo:hi],
+                          search.values[sl]))
+    for f in range(nfl):
+        for lo, hi, st, fn, lv, pv, cv, vv in parts:
+            with torch.cuda.stream(st):
+                select(first_game + lo, hi - lo, f, lv, pv, cv, st.cuda_stream)
+                evaluate_backup(first_game + lo, hi - lo, f, fn, lv, pv, cv, vv, st.cuda_stream)
+    for st in streams[1:]:
+        main.wait_stream(st)
+
+
+def _value_backup(sims: int, bs: int, backup):
+    """evaluate_backup of a value search's part (_split_flushes): the part's network on its
+    leaves (a short last flush on its nb leaves only, NetValue.rows), then backup(first, n,
+    flush, values, stream)."""
+    def evaluate_backup(first, m, f, fn, lv, pv, cv, vv, st):
+        nb = min(bs, sims - f * bs)
+        if nb < bs and hasattr(fn, "rows") and pv is not None:
+            v = fn.rows(pv, m, bs, nb, vv)
+        else:
+            v = fn(lv, pv, cv)
+        if v.data_ptr() != vv.data_ptr():
+            vv.copy_(v.reshape(-1))
+        backup(first, m, f, vv.data_ptr(), st)
+    return evaluate_backup
+
+
+def _warm_parts(search, fns):
+    """Each part's function once on its own slice (graph capture warms kernels and buffers)."""
+    k, n, bs = len(fns), search.n, search.bs
+    for i, fn in enumerate(fns):
+        lo, hi = i * n // k, (i + 1) * n // k
+        fn(search.leaves[lo * bs:hi * bs] if search.leaves is not None else None,
+           search.planes[lo * bs:hi * bs] if search.planes is not None else None, search.counts[lo:hi])
+
+
 class C4ValuedSearch:
     def __init__(self, eng: "_native.NativeEngine", n_games: int, batch_size: int = 32,
                  planes_dtype: torch.dtype = torch.float16, leaves: bool = True, planes: bool = True):
@@ -62,7 +120,15 @@ class C4ValuedSearch:
         s = _stream(self.dev)
         e, n = self.eng, self.n
         e.c4_ext_begin(first_game, n, roots.data_ptr(), sims, c, self.bs, s)
-        for f in range((sims + self.bs - 1) // self.bs):
+        nfl = (sims + self.bs - 1) // self.bs
+        if isinstance(value_fn, (list, tuple)):   # the games in parts on their own streams (_split_flushes)
+            def select(first, m, f, lv, pv, cv, st):
+                e.c4_ext_select(first, m, f, self._ptr(lv), self._ptr(pv), pv is None or pv.dtype == torch.float16,
+                                cv.data_ptr(), st)
+            _split_flushes(self, nfl, list(value_fn), first_game, select,
+                           _value_backup(sims, self.bs, e.c4_ext_backup))
+            nfl = 0
+        for f in range(nfl):
             e.c4_ext_select(first_game, n, f, self._ptr(self.leaves), self._ptr(self.planes),
                             self.planes is None or self.planes.dtype == torch.float16, self.counts.data_ptr(), s)
             nb = min(self.bs, sims - f * self.bs)   # every game's pending leaves (0 after an error)
@@ -89,7 +155,7 @@ class C4ValuedSearch:
         side = torch.cuda.Stream(self.dev)
         side.wait_stream(torch.cuda.current_stream(self.dev))
         with torch.cuda.stream(side):  # warm the value function's kernels outside capture
-            value_fn(self.leaves, self.planes, self.counts)
+            _warm_parts(self, value_fn if isinstance(value_fn, (list, tuple)) else [value_fn])
         torch.cuda.current_stream(self.dev).wait_stream(side)
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
@@ -181,7 +247,15 @@ class ChessValuedSearch:
         p = lambda t: t.data_ptr() if t is not None else 0  # noqa: E731
         e.chess_ext_begin(first_game, n, roots.data_ptr(), sims, c, self.bs, self.policy, self.freedom,
                           _stream(self.dev))
-        for f in range((sims + self.bs - 1) // self.bs):
+        nfl = (sims + self.bs - 1) // self.bs
+        if isinstance(value_fn, (list, tuple)):   # the games in parts on their own streams (_split_flushes)
+            def select(first, m, f, lv, pv, cv, st):
+                e.chess_ext_select(first, m, f, p(lv), p(pv), pv is None or pv.dtype == torch.float16,
+                                   cv.data_ptr(), st)
+            _split_flushes(self, nfl, list(value_fn), first_game, select,
+                           _value_backup(sims, self.bs, e.chess_ext_backup))
+            nfl = 0
+        for f in range(nfl):
             e.chess_ext_select(first_game, n, f, p(self.leaves), p(self.planes),
                                self.planes is None or self.planes.dtype == torch.float16, self.counts.data_ptr(),
                                _stream(self.dev))
@@ -264,40 +338,21 @@ class ChessPuctSearch:
         return self.move, self.na, self.stats
 
     def _enqueue_split(self, nfl: int, fns: list, first_game: int):
-        """The flushes of k contiguous game parts, part i on stream i (stream 0: the current
-        one; the others fork from it and join back).  The parts share no tree, buffer or
-        counter — select / backup of a part touch only its games, its slices of the leaf /
-        plane / value buffers, and net_fn i owns its network buffers — so the order of the
-        launches across parts does not matter, and the GPU runs one part's search kernels and
-        policy GEMM beside another part's tower."""
-        e, n, bs, k = self.eng, self.n, self.bs, len(fns)
-        main = torch.cuda.current_stream(self.dev)
-        if getattr(self, "_side", None) is None or len(self._side) < k - 1:
-            self._side = [torch.cuda.Stream(self.dev) for _ in range(k - 1)]
-        streams = [main] + self._side[:k - 1]
-        for st in streams[1:]:
-            st.wait_stream(main)
-        parts = [(i * n // k, (i + 1) * n // k) for i in range(k)]
-        views = []
-        for lo, hi in parts:
-            views.append((self.leaves[lo * bs:hi * bs] if self.leaves is not None else None,
-                          self.planes[lo * bs:hi * bs], self.counts[lo:hi], self.values[lo * bs:hi * bs]))
-        for f in range(nfl):
-            for (lo, hi), st, fn, (lv, pv, cv, vv) in zip(parts, streams, fns, views):
-                if hi == lo:
-                    continue
-                with torch.cuda.stream(st):
-                    s = st.cuda_stream
-                    e.chess_puct_select(first_game + lo, hi - lo, f, lv.data_ptr() if lv is not None else 0,
-                                        pv.data_ptr(), pv.dtype == torch.float16, cv.data_ptr(), s)
-                    v, logits = fn(lv, pv, cv)
-                    if v.data_ptr() != vv.data_ptr():
-                        vv.copy_(v.reshape(-1))
-                    logits = logits.contiguous()
-                    e.chess_puct_backup(first_game + lo, hi - lo, f, vv.data_ptr(), logits.data_ptr(),
-                                        logits.dtype == torch.float16, s)
-        for st in streams[1:]:
-            main.wait_stream(st)
+        """The search split over len(fns) streams (_split_flushes): one part's select and
+        backup beside another part's tower."""
+        e = self.eng
+
+        def select(first, n, f, lv, pv, cv, s):
+            e.chess_puct_select(first, n, f, lv.data_ptr() if lv is not None else 0, pv.data_ptr(),
+                                pv.dtype == torch.float16, cv.data_ptr(), s)
+
+        def evaluate_backup(first, n, f, fn, lv, pv, cv, vv, s):
+            v, logits = fn(lv, pv, cv)
+            if v.data_ptr() != vv.data_ptr():
+                vv.copy_(v.reshape(-1))
+            logits = logits.contiguous()
+            e.chess_puct_backup(first, n, f, vv.data_ptr(), logits.data_ptr(), logits.dtype == torch.float16, s)
+        _split_flushes(self, nfl, fns, first_game, select, evaluate_backup)
 
     def run(self, roots, sims, net_fn, temperature: float = 0.0, first_game: int = 0):
         self.enqueue(roots, sims, net_fn, temperature, first_game)
@@ -308,14 +363,7 @@ class ChessPuctSearch:
         side = torch.cuda.Stream(self.dev)
         side.wait_stream(torch.cuda.current_stream(self.dev))
         with torch.cuda.stream(side):
-            if isinstance(net_fn, (list, tuple)):   # warm each part's network on its own slice
-                k, n, bs = len(net_fn), self.n, self.bs
-                for i, fn in enumerate(net_fn):
-                    lo, hi = i * n // k, (i + 1) * n // k
-                    fn(self.leaves[lo * bs:hi * bs] if self.leaves is not None else None,
-                       self.planes[lo * bs:hi * bs], self.counts[lo:hi])
-            else:
-                net_fn(self.leaves, self.planes, self.counts)
+            _warm_parts(self, net_fn if isinstance(net_fn, (list, tuple)) else [net_fn])
         torch.cuda.current_stream(self.dev).wait_stream(side)
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
@@ -360,6 +408,19 @@ class C4PuctSearch:
         nfl = _native.check(_native.lib().zc_chess_puct_flushes(int(sims), int(self.bs)))
         e.c4_puct_begin(first_game, n, roots.data_ptr(), sims, self.c, self.bs, self.alpha, self.eps, self.seed,
                         self.search_no.data_ptr(), stream=_stream(self.dev))
+        if isinstance(net_fn, (list, tuple)):   # split over streams, as ChessPuctSearch
+            def select(first, m, f, lv, pv, cv, s):
+                e.c4_puct_select(first, m, f, lv.data_ptr() if lv is not None else 0, pv.data_ptr(),
+                                 pv.dtype == torch.float16, cv.data_ptr(), s)
+
+            def evaluate_backup(first, m, f, fn, lv, pv, cv, vv, s):
+                v, logits = fn(lv, pv, cv)
+                if v.data_ptr() != vv.data_ptr():
+                    vv.copy_(v.reshape(-1))
+                logits = logits.contiguous()
+                e.c4_puct_backup(first, m, f, vv.data_ptr(), logits.data_ptr(), logits.dtype == torch.float16, s)
+            _split_flushes(self, nfl, list(net_fn), first_game, select, evaluate_backup)
+            nfl = 0
         for f in range(nfl):
             e.c4_puct_select(first_game, n, f, p(self.leaves), p(self.planes), self.planes.dtype == torch.float16,
                              self.counts.data_ptr(), _stream(self.dev))
