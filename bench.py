@@ -421,7 +421,9 @@ def c4_puct_mode(src, games: int, sims: int, bs: int, steps: int, dev) -> dict:
             "steps": steps, "search_streams": streams,
             "config": MIXED + f"C2 + PUCT: {games} games x {sims} sims, c_puct 1.5, Dirichlet(0.3, 0.25), policy "
                               "(7 logits) + value ResNet 128x8 random init fp16 (MFMA tower), temperature 1",
-            **net_rates(flops_per_position(128, 8, 2, 6, 7), games, sims, bs, nfl, steps, dt)}
+            # flush 0 runs the network on the roots alone (valued.PolicyNet): 1 + (nfl - 1) x bs boards
+            **net_rates(flops_per_position(128, 8, 2, 6, 7), games, sims, bs, nfl, steps, dt,
+                        slots=1 + (nfl - 1) * bs)}
 
 
 def chess_burned_pool(dev, games: int = 1024, sims: int = 400, bs: int = 32, max_moves: int = 600):
@@ -507,7 +509,7 @@ def puct_mode(src, steps: int, dev, head: str = "conv", streams: int = 4) -> dic
                             "from; an epilogue of the tower launch, no GEMM)" if head == "conv" else
                             "linear (1x1 conv 128 -> 32 in the tower launch + Linear 2048 -> 4096 as a GEMM)"),
             "search_streams": streams,
-            **net_rates(flops_per_position(128, 8, 17, 8, 8), G, S, B, nfl, steps, dt)}
+            **net_rates(flops_per_position(128, 8, 17, 8, 8), G, S, B, nfl, steps, dt, slots=1 + (nfl - 1) * B)}
 
 
 def c1_mode(dev, sims: int = 100, games: int = 4) -> dict:

@@ -455,6 +455,14 @@ int zc_chess_puct_select(zc_engine *eng, int32_t first_game, int32_t n_games, in
                          void *hip_stream);
 int zc_chess_puct_backup(zc_engine *eng, int32_t first_game, int32_t n_games, int32_t flush, const double *d_values,
                          const void *d_logits, int32_t logits_dtype, void *hip_stream);
+/* zc_chess_puct_backup with the values / logits of game i's leaf j at row i * rows_per_game +
+ * j: 0 = batch_size (the layout select writes the planes in); for flush 0, the roots-only
+ * flush (one leaf a game), any rows_per_game >= 1 — 1 lets the caller evaluate the n root
+ * positions alone instead of n * batch_size slots.  EINVAL for rows_per_game > 0 on a later
+ * flush. */
+int zc_chess_puct_backup_ex(zc_engine *eng, int32_t first_game, int32_t n_games, int32_t flush,
+                            const double *d_values, const void *d_logits, int32_t logits_dtype,
+                            int32_t rows_per_game, void *hip_stream);
 int zc_chess_puct_end(zc_engine *eng, int32_t first_game, int32_t n_games, float temperature, uint16_t *d_out_move,
                       int32_t *d_out_root_na, float *d_out_root_prior, zc_game_stats *d_out_stats, void *hip_stream);
 
@@ -473,6 +481,9 @@ int zc_c4_puct_select(zc_engine *eng, int32_t first_game, int32_t n_games, int32
                       void *d_planes, int32_t planes_dtype, int32_t *d_counts, void *hip_stream);
 int zc_c4_puct_backup(zc_engine *eng, int32_t first_game, int32_t n_games, int32_t flush, const double *d_values,
                       const void *d_logits, int32_t logits_dtype, void *hip_stream);
+/* As zc_chess_puct_backup_ex, for the Connect4 PUCT search. */
+int zc_c4_puct_backup_ex(zc_engine *eng, int32_t first_game, int32_t n_games, int32_t flush, const double *d_values,
+                         const void *d_logits, int32_t logits_dtype, int32_t rows_per_game, void *hip_stream);
 int zc_c4_puct_end(zc_engine *eng, int32_t first_game, int32_t n_games, float temperature, int32_t *d_out_move,
                    int32_t *d_out_root_na, float *d_out_root_prior, zc_game_stats *d_out_stats, void *hip_stream);
 /* Test hook: game `game`'s Connect4 PUCT tree as raw 192-byte node records (stones X/O, move

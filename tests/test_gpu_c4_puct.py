@@ -285,3 +285,24 @@ def test_value_searches_split_over_streams_equal_the_single_stream_ones(eng):
     ce.close()
     for x, y in zip(*outs):
         assert torch.equal(x, y)
+
+
+@pytest.mark.parametrize("k", [1, 4])
+def test_c4_roots_flush_on_the_roots_alone_equals_the_full_flush(eng, k):
+    """As the chess test: PolicyNet's roots-only flush 0 against the all-slot flush."""
+    from zeroclone_amd.nets import MfmaPolicyValueNetwork
+    from zeroclone_amd.valued import C4PuctSearch, PolicyNet
+    net = MfmaPolicyValueNetwork(_c4_net(seed=9))
+    pos = (POSITIONS * 8)[:37]
+    r = _roots(pos)
+    outs = []
+    for trimmed in (False, True):
+        ps = C4PuctSearch(eng, len(pos), 16, seed=2)
+        if trimmed:
+            fn = PolicyNet(net) if k == 1 else [PolicyNet(net.replica()) for _ in range(k)]
+        else:
+            fn = (lambda l, p, c: net(p)) if k == 1 else [(lambda l, p, c, m=net.replica(): m(p)) for _ in range(k)]
+        mv, na, st = ps.run(r, 81, fn, temperature=1.0)
+        outs.append((mv.cpu().clone(), na.cpu().clone(), ps.prior.cpu().clone(), st[:, :3].cpu().clone()))
+    for x, y in zip(*outs):
+        assert torch.equal(x, y)

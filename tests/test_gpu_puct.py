@@ -226,3 +226,35 @@ def test_split_stream_search_equals_the_single_stream_search(eng, k):
     for x, y in zip(a1 + a2, b1 + b2):
         assert torch.equal(x, y)
     assert (a1[1].sum(dim=1) == 96).all()
+
+
+@pytest.mark.parametrize("k", [1, 2])
+def test_roots_flush_on_the_roots_alone_equals_the_full_flush(eng, k):
+    """valued.PolicyNet: flush 0 (one root a game) runs the network on the n roots alone and
+    backs up with one row a game (zc_chess_puct_backup_ex rows = 1); the search must equal the
+    one that evaluates all n * batch_size slots of flush 0 (a plain function)."""
+    from zeroclone_amd.nets import MfmaPolicyValueNetwork, PolicyValueNetwork
+    from zeroclone_amd.valued import ChessPuctSearch, PolicyNet
+    torch.manual_seed(5)
+    net = MfmaPolicyValueNetwork(PolicyValueNetwork(head="conv").eval())
+    fens = (FENS * 8)[:29]
+    roots = roots_of(fens)
+    outs = []
+    for trimmed in (False, True):
+        ps = ChessPuctSearch(eng, len(fens), 32, seed=4)
+        if trimmed:
+            fn = PolicyNet(net) if k == 1 else [PolicyNet(net.replica()) for _ in range(k)]
+        else:
+            fn = (lambda l, p, c: net(p)) if k == 1 else [(lambda l, p, c, m=net.replica(): m(p)) for _ in range(k)]
+        mv, na, st = ps.run(roots, 65, fn, temperature=1.0)
+        outs.append((mv.cpu().clone(), na.cpu().clone(), ps.prior.cpu().clone(), st[:, :3].cpu().clone()))
+    for x, y in zip(*outs):
+        assert torch.equal(x, y)
+
+
+def test_rows_per_game_only_for_the_roots_flush(eng):
+    from zeroclone_amd._native import lib
+    v = torch.zeros(64, dtype=torch.float64, device="cuda")
+    lg = torch.zeros((64, 4096), dtype=torch.float16, device="cuda")
+    rc = lib().zc_chess_puct_backup_ex(eng._h, 0, 1, 1, v.data_ptr(), lg.data_ptr(), 1, 1, None)
+    assert rc != 0

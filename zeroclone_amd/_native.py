@@ -208,6 +208,9 @@ SIGNATURES = [
                                             ctypes.c_void_p]),
     ("zc_chess_puct_backup", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
                                             ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p]),
+    ("zc_chess_puct_backup_ex", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                               ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32,
+                                               ctypes.c_void_p]),
     ("zc_chess_puct_end", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_float,
                                          ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                          ctypes.c_void_p]),
@@ -219,6 +222,9 @@ SIGNATURES = [
                                          ctypes.c_void_p]),
     ("zc_c4_puct_backup", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
                                          ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p]),
+    ("zc_c4_puct_backup_ex", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32,
+                                            ctypes.c_void_p]),
     ("zc_c4_puct_end", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_float,
                                       ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                       ctypes.c_void_p]),
@@ -650,10 +656,11 @@ class NativeEngine:
                                          ctypes.c_void_p(d_planes or None), ZC_F16 if planes_f16 else ZC_F32,
                                          ctypes.c_void_p(d_counts or None), ctypes.c_void_p(stream or None)))
 
-    def chess_puct_backup(self, first_game, n, flush, d_values, d_logits, logits_f16=False, stream=0):
-        check(lib().zc_chess_puct_backup(self._h, first_game, n, int(flush), ctypes.c_void_p(d_values),
-                                         ctypes.c_void_p(d_logits), ZC_F16 if logits_f16 else ZC_F32,
-                                         ctypes.c_void_p(stream or None)))
+    def chess_puct_backup(self, first_game, n, flush, d_values, d_logits, logits_f16=False, stream=0, rows=0):
+        """rows: values / logits rows per game (0: batch_size; flush 0 also takes 1 — the roots alone)."""
+        check(lib().zc_chess_puct_backup_ex(self._h, first_game, n, int(flush), ctypes.c_void_p(d_values),
+                                            ctypes.c_void_p(d_logits), ZC_F16 if logits_f16 else ZC_F32, int(rows),
+                                            ctypes.c_void_p(stream or None)))
 
     def chess_puct_end(self, first_game, n, temperature, d_move, d_na, d_prior, d_stats, stream=0):
         check(lib().zc_chess_puct_end(self._h, first_game, n, float(temperature), ctypes.c_void_p(d_move),
@@ -672,10 +679,11 @@ class NativeEngine:
                                       ctypes.c_void_p(d_planes or None), ZC_F16 if planes_f16 else ZC_F32,
                                       ctypes.c_void_p(d_counts or None), ctypes.c_void_p(stream or None)))
 
-    def c4_puct_backup(self, first_game, n, flush, d_values, d_logits, logits_f16=False, stream=0):
-        check(lib().zc_c4_puct_backup(self._h, first_game, n, int(flush), ctypes.c_void_p(d_values),
-                                      ctypes.c_void_p(d_logits), ZC_F16 if logits_f16 else ZC_F32,
-                                      ctypes.c_void_p(stream or None)))
+    def c4_puct_backup(self, first_game, n, flush, d_values, d_logits, logits_f16=False, stream=0, rows=0):
+        """rows: as chess_puct_backup."""
+        check(lib().zc_c4_puct_backup_ex(self._h, first_game, n, int(flush), ctypes.c_void_p(d_values),
+                                         ctypes.c_void_p(d_logits), ZC_F16 if logits_f16 else ZC_F32, int(rows),
+                                         ctypes.c_void_p(stream or None)))
 
     def c4_puct_end(self, first_game, n, temperature, d_move, d_na, d_prior, d_stats, stream=0):
         check(lib().zc_c4_puct_end(self._h, first_game, n, float(temperature), ctypes.c_void_p(d_move),

@@ -239,7 +239,7 @@ __global__ __launch_bounds__(64) void c4_puct_backup_kernel(C4PuctParams p) {
         const int node = (int)(mt & 0xFFFFu), d = (int)(mt >> 16);
         C4PNode *N = &T[node];
         const int nm = uni((int)N->nmoves);
-        const size_t li = (size_t)gl * p.bs + j;
+        const size_t li = (size_t)gl * (p.leaf_rows ? p.leaf_rows : p.bs) + j;
         double v;
         if (nm == 0) {
             v = uni((int)N->won) ? -1.0 : 0.0;  // the side to move has lost / a full board

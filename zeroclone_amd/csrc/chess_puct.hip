@@ -237,7 +237,7 @@ __global__ __launch_bounds__(64) void puct_backup_kernel(ChessParams p) {
         const int node = (int)(mt & 0xFFFFu), d = (int)(mt >> 16);
         ChessNode *N = &t.nodes[node];
         const int nm = uni((int)N->nmoves);
-        const size_t li = (size_t)gl * p.bs + j;
+        const size_t li = (size_t)gl * (p.leaf_rows ? p.leaf_rows : p.bs) + j;
         double v;
         if (nm == 0) {
             v = uni((int)N->check) ? -1.0 : 0.0;  // checkmated side to move / no moves

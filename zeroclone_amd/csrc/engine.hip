@@ -1200,10 +1200,12 @@ int zc_chess_puct_select(zc_engine *eng, int32_t first, int32_t n, int32_t flush
     return ZC_OK;
 }
 
-int zc_chess_puct_backup(zc_engine *eng, int32_t first, int32_t n, int32_t flush, const double *d_values,
-                         const void *d_logits, int32_t logits_dtype, void *hip_stream) {
+int zc_chess_puct_backup_ex(zc_engine *eng, int32_t first, int32_t n, int32_t flush, const double *d_values,
+                            const void *d_logits, int32_t logits_dtype, int32_t rows_per_game, void *hip_stream) {
     if (!eng || (n && (!d_values || !d_logits))) return fail(ZC_EINVAL, "null argument");
     if (logits_dtype != ZC_F32 && logits_dtype != ZC_F16) return fail(ZC_EINVAL, "logits_dtype must be ZC_F32 or ZC_F16");
+    if (rows_per_game < 0 || (rows_per_game > 0 && flush != 0))
+        return fail(ZC_EINVAL, "rows_per_game must be 0 (batch_size rows), or >= 1 for flush 0 (the roots)");
     std::lock_guard<std::mutex> lk(eng->mu);
     if (int r = check_px(eng, first, n, flush, true)) return r;
     if (!n) return ZC_OK;
@@ -1213,9 +1215,15 @@ int zc_chess_puct_backup(zc_engine *eng, int32_t first, int32_t n, int32_t flush
     p.values = d_values;
     p.logits = d_logits;
     p.logits_f16 = logits_dtype == ZC_F16;
+    p.leaf_rows = rows_per_game;
     zc::launch_chess_puct_backup(p, (hipStream_t)hip_stream);
     ZC_HIP(hipGetLastError());
     return ZC_OK;
+}
+
+int zc_chess_puct_backup(zc_engine *eng, int32_t first, int32_t n, int32_t flush, const double *d_values,
+                         const void *d_logits, int32_t logits_dtype, void *hip_stream) {
+    return zc_chess_puct_backup_ex(eng, first, n, flush, d_values, d_logits, logits_dtype, 0, hip_stream);
 }
 
 int zc_chess_puct_end(zc_engine *eng, int32_t first, int32_t n, float temperature, uint16_t *d_move, int32_t *d_na,
@@ -1338,10 +1346,12 @@ int zc_c4_puct_select(zc_engine *eng, int32_t first, int32_t n, int32_t flush, z
     return ZC_OK;
 }
 
-int zc_c4_puct_backup(zc_engine *eng, int32_t first, int32_t n, int32_t flush, const double *d_values,
-                      const void *d_logits, int32_t logits_dtype, void *hip_stream) {
+int zc_c4_puct_backup_ex(zc_engine *eng, int32_t first, int32_t n, int32_t flush, const double *d_values,
+                         const void *d_logits, int32_t logits_dtype, int32_t rows_per_game, void *hip_stream) {
     if (!eng || (n && (!d_values || !d_logits))) return fail(ZC_EINVAL, "null argument");
     if (logits_dtype != ZC_F32 && logits_dtype != ZC_F16) return fail(ZC_EINVAL, "logits_dtype must be ZC_F32 or ZC_F16");
+    if (rows_per_game < 0 || (rows_per_game > 0 && flush != 0))
+        return fail(ZC_EINVAL, "rows_per_game must be 0 (batch_size rows), or >= 1 for flush 0 (the roots)");
     std::lock_guard<std::mutex> lk(eng->mu);
     if (int r = check_qx(eng, first, n, flush, true)) return r;
     if (!n) return ZC_OK;
@@ -1351,9 +1361,15 @@ int zc_c4_puct_backup(zc_engine *eng, int32_t first, int32_t n, int32_t flush, c
     p.values = d_values;
     p.logits = d_logits;
     p.logits_f16 = logits_dtype == ZC_F16;
+    p.leaf_rows = rows_per_game;
     zc::launch_c4_puct_backup(p, (hipStream_t)hip_stream);
     ZC_HIP(hipGetLastError());
     return ZC_OK;
+}
+
+int zc_c4_puct_backup(zc_engine *eng, int32_t first, int32_t n, int32_t flush, const double *d_values,
+                      const void *d_logits, int32_t logits_dtype, void *hip_stream) {
+    return zc_c4_puct_backup_ex(eng, first, n, flush, d_values, d_logits, logits_dtype, 0, hip_stream);
 }
 
 int zc_c4_puct_end(zc_engine *eng, int32_t first, int32_t n, float temperature, int32_t *d_move, int32_t *d_na,

@@ -187,6 +187,7 @@ struct ChessParams {
     float temperature;          // end: 0 = most visits, > 0 = sample proportional to Na^(1/T)
     const void *logits;         // backup: [n*bs][4096] policy logits (from*64 + to)
     int logits_f16;
+    int leaf_rows;              // backup: rows of values / logits per game (0: bs; 1: a roots-only flush)
     float *out_prior;           // end (optional): root priors after noise [n][ZC_CHESS_MAX_MOVES]
     // host-policy search (zc_chess_hp_*): leaf index in the flush, untried index, walk output
     int hp_leaf, hp_index;
@@ -239,6 +240,7 @@ struct C4PuctParams {
     const double *values;
     const void *logits;       // backup: [n*bs][7] column logits
     int logits_f16;
+    int leaf_rows;            // backup: rows of values / logits per game (0: bs; 1: a roots-only flush)
     float dir_alpha, dir_eps;
     uint64_t seed;
     int32_t *search_no;       // [n] per-game search number (counter word; end adds 1), or null

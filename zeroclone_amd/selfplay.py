@@ -228,16 +228,17 @@ def _room(traj):
 
 
 def _warm(search, fn, sims: int):
-    """Each part's network once on its own slice of the search's buffers, and once at the
-    short last flush's shape (NetValue.rows) when the simulations are not a multiple of the
-    batch: kernels loaded and buffers allocated before a graph capture."""
+    """Each part's network once on its own slice of the search's buffers (and at a PolicyNet's
+    roots shape: valued._warm_parts), and once at the short last flush's shape
+    (NetValue.rows) when the simulations are not a multiple of the batch: kernels loaded and
+    buffers allocated before a graph capture."""
     from .valued import _warm_parts
     fns = list(fn) if isinstance(fn, (list, tuple)) else [fn]
     _warm_parts(search, fns)
     nb, k, n, bs = sims % search.bs, len(fns), search.n, search.bs
     for i, f in enumerate(fns):
+        lo, hi = i * n // k, (i + 1) * n // k
         if nb and hasattr(f, "rows"):
-            lo, hi = i * n // k, (i + 1) * n // k
             f.rows(search.planes[lo * bs:hi * bs], hi - lo, bs, nb, search.values[lo * bs:hi * bs])
 
 
@@ -282,11 +283,11 @@ class C4SelfPlay:
             if streams > 1:   # the games in parts on their own streams (valued._split_flushes)
                 self.value_fn = [NetValue(net.replica() if hasattr(net, "replica") else net) for _ in range(streams)]
         if puct_net is not None:
-            from .valued import C4PuctSearch
+            from .valued import C4PuctSearch, PolicyNet
             self.ps = C4PuctSearch(self.eng, games, batch_size, seed=puct_seed, leaves=False)
-            self.net_fn = lambda leaves, planes, counts: puct_net(planes)
+            self.net_fn = PolicyNet(puct_net)
             if streams > 1:
-                self.net_fn = [(lambda leaves, planes, counts, m=puct_net.replica(): m(planes)) for _ in range(streams)]
+                self.net_fn = [PolicyNet(puct_net.replica()) for _ in range(streams)]
 
     def start(self, quota: int | None = None):
         """Every slot back to the opening; with a quota, slots beyond it idle and finished
@@ -505,12 +506,11 @@ class ChessSelfPlay:
             if streams > 1:   # the games in parts on their own streams (valued._split_flushes)
                 self.value_fn = [NetValue(net.replica() if hasattr(net, "replica") else net) for _ in range(streams)]
         if puct_net is not None:
-            from .valued import ChessPuctSearch
+            from .valued import ChessPuctSearch, PolicyNet
             self.ps = ChessPuctSearch(self.eng, games, batch_size, seed=puct_seed, leaves=False)
-            self.net_fn = lambda leaves, planes, counts: puct_net(planes)
-            if puct_streams > 1:   # the games in parts on their own streams (ChessPuctSearch._enqueue_split)
-                self.net_fn = [(lambda leaves, planes, counts, m=puct_net.replica(): m(planes))
-                               for _ in range(puct_streams)]
+            self.net_fn = PolicyNet(puct_net)
+            if puct_streams > 1:   # the games in parts on their own streams (valued._split_flushes)
+                self.net_fn = [PolicyNet(puct_net.replica()) for _ in range(puct_streams)]
         self.hist_cap = hist_cap  # moves per side
         self.hist = torch.zeros((games, 2, self.hist_cap), dtype=torch.int16, device=self.dev)
         self.hlen = torch.zeros((games, 2), dtype=torch.int32, device=self.dev)

@@ -78,13 +78,49 @@ def _value_backup(sims: int, bs: int, backup):
     return evaluate_backup
 
 
+class PolicyNet:
+    """A policy + value network as a PUCT search's net_fn: net(planes) -> (values fp64 [rows],
+    logits [rows, n_logits]).  It depends on the planes alone, so the search may call it on
+    the n root positions of flush 0 (one leaf a game) instead of all n * batch_size slots."""
+    roots_only = True
+
+    def __init__(self, net):
+        self.net = net
+
+    def __call__(self, leaves, planes, counts):
+        return self.net(planes)
+
+
+def _puct_backup(bs: int, backup):
+    """evaluate_backup of a PUCT search (part): fn on the flush's planes, then backup(first, n,
+    flush, values, logits, logits_f16, stream, rows).  Flush 0 holds the roots only: a
+    roots_only fn evaluates the n root positions alone (rows = 1)."""
+    def evaluate_backup(first, m, f, fn, lv, pv, cv, vv, st):
+        if f == 0 and getattr(fn, "roots_only", False):
+            roots = pv.view(m, bs, *pv.shape[1:])[:, 0].contiguous()
+            v, logits = fn(None, roots, cv)
+            v = v.reshape(-1).to(torch.float64).contiguous()
+            logits = logits.contiguous()
+            backup(first, m, f, v.data_ptr(), logits.data_ptr(), logits.dtype == torch.float16, st, rows=1)
+            return
+        v, logits = fn(lv, pv, cv)
+        if v.data_ptr() != vv.data_ptr():
+            vv.copy_(v.reshape(-1))
+        logits = logits.contiguous()
+        backup(first, m, f, vv.data_ptr(), logits.data_ptr(), logits.dtype == torch.float16, st)
+    return evaluate_backup
+
+
 def _warm_parts(search, fns):
-    """Each part's function once on its own slice (graph capture warms kernels and buffers)."""
+    """Each part's function once on its own slice, and a PolicyNet also at the roots flush's
+    shape (graph capture warms kernels and buffers)."""
     k, n, bs = len(fns), search.n, search.bs
     for i, fn in enumerate(fns):
         lo, hi = i * n // k, (i + 1) * n // k
         fn(search.leaves[lo * bs:hi * bs] if search.leaves is not None else None,
            search.planes[lo * bs:hi * bs] if search.planes is not None else None, search.counts[lo:hi])
+        if getattr(fn, "roots_only", False):
+            fn(None, search.planes[lo * bs:hi * bs:bs].contiguous(), search.counts[lo:hi])
 
 
 class C4ValuedSearch:
@@ -324,15 +360,12 @@ class ChessPuctSearch:
             e.chess_puct_end(first_game, n, temperature, self.move.data_ptr(), self.na.data_ptr(),
                              self.prior.data_ptr(), self.stats.data_ptr(), _stream(self.dev))
             return self.move, self.na, self.stats
+        evaluate_backup = _puct_backup(self.bs, e.chess_puct_backup)
         for f in range(nfl):
             e.chess_puct_select(first_game, n, f, p(self.leaves), p(self.planes),
                                 self.planes.dtype == torch.float16, self.counts.data_ptr(), _stream(self.dev))
-            v, logits = net_fn(self.leaves, self.planes, self.counts)
-            if v is not self.values:
-                self.values.copy_(v.reshape(-1))
-            logits = logits.contiguous()
-            e.chess_puct_backup(first_game, n, f, self.values.data_ptr(), logits.data_ptr(),
-                                logits.dtype == torch.float16, _stream(self.dev))
+            evaluate_backup(first_game, n, f, net_fn, self.leaves, self.planes, self.counts, self.values,
+                            _stream(self.dev))
         e.chess_puct_end(first_game, n, temperature, self.move.data_ptr(), self.na.data_ptr(), self.prior.data_ptr(),
                          self.stats.data_ptr(), _stream(self.dev))
         return self.move, self.na, self.stats
@@ -346,13 +379,7 @@ class ChessPuctSearch:
             e.chess_puct_select(first, n, f, lv.data_ptr() if lv is not None else 0, pv.data_ptr(),
                                 pv.dtype == torch.float16, cv.data_ptr(), s)
 
-        def evaluate_backup(first, n, f, fn, lv, pv, cv, vv, s):
-            v, logits = fn(lv, pv, cv)
-            if v.data_ptr() != vv.data_ptr():
-                vv.copy_(v.reshape(-1))
-            logits = logits.contiguous()
-            e.chess_puct_backup(first, n, f, vv.data_ptr(), logits.data_ptr(), logits.dtype == torch.float16, s)
-        _split_flushes(self, nfl, fns, first_game, select, evaluate_backup)
+        _split_flushes(self, nfl, fns, first_game, select, _puct_backup(self.bs, e.chess_puct_backup))
 
     def run(self, roots, sims, net_fn, temperature: float = 0.0, first_game: int = 0):
         self.enqueue(roots, sims, net_fn, temperature, first_game)
@@ -413,23 +440,14 @@ class C4PuctSearch:
                 e.c4_puct_select(first, m, f, lv.data_ptr() if lv is not None else 0, pv.data_ptr(),
                                  pv.dtype == torch.float16, cv.data_ptr(), s)
 
-            def evaluate_backup(first, m, f, fn, lv, pv, cv, vv, s):
-                v, logits = fn(lv, pv, cv)
-                if v.data_ptr() != vv.data_ptr():
-                    vv.copy_(v.reshape(-1))
-                logits = logits.contiguous()
-                e.c4_puct_backup(first, m, f, vv.data_ptr(), logits.data_ptr(), logits.dtype == torch.float16, s)
-            _split_flushes(self, nfl, list(net_fn), first_game, select, evaluate_backup)
+            _split_flushes(self, nfl, list(net_fn), first_game, select, _puct_backup(self.bs, e.c4_puct_backup))
             nfl = 0
+        evaluate_backup = _puct_backup(self.bs, e.c4_puct_backup)
         for f in range(nfl):
             e.c4_puct_select(first_game, n, f, p(self.leaves), p(self.planes), self.planes.dtype == torch.float16,
                              self.counts.data_ptr(), _stream(self.dev))
-            v, logits = net_fn(self.leaves, self.planes, self.counts)
-            if v is not self.values:
-                self.values.copy_(v.reshape(-1))
-            logits = logits.contiguous()
-            e.c4_puct_backup(first_game, n, f, self.values.data_ptr(), logits.data_ptr(),
-                             logits.dtype == torch.float16, _stream(self.dev))
+            evaluate_backup(first_game, n, f, net_fn, self.leaves, self.planes, self.counts, self.values,
+                            _stream(self.dev))
         e.c4_puct_end(first_game, n, temperature, self.move.data_ptr(), self.na.data_ptr(), self.prior.data_ptr(),
                       self.stats.data_ptr(), _stream(self.dev))
         return self.move, self.na, self.stats
