@@ -85,6 +85,18 @@ void free_arena(zc::Arena &a) {
     a = zc::Arena{};
 }
 
+// search_sync's packed call block per game: inputs (root, game id), outputs (move, the root's
+// visits per column, stats)
+constexpr size_t kIoIn = sizeof(zc_c4_state) + sizeof(int32_t);
+constexpr size_t kIoOut = sizeof(int32_t) * 8 + sizeof(zc_game_stats);
+constexpr size_t kIoBytes = kIoIn + kIoOut;
+
+void free_io(zc_engine *e) {
+    if (e->io_d) (void)hipFree(e->io_d);
+    if (e->io_h) (void)hipHostFree(e->io_h);
+    e->io_d = e->io_h = nullptr;
+}
+
 int check_games(const zc_engine *e, int32_t first, int32_t n) {
     if (first < 0 || n < 0 || (int64_t)first + n > e->cfg.max_games)
         return fail(ZC_ECAPACITY, "games [%d, %d) outside engine capacity %d", first, first + n, e->cfg.max_games);
@@ -211,6 +223,9 @@ int zc_engine_create(const zc_engine_config *cfg, zc_engine **out) {
     if (!rc) rc = dalloc(e, &a.ext_paths, G * (size_t)cfg->max_batch * zc::kMaxDepth);
     if (!rc) rc = dalloc(e, &a.ext_meta, G * (size_t)cfg->max_batch);
     if (!rc) rc = dalloc(e, &a.ext_roots, G);
+    if (!rc) rc = dalloc(e, &e->io_d, G * kIoBytes + 16);
+    if (!rc && hipHostMalloc((void **)&e->io_h, G * kIoBytes + 16, hipHostMallocDefault) != hipSuccess)
+        rc = fail(ZC_ENOMEM, "hipHostMalloc(%zu bytes) failed", G * kIoBytes + 16);
     if (!rc && hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess)
         rc = fail(ZC_EHIP, "hipStreamCreate failed");
     if (!rc) {
@@ -222,6 +237,7 @@ int zc_engine_create(const zc_engine_config *cfg, zc_engine **out) {
     }
     if (rc) {
         free_arena(a);
+        free_io(e);
         if (e->stream) (void)hipStreamDestroy(e->stream);
         delete e;
         return rc;
@@ -240,6 +256,7 @@ int zc_engine_destroy(zc_engine *eng) {
         (void)hipSetDevice(eng->cfg.device);
         (void)hipStreamSynchronize(eng->stream);
         free_arena(eng->a);
+        free_io(eng);
         free_chess(eng->ca);
         free_gen(eng);
         void *c4p[] = {eng->c4p_nodes, eng->c4p_ctl, eng->c4p_paths, eng->c4p_meta};
@@ -414,20 +431,28 @@ int search_sync(zc_engine *eng, int32_t first, int32_t n, const int32_t *ids, co
                 double c, int32_t bs, int32_t *out_move, int32_t *out_na, zc_game_stats *out_stats) {
     std::lock_guard<std::mutex> lk(eng->mu);
     ZC_HIP(hipSetDevice(eng->cfg.device));
-    zc::Arena &a = eng->a;
     hipStream_t s = eng->stream;
-    ZC_HIP(hipMemcpyAsync(a.roots, roots, (size_t)n * sizeof(zc_c4_state), hipMemcpyHostToDevice, s));
-    if (ids) ZC_HIP(hipMemcpyAsync(a.ids, ids, (size_t)n * sizeof(int32_t), hipMemcpyHostToDevice, s));
-    zc::SearchParams p = make_params(eng, first, n, a.roots, sims, c, bs, a.move, a.na, a.stats);
-    p.game_ids = ids ? a.ids : nullptr;
+    // inputs [roots | ids] and outputs [moves | visits (n x 7) | stats] at 16-byte offsets in
+    // one block: one host-to-device and one device-to-host copy, both through pinned memory
+    const size_t rb = (size_t)n * sizeof(zc_c4_state), ib = ids ? (size_t)n * sizeof(int32_t) : 0;
+    const size_t ob = (rb + ib + 15) & ~(size_t)15;
+    const size_t outb = (size_t)n * kIoOut;
+    uint8_t *const hb = eng->io_h, *const db = eng->io_d;
+    memcpy(hb, roots, rb);
+    if (ids) memcpy(hb + rb, ids, ib);
+    ZC_HIP(hipMemcpyAsync(db, hb, rb + ib, hipMemcpyHostToDevice, s));
+    int32_t *const d_move = (int32_t *)(db + ob);
+    zc::SearchParams p = make_params(eng, first, n, (const zc_c4_state *)db, sims, c, bs, d_move, d_move + n,
+                                     (zc_game_stats *)(db + ob + (size_t)n * 32));
+    p.game_ids = ids ? (const int32_t *)(db + rb) : nullptr;
     zc::launch_c4_search(p, s);
     ZC_HIP(hipGetLastError());
-    std::vector<zc_game_stats> st((size_t)n);
-    ZC_HIP(hipMemcpyAsync(out_move, a.move, (size_t)n * sizeof(int32_t), hipMemcpyDeviceToHost, s));
-    ZC_HIP(hipMemcpyAsync(out_na, a.na, (size_t)n * 7 * sizeof(int32_t), hipMemcpyDeviceToHost, s));
-    ZC_HIP(hipMemcpyAsync(st.data(), a.stats, (size_t)n * sizeof(zc_game_stats), hipMemcpyDeviceToHost, s));
+    ZC_HIP(hipMemcpyAsync(hb + ob, db + ob, outb, hipMemcpyDeviceToHost, s));
     ZC_HIP(hipStreamSynchronize(s));
-    if (out_stats) memcpy(out_stats, st.data(), st.size() * sizeof(zc_game_stats));
+    memcpy(out_move, hb + ob, (size_t)n * sizeof(int32_t));
+    memcpy(out_na, hb + ob + (size_t)n * 4, (size_t)n * 7 * sizeof(int32_t));
+    const zc_game_stats *const st = (const zc_game_stats *)(hb + ob + (size_t)n * 32);
+    if (out_stats) memcpy(out_stats, st, (size_t)n * sizeof(zc_game_stats));
     for (int32_t i = 0; i < n; ++i) {
         const int g = ids ? ids[i] : first + i;
         if (st[i].status == ZC_STATUS_NO_MOVES)

@@ -385,6 +385,9 @@ struct zc_engine {
     int M = 0;
     hipStream_t stream = nullptr;
     zc::Arena a;
+    // zc_c4_search / zc_c4_search_games: the call's inputs and outputs packed in one device
+    // block and staged through one pinned host block (one copy each way per call)
+    uint8_t *io_d = nullptr, *io_h = nullptr;
     int64_t bytes = 0;
     int stamp = 0;
     int rollout_mode = 0;        // ZC_ROLLOUT_EXACT / ZC_ROLLOUT_PHILOX
