@@ -2,7 +2,7 @@
 # Runs ON THE GPU BOX (via gpurun): stages given as arguments, in order, each under its own
 # time limit; stops at the first stage that faults / aborts / times out (pytest failures,
 # rc=1, still let later stages run so a bench line is recorded).
-#   stages: pytest smoke bench bench8 prof pmc sel walk wprof whbm wpmc cprof cpmc ...
+#   stages: pytest smoke bench bench8 prof pmc sel walk wprof whbm wpmc cprof cpmc c5prof ...
 set -u
 cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
@@ -64,6 +64,8 @@ for st in "$@"; do
     cpmc)   run cpmc 600 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/cpmc -o pmc \
                 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE \
                 -- python3 tools/bench_chess.py --mode crude --steps 2 || exit $? ;;
+    c5prof) ZC_PUCT_STREAMS=4 run c5prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/c5prof -o run --output-format csv \
+                -- python3 tools/prof_c5.py --mode c5 --steps 3 || exit $? ;;
     ab)     run ab 900 env AB_ROOTS=mixed AB_ROUNDS=${AB_ROUNDS:-3} python tools/ab_search.py ${AB_LIBS} || exit $? ;;
     *) echo "unknown stage $st"; exit 2 ;;
   esac

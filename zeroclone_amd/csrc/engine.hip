@@ -8,6 +8,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <mutex>
 #include <vector>
 
 #include "c4_order_table.h"
@@ -77,24 +78,101 @@ void free_gen(zc_engine *e) {
     g = zc::GenArena{};
 }
 
-void free_arena(zc::Arena &a) {
-    void *ptrs[] = {a.nodes, a.ring,  a.rngpos, a.logtab,  a.phase,    a.roots,    a.move,
-                    a.na,    a.ids,   a.stats, a.ext_ctl, a.ext_paths, a.ext_meta, a.ext_roots};
-    for (void *p : ptrs)
-        if (p) (void)hipFree(p);
-    a = zc::Arena{};
-}
-
+// The Connect4 arena and the synchronous calls' IO block are carved from ONE device
+// allocation (base == nullptr: the offsets only, for the size), at 256-byte offsets: an
+// engine's creation and destruction cost one hipMalloc / hipFree, not sixteen (a hipFree of a
+// megabyte-sized block takes ~0.1 ms on this stack).
 // search_sync's packed call block per game: inputs (root, game id), outputs (move, the root's
 // visits per column, stats)
 constexpr size_t kIoIn = sizeof(zc_c4_state) + sizeof(int32_t);
 constexpr size_t kIoOut = sizeof(int32_t) * 8 + sizeof(zc_game_stats);
 constexpr size_t kIoBytes = kIoIn + kIoOut;
 
-void free_io(zc_engine *e) {
-    if (e->io_d) (void)hipFree(e->io_d);
-    if (e->io_h) (void)hipHostFree(e->io_h);
-    e->io_d = e->io_h = nullptr;
+template <class T>
+void carve(uint8_t *base, size_t &off, T **p, size_t count) {
+    off = (off + 255) & ~(size_t)255;
+    *p = base ? (T *)(base + off) : nullptr;
+    off += (count ? count : 1) * sizeof(T);
+}
+
+size_t carve_arena(zc_engine *e, uint8_t *base) {
+    zc::Arena &a = e->a;
+    const size_t G = (size_t)e->cfg.max_games, M = (size_t)e->M, B = (size_t)e->cfg.max_batch;
+    size_t off = 0;
+    carve(base, off, &a.nodes, G * M * zc::kRecBytes);
+    carve(base, off, &a.ring, G * zc::kRingWords);
+    carve(base, off, &a.rngpos, G * 2);
+    carve(base, off, &a.logtab, M + 2);
+    carve(base, off, &a.phase, G * zc::kPhases);
+    carve(base, off, &a.roots, G);
+    carve(base, off, &a.move, G);
+    carve(base, off, &a.na, G * 7);
+    carve(base, off, &a.ids, G);
+    carve(base, off, &a.stats, G);
+    carve(base, off, &a.ext_ctl, G * zc::kCtlWords);
+    carve(base, off, &a.ext_paths, G * B * zc::kMaxDepth);
+    carve(base, off, &a.ext_meta, G * B);
+    carve(base, off, &a.ext_roots, G);
+    carve(base, off, &e->io_d, G * kIoBytes + 16);
+    return off;
+}
+
+// Streams and pinned host blocks outlive their engines in per-process pools: creating a HIP
+// stream costs milliseconds on this stack (a hardware queue), and an engine per game (the
+// reference's Engine per game) would pay it every game.
+std::mutex g_pool_mu;
+std::vector<std::pair<int, hipStream_t>> g_streams;      // (device, idle stream)
+std::vector<std::pair<size_t, uint8_t *>> g_pinned;      // (bytes, idle pinned block)
+
+hipStream_t take_stream(int dev) {
+    {
+        std::lock_guard<std::mutex> lk(g_pool_mu);
+        for (size_t i = 0; i < g_streams.size(); ++i)
+            if (g_streams[i].first == dev) {
+                hipStream_t s = g_streams[i].second;
+                g_streams.erase(g_streams.begin() + (long)i);
+                return s;
+            }
+    }
+    hipStream_t s = nullptr;
+    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return nullptr;
+    return s;
+}
+
+void give_stream(int dev, hipStream_t s) {  // s is idle (synchronised)
+    if (!s) return;
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    g_streams.emplace_back(dev, s);
+}
+
+uint8_t *take_pinned(size_t bytes) {
+    {
+        std::lock_guard<std::mutex> lk(g_pool_mu);
+        for (size_t i = 0; i < g_pinned.size(); ++i)
+            if (g_pinned[i].first >= bytes) {
+                uint8_t *p = g_pinned[i].second;
+                g_pinned.erase(g_pinned.begin() + (long)i);
+                return p;
+            }
+    }
+    void *p = nullptr;
+    if (hipHostMalloc(&p, bytes, hipHostMallocDefault) != hipSuccess) return nullptr;
+    return (uint8_t *)p;
+}
+
+void give_pinned(size_t bytes, uint8_t *p) {
+    if (!p) return;
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    g_pinned.emplace_back(bytes, p);
+}
+
+void free_arena(zc_engine *e) {
+    if (e->a_block) (void)hipFree(e->a_block);
+    e->a_block = nullptr;
+    e->a = zc::Arena{};
+    e->io_d = nullptr;
+    give_pinned(e->io_h_bytes, e->io_h);
+    e->io_h = nullptr;
 }
 
 int check_games(const zc_engine *e, int32_t first, int32_t n) {
@@ -207,38 +285,36 @@ int zc_engine_create(const zc_engine_config *cfg, zc_engine **out) {
     const size_t G = (size_t)cfg->max_games, M = (size_t)e->M;
     zc::Arena &a = e->a;
     int rc = ZC_OK;
-    if (!rc) rc = dalloc(e, &a.nodes, G * M * zc::kRecBytes);
-    if (!rc) rc = dalloc(e, &a.ring, G * zc::kRingWords);
-    if (!rc) rc = dalloc(e, &a.rngpos, G * 2);
-    if (!rc) rc = dalloc(e, &a.logtab, M + 2);
-    if (!rc) rc = dalloc(e, &a.phase, G * zc::kPhases);
-    if (!rc && hipMemset(a.phase, 0, G * zc::kPhases * sizeof(int64_t)) != hipSuccess) rc = fail(ZC_EHIP, "memset failed");
-    if (!rc) rc = dalloc(e, &a.roots, G);
-    if (!rc) rc = dalloc(e, &a.move, G);
-    if (!rc) rc = dalloc(e, &a.na, G * 7);
-    if (!rc) rc = dalloc(e, &a.ids, G);
-    if (!rc) rc = dalloc(e, &a.stats, G);
-    if (!rc) rc = dalloc(e, &a.ext_ctl, G * zc::kCtlWords);
-    if (!rc && hipMemset(a.ext_ctl, 0, G * zc::kCtlWords * sizeof(int32_t)) != hipSuccess) rc = fail(ZC_EHIP, "memset failed");
-    if (!rc) rc = dalloc(e, &a.ext_paths, G * (size_t)cfg->max_batch * zc::kMaxDepth);
-    if (!rc) rc = dalloc(e, &a.ext_meta, G * (size_t)cfg->max_batch);
-    if (!rc) rc = dalloc(e, &a.ext_roots, G);
-    if (!rc) rc = dalloc(e, &e->io_d, G * kIoBytes + 16);
-    if (!rc && hipHostMalloc((void **)&e->io_h, G * kIoBytes + 16, hipHostMallocDefault) != hipSuccess)
-        rc = fail(ZC_ENOMEM, "hipHostMalloc(%zu bytes) failed", G * kIoBytes + 16);
-    if (!rc && hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess)
-        rc = fail(ZC_EHIP, "hipStreamCreate failed");
+    const size_t block = carve_arena(e, nullptr);
+    if (hipMalloc(&e->a_block, block) != hipSuccess) {
+        e->a_block = nullptr;
+        rc = fail(ZC_ENOMEM, "hipMalloc(%zu bytes) failed", block);
+    } else {
+        e->bytes += (int64_t)block;
+        carve_arena(e, (uint8_t *)e->a_block);
+    }
+    if (!rc) {
+        e->io_h_bytes = G * kIoBytes + 16;
+        e->io_h = take_pinned(e->io_h_bytes);
+        if (!e->io_h) rc = fail(ZC_ENOMEM, "hipHostMalloc(%zu bytes) failed", e->io_h_bytes);
+    }
+    if (!rc && !(e->stream = take_stream(cfg->device))) rc = fail(ZC_EHIP, "hipStreamCreate failed");
+    if (!rc && (hipMemsetAsync(a.phase, 0, G * zc::kPhases * sizeof(int64_t), e->stream) != hipSuccess ||
+                hipMemsetAsync(a.ext_ctl, 0, G * zc::kCtlWords * sizeof(int32_t), e->stream) != hipSuccess))
+        rc = fail(ZC_EHIP, "memset failed");
     if (!rc) {
         // log(N) exactly as the reference gets it: glibc log on the host (mcts.cpp:44).
         std::vector<double> lg(M + 2);
         for (size_t n = 0; n < M + 2; ++n) lg[n] = log((double)n);
-        if (hipMemcpy(a.logtab, lg.data(), lg.size() * sizeof(double), hipMemcpyHostToDevice) != hipSuccess)
+        if (hipMemcpyAsync(a.logtab, lg.data(), lg.size() * sizeof(double), hipMemcpyHostToDevice, e->stream) !=
+                hipSuccess ||
+            hipStreamSynchronize(e->stream) != hipSuccess)
             rc = fail(ZC_EHIP, "logtab upload failed");
     }
     if (rc) {
-        free_arena(a);
-        free_io(e);
-        if (e->stream) (void)hipStreamDestroy(e->stream);
+        (void)hipDeviceSynchronize();
+        free_arena(e);
+        give_stream(cfg->device, e->stream);
         delete e;
         return rc;
     }
@@ -255,14 +331,13 @@ int zc_engine_destroy(zc_engine *eng) {
         std::lock_guard<std::mutex> lk(eng->mu);
         (void)hipSetDevice(eng->cfg.device);
         (void)hipStreamSynchronize(eng->stream);
-        free_arena(eng->a);
-        free_io(eng);
+        free_arena(eng);
         free_chess(eng->ca);
         free_gen(eng);
         void *c4p[] = {eng->c4p_nodes, eng->c4p_ctl, eng->c4p_paths, eng->c4p_meta};
         for (void *q : c4p)
             if (q) (void)hipFree(q);
-        (void)hipStreamDestroy(eng->stream);
+        give_stream(eng->cfg.device, eng->stream);
     }
     delete eng;
     return ZC_OK;

@@ -388,6 +388,8 @@ struct zc_engine {
     // zc_c4_search / zc_c4_search_games: the call's inputs and outputs packed in one device
     // block and staged through one pinned host block (one copy each way per call)
     uint8_t *io_d = nullptr, *io_h = nullptr;
+    size_t io_h_bytes = 0;
+    void *a_block = nullptr;  // the one device allocation `a` and io_d are carved from
     int64_t bytes = 0;
     int stamp = 0;
     int rollout_mode = 0;        // ZC_ROLLOUT_EXACT / ZC_ROLLOUT_PHILOX
