@@ -833,6 +833,53 @@ __device__ __forceinline__ void tower_epilogue16(_Float16 *dst, const float4 (&b
     }
 }
 
+// tower_epilogue16 with the residual layer's reads issued together (one wait for all 16
+// instead of a read-wait-add chain per 4 channels), no per-tile branch when the tile is full
+// and the residual switch resolved per layer (RES): the same per-element arithmetic.
+template <int NN, bool RES, bool CHECK>
+__device__ __forceinline__ void tower_epilogue16_batch(_Float16 *dst, const float4 (&bv)[2], int npix, int wave,
+                                                       int l16, int q, const f4x (&acc)[2][NN]) {
+    constexpr int LD = tower_ld<16>();
+    _Float16 *const base = dst + l16 * LD + wave * 32 + 4 * q;
+    h4 rv[2][NN];
+    if constexpr (RES) {
+#pragma unroll
+        for (int n = 0; n < NN; ++n) {
+            const int P = CHECK ? min(n * 16 + l16, npix - 1) - l16 : n * 16;  // a valid row to read
+#pragma unroll
+            for (int m = 0; m < 2; ++m) rv[m][n] = *(const h4 *)(base + P * LD + 16 * m);
+        }
+    }
+#pragma unroll
+    for (int n = 0; n < NN; ++n) {
+#pragma unroll
+        for (int m = 0; m < 2; ++m) {
+            float v[4] = {acc[m][n][0] + bv[m].x, acc[m][n][1] + bv[m].y, acc[m][n][2] + bv[m].z,
+                          acc[m][n][3] + bv[m].w};
+            if constexpr (RES) {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) v[e] += (float)rv[m][n][e];
+            }
+            h4 ov;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) ov[e] = (_Float16)fmaxf(v[e], 0.0f);
+            if (!CHECK || n * 16 + l16 < npix) *(h4 *)(base + n * 16 * LD + 16 * m) = ov;
+        }
+    }
+}
+
+template <int NN>
+__device__ __forceinline__ void tower_epilogue16b(_Float16 *dst, const float4 (&bv)[2], bool res, int npix, int wave,
+                                                  int l16, int q, const f4x (&acc)[2][NN]) {
+    if (npix >= NN * 16) {
+        if (res) tower_epilogue16_batch<NN, true, false>(dst, bv, npix, wave, l16, q, acc);
+        else tower_epilogue16_batch<NN, false, false>(dst, bv, npix, wave, l16, q, acc);
+    } else {
+        if (res) tower_epilogue16_batch<NN, true, true>(dst, bv, npix, wave, l16, q, acc);
+        else tower_epilogue16_batch<NN, false, true>(dst, bv, npix, wave, l16, q, acc);
+    }
+}
+
 // tower_epilogue16 with whole 16-byte stores: the per-element arithmetic in the MFMA layout
 // (residual read per 4 channels, as there), then one v_permlane16_swap per dword hands lane
 // (pixel, q) the 8 consecutive channels wave * 32 + 16 (q & 1) + 8 (q >> 1) .. + 7 of its
@@ -967,8 +1014,10 @@ __global__ __launch_bounds__(256 * PG) __attribute__((amdgpu_waves_per_eu(WPE, W
             tower_mfma16<H, W, NP, KC, 8, LD, tower_zero<NT>(), ZR>(lds, src, wa, wn, a, l16, py16, q4, acc);
             if constexpr (EPI == 1)
                 tower_epilogue16_swap<NP>(lds + dst * LD, bv, l >= 2 && !(l & 1), npix, wave, l16, q4, acc);
-            else
+            else if constexpr (EPI == 2)
                 tower_epilogue16<NP>(lds + dst * LD, bv, l >= 2 && !(l & 1), npix, wave, l16, q4, acc);
+            else
+                tower_epilogue16b<NP>(lds + dst * LD, bv, l >= 2 && !(l & 1), npix, wave, l16, q4, acc);
         } else {
             int pr[NT], py[NT];
 #pragma unroll
@@ -1063,9 +1112,10 @@ __global__ __launch_bounds__(256 * PG) __attribute__((amdgpu_waves_per_eu(WPE, W
     }
 }
 
-int tower_epi() {  // ZC_TOWER_EPI=1: the 16x16x32 form's epilogue with 16-byte stores (A/B switch)
+int tower_epi() {  // A/B switch, ZC_TOWER_EPI: 1 = the 16x16x32 form's epilogue with 16-byte stores,
+                  // 2 = the per-tile read-wait-add epilogue (before the batched one)
     const char *e = getenv("ZC_TOWER_EPI");
-    return e && !strcmp(e, "1") ? 1 : 0;
+    return e && !strcmp(e, "1") ? 1 : e && !strcmp(e, "2") ? 2 : 0;
 }
 
 template <int H, int W, int BPH, int NT, int WPE, int PG = 1, int MF = 32>
@@ -1074,6 +1124,12 @@ void launch_tower(int n, int nconv, const void *in, const void *wall, const floa
     if constexpr (MF == 16) {
         if (tower_epi() == 1) {
             hipLaunchKernelGGL((tower_kernel<H, W, BPH, 32, NT, WPE, PG, MF, 1>), dim3((n + BPH - 1) / BPH),
+                               dim3(256 * PG), (tower_lds<NT, PG, MF>()), s, n, nconv, (const _Float16 *)in,
+                               (const _Float16 *)wall, ball, (_Float16 *)out, fcw, fcb, values, pol);
+            return;
+        }
+        if (tower_epi() == 2) {
+            hipLaunchKernelGGL((tower_kernel<H, W, BPH, 32, NT, WPE, PG, MF, 2>), dim3((n + BPH - 1) / BPH),
                                dim3(256 * PG), (tower_lds<NT, PG, MF>()), s, n, nconv, (const _Float16 *)in,
                                (const _Float16 *)wall, ball, (_Float16 *)out, fcw, fcb, values, pol);
             return;
