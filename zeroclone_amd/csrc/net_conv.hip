@@ -891,6 +891,14 @@ __device__ __forceinline__ void tower_epilogue16_swap(_Float16 *dst, const float
                                                       int wave, int l16, int q, const f4x (&acc)[2][NN]) {
     constexpr int LD = tower_ld<16>();
     const int co8 = wave * 32 + 16 * (q & 1) + 8 * (q >> 1);
+    h4 rv[2][NN];  // the residual, every read issued before the first use
+    if (res) {
+#pragma unroll
+        for (int n = 0; n < NN; ++n)
+#pragma unroll
+            for (int m = 0; m < 2; ++m)
+                rv[m][n] = *(const h4 *)(dst + min(n * 16 + l16, npix - 1) * LD + wave * 32 + 16 * m + 4 * q);
+    }
 #pragma unroll
     for (int n = 0; n < NN; ++n) {
         const int P = n * 16 + l16;
@@ -900,9 +908,8 @@ __device__ __forceinline__ void tower_epilogue16_swap(_Float16 *dst, const float
             float v[4] = {acc[m][n][0] + bv[m].x, acc[m][n][1] + bv[m].y, acc[m][n][2] + bv[m].z,
                           acc[m][n][3] + bv[m].w};
             if (res) {
-                const h4 rv = *(const h4 *)(dst + P * LD + wave * 32 + 16 * m + 4 * q);
 #pragma unroll
-                for (int e = 0; e < 4; ++e) v[e] += (float)rv[e];
+                for (int e = 0; e < 4; ++e) v[e] += (float)rv[m][n][e];
             }
             h4 ov;
 #pragma unroll
