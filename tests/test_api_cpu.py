@@ -21,6 +21,28 @@ def test_c4_backend_matches_reference_fixtures(golden):
         assert "".join("1" if v else "0" for v in t[1].ravel()) == c["opp"]
 
 
+def _four_scan(board, tok):
+    """The reference's check_win scans (engine/games/connect4/c4_backend.py), cell by cell."""
+    R, C = 6, 7
+    lines = [[(r, c + i) for i in range(4)] for r in range(R) for c in range(C - 3)]
+    lines += [[(r + i, c) for i in range(4)] for c in range(C) for r in range(R - 3)]
+    lines += [[(r + i, c + i) for i in range(4)] for r in range(R - 3) for c in range(C - 3)]
+    lines += [[(r - i, c + i) for i in range(4)] for r in range(3, R) for c in range(C - 3)]
+    return any(all(board[y][x] == tok for y, x in ln) for ln in lines)
+
+
+def test_bitboard_check_win_equals_the_reference_scans():
+    """c4_backend._four tests all four directions on a bitboard; on random boards (any mix of
+    cells, not only reachable positions, and foreign cell values) it equals the scans."""
+    rng = np.random.default_rng(5)
+    for k in range(4000):
+        p = rng.uniform(0.2, 0.8)
+        cells = rng.choice(["X", "O", " ", "?"], size=(6, 7), p=[p / 2, p / 2, 1 - p - 0.02, 0.02])
+        board = [list(row) for row in cells]
+        for tok in ("X", "O"):
+            assert c4._four(board, tok) == _four_scan(board, tok), (k, tok)
+
+
 def test_bitboard_conversion_matches_c_abi(golden):
     from zeroclone_amd import _native
     for c in golden("c4_backend.json")["cases"][:80]:

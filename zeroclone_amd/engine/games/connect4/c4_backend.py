@@ -37,22 +37,19 @@ def play_move(state, move):
 
 
 def _four(board, tok):
+    """Four cells == tok in a row, column or diagonal (the reference's four scans), as one
+    bitboard test: cell (r, c) -> bit 7 c + 5 - r, a zero sentinel bit on top of each column."""
+    b = 0
     for r in range(ROWS):
-        for c in range(COLS - 3):
-            if board[r][c] == tok and board[r][c + 1] == tok and board[r][c + 2] == tok and board[r][c + 3] == tok:
-                return True
-    for c in range(COLS):
-        for r in range(ROWS - 3):
-            if board[r][c] == tok and board[r + 1][c] == tok and board[r + 2][c] == tok and board[r + 3][c] == tok:
-                return True
-    for r in range(ROWS - 3):
-        for c in range(COLS - 3):
-            if all(board[r + i][c + i] == tok for i in range(4)):
-                return True
-    for r in range(3, ROWS):
-        for c in range(COLS - 3):
-            if all(board[r - i][c + i] == tok for i in range(4)):
-                return True
+        row = board[r]
+        sh = 5 - r
+        for c in range(COLS):
+            if row[c] == tok:
+                b |= 1 << (7 * c + sh)
+    for d in (1, 7, 6, 8):  # vertical, horizontal, the two diagonals
+        m = b & (b >> d)
+        if m & (m >> (2 * d)):
+            return True
     return False
 
 
