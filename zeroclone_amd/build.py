@@ -40,7 +40,8 @@ FLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math", "-
 # profiles/r03_ab_sched.log; max-memory-clause and iterative-maxocc were 0.9 % slower).  Only
 # there: ROCm 7.2's clang crashes in register allocation with it on chess_search.hip.  The
 # network tower (net_conv.hip) too: 6x7 x 131072 18.85 -> 18.66 ms, 8x8 x 32768 equal, outputs
-# identical (profiles/r05_ab_tower_sched.log; max-ilp: no gain).
+# identical (profiles/r05_ab_tower_sched.log; max-ilp: no gain).  chess_search.hip under
+# max-ilp or iterative-maxocc: equal to the default (profiles/r05_ab_chess_sched.log).
 SOURCE_FLAGS = {"c4_search.hip": ["-mllvm", "-amdgpu-sched-strategy=iterative-ilp"],
                 "net_conv.hip": ["-mllvm", "-amdgpu-sched-strategy=iterative-ilp"]}
 
