@@ -62,6 +62,10 @@ const char *zc_version(void);
 const char *zc_last_error(void);
 int zc_device_count(int32_t *count);
 
+/* An engine: its games' arena in ONE device allocation, a HIP stream and a pinned staging block
+ * for the synchronous calls.  Streams and pinned blocks are taken from / returned to per-process
+ * pools (creating a HIP stream costs milliseconds), so they outlive a destroyed engine until the
+ * process exits.  Every game starts as random.seed(game index). */
 int zc_engine_create(const zc_engine_config *cfg, zc_engine **out);
 int zc_engine_destroy(zc_engine *eng);
 /* Device bytes held by the engine. */
