@@ -922,10 +922,10 @@ def tower_mode(dev, reps: int = 5) -> dict:
     flop = flops_per_position(128, 8, 32, 8, 8) * n
     out = {"boards": n, "board": "8x8", "net": "ValueNetwork(128, 8), fp16, BN folded",
            "form": "fused: 16x16x32 MFMA form (the default); fused_32x32x16: the round-3 form (ZC_TOWER_MF=32)"}
-    saved = os.environ.pop("ZC_TOWER_MF", None)
-    for key, fused, mf in (("fused", True, None), ("fused_32x32x16", True, "32"), ("layered", False, None)):
-        if mf:
-            os.environ["ZC_TOWER_MF"] = mf
+    from zeroclone_amd import _native
+    saved = _native.net_switch("tower_mf", 0)
+    for key, fused, mf in (("fused", True, 0), ("fused_32x32x16", True, 32), ("layered", False, 0)):
+        _native.net_switch("tower_mf", mf)
         net.tower(x, fused=fused)
         ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
         torch.cuda.synchronize(dev)
@@ -934,12 +934,10 @@ def tower_mode(dev, reps: int = 5) -> dict:
             net.tower(x, fused=fused)
         ev[1].record()
         torch.cuda.synchronize(dev)
-        os.environ.pop("ZC_TOWER_MF", None)
         ms = ev[0].elapsed_time(ev[1]) / reps
         out[key] = {"ms": round(ms, 3), "tflops": round(flop / ms / 1e9, 1),
                     "frac_of_2p5PF": round(flop / ms / 1e9 / MFMA_F16_PEAK_TFLOPS, 4)}
-    if saved is not None:
-        os.environ["ZC_TOWER_MF"] = saved
+    _native.net_switch("tower_mf", saved)
     out["pmc"] = "profiles/r05_tower_pmc.json (MFMA busy, held clock)"
     return out
 

@@ -703,6 +703,14 @@ int zc_debug_phase_cycles(zc_engine *eng, int32_t enable, int64_t *out8);
 /* The same stamps per game (no reset): out[g * 8 + k] for games 0 .. n_games-1. */
 int zc_debug_phase_cycles_games(zc_engine *eng, int32_t n_games, int64_t *out);
 
+/* The network launches' A/B and test switches (process-wide; read from ZC_TOWER_MF,
+ * ZC_TOWER_EPI, ZC_HEAD_RAW once when the library loads, never per launch): name "tower_mf"
+ * (16 or 32: the fused tower's MFMA form; 0 = default), "tower_epi" (0 default, 1 the 16-byte
+ * store epilogue, 2 the per-tile epilogue), "head_raw" (1: the value head returns its pre-tanh
+ * sum — tests only).  Returns the previous value in *old (may be NULL); ZC_EINVAL for an
+ * unknown name or value. */
+int zc_debug_net_switch(const char *name, int32_t value, int32_t *old);
+
 #ifdef __cplusplus
 }
 #endif

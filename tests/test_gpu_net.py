@@ -5,6 +5,21 @@ import numpy as np
 import pytest
 import torch
 
+
+@pytest.fixture
+def net_sw():
+    """Set the network launches' switches (zc_debug_net_switch) for one test; restored after."""
+    from zeroclone_amd import _native
+    saved = {}
+
+    def set_(name, value):
+        old = _native.net_switch(name, value)
+        saved.setdefault(name, old)
+    yield set_
+    for name, old in saved.items():
+        _native.net_switch(name, old)
+
+
 pytestmark = pytest.mark.gpu
 
 
@@ -62,12 +77,12 @@ def test_mfma_network_matches_torch(shape, n):
 
 
 @pytest.mark.parametrize("mf", ["32", "16"])
-def test_single_conv_layer_exactness(mf, monkeypatch):
+def test_single_conv_layer_exactness(mf, net_sw):
     """One conv layer with small-integer data is exact in fp32 accumulation: checks the
     MFMA operand/accumulator layouts, the tap shifts and the board edges bit for bit (the
     packed form in both MFMA forms)."""
     from zeroclone_amd import _native
-    monkeypatch.setenv("ZC_TOWER_MF", mf)
+    net_sw("tower_mf", int(mf))
     L = _native.lib()
     for (h, w, cin) in [(8, 8, 128), (6, 7, 32), (8, 8, 32), (6, 7, 128)]:
         n = 13
@@ -122,17 +137,17 @@ def test_packed_conv_is_bit_identical_to_the_staged_form():
 @pytest.mark.parametrize("mf", ["32", "16", "default"])
 @pytest.mark.parametrize("shape", [(17, 8, 8), (2, 6, 7)])
 @pytest.mark.parametrize("n", [1, 7, 301, 4099])
-def test_fused_tower_is_bit_identical_to_layered(shape, n, mf, monkeypatch):
+def test_fused_tower_is_bit_identical_to_layered(shape, n, mf, net_sw):
     """zc_net_tower_async (the whole tower in one launch, activations on chip) against the
     layer-by-layer packed launches: the tower's output activation bit for bit, ragged last
-    tiles included — in both MFMA forms (ZC_TOWER_MF selects the form of both launches), and
-    in the default pairing (ZC_TOWER_MF unset: the fused tower on 16x16x32, the layered
+    tiles included — in both MFMA forms (the "tower_mf" switch selects the form of both launches), and
+    in the default pairing ("tower_mf" 0: the fused tower on 16x16x32, the layered
     launches on 32x32x16)."""
     from zeroclone_amd.nets import MfmaValueNetwork
     if mf == "default":
-        monkeypatch.delenv("ZC_TOWER_MF", raising=False)
+        net_sw("tower_mf", 0)
     else:
-        monkeypatch.setenv("ZC_TOWER_MF", mf)
+        net_sw("tower_mf", int(mf))
     c, h, w = shape
     net = MfmaValueNetwork(_net(c, seed=100 + n))
     x = (torch.rand(n, c, h, w, device="cuda") < 0.3).half()
@@ -169,13 +184,13 @@ def _integer_net(c, blocks, seed, density=0.002):
 
 @pytest.mark.parametrize("mf", ["32", "16", "16e"])
 @pytest.mark.parametrize("shape", [(17, 8, 8), (2, 6, 7)])
-def test_tower_forms_exact_on_integers(mf, shape, monkeypatch):
-    """Both MFMA forms of the fused tower (ZC_TOWER_MF: 32x32x16, 16x16x32; "16e": the
-    16x16x32 form with the swap epilogue, ZC_TOWER_EPI=1) on an integer network, 2 residual
+def test_tower_forms_exact_on_integers(mf, shape, net_sw):
+    """Both MFMA forms of the fused tower ("tower_mf": 32x32x16, 16x16x32; "16e": the
+    16x16x32 form with the swap epilogue, "tower_epi" 1) on an integer network, 2 residual
     blocks, ragged board counts: equal to float64 exactly."""
     from zeroclone_amd.nets import FoldedValueNetwork, MfmaValueNetwork
-    monkeypatch.setenv("ZC_TOWER_MF", mf[:2])
-    monkeypatch.setenv("ZC_TOWER_EPI", "1" if mf.endswith("e") else "0")
+    net_sw("tower_mf", int(mf[:2]))
+    net_sw("tower_epi", 1 if mf.endswith("e") else 0)
     c, h, w = shape
     vnet = _integer_net(c, 2, seed=h * 10 + int(mf[:2]))
     net = MfmaValueNetwork(vnet)
@@ -233,15 +248,15 @@ def _integer_head(vnet, hw, seed):
 
 @pytest.mark.parametrize("mf", ["32", "16"])
 @pytest.mark.parametrize("shape", [(17, 8, 8), (2, 6, 7)])
-def test_value_head_exact_on_integers(mf, shape, monkeypatch):
+def test_value_head_exact_on_integers(mf, shape, net_sw):
     """The value head (avg-pool, Linear(128, 1), + bias) on an integer network: its pre-tanh
-    sum (ZC_HEAD_RAW=1) equals float64 exactly, in the fused tower launch and in the layered
+    sum ("head_raw" 1) equals float64 exactly, in the fused tower launch and in the layered
     value_head_kernel, ragged tiles included (on 6x7 too: each lane's sum is a multiple of
     42/64, so the kernel's correctly rounded division by 42 is exact).  With the
     tanh (the product path) the values equal float64 tanh of that sum within tanhf's precision.
     A head without its bias or without its Linear would fail every one of these."""
     from zeroclone_amd.nets import FoldedValueNetwork, MfmaValueNetwork
-    monkeypatch.setenv("ZC_TOWER_MF", mf)
+    net_sw("tower_mf", int(mf))
     c, h, w = shape
     vnet = _integer_head(_integer_net(c, 2, seed=h * 7 + int(mf)), h * w, seed=int(mf) + h)
     xs = [(torch.rand(n, c, h, w) < 0.3).half() for n in (1, 5, 131)]
@@ -264,12 +279,12 @@ def test_value_head_exact_on_integers(mf, shape, monkeypatch):
         assert pre.abs().max().item() < 2 ** 16
         if n > 1:
             assert pre.std().item() > 0
-        monkeypatch.setenv("ZC_HEAD_RAW", "1")
+        net_sw("head_raw", 1)
         for fused in (True, False):
             got = net(x.cuda(), fused=fused).clone()
             torch.cuda.synchronize()
             assert torch.equal(got.cpu(), pre), (mf, shape, n, fused)
-        monkeypatch.setenv("ZC_HEAD_RAW", "0")
+        net_sw("head_raw", 0)
         got = net(x.cuda()).clone()
         torch.cuda.synchronize()
         np.testing.assert_allclose(got.cpu().numpy(), np.tanh(pre.numpy()), rtol=0, atol=1e-6)

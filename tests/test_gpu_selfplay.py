@@ -129,6 +129,33 @@ def test_simulate_games_quota():
     sp.close()
 
 
+def test_quota_steps_on_a_side_stream_grow_the_pool_in_order():
+    """step(stream=s) under a quota with a pool too small for it: the pool grows between
+    steps (ensure_room) on s itself, so the growth reads the counts after the previous
+    step's record kernel and copies the pool before the next one writes — no game is dropped
+    or corrupted, every game is the oracle's game for its slot."""
+    G, sims, seed, total = 12, 24, 41, 20
+    sp = C4SelfPlay(G, sims, seed=seed, games_cap=2)   # 2 x 43 positions: must grow on the way
+    side = torch.cuda.Stream(sp.dev)
+    side.wait_stream(torch.cuda.current_stream(sp.dev))
+    sp.start(total)
+    cap0 = sp.traj.pool_cap
+    for _ in range(200):   # no host synchronisation between the steps
+        sp.step(stream=side.cuda_stream)
+    side.synchronize()
+    assert sp.traj.pool_cap > cap0
+    games = sp.finished_games()
+    assert len(games) == total
+    per_slot = {}
+    for gid, moves, r, pos in games:
+        assert pos.shape[0] == len(moves) + 1
+        assert np.array_equal((pos[:, 2] >> 32).astype(np.float32), dataset_labels(len(pos), r))
+        per_slot.setdefault(gid, []).append((moves, r))
+    for slot, got in per_slot.items():
+        assert got == oracle_games(seed + slot, len(got), sims), slot
+    sp.close()
+
+
 def test_record_labels_and_take_positions():
     """Pooled labels are Engine.get_dataset's (engine.py:60-89) and take_positions carries
     them in the high half of column 2, on the device."""

@@ -13,6 +13,7 @@ import torch
 
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
 from zeroclone_amd.nets import FoldedValueNetwork, MfmaValueNetwork, ValueNetwork, flops_per_position  # noqa: E402
+from zeroclone_amd import _native  # noqa: E402
 
 
 def main():
@@ -33,8 +34,8 @@ def main():
         outs = {}
         for _ in range(rounds):
             for mf in ("32", "16", "16e"):
-                os.environ["ZC_TOWER_MF"] = mf[:2]
-                os.environ["ZC_TOWER_EPI"] = "1" if mf.endswith("e") else "0"
+                _native.net_switch("tower_mf", int(mf[:2]))
+                _native.net_switch("tower_epi", 1 if mf.endswith("e") else 0)
                 a, _ = net.tower(x)
                 torch.cuda.synchronize()
                 outs[mf] = a.clone()
@@ -47,12 +48,12 @@ def main():
                 res[mf].append(e0.elapsed_time(e1) / reps)
         same = {}
         for mf in ("32", "16"):
-            os.environ["ZC_TOWER_MF"] = mf
+            _native.net_switch("tower_mf", int(mf))
             layered, _ = net.tower(x, fused=False)
             torch.cuda.synchronize()
             same[mf] = bool(torch.equal(outs[mf], layered))
-        os.environ.pop("ZC_TOWER_MF", None)
-        os.environ.pop("ZC_TOWER_EPI", None)
+        _native.net_switch("tower_mf", 0)
+        _native.net_switch("tower_epi", 0)
         # torch fp32 reference on 2048 boards (the folded network, NHWC-compared)
         k = 2048
         f = FoldedValueNetwork(vnet).float().cuda()

@@ -282,6 +282,7 @@ SIGNATURES = [
                                          ctypes.c_int32, ctypes.c_void_p]),
     ("zc_debug_phase_cycles", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, P(ctypes.c_int64)]),
     ("zc_debug_phase_cycles_games", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, P(ctypes.c_int64)]),
+    ("zc_debug_net_switch", ctypes.c_int, [ctypes.c_char_p, ctypes.c_int32, P(ctypes.c_int32)]),
     ("zc_debug_c4_rollout", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p,
                                            ctypes.c_void_p, ctypes.c_void_p]),
 ]
@@ -733,3 +734,11 @@ class NativeEngine:
         w = np.zeros(n, np.int64)
         check(lib().zc_debug_c4_rollout(self._h, first_game, n, _ptr(states), _ptr(v), _ptr(w)))
         return v, w
+
+
+def net_switch(name: str, value: int) -> int:
+    """Set one of the network launches' A/B / test switches (zc_debug_net_switch: "tower_mf",
+    "tower_epi", "head_raw"); returns the previous value."""
+    old = ctypes.c_int32(0)
+    check(lib().zc_debug_net_switch(name.encode(), int(value), ctypes.byref(old)))
+    return old.value

@@ -388,7 +388,12 @@ __device__ __forceinline__ int chess_select_flush(const ChessParams &p, const CT
         }
         // the next simulation expands the same node (its untried moves are still cached):
         // take its pick now and let the helper generate its child
-        const bool pair = h != nullptr && rs.cached && j + 1 < nb;
+        // Only where a cannot run out of capacity on nodes or slots: b's sim_front erases b's
+        // move from the node's untried list, which a failing a could not undo, so near the
+        // arena's end the two run one at a time, as the one-wave search does (a position with
+        // more than ZC_CHESS_MAX_MOVES legal moves, the one failure left, is unreachable chess).
+        const bool pair = h != nullptr && rs.cached && j + 1 < nb && nnodes + 2 <= p.M &&
+                          (int64_t)slots + 2 * ZC_CHESS_MAX_MOVES <= t.S;
         Expansion b{};
         const Rng rng_a = rng;  // the stream after a's draw: restored when a ends the flush
         if (pair) {
@@ -409,7 +414,7 @@ __device__ __forceinline__ int chess_select_flush(const ChessParams &p, const CT
         record(ida, a.depth + 1, leaf_path(a));
         if (pair) {
             __syncthreads();  // b's child is generated
-            if (status) {  // a ended the flush (capacity): b never ran, its draw is not consumed
+            if (status) {  // a ended the flush (a list past ZC_CHESS_MAX_MOVES): b's draw is not consumed
                 rng = rng_a;
                 break;
             }

@@ -145,18 +145,24 @@ void give_stream(int dev, hipStream_t s) {  // s is idle (synchronised)
     g_streams.emplace_back(dev, s);
 }
 
-uint8_t *take_pinned(size_t bytes) {
+// *bytes: the size wanted in, the block's real capacity out (the capacity is what the block
+// returns to the pool under).  Best fit: the smallest idle block that is large enough.
+uint8_t *take_pinned(size_t *bytes) {
     {
         std::lock_guard<std::mutex> lk(g_pool_mu);
+        long best = -1;
         for (size_t i = 0; i < g_pinned.size(); ++i)
-            if (g_pinned[i].first >= bytes) {
-                uint8_t *p = g_pinned[i].second;
-                g_pinned.erase(g_pinned.begin() + (long)i);
-                return p;
-            }
+            if (g_pinned[i].first >= *bytes && (best < 0 || g_pinned[i].first < g_pinned[(size_t)best].first))
+                best = (long)i;
+        if (best >= 0) {
+            uint8_t *p = g_pinned[(size_t)best].second;
+            *bytes = g_pinned[(size_t)best].first;
+            g_pinned.erase(g_pinned.begin() + best);
+            return p;
+        }
     }
     void *p = nullptr;
-    if (hipHostMalloc(&p, bytes, hipHostMallocDefault) != hipSuccess) return nullptr;
+    if (hipHostMalloc(&p, *bytes, hipHostMallocDefault) != hipSuccess) return nullptr;
     return (uint8_t *)p;
 }
 
@@ -295,7 +301,7 @@ int zc_engine_create(const zc_engine_config *cfg, zc_engine **out) {
     }
     if (!rc) {
         e->io_h_bytes = G * kIoBytes + 16;
-        e->io_h = take_pinned(e->io_h_bytes);
+        e->io_h = take_pinned(&e->io_h_bytes);
         if (!e->io_h) rc = fail(ZC_ENOMEM, "hipHostMalloc(%zu bytes) failed", e->io_h_bytes);
     }
     if (!rc && !(e->stream = take_stream(cfg->device))) rc = fail(ZC_EHIP, "hipStreamCreate failed");
@@ -516,6 +522,12 @@ int search_sync(zc_engine *eng, int32_t first, int32_t n, const int32_t *ids, co
     memcpy(hb, roots, rb);
     if (ids) memcpy(hb + rb, ids, ib);
     ZC_HIP(hipMemcpyAsync(db, hb, rb + ib, hipMemcpyHostToDevice, s));
+    // from here on the pinned block may be in flight: every return drains the stream first, so
+    // the next call's memcpy into the block cannot race this call's copies
+    struct Drain {
+        hipStream_t s;
+        ~Drain() { (void)hipStreamSynchronize(s); }
+    } drain{s};
     int32_t *const d_move = (int32_t *)(db + ob);
     zc::SearchParams p = make_params(eng, first, n, (const zc_c4_state *)db, sims, c, bs, d_move, d_move + n,
                                      (zc_game_stats *)(db + ob + (size_t)n * 32));
@@ -1795,6 +1807,14 @@ int zc_debug_rng_copy(zc_engine *eng, int32_t first, int32_t n, void *d_buf, int
     const size_t rb = (size_t)n * zc::kRingWords * sizeof(uint32_t), pb = (size_t)n * 2 * sizeof(uint64_t);
     ZC_HIP(hipMemcpyAsync(restore ? ring : b, restore ? b : ring, rb, hipMemcpyDeviceToDevice, s));
     ZC_HIP(hipMemcpyAsync(restore ? pos : b + rb, restore ? b + rb : pos, pb, hipMemcpyDeviceToDevice, s));
+    return ZC_OK;
+}
+
+int zc_debug_net_switch(const char *name, int32_t value, int32_t *old) {
+    int prev = 0;
+    if (!zc::net_switch(name, value, &prev))
+        return fail(ZC_EINVAL, "zc_debug_net_switch: unknown switch or value (%s = %d)", name ? name : "(null)", value);
+    if (old) *old = prev;
     return ZC_OK;
 }
 

@@ -1086,7 +1086,7 @@ __global__ __launch_bounds__(256 * PG) __attribute__((amdgpu_waves_per_eu(WPE, W
             float4 pbv[4];
 #pragma unroll
             for (int g = 0; g < 4; ++g) pbv[g] = *(const float4 *)(pol.pb + 32 * mb + 8 * g + 4 * hh);
-            const float lo = pol.relu ? 0.0f : -INFINITY;
+            const bool relu = pol.relu != 0;
             for (int t = wave; t < NT; t += 4) {
                 const int P = pbase + t * 32 + r;
                 f16x acc;
@@ -1103,7 +1103,10 @@ __global__ __launch_bounds__(256 * PG) __attribute__((amdgpu_waves_per_eu(WPE, W
                         const float bb[4] = {pbv[g].x, pbv[g].y, pbv[g].z, pbv[g].w};
                         h4 ov;
 #pragma unroll
-                        for (int e = 0; e < 4; ++e) ov[e] = (_Float16)fmaxf(acc[4 * g + e] + bb[e], lo);
+                        for (int e = 0; e < 4; ++e) {  // logits (relu = 0): no floor, a NaN stays a NaN
+                            const float y = acc[4 * g + e] + bb[e];
+                            ov[e] = (_Float16)(relu ? fmaxf(y, 0.0f) : y);
+                        }
                         *(h4 *)(pol.out + ((size_t)b0 * HW + P) * nout + 32 * mb + 8 * g + 4 * hh) = ov;
                     }
                 }
@@ -1119,10 +1122,24 @@ __global__ __launch_bounds__(256 * PG) __attribute__((amdgpu_waves_per_eu(WPE, W
     }
 }
 
-int tower_epi() {  // A/B switch, ZC_TOWER_EPI: 1 = the 16x16x32 form's epilogue with 16-byte stores,
+// A/B and test switches of the network launches.  Read from the environment ONCE, when the
+// library loads (ZC_TOWER_MF, ZC_TOWER_EPI, ZC_HEAD_RAW), and changed afterwards only through
+// zc_debug_net_switch — a product process never re-reads the environment per launch.
+struct NetSwitches {
+    int tower_mf, tower_epi, head_raw;
+};
+int env_switch(const char *name, int dflt, int (*parse)(const char *)) {
+    const char *e = getenv(name);
+    return e ? parse(e) : dflt;
+}
+NetSwitches g_net_sw = {
+    env_switch("ZC_TOWER_MF", 0, [](const char *e) { return !strcmp(e, "32") ? 32 : !strcmp(e, "16") ? 16 : 0; }),
+    env_switch("ZC_TOWER_EPI", 0, [](const char *e) { return !strcmp(e, "1") ? 1 : !strcmp(e, "2") ? 2 : 0; }),
+    env_switch("ZC_HEAD_RAW", 0, [](const char *e) { return !strcmp(e, "1") ? 1 : 0; })};
+
+int tower_epi() {  // 1 = the 16x16x32 form's epilogue with 16-byte stores,
                   // 2 = the per-tile read-wait-add epilogue (before the batched one)
-    const char *e = getenv("ZC_TOWER_EPI");
-    return e && !strcmp(e, "1") ? 1 : e && !strcmp(e, "2") ? 2 : 0;
+    return g_net_sw.tower_epi;
 }
 
 template <int H, int W, int BPH, int NT, int WPE, int PG = 1, int MF = 32>
@@ -1208,12 +1225,9 @@ __global__ __launch_bounds__(256) void value_head_kernel(int n, int hw, const _F
     if (lane == 0) values[i] = raw ? (double)(d + fcb) : (double)tanhf(d + fcb);
 }
 
-// ZC_HEAD_RAW=1 (tests only): the value head returns its pre-tanh sum, so the pooled Linear
+// head_raw = 1 (tests only): the value head returns its pre-tanh sum, so the pooled Linear
 // can be checked exactly against float64 on integer networks
-int head_raw() {
-    const char *e = getenv("ZC_HEAD_RAW");
-    return e && !strcmp(e, "1") ? 1 : 0;
-}
+int head_raw() { return g_net_sw.head_raw; }
 
 int conv_impl() {  // ZC_CONV_IMPL=tile: 256-pixel tiles for every layer; default: half tiles for 128 planes
     static const int v = [] {
@@ -1223,18 +1237,12 @@ int conv_impl() {  // ZC_CONV_IMPL=tile: 256-pixel tiles for every layer; defaul
     return v;
 }
 
-// The MFMA form (read per launch, so an A/B can alternate in one process): the fused tower
+// The MFMA form (zc_debug_net_switch("tower_mf", ...) between launches, so an A/B can alternate in one process): the fused tower
 // runs the 16x16x32 form (+9 % over 32x32x16 at the power-held clock, outputs bit-identical:
 // profiles/r04_ab_tower_mf.log) unless ZC_TOWER_MF=32; the packed per-layer conv keeps the
 // 32x32x16 form at three workgroups per CU unless ZC_TOWER_MF=16
-int tower_mf() {
-    const char *e = getenv("ZC_TOWER_MF");
-    return e && !strcmp(e, "32") ? 32 : 16;
-}
-int stream_mf() {
-    const char *e = getenv("ZC_TOWER_MF");
-    return e && !strcmp(e, "16") ? 16 : 32;
-}
+int tower_mf() { return g_net_sw.tower_mf == 32 ? 32 : 16; }
+int stream_mf() { return g_net_sw.tower_mf == 16 ? 16 : 32; }
 
 int stream_wpe() {  // ZC_CONV_WPE=2: the packed form at two workgroups per CU (default 3)
     static const int v = [] {
@@ -1346,4 +1354,26 @@ void launch_net_value_head(int n, int hw, const void *act, const float *fcw, flo
                        (const _Float16 *)act, fcw, fcb, values, head_raw());
 }
 
+}  // namespace zc
+
+namespace zc {
+// zc_debug_net_switch (engine.hip): false for an unknown name or value
+bool net_switch(const char *name, int value, int *old) {
+    int *slot = nullptr;
+    bool ok = false;
+    if (name && !strcmp(name, "tower_mf")) {
+        slot = &g_net_sw.tower_mf;
+        ok = value == 0 || value == 16 || value == 32;
+    } else if (name && !strcmp(name, "tower_epi")) {
+        slot = &g_net_sw.tower_epi;
+        ok = value >= 0 && value <= 2;
+    } else if (name && !strcmp(name, "head_raw")) {
+        slot = &g_net_sw.head_raw;
+        ok = value == 0 || value == 1;
+    }
+    if (!slot || !ok) return false;
+    if (old) *old = *slot;
+    *slot = value;
+    return true;
+}
 }  // namespace zc

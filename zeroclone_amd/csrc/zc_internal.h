@@ -351,6 +351,7 @@ bool launch_net_conv3x3_packed(int n, int h, int w, int cin, const void *in, con
 bool launch_net_pack_conv_weight(int cin, const void *w, void *packed, hipStream_t s);
 void launch_net_planes_to_nhwc(int n, int cin, int hw, int cpad, const void *planes, void *out, hipStream_t s);
 void launch_net_value_head(int n, int hw, const void *act, const float *fcw, float fcb, double *values, hipStream_t s);
+bool net_switch(const char *name, int value, int *old);  // zc_debug_net_switch
 
 size_t c4_search_lds_bytes(int bs);
 void launch_c4_ext_begin(const ExtParams &p, hipStream_t s);

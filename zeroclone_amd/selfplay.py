@@ -219,11 +219,19 @@ class Trajectories:
         return out
 
 
-def _room(traj):
+def _room(traj, stream: int | None = None):
     """Before a step under a game quota: grow the trajectory pool so the step cannot overflow
     it (not while a step is being captured into a graph: the unlimited quota is the graphs'
-    case, and their pool is pinned)."""
-    if traj is not None and traj.quota != _UNLIMITED and not torch.cuda.is_current_stream_capturing():
+    case, and their pool is pinned).  `stream`: the stream the step runs on (None: torch's
+    current one).  The control read and the pool copy run ON that stream, so the read sees the
+    previous step's record kernel finished and the copy is ordered before the next one."""
+    if traj is None or traj.quota == _UNLIMITED or torch.cuda.is_current_stream_capturing():
+        return
+    cur = torch.cuda.current_stream(traj.dev)
+    if stream is None or stream == cur.cuda_stream:
+        traj.ensure_room()
+        return
+    with torch.cuda.stream(torch.cuda.ExternalStream(stream, device=traj.dev)):
         traj.ensure_room()
 
 
@@ -300,7 +308,7 @@ class C4SelfPlay:
         """One move for every game (on torch's current stream unless given); returns the
         per-game results tensor (ONGOING = 2, IDLE = 3).  Finished games restart from the
         opening."""
-        _room(self.traj)
+        _room(self.traj, stream)
         self.step_search(stream)
         return self.step_finish(stream)
 
@@ -534,7 +542,7 @@ class ChessSelfPlay:
     def step(self, stream: int | None = None) -> torch.Tensor:
         """One move for every game; returns the per-game results tensor (ONGOING = 2,
         IDLE = 3).  Finished games restart from the initial position."""
-        _room(self.traj)
+        _room(self.traj, stream)
         s = self._stream(stream)
         if self.ps is not None:
             mv, _, st = self.ps.enqueue(self.roots, self.sims, self.net_fn, temperature=self.temperature)
