@@ -124,6 +124,21 @@ __device__ __forceinline__ void argmax8(T &v, int &i) {
     argmax_step(v, i, dpp<0x141>(v), dpp<0x141>(i));  // row_half_mirror
 }
 
+// The same first maximum for the walk's UCT scores: the maximum over lanes 0..7 by three DPP
+// v_max_f64 steps (no index carried, no per-step branch: the compare-and-swap form compiled to
+// exec-mask juggling, ~8 SALU per step), then the first slot holding it from one ballot.  The
+// scores are finite or -inf (never NaN), and a slot holding the maximum compares equal to it,
+// so this is the strict `>` scan of mcts.cpp:55-58 (+0 and -0 compare equal there too).
+// Returns the maximum; *first = the lowest slot k < 8 with v == max.
+__device__ __forceinline__ double max8_first(double v, int *first) {
+    double m = v;
+    m = fmax(m, dpp<0xB1>(m));   // quad_perm [1,0,3,2]
+    m = fmax(m, dpp<0x4E>(m));   // quad_perm [2,3,0,1]
+    m = fmax(m, dpp<0x141>(m));  // row_half_mirror
+    *first = __builtin_ctzll((__ballot(v == m) & 0xFFull) | 0x100ull);
+    return m;
+}
+
 // ------------------------------------------------------------------ Connect4 bitboards
 __device__ __forceinline__ uint64_t drop_bit(uint64_t occ, int col) {
     // c4_backend.play_move (:14-23): lowest empty row of `col`; a full column drops nothing.
@@ -541,6 +556,11 @@ struct FlushSel {
     uint32_t ppath;  // lane l (l <= d0): level l of root..X0 = node | slot << 16
     bool x0_dirty;   // X0 expanded during the flush (its record must be rewritten)
     uint32_t x_u, x_ch;  // X0's untried word / child slot `lane & 7` as last seen
+    // select_flush_plan2 only (planned = true): the fresh nodes are the draws 0..D-1; bit j of
+    // Sm: draw j is a chain node's first draw; bit j of Z: draw j created the next chain node
+    bool planned = false;
+    int D = 0;
+    uint64_t Sm = 0, Z = 0;
 };
 
 // The walk from the root over HBM records (select, mcts.cpp:47-63): the UCT child (first
@@ -589,11 +609,22 @@ __device__ __forceinline__ WalkEnd walk_hbm(const Tree &t, ConstDouble *logtab, 
         } else {
             // UCT (mcts.cpp:41-45) = fma(c, sqrt(log(N)/Na), Qa), first max in slot order
             const double q = valid ? qw / (double)na : 0.0;
-            double v = valid ? fma(c, sqrt(lg / (double)na), q) : -INFINITY;
-            int bi = (int)k;
-            argmax8(v, bi);
-            if ((__ballot(v == -INFINITY) & 1ull) != 0) break;  // no child: terminal leaf
-            best = uni(bi);
+            const double v = valid ? fma(c, sqrt(lg / (double)na), q) : -INFINITY;
+#ifndef ZC_MAX8
+#define ZC_MAX8 1  // 0: the compare-and-swap argmax8 (A/B runs)
+#endif
+            int bi;
+            if (ZC_MAX8) {
+                const double mx = max8_first(v, &bi);
+                if ((__ballot(mx == -INFINITY) & 1ull) != 0) break;  // no child: terminal leaf
+            } else {
+                double vv = v;
+                bi = (int)k;
+                argmax8(vv, bi);
+                if ((__ballot(vv == -INFINITY) & 1ull) != 0) break;
+                bi = uni(bi);
+            }
+            best = bi;
         }
         const int nxt = __builtin_amdgcn_readlane((int)ch, best);
         nN = __builtin_amdgcn_readlane(na, best);

@@ -524,11 +524,19 @@ __device__ __forceinline__ WalkEnd walk_hbm_prefetch(const Tree &t, ConstDouble 
         } else {
             // UCT (mcts.cpp:41-45) = fma(c, sqrt(log(N)/Na), Qa), first max in slot order
             const double q = valid ? (double)wa / (double)na : 0.0;
-            double v = valid ? fma(c, sqrt(lg / (double)na), q) : -INFINITY;
-            int bi = (int)k;
-            argmax8(v, bi);
-            if ((__ballot(v == -INFINITY) & 1ull) != 0) break;  // no child: terminal leaf
-            best = uni(bi);
+            const double v = valid ? fma(c, sqrt(lg / (double)na), q) : -INFINITY;
+            int bi;
+            if (ZC_MAX8) {
+                const double mx = max8_first(v, &bi);
+                if ((__ballot(mx == -INFINITY) & 1ull) != 0) break;  // no child: terminal leaf
+            } else {
+                double vv = v;
+                bi = (int)k;
+                argmax8(vv, bi);
+                if ((__ballot(vv == -INFINITY) & 1ull) != 0) break;
+                bi = uni(bi);
+            }
+            best = bi;
         }
         nN = __builtin_amdgcn_readlane(na, best);
         const uint64_t bit = drop_bit(b0 | b1, (int)((ow >> (3 * best)) & 7u));
@@ -755,6 +763,290 @@ __device__ __forceinline__ void select_flush_plan(const Tree &t, Fresh *fresh, L
     stamp.mark(3);
 }
 
+// ------------------------------------------------------------------ the planned flush, draws as a table chase
+// select_flush_plan's step (1) spends ~110 scalar instructions per chain node (seven unrolled
+// draw steps of five to seven SALU each, whatever the node's draw count, the view bookkeeping,
+// the descent and the node's table entry written by lane 0) — about 26 SALU per simulation, the
+// largest scalar cost of the walk.  But the chain's shape is known before any draw (see above),
+// and with it the whole flush's sequence of draw counts: draw d of chain node i is over
+// n_i - (d - d_i) moves.  _randbelow(cnt) accepts a word when its top three bits t3 are below
+// T(cnt) (4, 4, 6, 4, 5, 6, 7 for cnt = 1..7): four acceptance classes c = T - 4.
+// select_flush_plan2 therefore
+//   (1a) walks the chain's shape on the scalar unit (boards, counts, first draws; each node's
+//        fields go to VGPR lane i by v_writelane, no LDS table, no exec juggling);
+//   (1b) builds, lane-parallel, a NEXT table over the 64-word view: lane l, byte c = 1 + the
+//        first word >= l (of words 0..61) that a class-c draw accepts, or 63 (none; lanes 62
+//        and 63 hold 63 in every byte, so the chase stays there);
+//   (1c) chases it: draw d is q_{d+1} = byte c_d of readlane(table, q_d), one v_readlane and
+//        one s_bfe_u32 per draw, and s_bitset1 records bit q of F; 63 -> bit 63 = the view ran
+//        out (the failed draw rejected words q..61 and goes on at word 62 of a fresh view);
+//   (2)  as select_flush_plan, the chain nodes' fields fetched by ds_bpermute.
+// Same draws, same tree, same leaves, same stream consumption as select_flush_plan.
+// s_bfe_u32 operand of a class-c draw: byte c of the table entry, 6 bits
+__device__ __forceinline__ uint32_t draw_class_bfe(uint32_t cnt) {  // c = T(cnt) - 4
+    return (6u << 16) | (((0xE480u >> (2u * cnt)) & 3u) << 3);
+}
+
+// The view's next-draw table (1b).
+__device__ __forceinline__ uint32_t draw_table(uint32_t w) {
+    const uint32_t lane = lane_id();
+    const uint32_t t3 = lane < 62u ? (w >> 29) : 7u;
+    uint32_t nx = 0;
+#pragma unroll
+    for (uint32_t c = 0; c < 4; ++c) {
+        const uint64_t s = __ballot(t3 < 4u + c) >> lane;
+        const uint32_t f = s ? lane + 1u + (uint32_t)__builtin_ctzll(s) : 63u;
+        nx |= f << (8u * c);
+    }
+    return nx;
+}
+
+// lane i of v := the uniform value x (v_writelane_b32; no builtin in this toolchain; the lane
+// select in M0, since one VALU instruction reads at most one SGPR here)
+__device__ __forceinline__ void write_lane(int &v, uint32_t x, int i) {
+    __asm__("v_writelane_b32 %0, %1, m0" : "+v"(v) : "s"(x), "{m0}"(i));
+}
+
+// one draw of the chase: the next position q = byte c of the table entry at q
+__device__ __forceinline__ uint32_t draw_step(uint32_t nx, uint32_t q, uint32_t op) {
+    const uint32_t x = (uint32_t)__builtin_amdgcn_readlane((int)nx, (int)q);
+    uint32_t r;
+    __asm__("s_bfe_u32 %0, %1, %2" : "=s"(r) : "s"(x), "s"(op));
+    return r;
+}
+
+// The first NDRAW draws of a view chased through its table: bit q of the result set for each
+// draw's next position q (= its word + 1, 1..62), bit 63 = the view ran out.
+template <int NDRAW>
+__device__ __forceinline__ uint64_t draw_chase_fixed(uint32_t nx, uint32_t clsv) {
+    uint64_t F = 0;
+    uint32_t q = 0;
+#pragma unroll
+    for (int k = 0; k < NDRAW; ++k) {
+        q = draw_step(nx, q, (uint32_t)__builtin_amdgcn_readlane((int)clsv, k));
+        __asm__("s_bitset1_b64 %0, %1" : "+s"(F) : "s"(q));  // F |= 1 << q in one SALU
+    }
+    return F;
+}
+
+template <bool STAMP, class RNG>
+__device__ __forceinline__ void select_flush_plan2(const Tree &t, Fresh *fresh, Leaf *leaves, const uint32_t *s_order,
+                                                   ConstDouble *logtab, RNG &rng, Counters &cn, Stamp<STAMP> &stamp,
+                                                   int &nnodes, int &status, uint64_t rp0, uint64_t rp1, int rturn,
+                                                   int done, int nb, double c, FlushSel &fs) {
+    const uint32_t lane = lane_id();
+    const int f0 = nnodes;
+#ifndef ZC_MERGED_BACKUP
+#define ZC_MERGED_BACKUP 1  // 0: the fresh edges by LDS atomics up the parent links (A/B runs)
+#endif
+    for (int i = (int)lane; i < nb; i += 64) {  // fresh slots: no children (the in-edge counters: the backup)
+        if (!ZC_MERGED_BACKUP) {
+            fresh[i].na = 0;
+            fresh[i].w = 0;
+        }
+        *(uint4 *)fresh[i].ch = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
+    }
+    const WalkEnd we = walk_hbm_prefetch(t, logtab, rp0, rp1, rturn, done, c, status);
+    fs.f0 = f0;
+    fs.x0node = we.node;
+    fs.d0 = we.depth;
+    fs.ppath = we.pathv;
+    fs.x_u = we.u;
+    fs.x_ch = we.ch;
+    fs.x0_dirty = false;
+    stamp.mark(1);
+    const uint32_t cnt0 = untried_count(we.u);
+    if (cnt0 == 0) {  // X0 has no move (full board): every leaf of the flush is X0
+        const uint32_t meta = (uint32_t)we.node | ((uint32_t)we.depth << 16) | ((uint32_t)we.turn << 24) |
+                              ((uint32_t)legal_mask(we.b0 | we.b1) << 25);
+        for (int i = (int)lane; i < nb; i += 64) leaves[i] = Leaf{we.b0, we.b1, meta, 0, we.ow, 0};
+        wave_mem_order();
+        fs.planned = ZC_MERGED_BACKUP;  // D = 0: no fresh node
+        stamp.mark(3);
+        return;
+    }
+
+    // ---- (1a) the chain's shape: node i's fields in lane i of six VGPRs
+    uint64_t b0 = we.b0, b1 = we.b1;
+    int turn = we.turn;
+    uint32_t ow = we.ow, cm = (uint32_t)legal_mask(b0 | b1), n = cnt0;
+    uint32_t slot = (uint32_t)__builtin_ctz(we.u & 0x7Fu);  // X0: its lowest untried slot; fresh nodes: slot 0
+    int d = 0, i = 0, T = -1;
+    uint64_t Sm = 0;  // bit s: a chain node's first draw
+    int v_b0l = 0, v_b0h = 0, v_b1l = 0, v_b1h = 0, v_ow = 0, v_cd = 0;  // v_cd: cm | first draw << 8 | n << 16
+    for (;;) {
+        const int m = min((int)n, nb - d);
+        write_lane(v_b0l, (uint32_t)b0, i);
+        write_lane(v_b0h, (uint32_t)(b0 >> 32), i);
+        write_lane(v_b1l, (uint32_t)b1, i);
+        write_lane(v_b1h, (uint32_t)(b1 >> 32), i);
+        write_lane(v_ow, ow, i);
+        write_lane(v_cd, cm | ((uint32_t)d << 8) | (n << 16), i);
+        if (m == 0) {  // a chain node without moves: the flush's remaining leaves are all it
+            T = i;
+            break;
+        }
+        Sm |= 1ull << d;
+        d += m;
+        if (d >= nb) break;
+        // the next walk enters this node's lowest untried slot
+        const int col = (int)((ow >> (3 * slot)) & 7u);
+        const uint64_t bit = drop_bit(b0 | b1, col);
+        if (turn) b1 |= bit; else b0 |= bit;
+        turn ^= 1;
+        if (bit & kTop) {
+            cm &= ~(1u << col);
+            ow = uni(s_order[cm]);
+        }
+        n = (ow >> 24) & 15u;
+        slot = 0;
+        ++i;
+    }
+    const int D = d;  // fresh nodes f0 .. f0 + D - 1
+
+    // lane d < D: its chain node's fields (ds_bpermute from lane seg), the draw's count and class
+    const bool act = (int)lane < D;
+    const uint32_t seg = act ? mbcnt64(Sm) + (uint32_t)((Sm >> lane) & 1ull) - 1u : 0u;
+    const int sa = (int)(seg << 2);
+    const uint32_t e_cd = (uint32_t)__builtin_amdgcn_ds_bpermute(sa, v_cd);
+    const uint32_t s_i = (e_cd >> 8) & 0xFFu;  // the chain node's first draw
+    const uint32_t dd = lane - s_i;            // the draw's index inside its node
+    const uint32_t cnt = act ? (e_cd >> 16) - dd : 1u;
+    const uint32_t clsv = draw_class_bfe(act ? cnt : 1u);
+
+    // ---- (1b, 1c) the draws: raw (lane d: the accepted word of draw d)
+    uint32_t raw = 0;
+    {
+        if (rng.off >= (uint32_t)kWin) rng_advance(rng);
+        uint32_t w = rng_view(rng);
+        uint32_t nx = draw_table(w);
+        int V = 0;  // draws done
+        uint64_t F = draw_chase_fixed<32>(nx, clsv);
+        for (;;) {
+            // this view's valid draws (bits 1..62 = the word after each), in draw order
+            const uint64_t Fv = F & 0x7FFFFFFFFFFFFFFEull;
+            const uint64_t G = Fv >> 1;  // lane p: word p is a draw
+            const int nv = __popcll(G), need = D - V, take = min(nv, need);
+            const uint32_t rank = mbcnt64(G);
+            const bool send = ((G >> lane) & 1ull) && (int)rank < take;
+            const uint32_t got = (uint32_t)__builtin_amdgcn_ds_permute(
+                (int)((send ? (uint32_t)V + rank : 63u) << 2), (int)w);
+            raw = mask_sel(lanes_in(V, V + take), raw, got);
+            V += take;
+            if (nv >= need) {  // done: the stream goes on after draw D-1's word
+                const uint64_t lastw = __ballot(((G >> lane) & 1ull) && (int)rank == take - 1);
+                rng.off += (uint32_t)__builtin_ctzll(lastw) + 1u;
+                break;
+            }
+            uint32_t q;
+            if (F >> 63) {  // ran out: the failed draw rejected words q..61 and goes on at word 62
+                rng.off += 62u;
+                if (rng.off >= (uint32_t)kWin) rng_advance(rng);
+                w = rng_view(rng);
+                nx = draw_table(w);
+                q = 0;
+            } else {  // (nb > 32) the fixed chase ended with the view left: go on in it
+                q = nv ? 64u - (uint32_t)__clzll(G) : 0u;
+                rng.off += q;
+                if (rng.off >= (uint32_t)kWin) rng_advance(rng);
+                w = rng_view(rng);
+                nx = draw_table(w);
+                q = 0;
+            }
+            // the rest of the draws from V, one at a time, in this view
+            F = 0;
+            for (int k = V; k < D; ++k) {
+                q = draw_step(nx, q, (uint32_t)__builtin_amdgcn_readlane((int)clsv, k));
+                F |= 1ull << q;
+                if (q == 63u) break;
+            }
+        }
+    }
+    wave_mem_order();
+    stamp.mark(2);
+
+    // ---- (2) every fresh node and leaf, lane d = draw d
+    const uint32_t e_ow = (uint32_t)__builtin_amdgcn_ds_bpermute(sa, v_ow);
+    const uint64_t e_p0 = ((uint64_t)(uint32_t)__builtin_amdgcn_ds_bpermute(sa, v_b0h) << 32) |
+                          (uint32_t)__builtin_amdgcn_ds_bpermute(sa, v_b0l);
+    const uint64_t e_p1 = ((uint64_t)(uint32_t)__builtin_amdgcn_ds_bpermute(sa, v_b1h) << 32) |
+                          (uint32_t)__builtin_amdgcn_ds_bpermute(sa, v_b1l);
+    const uint32_t r = raw >> __clz(cnt);
+    // draw dd's position in the node's untried list as it was before the node's draws
+    // (select_flush's Lehmer decode, each lane against its own node's earlier draws)
+    uint32_t rp[6];
+#pragma unroll
+    for (int s = 0; s < 6; ++s) rp[s] = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((s_i + (uint32_t)s) << 2), (int)r);
+    uint32_t pl = r;
+#pragma unroll
+    for (int s = 5; s >= 0; --s) pl += (dd > (uint32_t)s && pl >= rp[s]) ? 1u : 0u;
+    // the move index: X0's untried list is the set bits of its untried mask in order (the
+    // select table's row); a fresh node's is 0, 1, ..., n-1
+    const uint32_t mi = seg == 0 ? (uint32_t)sel_table(s_order)[8u * (we.u & 0x7Fu) + (pl & 7u)] : pl;
+    const uint64_t Z = __ballot(act && pl == 0);  // per chain node: the draw holding its lowest untried slot
+    const uint64_t zl = Z & ((1ull << s_i) - 1ull);
+    const int parent = seg == 0 ? we.node : f0 + 63 - __clzll(zl | 1ull);
+    {
+        const uint32_t col = (e_ow >> (3 * mi)) & 7u;
+        const uint64_t bit = drop_bit(e_p0 | e_p1, (int)col);
+        const uint32_t tn = (uint32_t)we.turn ^ (seg & 1u), ldepth = (uint32_t)we.depth + seg + 1u;
+        const bool filled = (bit & kTop) != 0;
+        const uint32_t c_lmask = (e_cd & 0x7Fu) & ~(filled ? 1u << col : 0u);
+        uint32_t c_low = e_ow;
+        if (act && filled) c_low = s_order[c_lmask];
+        if (act) {
+            *(uint4 *)&fresh[lane] = make_uint4(untried_init((c_low >> 24) & 15u), c_low,
+                                                (uint32_t)parent | (mi << 16) | (ldepth << 24), c_lmask);
+            leaves[lane] = Leaf{tn ? e_p0 : (e_p0 | bit), tn ? (e_p1 | bit) : e_p1,
+                                ((uint32_t)f0 + lane) | (ldepth << 16) | ((tn ^ 1u) << 24) | (c_lmask << 25), 0,
+                                c_low, 0};
+        }
+    }
+    if (T >= 0) {  // the terminal chain node (entered from the full node before it)
+        const uint64_t tp0 = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(v_b0h, T) << 32) |
+                             (uint32_t)__builtin_amdgcn_readlane(v_b0l, T);
+        const uint64_t tp1 = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(v_b1h, T) << 32) |
+                             (uint32_t)__builtin_amdgcn_readlane(v_b1l, T);
+        const uint32_t tcm = (uint32_t)__builtin_amdgcn_readlane(v_cd, T) & 0x7Fu;
+        const uint32_t tow = (uint32_t)__builtin_amdgcn_readlane(v_ow, T);
+        const uint32_t meta = (uint32_t)(f0 + 63 - __clzll(Z | 1ull)) | (((uint32_t)we.depth + (uint32_t)T) << 16) |
+                              (((uint32_t)we.turn ^ ((uint32_t)T & 1u)) << 24) | (tcm << 25);
+        for (int jj = D + (int)lane; jj < nb; jj += 64) leaves[jj] = Leaf{tp0, tp1, meta, 0, tow, 0};
+    }
+    wave_mem_order();
+    // ---- (3) the chain nodes' child slots and untried words; X0's
+    if (act && seg != 0) {
+        Fresh &P = fresh[parent - f0];
+        P.ch[mi] = (uint16_t)(f0 + (int)lane);
+        atomicAnd(&P.u, ~(1u << mi));
+    }
+    uint32_t slotbit = (act && seg == 0) ? 1u << mi : 0u;  // X0's draws are lanes 0 .. m0-1 (< 8)
+    slotbit |= (uint32_t)dpp<0xB1>((int)slotbit);
+    slotbit |= (uint32_t)dpp<0x4E>((int)slotbit);
+    slotbit |= (uint32_t)dpp<0x141>((int)slotbit);
+    const uint32_t ucl = uni(slotbit);
+    const uint32_t sent =
+        (uint32_t)__builtin_amdgcn_ds_permute((int)(((act && seg == 0) ? mi : 63u) << 2), (int)((uint32_t)f0 + lane));
+    fs.x_ch = ((ucl >> (lane & 7u)) & 1u) ? sent : we.ch;
+    fs.x_u = we.u & ~ucl;
+    fs.x0_dirty = true;
+    fs.planned = ZC_MERGED_BACKUP;
+    fs.D = D;
+    fs.Sm = Sm;
+    fs.Z = Z;
+    nnodes = f0 + D;
+    wave_mem_order();
+    {  // the flush's expansions and their depths: depth_sum = sum over draws of (we.depth + seg + 1)
+        const uint32_t dep = act ? (uint32_t)we.depth + seg + 1u : 0u;
+        int dsum = 0;
+#pragma unroll
+        for (int bit = 0; bit < 6; ++bit) dsum += __popcll(__ballot((dep >> bit) & 1u)) << bit;
+        cn.add(cn.expansions, D);
+        cn.add(cn.depth_sum, dsum);
+    }
+    stamp.mark(3);
+}
+
 // ------------------------------------------------------------------ the search kernel
 constexpr int kSearchWaves = 4;  // games (waves) per workgroup
 __host__ __device__ constexpr size_t c4_search_wave_lds(int bs) {
@@ -822,7 +1114,14 @@ __device__ __forceinline__ void search_move(const SearchParams &p, const SearchL
 #endif
             // one lane per draw and lane 63 free as the permutes' discard slot (bs < 64); the chain
             // table lives in the leaf-path area, which this search does not use
-            if (!ZC_NO_PLAN && p.bs < 64)
+#ifndef ZC_PLAN2
+#define ZC_PLAN2 1  // 0: the chain's draws node by node (select_flush_plan), for A/B runs
+#endif
+            if (!ZC_NO_PLAN && ZC_PLAN2 && p.bs < 64)
+                select_flush_plan2<STAMP>(t, fresh, leaves, s_order, logtab, rng, cn, stamp, nnodes, status,
+                                          uni64(root.stones[0]), uni64(root.stones[1]), uni(root.turn), done, nb,
+                                          p.c, fs);
+            else if (!ZC_NO_PLAN && p.bs < 64)
                 select_flush_plan<STAMP>(t, fresh, leaves, (ChainNode *)L.paths, s_order, logtab, rng, cn, stamp,
                                          nnodes, status, uni64(root.stones[0]), uni64(root.stones[1]),
                                          uni(root.turn), done, nb, p.c, fs);
@@ -879,72 +1178,139 @@ __device__ __forceinline__ void search_move(const SearchParams &p, const SearchL
             na0 = t.na(par)[act];
             w0 = t.w(par)[act];
         }
-        int S = 0;
-        for (int base = 0; base < nb; base += 64) {
-            // lane = leaf: S, and the fresh edges (levels d0+1..d of the leaf's path), one level
-            // per step for all leaves at once
-            const int jj = base + (int)lane;
-            int v = 0, d = -1, sv = 0;
+        if (fs.planned) {
+            // The planned flush's fresh nodes are the draws 0..D-1 (leaf j <-> node f0 + j for
+            // j < D; the leaves D..nb-1 sit on the terminal chain node).  A fresh node's subtree is
+            // itself, plus — for a chain node (a Z draw) — every leaf from the next chain node's
+            // first draw on (the chain runs to the flush's end), so every fresh in-edge's counters
+            // come from one prefix sum over the leaves (lane = leaf) of sv_j = v_j (-1)^d_j:
+            //   Na = 1 + #leaves from there,  Wa = -(-1)^l (sv_self + suffix sum from there)
+            // (Wa -= v_j (-1)^(d_j - l) summed; integers, so in any order) — no atomics, no
+            // walk up the parent links.  They are written straight into the records below.
+            const int jj = (int)lane;
+            int v = 0, dl = 0;
             if (jj < nb) {
-                const uint32_t meta = leaves[jj].meta;
                 v = leaves[jj].val;
-                d = (int)((meta >> 16) & 0xFFu);
-                sv = (d & 1) ? -v : v;
+                dl = (int)((leaves[jj].meta >> 16) & 0xFFu);
             }
-            S += __popcll(__ballot(sv > 0)) - __popcll(__ballot(sv < 0));
-            // the fresh edges: from the leaf up to X0's child along the fresh nodes' parent
-            // links (every node below X0 is fresh, X0 and above are not)
-            int nd = jj < nb ? (int)(leaves[jj].meta & 0xFFFFu) : -1, l = d;
-            while (__ballot(nd >= f0)) {
-                if (nd >= f0) {
-                    const int fi = nd - f0;
-                    const int vl = ((d - l) & 1) ? -v : v;
-                    atomicAdd(&fresh[fi].na, 1);
-                    atomicAdd(&fresh[fi].w, -vl);
-                    nd = (int)(fresh[fi].link & 0xFFFFu);
-                    --l;
+            const int sv = (dl & 1) ? -v : v;
+            const int P = (int)scan_add32((uint32_t)sv);
+            const int S = __builtin_amdgcn_readlane(P, 63);  // sum over every leaf (the prefix levels' S)
+            const int suf = S - P + sv;                      // sum over the leaves jj..nb-1
+            const uint64_t above = jj < 63 ? fs.Sm >> (jj + 1) : 0ull;
+            const int nxt = above ? jj + 1 + __builtin_ctzll(above) : fs.D;  // next chain node's first draw
+            const int sufn = __builtin_amdgcn_ds_bpermute(nxt << 2, suf);
+            const bool isz = (fs.Z >> jj) & 1ull;
+            const int na_e = 1 + (isz ? nb - nxt : 0);
+            const int ss = sv + (isz ? sufn : 0);
+            const int w_e = (dl & 1) ? ss : -ss;
+            if (pre) {
+                const int dw = (lane & 1u) ? S : -S;  // Wa -= (-1)^l * S
+                t.na(par)[act] = na0 + nb;
+                t.w(par)[act] = w0 + dw;
+            }
+            stamp.mark(5);
+            // ---- publish: each fresh node's header and child slots (its Na / Wa slots only hold
+            // data where a child exists: the walk reads them for those slots alone), the fresh
+            // in-edges' counters into their fresh parents, and X0's changes
+            if (jj < fs.D) {
+                const Fresh &F = fresh[jj];
+                const uint4 ch = *(const uint4 *)F.ch;
+                const uint32_t link = F.link;
+                uint8_t *R = t.rec(f0 + jj);
+                *(uint4 *)R = make_uint4(0u, F.u, link, F.ow);
+                *(uint4 *)(R + 16) = ch;
+                const int pn = (int)(link & 0xFFFFu);
+                if (pn >= f0) {
+                    const int pa = (int)((link >> 16) & 0xFFu);
+                    t.na(pn)[pa] = na_e;
+                    t.w(pn)[pa] = w_e;
                 }
             }
-        }
-        if (pre) {
-            const int dw = (lane & 1u) ? S : -S;  // Wa -= (-1)^l * S
-            t.na(par)[act] = na0 + nb;
-            t.w(par)[act] = w0 + dw;
-        }
-        wave_mem_order();
-        stamp.mark(5);
-
-        // ---- publish: X0's changes and every fresh node, in coalesced stores ------------------
-        if (fs.x0_dirty) {
-            const int x0node = fs.x0node;
-            const uint32_t x_ch = fs.x_ch;
-            if (lane == 0) t.hdr(x0node)[1] = fs.x_u;
-            if (lane < kSlots) {
-                t.child(x0node)[lane] = (uint16_t)x_ch;
-                if (x_ch != 0xFFFF && (int)x_ch >= f0) {  // edge into a fresh child
-                    t.na(x0node)[lane] = fresh[x_ch - f0].na;
-                    t.w(x0node)[lane] = fresh[x_ch - f0].w;
-                }
-            }
-        }
-        {
-            const int nf = nnodes - f0;
-            for (int base = 0; base < nf * 8; base += 64) {
-                const int idx = base + (int)lane;
-                if (idx < nf * 8) {
-                    const int r = idx >> 3, slot = idx & 7;
-                    const Fresh &F = fresh[r];
-                    const uint16_t c = F.ch[slot];
-                    int32_t na = 0, w = 0;
-                    if (c != 0xFFFF) {
-                        na = fresh[c - f0].na;
-                        w = fresh[c - f0].w;
+            if (fs.x0_dirty) {
+                const int x0node = fs.x0node;
+                const uint32_t x_ch = fs.x_ch;
+                const bool xf = x_ch != 0xFFFF && (int)x_ch >= f0;
+                const int src = (xf ? (int)x_ch - f0 : 0) << 2;
+                const int xna = __builtin_amdgcn_ds_bpermute(src, na_e);
+                const int xw = __builtin_amdgcn_ds_bpermute(src, w_e);
+                if (lane == 0) t.hdr(x0node)[1] = fs.x_u;
+                if (lane < kSlots) {
+                    t.child(x0node)[lane] = (uint16_t)x_ch;
+                    if (xf) {  // edge into a fresh child
+                        t.na(x0node)[lane] = xna;
+                        t.w(x0node)[lane] = xw;
                     }
-                    uint8_t *R = t.rec(f0 + r);
-                    if (slot == 0) *(uint4 *)R = make_uint4(0u, F.u, F.link, F.ow);
-                    ((uint16_t *)(R + 16))[slot] = c;
-                    ((int32_t *)(R + 32))[slot] = na;
-                    ((int32_t *)(R + 64))[slot] = w;
+                }
+            }
+        } else {
+            int S = 0;
+            for (int base = 0; base < nb; base += 64) {
+                // lane = leaf: S, and the fresh edges (levels d0+1..d of the leaf's path), one level
+                // per step for all leaves at once
+                const int jj = base + (int)lane;
+                int v = 0, d = -1, sv = 0;
+                if (jj < nb) {
+                    const uint32_t meta = leaves[jj].meta;
+                    v = leaves[jj].val;
+                    d = (int)((meta >> 16) & 0xFFu);
+                    sv = (d & 1) ? -v : v;
+                }
+                S += __popcll(__ballot(sv > 0)) - __popcll(__ballot(sv < 0));
+                // the fresh edges: from the leaf up to X0's child along the fresh nodes' parent
+                // links (every node below X0 is fresh, X0 and above are not)
+                int nd = jj < nb ? (int)(leaves[jj].meta & 0xFFFFu) : -1, l = d;
+                while (__ballot(nd >= f0)) {
+                    if (nd >= f0) {
+                        const int fi = nd - f0;
+                        const int vl = ((d - l) & 1) ? -v : v;
+                        atomicAdd(&fresh[fi].na, 1);
+                        atomicAdd(&fresh[fi].w, -vl);
+                        nd = (int)(fresh[fi].link & 0xFFFFu);
+                        --l;
+                    }
+                }
+            }
+            if (pre) {
+                const int dw = (lane & 1u) ? S : -S;  // Wa -= (-1)^l * S
+                t.na(par)[act] = na0 + nb;
+                t.w(par)[act] = w0 + dw;
+            }
+            wave_mem_order();
+            stamp.mark(5);
+
+            // ---- publish: X0's changes and every fresh node, in coalesced stores ------------------
+            if (fs.x0_dirty) {
+                const int x0node = fs.x0node;
+                const uint32_t x_ch = fs.x_ch;
+                if (lane == 0) t.hdr(x0node)[1] = fs.x_u;
+                if (lane < kSlots) {
+                    t.child(x0node)[lane] = (uint16_t)x_ch;
+                    if (x_ch != 0xFFFF && (int)x_ch >= f0) {  // edge into a fresh child
+                        t.na(x0node)[lane] = fresh[x_ch - f0].na;
+                        t.w(x0node)[lane] = fresh[x_ch - f0].w;
+                    }
+                }
+            }
+            {
+                const int nf = nnodes - f0;
+                for (int base = 0; base < nf * 8; base += 64) {
+                    const int idx = base + (int)lane;
+                    if (idx < nf * 8) {
+                        const int r = idx >> 3, slot = idx & 7;
+                        const Fresh &F = fresh[r];
+                        const uint16_t c = F.ch[slot];
+                        int32_t na = 0, w = 0;
+                        if (c != 0xFFFF) {
+                            na = fresh[c - f0].na;
+                            w = fresh[c - f0].w;
+                        }
+                        uint8_t *R = t.rec(f0 + r);
+                        if (slot == 0) *(uint4 *)R = make_uint4(0u, F.u, F.link, F.ow);
+                        ((uint16_t *)(R + 16))[slot] = c;
+                        ((int32_t *)(R + 32))[slot] = na;
+                        ((int32_t *)(R + 64))[slot] = w;
+                    }
                 }
             }
         }
@@ -1027,7 +1393,7 @@ __device__ __forceinline__ void search_games(const SearchParams &p, uint8_t *s_d
 }
 
 template <bool STAMP, bool PHILOX>
-__global__ __launch_bounds__(kSearchWaves * kBlock) void c4_search_kernel(SearchParams p) {
+__global__ __launch_bounds__(kSearchWaves * kBlock, 4) void c4_search_kernel(SearchParams p) {
     extern __shared__ __attribute__((aligned(16))) uint8_t s_dyn[];
     search_games<STAMP, PHILOX, 0>(p, s_dyn);
 }
@@ -1035,7 +1401,7 @@ __global__ __launch_bounds__(kSearchWaves * kBlock) void c4_search_kernel(Search
 // Diagnostic: the lockstep search with its rollouts recorded (WALK 1) or replayed (WALK 2):
 // the tree-walk-only kernel whose time and HBM traffic measure the walk (tools/prof_walk.py).
 template <int WALK>
-__global__ __launch_bounds__(kSearchWaves * kBlock) void c4_walk_kernel(SearchParams p) {
+__global__ __launch_bounds__(kSearchWaves * kBlock, 4) void c4_walk_kernel(SearchParams p) {
     extern __shared__ __attribute__((aligned(16))) uint8_t s_dyn[];
     search_games<false, false, WALK>(p, s_dyn);
 }
@@ -1050,7 +1416,7 @@ __global__ __launch_bounds__(kSearchWaves * kBlock) void c4_walk_kernel(SearchPa
 // out_results[...] (the inputs of zc_traj_record_async for step k, replayed in step order
 // after the launch); out_stats[gl] accumulates over the moves.
 template <bool PHILOX>
-__global__ __launch_bounds__(kSearchWaves * kBlock) void c4_selfplay_kernel(SearchParams p) {
+__global__ __launch_bounds__(kSearchWaves * kBlock, 4) void c4_selfplay_kernel(SearchParams p) {
     extern __shared__ __attribute__((aligned(16))) uint8_t s_dyn[];
     const SearchLds L = search_lds(s_dyn, p.bs);
     load_tables(L.s_order);

@@ -413,6 +413,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 }
 
 
+// ---- the swizzled activation layout (the 16x16x32 form, EPI = 3): unpadded 256-byte rows
+// (128 halfs, sixteen 16-byte chunks) whose chunk c sits at c ^ hsw(row).  hsw depends on
+// row & 7 only (so a zero row, 8 of them, stands for any row of its class) and was chosen
+// (an exhaustive search over the XOR-linear maps) so that every LDS access of the tower is
+// conflict-free on gfx950's banking (MI355X_MICROARCH §LDS):
+//   - the MFMA B operand (ds_read_b128, lane (pixel l & 15, k-chunk l >> 4), rows shifted by
+//     any tap offset): each lane group's 16 chunks land on 16 distinct bank quads;
+//   - the epilogue, in 8-consecutive-channel form (permlane16_swap, as tower_epilogue16_swap):
+//     the residual ds_read_b128 and the ds_write_b128 (8 aligned rows, one chunk) alike;
+//   - the value head's and the output copy's row reads, the input staging's stores.
+// Only the policy 1x1 conv's 32-pixel reads stay 2-way (once per tower).  The padded layout it
+// replaces (144-half rows) left the epilogue's ds_write_b64 4-way and its residual reads 2-way.
+constexpr int kSwzLD = kCout;
+__device__ __forceinline__ int hsw(int row) { return (int)((0xAE9D7340u >> ((row & 7) << 2)) & 15u); }
+__device__ __forceinline__ int swz(int row, int chunk) { return row * kSwzLD + ((chunk ^ hsw(row)) << 3); }
+template <int NT> constexpr size_t tower_lds_swz() { return (size_t)(64 * NT + 8) * kSwzLD * sizeof(_Float16); }
+
 // One layer's MFMA loop in the 16x16x32 form: each wave its 32 output channels (two 16-row
 // M tiles) x the tile's pixels as NN 16-pixel N tiles, k-steps of 32 channels.  Lane l takes
 // pixel l & 15 of each N tile and k-chunk q = l >> 4; the weight fragments come from the same
@@ -469,6 +486,71 @@ __device__ __forceinline__ void tower_mfma16(const _Float16 *lds, int src, const
         if (tap + 1 < 9) {
 #pragma unroll
             for (int n = 0; n < NN; ++n) xb[n] = xbn[n];
+        }
+    }
+    if (JN != J && wn) {
+#pragma unroll
+        for (int j = 0; j < JN; ++j)
+#pragma unroll
+            for (int m = 0; m < 2; ++m) a[2 * j + m] = *(const h8 *)(wn + (size_t)(2 * j) * 2048 + m * 128);
+    }
+}
+
+// tower_mfma16 on the swizzled layout: the same MFMAs in the same order; lane (pixel l16,
+// k-chunk q) of N tile n reads chunk 4 j + q of its row at (4 j + q) ^ hsw(row) — the row's
+// chunk offset for j = 0 XOR 64 j bytes (hsw of the tap-shifted row does not depend on n).
+template <int H, int W, int NN, int KC, int KCN, int ZERO, int NA>
+__device__ __forceinline__ void tower_mfma16_swz(const _Float16 *lds, int src, const _Float16 *wa, const _Float16 *wn,
+                                                 h8 (&a)[NA], int l16, const int (&pyx)[NN], int q,
+                                                 f4x (&acc)[2][NN]) {
+    constexpr int J = KC / 2, JN = KCN / 2;
+    auto rows = [&](int tap, int (&xo)[NN]) {
+        const int dy = tap / 3 - 1, dx = tap % 3 - 1;
+        const int qh = (q ^ hsw(l16 + dy * W + dx)) << 3;  // the same for every N tile (16 n = 0 mod 8)
+#pragma unroll
+        for (int n = 0; n < NN; ++n) {
+            const int sy = (pyx[n] >> 8) + dy, sx = (pyx[n] & 255) + dx;
+            const bool sv = (unsigned)sy < (unsigned)H && (unsigned)sx < (unsigned)W;
+            const int row = l16 + (n * 16 + dy * W + dx);
+            xo[n] = (sv ? src + row : ZERO + (row & 7)) * kSwzLD + qh;
+        }
+    };
+    int xo[NN];
+    rows(0, xo);
+    h8 x[NN], xn[NN];
+#pragma unroll
+    for (int n = 0; n < NN; ++n) x[n] = *(const h8 *)(lds + xo[n]);
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) {
+        int xon[NN];
+        if (tap + 1 < 9) rows(tap + 1, xon);
+#pragma unroll
+        for (int j = 0; j < J; ++j) {
+            if (j + 1 < J) {
+#pragma unroll
+                for (int n = 0; n < NN; ++n) xn[n] = *(const h8 *)(lds + (xo[n] ^ ((j + 1) * 32)));
+            } else if (tap + 1 < 9) {
+#pragma unroll
+                for (int n = 0; n < NN; ++n) xn[n] = *(const h8 *)(lds + xon[n]);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int n = 0; n < NN; ++n)
+#pragma unroll
+                for (int m = 0; m < 2; ++m)
+                    acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[2 * j + m], x[n], acc[m][n], 0, 0, 0);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int m = 0; m < 2; ++m) {
+                if (tap + 1 < 9) a[2 * j + m] = *(const h8 *)(wa + (size_t)((tap + 1) * KC + 2 * j) * 2048 + m * 128);
+                else if (JN == J && wn) a[2 * j + m] = *(const h8 *)(wn + (size_t)(2 * j) * 2048 + m * 128);
+            }
+#pragma unroll
+            for (int n = 0; n < NN; ++n) x[n] = xn[n];
+        }
+        if (tap + 1 < 9) {
+#pragma unroll
+            for (int n = 0; n < NN; ++n) xo[n] = xon[n];
         }
     }
     if (JN != J && wn) {
@@ -719,6 +801,7 @@ template <int NT, int PG = 1, int MF = 32> constexpr size_t tower_lds() {
     return (size_t)(64 * NT * PG + tower_zr<MF>()) * tower_ld<MF>() * sizeof(_Float16);
 }
 
+
 // One layer's MFMA loop: acc[t] += sum over taps and k of W * X (X from the LDS buffer at
 // row `src`).  a[0..KC) holds the layer's tap-0 fragments on entry; on exit it holds the
 // next layer's (KCN fragments from wn, when wn != nullptr and KCN == KC: in the ring at the
@@ -922,6 +1005,58 @@ __device__ __forceinline__ void tower_epilogue16_swap(_Float16 *dst, const float
     }
 }
 
+// The epilogue on the swizzled layout: the fp32 accumulators are first handed over by
+// v_permlane16_swap (4 per N tile) so that lane (pixel l16, q) holds the 8 consecutive
+// channels co8 = wave * 32 + 16 (q & 1) + 8 (q >> 1) .. + 7 of its pixel — one chunk — and the
+// residual read, + bias, + residual, ReLU, fp16 and the store are whole 16-byte chunks
+// (conflict-free, see hsw).  Per element the arithmetic of tower_epilogue16: bit-identical.
+// bv8: this lane's 8 bias values (channels co8 ..).
+template <int NN, bool RES, bool CHECK>
+__device__ __forceinline__ void tower_epilogue16_swz(_Float16 *dst, const float (&bv8)[8], int npix, int wave, int l16,
+                                                     int q, const f4x (&acc)[2][NN]) {
+    const int c8 = wave * 4 + 2 * (q & 1) + (q >> 1);  // the lane's chunk (co8 / 8)
+    h8 rv[NN];
+    if constexpr (RES) {
+#pragma unroll
+        for (int n = 0; n < NN; ++n) {
+            const int P = CHECK ? min(n * 16 + l16, npix - 1) : n * 16 + l16;  // a valid row to read
+            rv[n] = *(const h8 *)(dst + swz(P, c8));
+        }
+    }
+#pragma unroll
+    for (int n = 0; n < NN; ++n) {
+        float v[8];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[0][n][e]), __float_as_uint(acc[1][n][e]),
+                                                             false, false);
+            v[e] = __uint_as_float(sw[0]);
+            v[4 + e] = __uint_as_float(sw[1]);
+        }
+        h8 ov;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            float y = v[e] + bv8[e];
+            if constexpr (RES) y += (float)rv[n][e];
+            ov[e] = (_Float16)fmaxf(y, 0.0f);
+        }
+        const int P = n * 16 + l16;
+        if (!CHECK || P < npix) *(h8 *)(dst + swz(P, c8)) = ov;
+    }
+}
+
+template <int NN>
+__device__ __forceinline__ void tower_epilogue16s(_Float16 *dst, const float (&bv8)[8], bool res, int npix, int wave,
+                                                  int l16, int q, const f4x (&acc)[2][NN]) {
+    if (npix >= NN * 16) {
+        if (res) tower_epilogue16_swz<NN, true, false>(dst, bv8, npix, wave, l16, q, acc);
+        else tower_epilogue16_swz<NN, false, false>(dst, bv8, npix, wave, l16, q, acc);
+    } else {
+        if (res) tower_epilogue16_swz<NN, true, true>(dst, bv8, npix, wave, l16, q, acc);
+        else tower_epilogue16_swz<NN, false, true>(dst, bv8, npix, wave, l16, q, acc);
+    }
+}
+
 // The policy head's 1x1 conv (PolicyValueNetwork.policy[0..2]: 128 -> 32 channels, BN folded,
 // ReLU) on the tower's output while it is still in LDS (tower_policy): pw = the folded
 // weights as 32x32x16 MFMA A fragments [8 k-steps][64 lanes][8] (lane = output channel
@@ -946,7 +1081,9 @@ __global__ __launch_bounds__(256 * PG) __attribute__((amdgpu_waves_per_eu(WPE, W
     constexpr int TP = 32 * NT * PG;
     constexpr int NTH = 256 * PG;   // threads
     constexpr int KC0 = CIN0 / 16;
-    constexpr int LD = tower_ld<MF>(), ZR = tower_zr<MF>(), BUF1 = tower_buf1<NT, PG, MF>();
+    constexpr bool SWZ = EPI == 3;  // the swizzled layout (hsw): unpadded rows, chunk c at c ^ hsw(row)
+    static_assert(!SWZ || (MF == 16 && PG == 1), "the swizzled layout is the 16x16x32 form's");
+    constexpr int LD = SWZ ? kSwzLD : tower_ld<MF>(), ZR = tower_zr<MF>(), BUF1 = tower_buf1<NT, PG, MF>();
     constexpr int NP = MF == 16 ? 2 * NT : NT;  // pixel tiles per wave (16 or 32 pixels)
     constexpr size_t kW0 = (size_t)9 * CIN0 * kCout, kW = (size_t)9 * kCout * kCout;  // halfs per layer
     extern __shared__ __attribute__((aligned(16))) _Float16 lds[];
@@ -980,7 +1117,7 @@ __global__ __launch_bounds__(256 * PG) __attribute__((amdgpu_waves_per_eu(WPE, W
             const int i = tid + q * NTH, row = i / C8, c8 = i - row * C8;
             if (row >= TP) break;
             const h8 t = *(const h8 *)(src + min(row, npix - 1) * CIN0 + c8 * 8);
-            *(h8 *)(lds + (BUF1 + row) * LD + c8 * 8) = row < npix ? t : zero;
+            *(h8 *)(lds + (SWZ ? swz(BUF1 + row, c8) : (BUF1 + row) * LD + c8 * 8)) = row < npix ? t : zero;
         }
         for (int z = tid; z < ZR * LD / 8; z += NTH)
             *(h8 *)(lds + tower_zero<NT, PG>() * LD + z * 8) = zero;
@@ -1015,6 +1152,15 @@ __global__ __launch_bounds__(256 * PG) __attribute__((amdgpu_waves_per_eu(WPE, W
             for (int m = 0; m < 2; ++m)
 #pragma unroll
                 for (int t = 0; t < NP; ++t) acc[m][t] = f4x{0.0f, 0.0f, 0.0f, 0.0f};
+            if constexpr (SWZ) {
+                const float *bp = ball + (size_t)l * kCout + wave * 32 + 16 * (q4 & 1) + 8 * (q4 >> 1);
+                const float4 b0 = *(const float4 *)bp, b1 = *(const float4 *)(bp + 4);
+                const float bv8[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+                tower_mfma16_swz<H, W, NP, KC, 8, tower_zero<NT>()>(lds, src, wa, wn, a, l16, py16, q4, acc);
+                tower_epilogue16s<NP>(lds + dst * LD, bv8, l >= 2 && !(l & 1), npix, wave, l16, q4, acc);
+                __syncthreads();
+                return;
+            }
             float4 bv[2];
 #pragma unroll
             for (int m = 0; m < 2; ++m) bv[m] = *(const float4 *)(ball + (size_t)l * kCout + wave * 32 + 16 * m + 4 * q4);
@@ -1057,7 +1203,7 @@ __global__ __launch_bounds__(256 * PG) __attribute__((amdgpu_waves_per_eu(WPE, W
             const _Float16 *act = lds + bi * HW * LD + c0;
             float sum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
             for (int p = lane >> 4; p < HW; p += 4) {
-                const h8 v = *(const h8 *)(act + p * LD);
+                const h8 v = *(const h8 *)(SWZ ? lds + swz(bi * HW + p, lane & 15) : act + p * LD);
 #pragma unroll
                 for (int e = 0; e < 8; ++e) sum[e] += (float)v[e];
             }
@@ -1094,7 +1240,7 @@ __global__ __launch_bounds__(256 * PG) __attribute__((amdgpu_waves_per_eu(WPE, W
                 for (int k = 0; k < 16; ++k) acc[k] = 0.0f;
 #pragma unroll
                 for (int kc = 0; kc < 8; ++kc) {
-                    const h8 x = *(const h8 *)(lds + (size_t)P * LD + kc * 16 + hh * 8);
+                    const h8 x = *(const h8 *)(lds + (SWZ ? swz(P, 2 * kc + hh) : P * LD + kc * 16 + hh * 8));
                     acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(pa[kc], x, acc, 0, 0, 0);
                 }
                 if (P < npix) {
@@ -1117,7 +1263,9 @@ __global__ __launch_bounds__(256 * PG) __attribute__((amdgpu_waves_per_eu(WPE, W
 #pragma unroll
         for (int q = 0; q < TP * (kCout / 8) / NTH; ++q) {
             const int i = tid + q * NTH, P = i >> 4, c0 = (i & 15) * 8;
-            if (P < npix) *(h8 *)(out + ((size_t)b0 * HW + P) * kCout + c0) = *(const h8 *)(lds + P * LD + c0);
+            if (P < npix)
+                *(h8 *)(out + ((size_t)b0 * HW + P) * kCout + c0) =
+                    *(const h8 *)(lds + (SWZ ? swz(P, i & 15) : P * LD + c0));
         }
     }
 }
@@ -1134,7 +1282,7 @@ int env_switch(const char *name, int dflt, int (*parse)(const char *)) {
 }
 NetSwitches g_net_sw = {
     env_switch("ZC_TOWER_MF", 0, [](const char *e) { return !strcmp(e, "32") ? 32 : !strcmp(e, "16") ? 16 : 0; }),
-    env_switch("ZC_TOWER_EPI", 0, [](const char *e) { return !strcmp(e, "1") ? 1 : !strcmp(e, "2") ? 2 : 0; }),
+    env_switch("ZC_TOWER_EPI", 0, [](const char *e) { return e[0] >= '0' && e[0] <= '3' && !e[1] ? e[0] - '0' : 0; }),
     env_switch("ZC_HEAD_RAW", 0, [](const char *e) { return !strcmp(e, "1") ? 1 : 0; })};
 
 int tower_epi() {  // 1 = the 16x16x32 form's epilogue with 16-byte stores,
@@ -1155,6 +1303,12 @@ void launch_tower(int n, int nconv, const void *in, const void *wall, const floa
         if (tower_epi() == 2) {
             hipLaunchKernelGGL((tower_kernel<H, W, BPH, 32, NT, WPE, PG, MF, 2>), dim3((n + BPH - 1) / BPH),
                                dim3(256 * PG), (tower_lds<NT, PG, MF>()), s, n, nconv, (const _Float16 *)in,
+                               (const _Float16 *)wall, ball, (_Float16 *)out, fcw, fcb, values, pol);
+            return;
+        }
+        if (tower_epi() == 3) {
+            hipLaunchKernelGGL((tower_kernel<H, W, BPH, 32, NT, WPE, PG, MF, 3>), dim3((n + BPH - 1) / BPH),
+                               dim3(256 * PG), (tower_lds_swz<NT>()), s, n, nconv, (const _Float16 *)in,
                                (const _Float16 *)wall, ball, (_Float16 *)out, fcw, fcb, values, pol);
             return;
         }
@@ -1366,7 +1520,7 @@ bool net_switch(const char *name, int value, int *old) {
         ok = value == 0 || value == 16 || value == 32;
     } else if (name && !strcmp(name, "tower_epi")) {
         slot = &g_net_sw.tower_epi;
-        ok = value >= 0 && value <= 2;
+        ok = value >= 0 && value <= 3;
     } else if (name && !strcmp(name, "head_raw")) {
         slot = &g_net_sw.head_raw;
         ok = value == 0 || value == 1;
