@@ -134,7 +134,7 @@ def test_packed_conv_is_bit_identical_to_the_staged_form():
             assert torch.equal(a.view(torch.int16), b.view(torch.int16)), (h, w, cin, n, use_res, relu)
 
 
-@pytest.mark.parametrize("mf", ["32", "16", "default", "16s"])
+@pytest.mark.parametrize("mf", ["32", "16", "default"])
 @pytest.mark.parametrize("shape", [(17, 8, 8), (2, 6, 7)])
 @pytest.mark.parametrize("n", [1, 7, 301, 4099])
 def test_fused_tower_is_bit_identical_to_layered(shape, n, mf, net_sw):
@@ -146,9 +146,8 @@ def test_fused_tower_is_bit_identical_to_layered(shape, n, mf, net_sw):
     from zeroclone_amd.nets import MfmaValueNetwork
     if mf == "default":
         net_sw("tower_mf", 0)
-    else:   # "16s": the 16x16x32 form on the swizzled activation layout ("tower_epi" 3)
-        net_sw("tower_mf", int(mf[:2]))
-        net_sw("tower_epi", 3 if mf.endswith("s") else 0)
+    else:
+        net_sw("tower_mf", int(mf))
     c, h, w = shape
     net = MfmaValueNetwork(_net(c, seed=100 + n))
     x = (torch.rand(n, c, h, w, device="cuda") < 0.3).half()
@@ -183,16 +182,15 @@ def _integer_net(c, blocks, seed, density=0.002):
     return net
 
 
-@pytest.mark.parametrize("mf", ["32", "16", "16e", "16s"])
+@pytest.mark.parametrize("mf", ["32", "16", "16e"])
 @pytest.mark.parametrize("shape", [(17, 8, 8), (2, 6, 7)])
 def test_tower_forms_exact_on_integers(mf, shape, net_sw):
     """Both MFMA forms of the fused tower ("tower_mf": 32x32x16, 16x16x32; "16e": the
-    16x16x32 form with the swap epilogue, "tower_epi" 1; "16s": the swizzled activation
-    layout, "tower_epi" 3) on an integer network, 2 residual blocks, ragged board counts:
-    equal to float64 exactly."""
+    16x16x32 form with the swap epilogue, "tower_epi" 1) on an integer network, 2 residual
+    blocks, ragged board counts: equal to float64 exactly."""
     from zeroclone_amd.nets import FoldedValueNetwork, MfmaValueNetwork
     net_sw("tower_mf", int(mf[:2]))
-    net_sw("tower_epi", 1 if mf.endswith("e") else 3 if mf.endswith("s") else 0)
+    net_sw("tower_epi", 1 if mf.endswith("e") else 0)
     c, h, w = shape
     vnet = _integer_net(c, 2, seed=h * 10 + int(mf[:2]))
     net = MfmaValueNetwork(vnet)
@@ -248,7 +246,7 @@ def _integer_head(vnet, hw, seed):
     return vnet
 
 
-@pytest.mark.parametrize("mf", ["32", "16", "16s"])
+@pytest.mark.parametrize("mf", ["32", "16"])
 @pytest.mark.parametrize("shape", [(17, 8, 8), (2, 6, 7)])
 def test_value_head_exact_on_integers(mf, shape, net_sw):
     """The value head (avg-pool, Linear(128, 1), + bias) on an integer network: its pre-tanh
@@ -258,9 +256,7 @@ def test_value_head_exact_on_integers(mf, shape, net_sw):
     tanh (the product path) the values equal float64 tanh of that sum within tanhf's precision.
     A head without its bias or without its Linear would fail every one of these."""
     from zeroclone_amd.nets import FoldedValueNetwork, MfmaValueNetwork
-    net_sw("tower_mf", int(mf[:2]))
-    net_sw("tower_epi", 3 if mf.endswith("s") else 0)
-    mf = mf[:2]
+    net_sw("tower_mf", int(mf))
     c, h, w = shape
     vnet = _integer_head(_integer_net(c, 2, seed=h * 7 + int(mf)), h * w, seed=int(mf) + h)
     xs = [(torch.rand(n, c, h, w) < 0.3).half() for n in (1, 5, 131)]
@@ -320,14 +316,12 @@ def _integer_pv_net(c, h, w, nl, seed, head="linear"):
     return net
 
 
-@pytest.mark.parametrize("epi", [0, 3])
 @pytest.mark.parametrize("shape", [(37, 17, 8, 8, 4096), (53, 2, 6, 7, 7)])
-def test_policy_head_exact_on_integers(shape, epi, net_sw):
+def test_policy_head_exact_on_integers(shape):
     """TowerPolicy (the 1x1 policy conv fused into the tower launch, zc_net_tower_policy_async)
     and the policy Linear on an integer PolicyValueNetwork: the conv's ReLU output and the
     logits equal float64 exactly (2 residual blocks, ragged last tiles)."""
     from zeroclone_amd.nets import MfmaPolicyValueNetwork
-    net_sw("tower_epi", epi)   # 3: the swizzled activation layout
     n, c, h, w, nl = shape
     net = _integer_pv_net(c, h, w, nl, seed=n)
     mnet = MfmaPolicyValueNetwork(net)

@@ -504,38 +504,34 @@ __device__ __forceinline__ void tower_mfma16_swz(const _Float16 *lds, int src, c
                                                  h8 (&a)[NA], int l16, const int (&pyx)[NN], int q,
                                                  f4x (&acc)[2][NN]) {
     constexpr int J = KC / 2, JN = KCN / 2;
-    // 32-bit LDS byte addresses (the dynamic LDS starts at 0: nothing static in the kernel), so
-    // that k-step j's address is one v_xor of 64 j and nothing else
-    typedef const __attribute__((address_space(3))) h8 lds_h8;
-    const uint32_t lb = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) _Float16 *)lds;
-    auto rows = [&](int tap, uint32_t (&xo)[NN]) {
+    auto rows = [&](int tap, int (&xo)[NN]) {
         const int dy = tap / 3 - 1, dx = tap % 3 - 1;
-        const int qh = (q ^ hsw(l16 + dy * W + dx)) << 4;  // the same for every N tile (16 n = 0 mod 8)
+        const int qh = (q ^ hsw(l16 + dy * W + dx)) << 3;  // the same for every N tile (16 n = 0 mod 8)
 #pragma unroll
         for (int n = 0; n < NN; ++n) {
             const int sy = (pyx[n] >> 8) + dy, sx = (pyx[n] & 255) + dx;
             const bool sv = (unsigned)sy < (unsigned)H && (unsigned)sx < (unsigned)W;
             const int row = l16 + (n * 16 + dy * W + dx);
-            xo[n] = lb + (uint32_t)((sv ? src + row : ZERO + (row & 7)) * (kSwzLD * 2) + qh);
+            xo[n] = (sv ? src + row : ZERO + (row & 7)) * kSwzLD + qh;
         }
     };
-    uint32_t xo[NN];
+    int xo[NN];
     rows(0, xo);
     h8 x[NN], xn[NN];
 #pragma unroll
-    for (int n = 0; n < NN; ++n) x[n] = *(lds_h8 *)(uintptr_t)xo[n];
+    for (int n = 0; n < NN; ++n) x[n] = *(const h8 *)(lds + xo[n]);
 #pragma unroll
     for (int tap = 0; tap < 9; ++tap) {
-        uint32_t xon[NN];
+        int xon[NN];
         if (tap + 1 < 9) rows(tap + 1, xon);
 #pragma unroll
         for (int j = 0; j < J; ++j) {
             if (j + 1 < J) {
 #pragma unroll
-                for (int n = 0; n < NN; ++n) xn[n] = *(lds_h8 *)(uintptr_t)(xo[n] ^ (uint32_t)((j + 1) * 64));
+                for (int n = 0; n < NN; ++n) xn[n] = *(const h8 *)(lds + (xo[n] ^ ((j + 1) * 32)));
             } else if (tap + 1 < 9) {
 #pragma unroll
-                for (int n = 0; n < NN; ++n) xn[n] = *(lds_h8 *)(uintptr_t)xon[n];
+                for (int n = 0; n < NN; ++n) xn[n] = *(const h8 *)(lds + xon[n]);
             }
             __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
