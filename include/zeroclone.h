@@ -710,6 +710,11 @@ int zc_debug_phase_cycles_games(zc_engine *eng, int32_t n_games, int64_t *out);
  * sum — tests only).  Returns the previous value in *old (may be NULL); ZC_EINVAL for an
  * unknown name or value. */
 int zc_debug_net_switch(const char *name, int32_t value, int32_t *old);
+/* Launch-timeline stamps of the Connect4 self-play launches (the pooled launch's tail,
+ * tools/launch_tail.py): with d_buf != NULL (device, 4 x uint64 per game of the engine),
+ * every later zc_c4_selfplay(_pooled)_async writes per game {s_memrealtime at its wave's
+ * start, at the start of its last move, at its end, moves played}; NULL switches them off. */
+int zc_debug_c4_launch_stamps(zc_engine *eng, uint64_t *d_buf);
 
 #ifdef __cplusplus
 }

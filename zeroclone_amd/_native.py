@@ -283,6 +283,7 @@ SIGNATURES = [
     ("zc_debug_phase_cycles", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, P(ctypes.c_int64)]),
     ("zc_debug_phase_cycles_games", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, P(ctypes.c_int64)]),
     ("zc_debug_net_switch", ctypes.c_int, [ctypes.c_char_p, ctypes.c_int32, P(ctypes.c_int32)]),
+    ("zc_debug_c4_launch_stamps", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
     ("zc_debug_c4_rollout", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p,
                                            ctypes.c_void_p, ctypes.c_void_p]),
 ]

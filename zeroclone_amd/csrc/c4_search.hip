@@ -1435,12 +1435,15 @@ __global__ __launch_bounds__(kSearchWaves * kBlock, 4) void c4_selfplay_kernel(S
     int status = 0;
     int finished = 0;
     int mv = 0;
+    uint64_t t_start = 0, t_last = 0;
+    if (p.tstamps) t_start = t_last = __builtin_amdgcn_s_memrealtime();
     for (; mv < p.moves; ++mv) {
         if (p.ticket) {  // pooled run: the next move only while the shared budget lasts
             int tk = 0;
             if (lane == 0) tk = atomicAdd(p.ticket, 1);
             if (uni(tk) >= p.budget) break;
         }
+        if (p.tstamps) t_last = __builtin_amdgcn_s_memrealtime();
         zc_c4_state root = p.roots[gl];
         uint64_t s0 = uni64(root.stones[0]), s1 = uni64(root.stones[1]);
         int turn = uni(root.turn);
@@ -1474,6 +1477,13 @@ __global__ __launch_bounds__(kSearchWaves * kBlock, 4) void c4_selfplay_kernel(S
         wave_mem_order();
     }
     if (p.ticket && lane == 0) atomicMax(p.ticket + 1, mv);
+    if (p.tstamps && lane == 0) {
+        uint64_t *ts = p.tstamps + 4 * (size_t)g;
+        ts[0] = t_start;
+        ts[1] = t_last;
+        ts[2] = __builtin_amdgcn_s_memrealtime();
+        ts[3] = (uint64_t)mv;
+    }
     // steps this game did not reach (budget spent, or a bad root): skipped by the recording
     for (int k = mv + (int)lane; k < p.moves; k += kBlock) {
         const size_t o = (size_t)k * p.n_games + gl;

@@ -27,6 +27,9 @@
 namespace zc {
 namespace {
 
+// meta[j] bit 31: leaf j's walk created its node (its moves are generated after the walks)
+constexpr uint32_t kMetaCreated = 0x80000000u;
+
 // flushes: 0 = the root alone, then batches of bs
 __device__ __forceinline__ int flush_leaves(const ChessParams &p, int f) {
     if (f == 0) return 1;
@@ -35,8 +38,16 @@ __device__ __forceinline__ int flush_leaves(const ChessParams &p, int f) {
 
 // One PUCT walk + expansion; returns the leaf, its depth, and the edge slots of its path
 // in lanes 1..depth of pathv.  Applies the virtual loss on every edge it takes.
+//
+// The expansion is DEFERRED: the new node gets its id, position, parent, depth and
+// `evaluated = 0` here — everything a later walk of the same flush looks at (it stops at a node
+// not yet evaluated) — and *created is set; its legal moves are generated after the flush's
+// walks, every created node of every game in parallel (puct_expand_kernel, one wave each), and
+// committed in creation order (puct_commit_kernel: slot ranges by a prefix sum over the
+// creation order, i.e. exactly the ranges the serial create_node would have taken).  Nothing
+// reads a node's moves before its first backup, so the tree is the serial one.
 __device__ int puct_walk(const ChessParams &p, const CTree &t, CLds &L, int &nnodes, int &slots, int &status,
-                         int &ldepth, uint32_t &pathv, Counters &cn) {
+                         int &ldepth, uint32_t &pathv, Counters &cn, bool &created) {
     const uint32_t lane = lane_id();
     int node = 0, depth = 0;
     pathv = 0;
@@ -121,8 +132,19 @@ __device__ int puct_walk(const ChessParams &p, const CTree &t, CLds &L, int &nno
             status = ZC_STATUS_CAPACITY;
             break;
         }
-        create_node(t, L, id, node, best, depth, slots, status);
-        if (lane == 0) t.ch[s] = (uint16_t)id;
+        ChessNode *C = &t.nodes[id];  // the record without its moves (puct_commit_kernel adds them)
+        if (lane < 18) ((uint32_t *)&C->st)[lane] = ((const uint32_t *)&L.st)[lane];
+        if (lane == 0) {
+            C->base = 0;
+            C->nmoves = 0;
+            C->nu = 0;
+            C->parent = (uint16_t)node;
+            C->pact = (uint16_t)best;
+            C->depth = (uint16_t)depth;
+            C->evaluated = 0;
+            t.ch[s] = (uint16_t)id;
+        }
+        created = true;
         cn.add(cn.expansions, 1);
         cn.add(cn.depth_sum, depth);
         wave_sync_mem();
@@ -178,15 +200,15 @@ __global__ __launch_bounds__(64) void puct_select_kernel(ChessParams p) {
     for (; j < nb && !status; ++j) {
         int d = 0;
         uint32_t pathv = 0;
-        const int leaf = p.flush == 0 ? 0 : puct_walk(p, t, L, nnodes, slots, status, d, pathv, cn);
+        bool created = false;
+        const int leaf = p.flush == 0 ? 0 : puct_walk(p, t, L, nnodes, slots, status, d, pathv, cn, created);
         if (lane < (uint32_t)kChessPath) paths[(size_t)j * kChessPath + lane] = pathv;
-        if (lane == 0) meta[j] = (uint32_t)leaf | ((uint32_t)d << 16);
+        if (lane == 0) meta[j] = (uint32_t)leaf | ((uint32_t)d << 16) | (created ? kMetaCreated : 0u);
     }
     if (status) nb = 0;
     wave_sync_mem();
     if (lane == 0) {
         ctl[cNodes] = nnodes;
-        ctl[cSlots] = slots;
         ctl[cStatus] = status;
         ctl[cNb] = nb;
         ctl[cExp] += cn.expansions;
@@ -195,7 +217,7 @@ __global__ __launch_bounds__(64) void puct_select_kernel(ChessParams p) {
     }
     const size_t obase = (size_t)gl * p.bs;
     for (int k = 0; k < nb; ++k) {
-        const ChessNode *N = &t.nodes[uni(meta[k]) & 0xFFFFu];
+        const ChessNode *N = &t.nodes[uni(meta[k]) & 0xFFFFu];  // (the position is in the record already)
         if (p.leaves && lane < 18) ((uint32_t *)&p.leaves[obase + k])[lane] = ((const uint32_t *)&N->st)[lane];
         if (p.planes) {
             const uint32_t pc = N->st.board[lane];
@@ -220,6 +242,95 @@ __global__ __launch_bounds__(64) void puct_select_kernel(ChessParams p) {
     }
 }
 
+// The deferred expansions of a flush, one wave per (leaf, game) whose walk created a node: its
+// legal moves (order, capture values, the check flag of a position without moves: create_node's
+// generation) into the per-leaf scratch.
+__global__ __launch_bounds__(64) void puct_expand_kernel(ChessParams p) {
+    __shared__ CLds L;
+    const int j = blockIdx.x, gl = blockIdx.y;
+    if (gl >= p.n_games) return;
+    const int g = p.first_game + gl;
+    const int32_t *ctl = p.ca.ctl + (size_t)g * kCtlWords;
+    if (j >= uni(ctl[cNb])) return;
+    const uint32_t mt = uni(p.ca.meta[(size_t)g * p.max_batch + j]);
+    if (!(mt & kMetaCreated)) return;
+    const CTree t = ctree(p, g);
+    const uint32_t lane = lane_id();
+    const ChessNode *C = &t.nodes[mt & 0xFFFFu];
+    if (lane < 18) ((uint32_t *)&L.st)[lane] = ((const uint32_t *)&C->st)[lane];
+    wave_sync_mem();
+    const NodeGen gen = create_node_gen(L);
+    const size_t x = (size_t)g * p.max_batch + j;
+    uint16_t *xm = p.ca.xmv + x * ZC_CHESS_MAX_MOVES;
+    for (int k = (int)lane; k < gen.n; k += 64) xm[k] = L.s.legal[k];
+    if (lane == 0) {
+        p.ca.xinfo[2 * x] = gen.n;
+        p.ca.xinfo[2 * x + 1] = (int32_t)(((uint32_t)gen.mat & 0xFFFFu) | ((uint32_t)gen.check << 16));
+    }
+}
+
+// ... and their commit, one wave per (leaf, game) again: the node's slot range is the slots in
+// use before the flush plus the move counts of the nodes created before it in this flush
+// (create_node_take's arithmetic, capacity included), then create_node_commit's writes.  The
+// last created node of the game publishes the new slot count.
+__global__ __launch_bounds__(64) void puct_commit_kernel(ChessParams p) {
+    const int j = blockIdx.x, gl = blockIdx.y;
+    if (gl >= p.n_games) return;
+    const int g = p.first_game + gl;
+    int32_t *ctl = p.ca.ctl + (size_t)g * kCtlWords;
+    const int nb = uni(ctl[cNb]);
+    if (j >= nb) return;
+    const uint32_t *meta = p.ca.meta + (size_t)g * p.max_batch;
+    const uint32_t mt = uni(meta[j]);
+    if (!(mt & kMetaCreated)) return;
+    const CTree t = ctree(p, g);
+    const uint32_t lane = lane_id();
+    const size_t x0 = (size_t)g * p.max_batch;
+    // the move counts of the nodes created before this one (leaves i < j), and whether a node
+    // was created after it (leaves j < i < nb)
+    int before = 0;
+    bool later = false;
+    for (int b = 0; b < nb; b += 64) {
+        const int i = b + (int)lane;
+        const bool cr = i < nb && (meta[min(i, nb - 1)] & kMetaCreated);
+        if (cr && i < j) before += max(p.ca.xinfo[2 * (x0 + i)], 0);
+        later |= cr && i > j;
+    }
+    for (int o = 32; o > 0; o >>= 1) before += __shfl_xor(before, o);
+    const bool last = __ballot(later) == 0ull;
+    const int slots0 = uni(ctl[cSlots]);
+    int n = uni(p.ca.xinfo[2 * (x0 + j)]);
+    const uint32_t mc = (uint32_t)uni(p.ca.xinfo[2 * (x0 + j) + 1]);
+    const int base = slots0 + before;
+    int status = 0;
+    if (n < 0) {
+        status = ZC_STATUS_CAPACITY;
+        n = 0;
+    }
+    if ((int64_t)base + n > t.S) {
+        status = ZC_STATUS_CAPACITY;
+        n = 0;
+    }
+    const uint16_t *xm = p.ca.xmv + (x0 + j) * ZC_CHESS_MAX_MOVES;
+    for (int k = (int)lane; k < n; k += 64) {
+        t.mv[base + k] = xm[k];
+        t.ut[base + k] = (uint8_t)k;
+        t.ch[base + k] = 0xFFFF;
+        t.na[base + k] = 0;
+        t.w[base + k] = 0.0;
+    }
+    ChessNode *C = &t.nodes[mt & 0xFFFFu];
+    if (lane == 0) {
+        C->base = (uint32_t)base;
+        C->nmoves = (uint16_t)n;
+        C->nu = (uint16_t)n;
+        C->material = (int16_t)(mc & 0xFFFFu);
+        C->check = (mc >> 16) & 1u;
+        if (status) ctl[cStatus] = status;
+        if (last) ctl[cSlots] = base + n;  // the flush's last created node
+    }
+}
+
 __global__ __launch_bounds__(64) void puct_backup_kernel(ChessParams p) {
     const int gl = blockIdx.x;
     if (gl >= p.n_games) return;
@@ -234,7 +345,7 @@ __global__ __launch_bounds__(64) void puct_backup_kernel(ChessParams p) {
     const uint2 key = make_uint2((uint32_t)p.seed, (uint32_t)(p.seed >> 32));
     for (int j = 0; j < nb; ++j) {
         const uint32_t mt = uni(meta[j]);
-        const int node = (int)(mt & 0xFFFFu), d = (int)(mt >> 16);
+        const int node = (int)(mt & 0xFFFFu), d = (int)((mt >> 16) & 0xFFu);
         ChessNode *N = &t.nodes[node];
         const int nm = uni((int)N->nmoves);
         const size_t li = (size_t)gl * (p.leaf_rows ? p.leaf_rows : p.bs) + j;
@@ -377,6 +488,10 @@ void launch_chess_puct_begin(const ChessParams &p, hipStream_t s) {
 }
 void launch_chess_puct_select(const ChessParams &p, hipStream_t s) {
     hipLaunchKernelGGL(puct_select_kernel, dim3(p.n_games), dim3(64), 0, s, p);
+    if (p.flush > 0) {  // flush 0 evaluates the root alone: nothing is created
+        hipLaunchKernelGGL(puct_expand_kernel, dim3(p.bs, p.n_games), dim3(64), 0, s, p);
+        hipLaunchKernelGGL(puct_commit_kernel, dim3(p.bs, p.n_games), dim3(64), 0, s, p);
+    }
 }
 void launch_chess_puct_backup(const ChessParams &p, hipStream_t s) {
     hipLaunchKernelGGL(puct_backup_kernel, dim3(p.n_games), dim3(64), 0, s, p);

@@ -64,7 +64,7 @@ int dalloc(zc_engine *e, T **p, size_t count) {
 }
 
 void free_chess(zc::ChessArena &c) {
-    void *ptrs[] = {c.nodes, c.mv, c.ut, c.ch, c.na, c.w, c.prior, c.ctl, c.paths, c.meta, c.roots};
+    void *ptrs[] = {c.nodes, c.mv, c.ut, c.ch, c.na, c.w, c.prior, c.ctl, c.paths, c.meta, c.roots, c.xmv, c.xinfo};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
     c = zc::ChessArena{};
@@ -224,6 +224,7 @@ zc::SearchParams make_params(zc_engine *e, int32_t first, int32_t n, const zc_c4
     p.a = e->a;
     p.max_batch = e->cfg.max_batch;
     p.stamp = e->stamp;
+    p.tstamps = e->tstamps;
     p.philox = e->rollout_mode == ZC_ROLLOUT_PHILOX;
     p.philox_seed = e->rollout_seed;
     return p;
@@ -877,6 +878,8 @@ int ensure_chess(zc_engine *e) {
     if (!rc) rc = dalloc(e, &n.paths, G * (size_t)e->cfg.max_batch * zc::kChessPath);
     if (!rc) rc = dalloc(e, &n.meta, G * (size_t)e->cfg.max_batch);
     if (!rc) rc = dalloc(e, &n.roots, G);
+    if (!rc) rc = dalloc(e, &n.xmv, G * (size_t)e->cfg.max_batch * ZC_CHESS_MAX_MOVES);
+    if (!rc) rc = dalloc(e, &n.xinfo, G * (size_t)e->cfg.max_batch * 2);
     if (!rc && hipMemset(n.ctl, 0, G * zc::kCtlWords * sizeof(int32_t)) != hipSuccess) rc = fail(ZC_EHIP, "memset failed");
     if (rc) {
         free_chess(n);
@@ -1807,6 +1810,13 @@ int zc_debug_rng_copy(zc_engine *eng, int32_t first, int32_t n, void *d_buf, int
     const size_t rb = (size_t)n * zc::kRingWords * sizeof(uint32_t), pb = (size_t)n * 2 * sizeof(uint64_t);
     ZC_HIP(hipMemcpyAsync(restore ? ring : b, restore ? b : ring, rb, hipMemcpyDeviceToDevice, s));
     ZC_HIP(hipMemcpyAsync(restore ? pos : b + rb, restore ? b + rb : pos, pb, hipMemcpyDeviceToDevice, s));
+    return ZC_OK;
+}
+
+int zc_debug_c4_launch_stamps(zc_engine *eng, uint64_t *d_buf) {
+    if (!eng) return fail(ZC_EINVAL, "null argument");
+    std::lock_guard<std::mutex> lk(eng->mu);
+    eng->tstamps = d_buf;
     return ZC_OK;
 }
 

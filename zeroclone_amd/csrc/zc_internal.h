@@ -105,6 +105,10 @@ struct SearchParams {
     // [G][sims] and the rollout words of every flush [G][ceil(sims / bs)]
     int8_t *walk_vals;
     uint32_t *walk_words;
+    // launch-timeline diagnostic (zc_debug_c4_launch_stamps; null: off): per game of a
+    // self-play launch {s_memrealtime at the wave's start, at its last move's start, at its end,
+    // moves played}
+    uint64_t *tstamps;
 };
 
 struct ExtParams {
@@ -158,6 +162,11 @@ struct ChessArena {
     uint32_t *paths = nullptr;   // [G][max_batch][kChessPath] slot of the edge into each level
     uint32_t *meta = nullptr;    // [G][max_batch] leaf node | depth << 16
     zc_chess_state *roots = nullptr;  // [G]
+    // the PUCT select's deferred expansions (chess_puct.hip): per leaf of the flush that created
+    // its node, the node's generated moves [G][max_batch][256] and {#moves (-1: overflow),
+    // material | check << 16} [G][max_batch][2], between the expand and commit kernels
+    uint16_t *xmv = nullptr;
+    int32_t *xinfo = nullptr;
     int64_t S = 0;
 };
 
@@ -393,6 +402,7 @@ struct zc_engine {
     void *a_block = nullptr;  // the one device allocation `a` and io_d are carved from
     int64_t bytes = 0;
     int stamp = 0;
+    uint64_t *tstamps = nullptr;  // zc_debug_c4_launch_stamps: device buffer, 4 words per game
     int rollout_mode = 0;        // ZC_ROLLOUT_EXACT / ZC_ROLLOUT_PHILOX
     uint64_t rollout_seed = 0;
     zc::ChessArena ca;  // allocated on the first chess search
