@@ -218,6 +218,9 @@ int zc_c4_ext_select(zc_engine *eng, int32_t first_game, int32_t n_games, int32_
                      void *hip_stream);
 #define ZC_F32 0
 #define ZC_F16 1
+/* planes only (zc_chess_puct_select): fp16 in the MFMA tower's input layout, NHWC
+ * [n][64 squares][32 channels] (the 17 planes, then zeros) — no separate conversion launch */
+#define ZC_F16_NHWC32 2
 /* Backprop of flush `flush` (mcts.cpp:80-100 in pending order): d_values[i*bs + j] is the
  * value of leaf j for ITS side to move, as Value.batch returns it. */
 int zc_c4_ext_backup(zc_engine *eng, int32_t first_game, int32_t n_games, int32_t flush, const double *d_values,
@@ -447,7 +450,8 @@ int zc_chess_pooled_max_games(int32_t hist_cap, int32_t *out);
  * ceil((sims - 1) / batch_size) flushes of up to batch_size leaves: zc_chess_puct_flushes.
  * select exports leaves/planes as zc_chess_ext_select; backup takes per leaf slot the value
  * for the leaf's side to move and 4096 policy logits indexed from*64 + to (logits_dtype
- * ZC_F32 / ZC_F16); end picks the move with the most visits (temperature 0) or samples
+ * ZC_F32 / ZC_F16, or ZC_F16_NHWC32: the tower's input layout straight away); end picks
+ * the move with the most visits (temperature 0) or samples
  * proportionally to N^(1/temperature), and writes root visits (and, optionally, the root
  * priors after noise, float [n][ZC_CHESS_MAX_MOVES]). */
 int zc_chess_puct_flushes(int32_t sims, int32_t batch_size);
@@ -712,7 +716,7 @@ int zc_debug_phase_cycles_games(zc_engine *eng, int32_t n_games, int64_t *out);
 int zc_debug_net_switch(const char *name, int32_t value, int32_t *old);
 /* Launch-timeline stamps of the Connect4 self-play launches (the pooled launch's tail,
  * tools/launch_tail.py): with d_buf != NULL (device, 4 x uint64 per game of the engine),
- * every later zc_c4_selfplay(_pooled)_async writes per game {s_memrealtime at its wave's
+ * every later Connect4 self-play launch (zc_c4_selfplay_async, its pooled form) writes per game {s_memrealtime at its wave's
  * start, at the start of its last move, at its end, moves played}; NULL switches them off. */
 int zc_debug_c4_launch_stamps(zc_engine *eng, uint64_t *d_buf);
 

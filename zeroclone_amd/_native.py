@@ -27,6 +27,7 @@ ROLLOUT_PHILOX = 1  # ZC_ROLLOUT_PHILOX
 ZC_STATUS_BAD_STATE = 2
 ZC_F32 = 0
 ZC_F16 = 1
+ZC_F16_NHWC32 = 2   # planes only: fp16 NHWC [n][h*w][32], the MFMA tower's input layout
 
 
 class C4State(ctypes.Structure):
@@ -653,9 +654,12 @@ class NativeEngine:
                                         int(batch_size), float(alpha), float(eps), int(seed) & (2**64 - 1),
                                         ctypes.c_void_p(d_search_no or None), ctypes.c_void_p(stream or None)))
 
-    def chess_puct_select(self, first_game, n, flush, d_leaves=0, d_planes=0, planes_f16=True, d_counts=0, stream=0):
+    def chess_puct_select(self, first_game, n, flush, d_leaves=0, d_planes=0, planes_f16=True, d_counts=0, stream=0,
+                          planes_nhwc=False):
+        """planes_nhwc: fp16 planes in the tower's input layout [n*bs][64][32] (ZC_F16_NHWC32)."""
+        code = ZC_F16_NHWC32 if planes_nhwc else ZC_F16 if planes_f16 else ZC_F32
         check(lib().zc_chess_puct_select(self._h, first_game, n, int(flush), ctypes.c_void_p(d_leaves or None),
-                                         ctypes.c_void_p(d_planes or None), ZC_F16 if planes_f16 else ZC_F32,
+                                         ctypes.c_void_p(d_planes or None), code,
                                          ctypes.c_void_p(d_counts or None), ctypes.c_void_p(stream or None)))
 
     def chess_puct_backup(self, first_game, n, flush, d_values, d_logits, logits_f16=False, stream=0, rows=0):

@@ -229,14 +229,30 @@ __global__ __launch_bounds__(64) void puct_select_kernel(ChessParams p) {
                     break;
                 }
             const int turn = N->st.turn, castle = N->st.castle;
-            for (int q = 0; q < 17; ++q) {
-                float v;
-                if (q < 12) v = q == which ? 1.0f : 0.0f;
-                else if (q == 12) v = turn == 0 ? 1.0f : 0.0f;
-                else v = (castle >> (q - 13)) & 1 ? 1.0f : 0.0f;
-                const size_t o = ((obase + k) * 17 + q) * 64 + lane;
-                if (p.planes_f16) ((__half *)p.planes)[o] = __float2half(v);
-                else ((float *)p.planes)[o] = v;
+            if (p.planes_f16 == 2) {  // ZC_F16_NHWC32: lane = square, its 32 channels (17 planes, zeros)
+                typedef _Float16 h8_t __attribute__((ext_vector_type(8)));
+                h8_t v8[4];
+#pragma unroll
+                for (int q = 0; q < 32; ++q) {
+                    float v = 0.0f;
+                    if (q < 12) v = q == which ? 1.0f : 0.0f;
+                    else if (q == 12) v = turn == 0 ? 1.0f : 0.0f;
+                    else if (q < 17) v = (castle >> (q - 13)) & 1 ? 1.0f : 0.0f;
+                    v8[q >> 3][q & 7] = (_Float16)v;
+                }
+                h8_t *o = (h8_t *)((_Float16 *)p.planes + ((obase + k) * 64 + lane) * 32);
+#pragma unroll
+                for (int c = 0; c < 4; ++c) o[c] = v8[c];
+            } else {
+                for (int q = 0; q < 17; ++q) {
+                    float v;
+                    if (q < 12) v = q == which ? 1.0f : 0.0f;
+                    else if (q == 12) v = turn == 0 ? 1.0f : 0.0f;
+                    else v = (castle >> (q - 13)) & 1 ? 1.0f : 0.0f;
+                    const size_t o = ((obase + k) * 17 + q) * 64 + lane;
+                    if (p.planes_f16) ((__half *)p.planes)[o] = __float2half(v);
+                    else ((float *)p.planes)[o] = v;
+                }
             }
         }
     }

@@ -1299,7 +1299,8 @@ int zc_chess_puct_begin(zc_engine *eng, int32_t first, int32_t n, const zc_chess
 int zc_chess_puct_select(zc_engine *eng, int32_t first, int32_t n, int32_t flush, zc_chess_state *d_leaves,
                          void *d_planes, int32_t planes_dtype, int32_t *d_counts, void *hip_stream) {
     if (!eng) return fail(ZC_EINVAL, "null argument");
-    if (planes_dtype != ZC_F32 && planes_dtype != ZC_F16) return fail(ZC_EINVAL, "planes_dtype must be ZC_F32 or ZC_F16");
+    if (planes_dtype != ZC_F32 && planes_dtype != ZC_F16 && planes_dtype != ZC_F16_NHWC32)
+        return fail(ZC_EINVAL, "planes_dtype must be ZC_F32, ZC_F16 or ZC_F16_NHWC32");
     std::lock_guard<std::mutex> lk(eng->mu);
     if (int r = check_px(eng, first, n, flush, true)) return r;
     if (!n) return ZC_OK;
@@ -1308,7 +1309,7 @@ int zc_chess_puct_select(zc_engine *eng, int32_t first, int32_t n, int32_t flush
     p.flush = flush;
     p.leaves = d_leaves;
     p.planes = d_planes;
-    p.planes_f16 = planes_dtype == ZC_F16;
+    p.planes_f16 = planes_dtype == ZC_F16 ? 1 : planes_dtype == ZC_F16_NHWC32 ? 2 : 0;
     p.counts = d_counts;
     zc::launch_chess_puct_select(p, (hipStream_t)hip_stream);
     ZC_HIP(hipGetLastError());

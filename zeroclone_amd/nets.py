@@ -220,17 +220,26 @@ class MfmaValueNetwork:
         tower activation is written."""
         import torch
         from . import _native
-        n, c, h, w = planes.shape
+        if planes.dim() == 3:   # already the tower's input layout, [n, h*w, cpad] fp16 (8x8 boards)
+            n, hw, cp = planes.shape
+            h = w = 8
+            if hw != 64 or cp != self.cpad or planes.dtype != torch.float16 or not planes.is_contiguous():
+                raise ValueError(f"NHWC planes must be contiguous fp16 [n, 64, {self.cpad}]")
+        else:
+            n, c, h, w = planes.shape
+            if c != self.in_planes or planes.dtype != torch.float16:
+                raise ValueError("planes must be fp16 [n, in_planes, h, w]")
         P = pout.shape[-1] if pout.dim() == 3 else 0
-        if c != self.in_planes or planes.dtype != torch.float16:
-            raise ValueError("planes must be fp16 [n, in_planes, h, w]")
         if P not in (32, 64) or pout.shape != (n, h * w, P) or pout.dtype != torch.float16 or not pout.is_contiguous():
             raise ValueError("pout must be contiguous fp16 [n, h*w, 32 or 64]")
-        planes = planes.contiguous()
         x0, _, _, _, vals = self._buffers(n, h * w)
         s = ctypes_stream(self.dev)
         L = _native.lib()
-        _native.check(L.zc_net_planes_to_nhwc_async(n, c, h * w, self.cpad, planes.data_ptr(), x0.data_ptr(), s))
+        if planes.dim() == 3:
+            x0 = planes
+        else:
+            planes = planes.contiguous()
+            _native.check(L.zc_net_planes_to_nhwc_async(n, c, h * w, self.cpad, planes.data_ptr(), x0.data_ptr(), s))
         _native.check(L.zc_net_tower_policy_ex_async(n, h, w, self.cpad, len(self.wp), x0.data_ptr(),
                                                      self.wall.data_ptr(), self.ball.data_ptr(), self.fcw.data_ptr(),
                                                      self.fcb, vals.data_ptr(), pw.data_ptr(), pb.data_ptr(), P,
@@ -367,7 +376,12 @@ class MfmaPolicyValueNetwork:
 
     def __call__(self, planes, fused: bool = True):
         import torch
-        n, _, h, w = planes.shape
+        if planes.dim() == 3:   # NHWC planes in the tower's input layout (ChessPuctSearch(planes_nhwc=True))
+            if not self.conv_head:
+                raise ValueError("NHWC planes need the convolutional head")
+            n, h, w = planes.shape[0], 8, 8
+        else:
+            n, _, h, w = planes.shape
         if self.conv_head:   # the logits straight from the tower launch: [n, 64 from, 64 to]
             key = (n, h * w)
             if key not in self._pout:

@@ -515,7 +515,10 @@ class ChessSelfPlay:
                 self.value_fn = [NetValue(net.replica() if hasattr(net, "replica") else net) for _ in range(streams)]
         if puct_net is not None:
             from .valued import ChessPuctSearch, PolicyNet
-            self.ps = ChessPuctSearch(self.eng, games, batch_size, seed=puct_seed, leaves=False)
+            # a network with the convolutional head takes the planes in its input layout straight
+            # from the select kernel (no conversion launch per flush)
+            self.ps = ChessPuctSearch(self.eng, games, batch_size, seed=puct_seed, leaves=False,
+                                      planes_nhwc=bool(getattr(puct_net, "conv_head", False)))
             self.net_fn = PolicyNet(puct_net)
             if puct_streams > 1:   # the games in parts on their own streams (valued._split_flushes)
                 self.net_fn = [PolicyNet(puct_net.replica()) for _ in range(puct_streams)]

@@ -326,16 +326,22 @@ class ChessPuctSearch:
 
     def __init__(self, eng: "_native.NativeEngine", n_games: int, batch_size: int = 32, c_puct: float = 1.5,
                  dirichlet_alpha: float = 0.3, dirichlet_eps: float = 0.25, seed: int = 0,
-                 planes_dtype: torch.dtype = torch.float16, leaves: bool = True):
+                 planes_dtype: torch.dtype = torch.float16, leaves: bool = True, planes_nhwc: bool = False):
+        """planes_nhwc: the select kernel writes the planes in the MFMA tower's input layout, fp16
+        [n * batch_size, 64, 32] (17 planes then zeros, square-major), so the network takes them
+        without a conversion launch (MfmaPolicyValueNetwork with the convolutional head)."""
         if batch_size > eng.max_batch:
             raise ValueError(f"batch_size {batch_size} > engine max_batch {eng.max_batch}")
+        if planes_nhwc and planes_dtype != torch.float16:
+            raise ValueError("planes_nhwc needs fp16 planes")
         self.eng, self.n, self.bs = eng, n_games, batch_size
         self.c, self.alpha, self.eps, self.seed = c_puct, dirichlet_alpha, dirichlet_eps, seed
         eng.chess_reserve()   # the tree arena exists before any graph capture
         self.dev = torch.device("cuda", eng.device)
         L = n_games * batch_size
+        self.planes_nhwc = planes_nhwc
         self.leaves = torch.zeros((L, 72), dtype=torch.uint8, device=self.dev) if leaves else None
-        self.planes = torch.zeros((L, 17, 8, 8), dtype=planes_dtype, device=self.dev)
+        self.planes = torch.zeros((L, 64, 32) if planes_nhwc else (L, 17, 8, 8), dtype=planes_dtype, device=self.dev)
         self.counts = torch.zeros(n_games, dtype=torch.int32, device=self.dev)
         self.values = torch.zeros(L, dtype=torch.float64, device=self.dev)
         self.move = torch.zeros(n_games, dtype=torch.int16, device=self.dev)
@@ -363,7 +369,8 @@ class ChessPuctSearch:
         evaluate_backup = _puct_backup(self.bs, e.chess_puct_backup)
         for f in range(nfl):
             e.chess_puct_select(first_game, n, f, p(self.leaves), p(self.planes),
-                                self.planes.dtype == torch.float16, self.counts.data_ptr(), _stream(self.dev))
+                                self.planes.dtype == torch.float16, self.counts.data_ptr(), _stream(self.dev),
+                                planes_nhwc=self.planes_nhwc)
             evaluate_backup(first_game, n, f, net_fn, self.leaves, self.planes, self.counts, self.values,
                             _stream(self.dev))
         e.chess_puct_end(first_game, n, temperature, self.move.data_ptr(), self.na.data_ptr(), self.prior.data_ptr(),
@@ -377,7 +384,7 @@ class ChessPuctSearch:
 
         def select(first, n, f, lv, pv, cv, s):
             e.chess_puct_select(first, n, f, lv.data_ptr() if lv is not None else 0, pv.data_ptr(),
-                                pv.dtype == torch.float16, cv.data_ptr(), s)
+                                pv.dtype == torch.float16, cv.data_ptr(), s, planes_nhwc=self.planes_nhwc)
 
         _split_flushes(self, nfl, fns, first_game, select, _puct_backup(self.bs, e.chess_puct_backup))
 
