@@ -258,3 +258,32 @@ def test_rows_per_game_only_for_the_roots_flush(eng):
     lg = torch.zeros((64, 4096), dtype=torch.float16, device="cuda")
     rc = lib().zc_chess_puct_backup_ex(eng._h, 0, 1, 1, v.data_ptr(), lg.data_ptr(), 1, 1, None)
     assert rc != 0
+
+
+@pytest.mark.parametrize("k", [1, 4])
+def test_nhwc_planes_equal_the_state_to_tensor_planes(eng, k):
+    """ChessPuctSearch(planes_nhwc=True): the select kernel writes the planes in the MFMA
+    tower's input layout (ZC_F16_NHWC32, [n*bs, 64, 32], the 17 planes then zeros) and the
+    network skips its conversion launch.  The planes are the converted state_to_tensor planes
+    bit for bit, and the search (moves, root visits, priors, counters) equals the one on the
+    [n*bs, 17, 8, 8] planes — one stream and split over 4, through PolicyNet (roots-only flush)."""
+    from zeroclone_amd.nets import MfmaPolicyValueNetwork, PolicyValueNetwork
+    from zeroclone_amd.valued import ChessPuctSearch, PolicyNet
+    torch.manual_seed(11)
+    net = MfmaPolicyValueNetwork(PolicyValueNetwork(head="conv").eval())
+    fens = (FENS * 8)[:23]
+    roots = roots_of(fens)
+    outs, planes = [], []
+    for nhwc in (False, True):
+        ps = ChessPuctSearch(eng, len(fens), 32, seed=6, planes_nhwc=nhwc)
+        fn = PolicyNet(net) if k == 1 else [PolicyNet(net.replica()) for _ in range(k)]
+        mv, na, st = ps.run(roots, 81, fn, temperature=1.0)
+        outs.append((mv.cpu().clone(), na.cpu().clone(), ps.prior.cpu().clone(), st[:, :3].cpu().clone()))
+        planes.append(ps.planes.clone())
+    for x, y in zip(*outs):
+        assert torch.equal(x, y)
+    # the last flush's planes: NCHW [L, 17, 8, 8] -> NHWC [L, 64, 32] zero-padded
+    a = planes[0].reshape(planes[0].shape[0], 17, 64).permute(0, 2, 1)
+    want = torch.zeros_like(planes[1])
+    want[:, :, :17] = a
+    assert torch.equal(planes[1], want)
