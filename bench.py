@@ -582,20 +582,29 @@ def burn_in(sp, max_steps: int = 200, check_every: int = 8) -> int:
     return steps
 
 
-def run_steps(sp, steps: int, warmup: int, world: int = 1, launch: str = "pooled") -> dict:
+def run_steps(sp, steps: int, warmup: int, world: int = 1, launch: str = "pooled", carry: bool = True) -> dict:
     """W untimed moves, then K timed steps (K x G moves) bracketed by barrier + device sync,
     as ONE self-play launch followed by its trajectory recording; HIP events around it on its
     stream.  launch "pooled" (the default, C4SelfPlay.run_pooled): the G games share a budget
     of K x G moves drawn from a device counter, at most 2K per game, every move a full search
     — a throughput schedule (train.py:151-170 itself is lockstep: one move per unfinished
     game per call; each game's moves are exactly its free-run moves); "free"
-    (C4SelfPlay.run): exactly K moves per game, so the launch waits for its slowest game."""
+    (C4SelfPlay.run): exactly K moves per game, so the launch waits for its slowest game.
+    carry (pooled only, zc_c4_selfplay_carry_async): the warmup is a pooled launch too, and
+    each launch's in-flight moves stop at their next flush once its budget is spent and
+    resume in the next launch — the steady state of back-to-back launches: the timed launch
+    finishes the moves the warmup left in flight and leaves its own for the (untimed) drain.
+    Expansions are counted as they are made, so the window's work is what ran inside it."""
     dev = sp.dev
     stream = torch.cuda.current_stream(dev)
     ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
           torch.cuda.Event(enable_timing=True))
+    carry = carry and launch == "pooled"
     if warmup:
-        sp.run(warmup)
+        if carry:
+            sp.run_pooled(warmup * sp.G, 2 * warmup, carry=True)
+        else:
+            sp.run(warmup)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -603,7 +612,7 @@ def run_steps(sp, steps: int, warmup: int, world: int = 1, launch: str = "pooled
     t0 = time.perf_counter()
     ev[0].record(stream)
     if launch == "pooled":
-        res = sp.run_pooled(steps * sp.G, 2 * steps, kernel_done=ev[2])
+        res = sp.run_pooled(steps * sp.G, 2 * steps, kernel_done=ev[2], carry=carry)
     else:
         res = sp.run(steps, kernel_done=ev[2])
     ev[1].record(stream)
@@ -618,6 +627,9 @@ def run_steps(sp, steps: int, warmup: int, world: int = 1, launch: str = "pooled
                & (res != _native.ZC_SLOT_SKIP)).sum().item())
     moves = int(((res != _native.ZC_SLOT_IDLE) & (res != _native.ZC_SLOT_SKIP)).sum().item())
     tot = [int(x) for x in st[:, [0, 1, 2]].sum(0).tolist()]
+    if carry:   # untimed: finish the moves left in flight (the pool's later users search it)
+        sp.drain()
+        torch.cuda.synchronize(dev)
     return {"dt": dt, "launch_ms": ev[0].elapsed_time(ev[2]), "launch_record_ms": ev[0].elapsed_time(ev[1]), "expansions": tot[0], "depth_sum": tot[1],
             "finished": fin, "leaves": tot[2], "moves": moves}
 
@@ -671,8 +683,8 @@ def exchange_positions(local, world: int, sync=lambda: None):
 # the committed rocprofv3 summaries (tools/summarize_profile.py, stamped with the sha256 of the
 # library they profiled): the self-play kernel (HBM bytes per launch from separate FETCH_SIZE /
 # WRITE_SIZE passes, SQ issue counters) and the walk-only replay kernel (tools/prof_walk.py)
-SEARCH_PROFILE = os.path.join("profiles", "r05_c4_search_summary.json")
-WALK_PROFILE = os.path.join("profiles", "r05_walk_summary.json")
+SEARCH_PROFILE = os.path.join("profiles", "r06_c4_search_summary.json")
+WALK_PROFILE = os.path.join("profiles", "r06_walk_summary.json")
 
 
 def lib_sha() -> str:
@@ -716,7 +728,7 @@ def run_rank(args, rank: int, world: int, local: int):
     sp = C4SelfPlay(G, S, c=args.c, batch_size=B, seed=args.seed, rank=rank, device=local, record=True)
     burn = burn_in(sp) if args.burn_in else 0
     snap = pool_snapshot(sp) if (world == 1 and not args.no_cpu_baseline) else None
-    r = run_steps(sp, args.steps, args.warmup, world, launch=args.launch)
+    r = run_steps(sp, args.steps, args.warmup, world, launch=args.launch, carry=not args.no_carry)
     gather = gather_trajectories(sp, world)
     counts, dt_max, kms = reduce_over_ranks([r["expansions"], r["depth_sum"], r["finished"], r["leaves"]], r["dt"],
                                             r["launch_ms"], dev)
@@ -747,6 +759,9 @@ def run_rank(args, rank: int, world: int, local: int):
                                    f"c {args.c}, random_rollout exact-RNG mode, steady state (mixed game ages)",
                        "launch": (f"pooled: each step = {G} moves drawn by the games from one shared budget "
                                   f"(K x {G} per launch, <= 2K per game; every move a full {S}-sim search)"
+                                  + ("; carry: once the budget is spent, in-flight moves stop at their next "
+                                     "flush and resume in the next launch (warmup launch -> timed launch -> "
+                                     "untimed drain), expansions counted as made" if not args.no_carry else "")
                                   if args.launch == "pooled" else f"free: K moves per game per launch"),
                        "games_per_gpu": G, "global_games": G * world, "sims": S, "batch_size": B,
                        "world_size": world, "rank_games": rank_ranges(world, G), "burn_in_steps": burn,
@@ -778,6 +793,14 @@ def run_rank(args, rank: int, world: int, local: int):
             out["extra"][f"launch_{other}"] = {"value": round(ro["expansions"] / ro["dt"], 1), "unit": "expansions/s",
                                                "ms_per_step": round(ro["dt"] / args.steps * 1e3, 3),
                                                "moves": ro["moves"], "expansions": ro["expansions"]}
+            if args.launch == "pooled" and not args.no_carry:   # the same launch without carry-over
+                rn = run_steps(sp, args.steps, 0, launch="pooled", carry=False)
+                out["extra"]["launch_pooled_no_carry"] = {
+                    "value": round(rn["expansions"] / rn["dt"], 1), "unit": "expansions/s",
+                    "ms_per_step": round(rn["dt"] / args.steps * 1e3, 3),
+                    "selfplay_launch_ms": round(rn["launch_ms"], 3), "moves": rn["moves"],
+                    "note": "every in-flight move finished inside the launch: its tail (games finishing the "
+                            "moves started just before the budget ran out, on an emptying device) is timed"}
             lock = out["value"] if args.launch == "free" else out["extra"]["launch_free"]["value"]
             out["extra"]["reference_schedule"] = {
                 "value": lock, "unit": "expansions/s",
@@ -1043,6 +1066,8 @@ def parse_args(argv=None):
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--launch", choices=["pooled", "free"], default="pooled",
                     help="pooled: the games share K x G moves per launch; free: K moves per game")
+    ap.add_argument("--no-carry", action="store_true",
+                    help="pooled launches finish their in-flight moves (no carry-over into the next launch)")
     ap.add_argument("--games", type=int, default=4096, help="games per GPU")
     ap.add_argument("--sims", type=int, default=800)
     ap.add_argument("--batch", type=int, default=32)

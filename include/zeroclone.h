@@ -130,14 +130,40 @@ int zc_c4_selfplay_async(zc_engine *eng, int32_t first_game, int32_t n_games, zc
  * move is exactly the k-th move of zc_c4_selfplay_async (same search, RNG stream, refill):
  * only how many moves each game gets differs (decided by the counter, not deterministic).
  * Steps a game did not reach get result ZC_SLOT_SKIP and move -1 in the [moves_cap][n]
- * outputs; zc_traj_record_async leaves such slots untouched.  d_stats[i].leaves = sims x the
- * moves game i played.  budget <= moves_cap * n_games, < 2^31; n_games <=
+ * outputs; zc_traj_record_async leaves such slots untouched.  d_stats[i].leaves = the
+ * simulations game i ran in this launch.  A move carried over by zc_c4_selfplay_carry_async
+ * is resumed first (no ticket) and finished.  budget <= moves_cap * n_games, < 2^31; n_games <=
  * zc_c4_pooled_max_games (ZC_EINVAL otherwise).  d_ticket: 2 int32 — the
  * counter, then the most moves any game played (the d_reached of zc_traj_record_steps_async). */
 int zc_c4_selfplay_pooled_async(zc_engine *eng, int32_t first_game, int32_t n_games, zc_c4_state *d_roots,
                                 int32_t sims, double c, int32_t batch_size, int32_t moves_cap, int64_t budget,
                                 int32_t *d_ticket, zc_c4_state *d_out_states, int16_t *d_out_moves,
                                 int32_t *d_out_results, zc_game_stats *d_stats, void *hip_stream);
+
+/* zc_c4_selfplay_pooled_async whose in-flight moves CARRY OVER instead of finishing: once the
+ * budget is spent (d_ticket[0] reached it), every game's search stops at its next flush boundary
+ * (batch_size simulations), and its progress — simulations done, tree nodes, and the tree, the
+ * MT19937 stream and the root, which stay in the engine's HBM arena — is kept for the game's
+ * next self-play launch (this one, zc_c4_selfplay_pooled_async or zc_c4_selfplay_async), which
+ * resumes that move first, without a ticket.  The launch's tail — games finishing moves
+ * started just before the budget ran out, on an emptying device — moves into the next launch,
+ * where it runs at full occupancy.  Each game's k-th finished move is still exactly the k-th
+ * move of zc_c4_selfplay_async (the search is cut only between flushes, and resumed with the
+ * same tree and stream).  Outputs as zc_c4_selfplay_pooled_async: the suspended move has no
+ * row (ZC_SLOT_SKIP); d_stats counts the expansions and simulations this launch ran.  Until a
+ * non-carry self-play launch over these games (or zc_c4_carry_discard), entry points that
+ * would search or reseed them (zc_c4_search*, zc_c4_ext_begin, zc_c4_rollouts, zc_rng_seed,
+ * zc_rng_set_state, the c4 debug searches) refuse with ZC_EINVAL. */
+int zc_c4_selfplay_carry_async(zc_engine *eng, int32_t first_game, int32_t n_games, zc_c4_state *d_roots,
+                               int32_t sims, double c, int32_t batch_size, int32_t moves_cap, int64_t budget,
+                               int32_t *d_ticket, zc_c4_state *d_out_states, int16_t *d_out_moves,
+                               int32_t *d_out_results, zc_game_stats *d_stats, void *hip_stream);
+
+/* Drop the carried moves of games [first_game, first_game + n_games) (stream-ordered): their
+ * next search starts afresh from whatever root they are given.  Their MT19937 streams stay
+ * where the dropped searches left them, so those games' moves no longer follow an
+ * uninterrupted run's — for restarting games (C4SelfPlay.start), not for pausing them. */
+int zc_c4_carry_discard(zc_engine *eng, int32_t first_game, int32_t n_games, void *hip_stream);
 
 /* The most games zc_c4_selfplay_pooled_async accepts at this batch size: the games the
  * self-play grid keeps resident on the device at once (occupancy x compute units).  A pooled

@@ -108,3 +108,58 @@ def test_pooled_run_is_a_prefix_of_the_free_run(mode):
         assert a.eng.get_rng_state(g)[1] == b.eng.get_rng_state(g)[1]
     a.close()
     b.close()
+
+
+@pytest.mark.parametrize("mode", ["exact", "philox"])
+def test_carried_moves_resume_to_the_free_run(mode):
+    """zc_c4_selfplay_carry_async: once a launch's budget is spent its in-flight moves stop at a
+    flush boundary and resume in the next launch.  Every ticketed move finishes exactly once
+    (the launches' finished moves, drain included, sum to their budgets), and each game's
+    finished moves, launch after launch, are its free-run moves (states, moves, results) —
+    the carried searches resume with the same tree and stream."""
+    G, S, B, cap = 160, 128, 16, 8
+    budgets = [G * cap // 2, G * cap // 3, G * cap // 2]
+    a = C4SelfPlay(G, S, batch_size=B, seed=13)
+    b = C4SelfPlay(G, S, batch_size=B, seed=13)
+    for sp in (a, b):
+        sp.eng.c4_rollout_mode(mode, 5)
+    total = len(budgets) * cap + 1
+    ra = a.run(total).clone()
+    sa, ma = a._run_states.clone(), a._run_moves.clone()
+    seq = [[] for _ in range(G)]
+    finished, leaves, carried = 0, 0, 0
+    for i, bud in enumerate(budgets + [0]):
+        rb = (b.run_pooled(bud, cap, carry=True) if i < len(budgets) else b.drain()).clone()
+        sb, mb = b._run_states.clone(), b._run_moves.clone()
+        played = rb != 4
+        m = played.sum(0)
+        k = rb.shape[0]
+        assert torch.equal(played, torch.arange(k, device=rb.device)[:, None] < m[None, :])
+        finished += int(m.sum())
+        leaves += int(b.stats[:, 2].sum())
+        if i < len(budgets):
+            carried = max(carried, int(sum(budgets[: i + 1])) - finished)   # in flight now
+            assert b.carry_pending
+            with pytest.raises(RuntimeError):
+                b.step()
+            with pytest.raises(ValueError):   # ZC_EINVAL: the engine refuses as well
+                b.eng.seed(0, list(range(G)))
+        for g in range(G):
+            for j in range(int(m[g])):
+                seq[g].append((int(rb[j, g]), int(mb[j, g]), sb[j, g].tolist()))
+    assert carried > 0                      # moves did carry over
+    assert finished == sum(budgets)         # ... and each finished exactly once
+    assert leaves == sum(budgets) * S       # simulations counted where they ran
+    assert not b.carry_pending
+    for g in range(G):
+        n = len(seq[g])
+        assert n <= total
+        exp = [(int(ra[j, g]), int(ma[j, g]), sa[j, g].tolist()) for j in range(n)]
+        assert seq[g] == exp, g
+    # the drained pool searches again; a restart drops carried moves
+    b.run_pooled(G, 2, carry=True)
+    b.start()
+    assert not b.carry_pending
+    b.step()
+    a.close()
+    b.close()

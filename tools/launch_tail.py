@@ -24,6 +24,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=str, default="20,60")
     ap.add_argument("--reps", type=int, default=2)
+    ap.add_argument("--carry", type=int, default=1, help="carry launches (warmup launch carries moves in)")
+    ap.add_argument("--warmup", type=int, default=2)
     a = ap.parse_args()
     torch.cuda.set_device(0)
     torch.cuda.set_stream(torch.cuda.Stream(torch.device("cuda", 0)))
@@ -35,12 +37,12 @@ def main():
     out = {"burn_in_steps": burn, "clock": "s_memrealtime, 100 MHz", "launches": []}
     for k in [int(x) for x in a.steps.split(",")] * a.reps:
         buf.zero_()
-        r = bench.run_steps(sp, k, warmup=0, launch="pooled")
+        r = bench.run_steps(sp, k, warmup=a.warmup, launch="pooled", carry=bool(a.carry))
         ts = buf.cpu().numpy().astype(np.float64) / 1e5   # ms
         start, last, end, moves = ts[:, 0], ts[:, 1], ts[:, 2], ts[:, 3] * 1e5
         t0, t1 = start.min(), end.max()
         budget_out = last.max()   # the last ticket was taken then (a wave's last move started)
-        rec = {"steps": k, "launch_ms": round(r["launch_ms"], 3), "per_step_ms": round(r["launch_ms"] / k, 4),
+        rec = {"steps": k, "carry": a.carry, "launch_ms": round(r["launch_ms"], 3), "per_step_ms": round(r["launch_ms"] / k, 4),
                "stamp_span_ms": round(t1 - t0, 3),
                "ramp_ms_mean": round(float((start - t0).mean()), 4),
                "tail_ms_mean": round(float((t1 - end).mean()), 4),

@@ -136,6 +136,11 @@ SIGNATURES = [
                                                    ctypes.c_int32, ctypes.c_double, ctypes.c_int32, ctypes.c_int32,
                                                    ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                                    ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    ("zc_c4_selfplay_carry_async", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p,
+                                                  ctypes.c_int32, ctypes.c_double, ctypes.c_int32, ctypes.c_int32,
+                                                  ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                                  ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    ("zc_c4_carry_discard", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p]),
     ("zc_chess_play_step_async", ctypes.c_int, [ctypes.c_int32, P(ChessPlayBuffers), ctypes.c_void_p, ctypes.c_void_p,
                                                 ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     ("zc_chess_selfplay_async", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, P(ChessPlayBuffers),
@@ -469,14 +474,19 @@ class NativeEngine:
 
     def c4_selfplay_pooled_async(self, d_roots: int, n: int, sims: int, c: float, batch_size: int, moves_cap: int,
                                  budget: int, d_ticket: int, d_states: int, d_moves16: int, d_results: int,
-                                 d_stats: int, stream: int = 0, first_game: int = 0) -> None:
+                                 d_stats: int, stream: int = 0, first_game: int = 0, carry: bool = False) -> None:
         """`budget` self-play moves shared by the games in one launch, at most `moves_cap` per
-        game (zc_c4_selfplay_pooled_async)."""
-        check(lib().zc_c4_selfplay_pooled_async(self._h, first_game, n, ctypes.c_void_p(d_roots), int(sims),
+        game (zc_c4_selfplay_pooled_async; carry: in-flight moves carry over into the next
+        launch, zc_c4_selfplay_carry_async)."""
+        fn = lib().zc_c4_selfplay_carry_async if carry else lib().zc_c4_selfplay_pooled_async
+        check(fn(self._h, first_game, n, ctypes.c_void_p(d_roots), int(sims),
                                                 float(c), int(batch_size), int(moves_cap), int(budget),
                                                 ctypes.c_void_p(d_ticket), ctypes.c_void_p(d_states),
                                                 ctypes.c_void_p(d_moves16), ctypes.c_void_p(d_results),
                                                 ctypes.c_void_p(d_stats), ctypes.c_void_p(stream or None)))
+
+    def c4_carry_discard(self, first_game: int, n: int, stream: int = 0) -> None:
+        check(lib().zc_c4_carry_discard(self._h, int(first_game), int(n), ctypes.c_void_p(stream or None)))
 
     def c4_pooled_max_games(self, batch_size: int) -> int:
         n = ctypes.c_int32(0)

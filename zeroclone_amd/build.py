@@ -44,6 +44,10 @@ FLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math", "-
 # max-ilp or iterative-maxocc: equal to the default (profiles/r05_ab_chess_sched.log).
 SOURCE_FLAGS = {"c4_search.hip": ["-mllvm", "-amdgpu-sched-strategy=iterative-ilp"],
                 "net_conv.hip": ["-mllvm", "-amdgpu-sched-strategy=iterative-ilp"]}
+# A/B builds only: ZC_C4_SCHED=<strategy> ("default": none) replaces c4_search.hip's strategy
+if os.environ.get("ZC_C4_SCHED"):
+    SOURCE_FLAGS["c4_search.hip"] = ([] if os.environ["ZC_C4_SCHED"] == "default" else
+                                     ["-mllvm", "-amdgpu-sched-strategy=" + os.environ["ZC_C4_SCHED"]])
 
 
 def build(force: bool = False, verbose: bool = False) -> str:

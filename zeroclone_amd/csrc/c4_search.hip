@@ -1083,9 +1083,14 @@ __device__ __forceinline__ SearchLds search_lds(uint8_t *s_dyn, int bs) {
 // WALK (diagnostic, zc_debug_c4_walk_async): 1 = record every leaf's rollout value and every
 // flush's rollout words (p.walk_vals / p.walk_words); 2 = replay them instead of running the
 // rollouts — the tree walk, expansion, backup and publish alone on the identical tree.
+// done / nnodes: the simulations already run and the tree's nodes (0 / 1: a new search from
+// the root; else a carried move resumes, its tree as the last flush published it).  stop
+// (carry launches): the pooled ticket counter — once it reaches `budget` the search returns
+// at the next flush boundary with done < p.sims (the move is suspended, not abandoned).
 template <bool STAMP, bool PHILOX, int WALK = 0>
 __device__ __forceinline__ void search_move(const SearchParams &p, const SearchLds &L, int gl, int g, const Tree &t,
-                                            LRng &rng, uint32_t tag, Counters &cn, int &status) {
+                                            LRng &rng, uint32_t tag, Counters &cn, int &status, int &done_io,
+                                            int &nnodes_io, const int32_t *stop = nullptr, int32_t budget = 0) {
     const uint32_t lane = lane_id();
     const uint32_t *const s_order = L.s_order;
     Fresh *const fresh = L.fresh;
@@ -1093,15 +1098,16 @@ __device__ __forceinline__ void search_move(const SearchParams &p, const SearchL
     // log(N) table read through the constant address space: uniform index -> scalar loads,
     // which do not sit in the vector-memory counter the walk waits on.
     ConstDouble *logtab = (ConstDouble *)p.a.logtab;
-    {
+    if (done_io == 0) {
         const zc_c4_state root = p.roots[gl];
         node_init(t, 0, 0xFFFF, 0xFF, 0, uni(s_order[legal_mask(uni64(root.stones[0]) | uni64(root.stones[1]))]));
     }
-    int nnodes = 1;
+    int nnodes = done_io == 0 ? 1 : nnodes_io;
     wave_mem_order();
 
     Stamp<STAMP> stamp;
-    for (int done = 0; done < p.sims;) {
+    int done = done_io;
+    while (done < p.sims) {
         const int nb = min(p.bs, p.sims - done);
         stamp.mark(0);
 
@@ -1149,7 +1155,10 @@ __device__ __forceinline__ void search_move(const SearchParams &p, const SearchL
             // chains (scalar-unit bound) first while the walk's and the backup's memory round
             // trips are in flight.  Priority 1, 2 or 3: 1.62 ms against 1.73 per 4096 x 800
             // lockstep search; the memory phases raised instead: 1.70 (profiles/r05_ab_c4_wave_priority.log).
-            __builtin_amdgcn_s_setprio(1);
+#ifndef ZC_ROLLOUT_PRIO
+#define ZC_ROLLOUT_PRIO 1  // A/B builds: the rollouts' wave priority
+#endif
+            __builtin_amdgcn_s_setprio(ZC_ROLLOUT_PRIO);
             c4_rollouts(leaves, nb, rng, s_order, cn, STAMP ? &stamp.ph[7] : nullptr);
             __builtin_amdgcn_s_setprio(0);
             if (WALK == 1) {
@@ -1173,11 +1182,14 @@ __device__ __forceinline__ void search_move(const SearchParams &p, const SearchL
         const bool pre = lane >= 1 && lane <= (uint32_t)d0;
         const int par = __shfl((int)(fs.ppath & 0xFFFFu), (int)lane - 1);
         const int act = (int)(fs.ppath >> 16);
-        int32_t na0 = 0, w0 = 0;
+        int32_t na0 = 0, w0 = 0, spent_v = 0;
+        // carry launches: the budget's state, read beside the prefix counters (one round trip)
+        if (stop) spent_v = __hip_atomic_load(stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (pre) {
             na0 = t.na(par)[act];
             w0 = t.w(par)[act];
         }
+        const int32_t spent = stop ? uni(spent_v) : 0;
         if (fs.planned) {
             // The planned flush's fresh nodes are the draws 0..D-1 (leaf j <-> node f0 + j for
             // j < D; the leaves D..nb-1 sit on the terminal chain node).  A fresh node's subtree is
@@ -1317,7 +1329,10 @@ __device__ __forceinline__ void search_move(const SearchParams &p, const SearchL
         wave_mem_order();
         stamp.mark(6);
         done += nb;
+        if (stop && done < p.sims && status == 0 && uni(spent) >= budget) break;  // suspend
     }
+    done_io = done;
+    nnodes_io = nnodes;
     if (STAMP && lane == 0)
         for (int k_ = 0; k_ < kPhases; ++k_) p.a.phase[kPhases * (size_t)g + k_] += (int64_t)stamp.ph[k_];
 }
@@ -1372,8 +1387,8 @@ __device__ __forceinline__ void search_games(const SearchParams &p, uint8_t *s_d
     const uint64_t use0 = uni64(a.rngpos[2 * (size_t)g]);
     lrng_open(rng, L.ring, a.ring + (size_t)g * kRingWords, use0, uni64(a.rngpos[2 * (size_t)g + 1]));
     Counters cn;
-    int status = 0;
-    search_move<STAMP, PHILOX, WALK>(p, L, gl, g, t, rng, uni((uint32_t)use0), cn, status);
+    int status = 0, done = 0, nnodes = 1;
+    search_move<STAMP, PHILOX, WALK>(p, L, gl, g, t, rng, uni((uint32_t)use0), cn, status, done, nnodes);
     int na_col;
     const int col = best_column(t, na_col);
     if (lane < 7) p.out_na[(size_t)gl * 7 + lane] = na_col;
@@ -1415,6 +1430,11 @@ __global__ __launch_bounds__(kSearchWaves * kBlock, 4) void c4_walk_kernel(Searc
 // Step k's post-move position / move / result go to out_states[k*n + gl], out_moves[...],
 // out_results[...] (the inputs of zc_traj_record_async for step k, replayed in step order
 // after the launch); out_stats[gl] accumulates over the moves.
+// Carried moves (zc_c4_selfplay_carry_async): a carry launch suspends each in-flight move at
+// its next flush boundary once the pooled budget is spent, saving {simulations done, tree
+// nodes, Philox tag} in a.carry[g] (the tree, the MT stream and the root stay in HBM).  EVERY
+// self-play launch first resumes a carried move, without a ticket, so the game's moves are
+// the moves an uninterrupted run plays; only carry launches suspend.
 template <bool PHILOX>
 __global__ __launch_bounds__(kSearchWaves * kBlock, 4) void c4_selfplay_kernel(SearchParams p) {
     extern __shared__ __attribute__((aligned(16))) uint8_t s_dyn[];
@@ -1435,10 +1455,14 @@ __global__ __launch_bounds__(kSearchWaves * kBlock, 4) void c4_selfplay_kernel(S
     int status = 0;
     int finished = 0;
     int mv = 0;
+    int64_t leaves = 0;
     uint64_t t_start = 0, t_last = 0;
     if (p.tstamps) t_start = t_last = __builtin_amdgcn_s_memrealtime();
+    uint4 cy = a.carry[g];   // a carried move: {done, nodes, tag, -} (done 0: none)
+    cy = make_uint4(uni(cy.x), uni(cy.y), uni(cy.z), 0u);
+    bool resume = cy.x != 0;
     for (; mv < p.moves; ++mv) {
-        if (p.ticket) {  // pooled run: the next move only while the shared budget lasts
+        if (p.ticket && !resume) {  // pooled run: the next move only while the shared budget lasts
             int tk = 0;
             if (lane == 0) tk = atomicAdd(p.ticket, 1);
             if (uni(tk) >= p.budget) break;
@@ -1451,8 +1475,18 @@ __global__ __launch_bounds__(kSearchWaves * kBlock, 4) void c4_selfplay_kernel(S
             status = ZC_STATUS_BAD_STATE;
             break;
         }
-        search_move<false, PHILOX>(p, L, gl, g, t, rng, uni((uint32_t)(use0 + (uint64_t)(int64_t)rng.use())), cn,
-                                   status);
+        int done = resume ? (int)cy.x : 0, nnodes = resume ? (int)cy.y : 1;
+        const uint32_t tag = resume ? cy.z : uni((uint32_t)(use0 + (uint64_t)(int64_t)rng.use()));
+        const int done0 = done;
+        search_move<false, PHILOX>(p, L, gl, g, t, rng, tag, cn, status, done, nnodes, p.carry ? p.ticket : nullptr,
+                                   p.budget);
+        leaves += done - done0;
+        if (done < p.sims) {  // suspended (carry launch, budget spent): the next launch resumes it
+            if (lane == 0) a.carry[g] = make_uint4((uint32_t)done, (uint32_t)nnodes, tag, 0u);
+            break;
+        }
+        if (resume && lane == 0) a.carry[g] = make_uint4(0u, 0u, 0u, 0u);
+        resume = false;
         int na_col;
         const int col = best_column(t, na_col);
         // play_move + _evaluate (c4_play_kernel): check_win -> turn*2-1 with the new turn
@@ -1495,7 +1529,7 @@ __global__ __launch_bounds__(kSearchWaves * kBlock, 4) void c4_selfplay_kernel(S
         st.status = status;
         st.expansions = cn.expansions;
         st.depth_sum = cn.depth_sum;
-        st.leaves = (int64_t)p.sims * mv;
+        st.leaves = leaves;
         st.rollout_plies = cn.plies;
         st.rollout_blocks = cn.blocks;
         st.rng_words = rng.use();

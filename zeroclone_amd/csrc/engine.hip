@@ -103,6 +103,7 @@ size_t carve_arena(zc_engine *e, uint8_t *base) {
     carve(base, off, &a.ring, G * zc::kRingWords);
     carve(base, off, &a.rngpos, G * 2);
     carve(base, off, &a.logtab, M + 2);
+    carve(base, off, &a.carry, G);
     carve(base, off, &a.phase, G * zc::kPhases);
     carve(base, off, &a.roots, G);
     carve(base, off, &a.move, G);
@@ -195,6 +196,23 @@ int check_search(const zc_engine *e, int32_t first, int32_t n, int32_t sims, dou
     if (bs > e->cfg.max_batch) return fail(ZC_ECAPACITY, "batch_size %d > engine max_batch %d", bs, e->cfg.max_batch);
     if (!isfinite(c)) return fail(ZC_EINVAL, "c must be finite");
     return ZC_OK;
+}
+
+// Games with a self-play move carried over by zc_c4_selfplay_carry_async ([carry_lo, carry_hi),
+// conservatively: every game a carry launch covered until a launch that resumes them all).
+// Their trees and MT streams belong to the suspended searches: entry points that would search
+// or reseed them refuse, so a game's moves stay the moves an uninterrupted run plays.
+int check_carry(const zc_engine *e, int32_t first, int32_t n) {
+    if (n > 0 && first < e->carry_hi && first + n > e->carry_lo)
+        return fail(ZC_EINVAL, "games [%d, %d) overlap games [%d, %d) whose self-play moves are carried over "
+                    "(zc_c4_selfplay_carry_async): finish them with zc_c4_selfplay_async / "
+                    "zc_c4_selfplay_pooled_async over those games, or drop them with zc_c4_carry_discard",
+                    first, first + n, e->carry_lo, e->carry_hi);
+    return ZC_OK;
+}
+
+void carry_covered(zc_engine *e, int32_t first, int32_t n) {  // a launch that leaves none carried
+    if (first <= e->carry_lo && first + n >= e->carry_hi) e->carry_lo = e->carry_hi = 0;
 }
 
 bool valid_c4(const zc_c4_state &s) {
@@ -307,7 +325,8 @@ int zc_engine_create(const zc_engine_config *cfg, zc_engine **out) {
     }
     if (!rc && !(e->stream = take_stream(cfg->device))) rc = fail(ZC_EHIP, "hipStreamCreate failed");
     if (!rc && (hipMemsetAsync(a.phase, 0, G * zc::kPhases * sizeof(int64_t), e->stream) != hipSuccess ||
-                hipMemsetAsync(a.ext_ctl, 0, G * zc::kCtlWords * sizeof(int32_t), e->stream) != hipSuccess))
+                hipMemsetAsync(a.ext_ctl, 0, G * zc::kCtlWords * sizeof(int32_t), e->stream) != hipSuccess ||
+                hipMemsetAsync(a.carry, 0, G * sizeof(uint4), e->stream) != hipSuccess))
         rc = fail(ZC_EHIP, "memset failed");
     if (!rc) {
         // log(N) exactly as the reference gets it: glibc log on the host (mcts.cpp:44).
@@ -359,6 +378,7 @@ int zc_engine_footprint(const zc_engine *eng, int64_t *bytes) {
 int zc_rng_seed(zc_engine *eng, int32_t first, int32_t n, const uint64_t *seeds) {
     if (!eng || (!seeds && n)) return fail(ZC_EINVAL, "null argument");
     if (int r = check_games(eng, first, n)) return r;
+    if (int r = check_carry(eng, first, n)) return r;
     std::lock_guard<std::mutex> lk(eng->mu);
     ZC_HIP(hipSetDevice(eng->cfg.device));
     std::vector<uint32_t> words((size_t)n * 624);
@@ -383,6 +403,7 @@ int zc_rng_seed(zc_engine *eng, int32_t first, int32_t n, const uint64_t *seeds)
 int zc_rng_set_state(zc_engine *eng, int32_t game, const uint32_t *mt624, int32_t index) {
     if (!eng || !mt624) return fail(ZC_EINVAL, "null argument");
     if (int r = check_games(eng, game, 1)) return r;
+    if (int r = check_carry(eng, game, 1)) return r;
     if (index < 0 || index > 624) return fail(ZC_EINVAL, "MT index must be in [0, 624] (got %d)", index);
     std::lock_guard<std::mutex> lk(eng->mu);
     ZC_HIP(hipSetDevice(eng->cfg.device));
@@ -440,13 +461,14 @@ int zc_c4_selfplay_async(zc_engine *eng, int32_t first, int32_t n, zc_c4_state *
     p.out_results = d_out_results;
     zc::launch_c4_selfplay(p, (hipStream_t)hip_stream);
     ZC_HIP(hipGetLastError());
+    carry_covered(eng, first, n);   // carried moves resume first and this launch suspends none
     return ZC_OK;
 }
 
-int zc_c4_selfplay_pooled_async(zc_engine *eng, int32_t first, int32_t n, zc_c4_state *d_roots, int32_t sims,
-                                double c, int32_t bs, int32_t moves_cap, int64_t budget, int32_t *d_ticket,
-                                zc_c4_state *d_out_states, int16_t *d_out_moves, int32_t *d_out_results,
-                                zc_game_stats *d_stats, void *hip_stream) {
+namespace {
+int c4_pooled(zc_engine *eng, int32_t first, int32_t n, zc_c4_state *d_roots, int32_t sims, double c, int32_t bs,
+              int32_t moves_cap, int64_t budget, int32_t *d_ticket, zc_c4_state *d_out_states, int16_t *d_out_moves,
+              int32_t *d_out_results, zc_game_stats *d_stats, void *hip_stream, int carry) {
     if (!eng || (n && (!d_roots || !d_out_states || !d_out_moves || !d_out_results || !d_stats || !d_ticket)))
         return fail(ZC_EINVAL, "null argument");
     if (int r = check_search(eng, first, n, sims, c, bs)) return r;
@@ -478,8 +500,46 @@ int zc_c4_selfplay_pooled_async(zc_engine *eng, int32_t first, int32_t n, zc_c4_
     p.out_results = d_out_results;
     p.ticket = d_ticket;
     p.budget = (int32_t)budget;
+    p.carry = carry;
     zc::launch_c4_selfplay(p, s);
     ZC_HIP(hipGetLastError());
+    if (!carry) {
+        carry_covered(eng, first, n);
+    } else if (eng->carry_hi <= eng->carry_lo) {
+        eng->carry_lo = first;
+        eng->carry_hi = first + n;
+    } else {
+        eng->carry_lo = std::min(eng->carry_lo, first);
+        eng->carry_hi = std::max(eng->carry_hi, first + n);
+    }
+    return ZC_OK;
+}
+}  // namespace
+
+int zc_c4_selfplay_pooled_async(zc_engine *eng, int32_t first, int32_t n, zc_c4_state *d_roots, int32_t sims,
+                                double c, int32_t bs, int32_t moves_cap, int64_t budget, int32_t *d_ticket,
+                                zc_c4_state *d_out_states, int16_t *d_out_moves, int32_t *d_out_results,
+                                zc_game_stats *d_stats, void *hip_stream) {
+    return c4_pooled(eng, first, n, d_roots, sims, c, bs, moves_cap, budget, d_ticket, d_out_states, d_out_moves,
+                     d_out_results, d_stats, hip_stream, 0);
+}
+
+int zc_c4_selfplay_carry_async(zc_engine *eng, int32_t first, int32_t n, zc_c4_state *d_roots, int32_t sims,
+                               double c, int32_t bs, int32_t moves_cap, int64_t budget, int32_t *d_ticket,
+                               zc_c4_state *d_out_states, int16_t *d_out_moves, int32_t *d_out_results,
+                               zc_game_stats *d_stats, void *hip_stream) {
+    return c4_pooled(eng, first, n, d_roots, sims, c, bs, moves_cap, budget, d_ticket, d_out_states, d_out_moves,
+                     d_out_results, d_stats, hip_stream, 1);
+}
+
+int zc_c4_carry_discard(zc_engine *eng, int32_t first, int32_t n, void *hip_stream) {
+    if (!eng) return fail(ZC_EINVAL, "null argument");
+    if (int r = check_games(eng, first, n)) return r;
+    if (!n) return ZC_OK;
+    std::lock_guard<std::mutex> lk(eng->mu);
+    ZC_HIP(hipSetDevice(eng->cfg.device));
+    ZC_HIP(hipMemsetAsync(eng->a.carry + first, 0, (size_t)n * sizeof(uint4), (hipStream_t)hip_stream));
+    carry_covered(eng, first, n);
     return ZC_OK;
 }
 
@@ -499,6 +559,7 @@ int zc_c4_search_async(zc_engine *eng, int32_t first, int32_t n, const zc_c4_sta
                        int32_t bs, int32_t *d_move, int32_t *d_na, zc_game_stats *d_stats, void *hip_stream) {
     if (!eng || (n && (!d_roots || !d_move || !d_na || !d_stats))) return fail(ZC_EINVAL, "null argument");
     if (int r = check_search(eng, first, n, sims, c, bs)) return r;
+    if (int r = check_carry(eng, first, n)) return r;
     if (!n) return ZC_OK;
     std::lock_guard<std::mutex> lk(eng->mu);
     ZC_HIP(hipSetDevice(eng->cfg.device));
@@ -567,6 +628,7 @@ int zc_c4_search(zc_engine *eng, int32_t first, int32_t n, const zc_c4_state *ro
                  int32_t bs, int32_t *out_move, int32_t *out_na, zc_game_stats *out_stats) {
     if (!eng || (n && (!roots || !out_move || !out_na))) return fail(ZC_EINVAL, "null argument");
     if (int r = check_search(eng, first, n, sims, c, bs)) return r;
+    if (int r = check_carry(eng, first, n)) return r;
     if (!n) return ZC_OK;
     return search_sync(eng, first, n, nullptr, roots, sims, c, bs, out_move, out_na, out_stats);
 }
@@ -581,6 +643,7 @@ int zc_c4_search_games(zc_engine *eng, int32_t n, const int32_t *games, const zc
         if (games[i] < 0 || games[i] >= eng->cfg.max_games)
             return fail(ZC_ECAPACITY, "game %d outside engine capacity %d", games[i], eng->cfg.max_games);
         if (seen[(size_t)games[i]]++) return fail(ZC_EINVAL, "game %d listed twice", games[i]);
+        if (int r = check_carry(eng, games[i], 1)) return r;
     }
     if (!n) return ZC_OK;
     return search_sync(eng, 0, n, games, roots, sims, c, bs, out_move, out_na, out_stats);
@@ -602,6 +665,7 @@ int zc_c4_rollouts(zc_engine *eng, int32_t game, int32_t n, const zc_c4_state *s
                    int64_t *out_words) {
     if (!eng || n < 0 || (n && (!states || !out_values))) return fail(ZC_EINVAL, "bad argument");
     if (int r = check_games(eng, game, 1)) return r;
+    if (int r = check_carry(eng, game, 1)) return r;
     for (int32_t i = 0; i < n; ++i)
         if (!valid_c4(states[i])) return fail(ZC_EINVAL, "state %d is not a valid Connect4 position", i);
     std::lock_guard<std::mutex> lk(eng->mu);
@@ -632,6 +696,7 @@ int zc_c4_ext_begin(zc_engine *eng, int32_t first, int32_t n, const zc_c4_state 
                     int32_t bs, void *hip_stream) {
     if (!eng || (n && !d_roots)) return fail(ZC_EINVAL, "null argument");
     if (int r = check_search(eng, first, n, sims, c, bs)) return r;
+    if (int r = check_carry(eng, first, n)) return r;
     std::lock_guard<std::mutex> lk(eng->mu);
     ZC_HIP(hipSetDevice(eng->cfg.device));
     eng->ext_first = first;
@@ -1759,6 +1824,7 @@ int zc_debug_c4_rollout(zc_engine *eng, int32_t first, int32_t n, const zc_c4_st
                         int64_t *out_words) {
     if (!eng || (n && (!states || !out_value || !out_words))) return fail(ZC_EINVAL, "null argument");
     if (int r = check_games(eng, first, n)) return r;
+    if (int r = check_carry(eng, first, n)) return r;
     for (int32_t i = 0; i < n; ++i)
         if (!valid_c4(states[i])) return fail(ZC_EINVAL, "state %d is not a valid Connect4 position", i);
     if (!n) return ZC_OK;
@@ -1785,6 +1851,7 @@ int zc_debug_c4_walk_async(zc_engine *eng, int32_t first, int32_t n, const zc_c4
         return fail(ZC_EINVAL, "null argument");
     if (mode != 1 && mode != 2) return fail(ZC_EINVAL, "mode must be 1 (record) or 2 (replay)");
     if (int r = check_search(eng, first, n, sims, c, bs)) return r;
+    if (int r = check_carry(eng, first, n)) return r;
     if (!n) return ZC_OK;
     std::lock_guard<std::mutex> lk(eng->mu);
     ZC_HIP(hipSetDevice(eng->cfg.device));

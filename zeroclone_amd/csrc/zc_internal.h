@@ -49,6 +49,7 @@ struct Arena {
     uint32_t *ring = nullptr;     // [G][kRingWords]    raw (untempered) MT words
     uint64_t *rngpos = nullptr;   // [G][2]             {next word to use, words generated}
     double *logtab = nullptr;     // [M+2]              glibc log(n), n = 0..M+1
+    uint4 *carry = nullptr;       // [G]                a carried self-play move {done, nodes, tag, 0}
     int64_t *phase = nullptr;     // [G][kPhases]       diagnostic phase cycles (stamp build)
     // staging for the synchronous host entry points
     zc_c4_state *roots = nullptr;
@@ -101,6 +102,7 @@ struct SearchParams {
     // ticket[1] = the most moves any game played
     int32_t *ticket;
     int32_t budget;
+    int carry;   // 1: suspend in-flight moves once the budget is spent (zc_c4_selfplay_carry_async)
     // walk diagnostic (c4_walk_kernel): per game the rollout value of every simulation
     // [G][sims] and the rollout words of every flush [G][ceil(sims / bs)]
     int8_t *walk_vals;
@@ -405,6 +407,7 @@ struct zc_engine {
     uint64_t *tstamps = nullptr;  // zc_debug_c4_launch_stamps: device buffer, 4 words per game
     int rollout_mode = 0;        // ZC_ROLLOUT_EXACT / ZC_ROLLOUT_PHILOX
     uint64_t rollout_seed = 0;
+    int carry_lo = 0, carry_hi = 0;  // games that may hold a carried self-play move (engine.hip check_carry)
     zc::ChessArena ca;  // allocated on the first chess search
     // the Connect4 PUCT tree (allocated on the first zc_c4_puct_begin) and its search in progress
     zc::C4PNode *c4p_nodes = nullptr;

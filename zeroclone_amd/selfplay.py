@@ -282,6 +282,7 @@ class C4SelfPlay:
             self.traj = Trajectories(games, torch.zeros(24, dtype=torch.uint8), self.MAX_LEN, cap,
                                      cap * self.MAX_LEN, self.dev)
         self.totals = torch.zeros(2, dtype=torch.int64, device=self.dev)   # expansions, depth sum since reset
+        self.carry_pending = False   # run_pooled(carry=True) left moves in flight (drain() finishes them)
         self.vs = self.value_fn = self.ps = self.net_fn = None
         self.temperature = float(temperature)
         if net is not None:
@@ -300,6 +301,9 @@ class C4SelfPlay:
     def start(self, quota: int | None = None):
         """Every slot back to the opening; with a quota, slots beyond it idle and finished
         slots start new games only while fewer than `quota` have started."""
+        if self.carry_pending:   # the games restart: their carried moves are dropped
+            self.eng.c4_carry_discard(0, self.G, torch.cuda.current_stream(self.dev).cuda_stream)
+            self.carry_pending = False
         self.roots.zero_()
         if self.traj is not None:
             self.traj.start(quota, games_cap=quota)
@@ -332,6 +336,7 @@ class C4SelfPlay:
         self.eng.c4_selfplay_async(self.roots.data_ptr(), self.G, self.sims, self.c, self.bs, moves,
                                    self._run_states.data_ptr(), self._run_moves.data_ptr(),
                                    self._run_results.data_ptr(), self.stats.data_ptr(), stream=s)
+        self.carry_pending = False   # carried moves were resumed first
         if kernel_done is not None:   # an event recorded after the launch, before the recording
             kernel_done.record()
         if self.record:
@@ -339,7 +344,8 @@ class C4SelfPlay:
         self.results.copy_(self._run_results[-1])
         return self._run_results
 
-    def run_pooled(self, budget: int, moves_cap: int, stream: int | None = None, kernel_done=None) -> torch.Tensor:
+    def run_pooled(self, budget: int, moves_cap: int, stream: int | None = None, kernel_done=None,
+                   carry: bool = False) -> torch.Tensor:
         """`budget` moves shared by all games in ONE launch (zc_c4_selfplay_pooled_async): each
         game takes its next move from a device counter while the budget lasts, at most
         `moves_cap` moves.  A throughput schedule, not the reference's: scripts/train.py:151-170
@@ -347,7 +353,10 @@ class C4SelfPlay:
         run() would play;
         how many moves each game gets follows the games' pace.  The trajectory recording
         replays the steps in order (slots without a k-th move: ZC_SLOT_SKIP, untouched).
-        Returns the per-step results [moves_cap, G]; self.stats sums the moves' counters."""
+        carry=True (zc_c4_selfplay_carry_async): once the budget is spent the in-flight moves
+        stop at their next flush and carry over — the next run()/run_pooled() resumes them
+        first; drain() finishes them; step() and the lockstep searches refuse until then.
+        Returns the per-step results [moves_cap, G]; self.stats sums the launch's counters."""
         if self.traj is not None and self.traj.quota != _UNLIMITED:
             raise ValueError("run_pooled() plays without a game quota; use step() under simulate_games' quota")
         if self.vs is not None or self.ps is not None:
@@ -363,7 +372,8 @@ class C4SelfPlay:
         self.eng.c4_selfplay_pooled_async(self.roots.data_ptr(), self.G, self.sims, self.c, self.bs, moves_cap,
                                           budget, self._ticket.data_ptr(), self._run_states.data_ptr(),
                                           self._run_moves.data_ptr(), self._run_results.data_ptr(),
-                                          self.stats.data_ptr(), stream=s)
+                                          self.stats.data_ptr(), stream=s, carry=carry)
+        self.carry_pending = bool(carry)
         if kernel_done is not None:
             kernel_done.record()
         if self.record:
@@ -371,9 +381,17 @@ class C4SelfPlay:
                                    reached=self._ticket[1:], stream=s)
         return self._run_results
 
+    def drain(self, stream: int | None = None) -> torch.Tensor:
+        """Finish the moves run_pooled(carry=True) left in flight (a pooled launch with no
+        budget: each carried move is resumed and finished, nothing new starts), recorded like
+        any launch's moves.  Returns that launch's per-step results."""
+        return self.run_pooled(0, 1, stream=stream)
+
     def step_search(self, stream: int | None = None) -> torch.Tensor:
         """The search half of a step (zc_c4_search_async); returns the results tensor the
         finish half will fill."""
+        if self.carry_pending:
+            raise RuntimeError("moves carried over by run_pooled(carry=True) are in flight: drain() first")
         s = stream if stream is not None else torch.cuda.current_stream(self.dev).cuda_stream
         if self.ps is not None or self.vs is not None:
             if self.ps is not None:
