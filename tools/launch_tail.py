@@ -36,9 +36,21 @@ def main():
     _native.check(_native.lib().zc_debug_c4_launch_stamps(sp.eng._h, buf.data_ptr()))
     out = {"burn_in_steps": burn, "clock": "s_memrealtime, 100 MHz", "launches": []}
     for k in [int(x) for x in a.steps.split(",")] * a.reps:
-        buf.zero_()
-        r = bench.run_steps(sp, k, warmup=a.warmup, launch="pooled", carry=bool(a.carry))
-        ts = buf.cpu().numpy().astype(np.float64) / 1e5   # ms
+        if a.carry:   # the timed launch's stamps, before the drain's launch overwrites them
+            sp.run_pooled(a.warmup * G, 2 * a.warmup, carry=True)
+            torch.cuda.synchronize()
+            buf.zero_()
+            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            ev[0].record()
+            sp.run_pooled(k * G, 2 * k, kernel_done=ev[1], carry=True)
+            torch.cuda.synchronize()
+            r = {"launch_ms": ev[0].elapsed_time(ev[1]), "expansions": int(sp.stats[:, 0].sum())}
+            ts = buf.cpu().numpy().astype(np.float64) / 1e5   # ms
+            sp.drain()
+        else:
+            buf.zero_()
+            r = bench.run_steps(sp, k, warmup=a.warmup, launch="pooled", carry=False)
+            ts = buf.cpu().numpy().astype(np.float64) / 1e5   # ms
         start, last, end, moves = ts[:, 0], ts[:, 1], ts[:, 2], ts[:, 3] * 1e5
         t0, t1 = start.min(), end.max()
         budget_out = last.max()   # the last ticket was taken then (a wave's last move started)
