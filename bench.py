@@ -582,7 +582,8 @@ def burn_in(sp, max_steps: int = 200, check_every: int = 8) -> int:
     return steps
 
 
-def run_steps(sp, steps: int, warmup: int, world: int = 1, launch: str = "pooled", carry: bool = True) -> dict:
+def run_steps(sp, steps: int, warmup: int, world: int = 1, launch: str = "pooled", carry: bool = True,
+              drain: bool = True) -> dict:
     """W untimed moves, then K timed steps (K x G moves) bracketed by barrier + device sync,
     as ONE self-play launch followed by its trajectory recording; HIP events around it on its
     stream.  launch "pooled" (the default, C4SelfPlay.run_pooled): the G games share a budget
@@ -627,7 +628,7 @@ def run_steps(sp, steps: int, warmup: int, world: int = 1, launch: str = "pooled
                & (res != _native.ZC_SLOT_SKIP)).sum().item())
     moves = int(((res != _native.ZC_SLOT_IDLE) & (res != _native.ZC_SLOT_SKIP)).sum().item())
     tot = [int(x) for x in st[:, [0, 1, 2]].sum(0).tolist()]
-    if carry:   # untimed: finish the moves left in flight (the pool's later users search it)
+    if carry and drain:   # untimed: finish the moves left in flight (the pool's later users search it)
         sp.drain()
         torch.cuda.synchronize(dev)
     return {"dt": dt, "launch_ms": ev[0].elapsed_time(ev[2]), "launch_record_ms": ev[0].elapsed_time(ev[1]), "expansions": tot[0], "depth_sum": tot[1],

@@ -21,13 +21,16 @@ ap.add_argument("--batch", type=int, default=32)
 ap.add_argument("--steps", type=int, default=8)
 ap.add_argument("--launch", choices=["pooled", "free"], default="pooled")
 ap.add_argument("--no-burn-in", dest="burn_in", action="store_false")
+ap.add_argument("--no-carry", dest="carry", action="store_false",
+                help="pooled launches without carry-over (default: a carry warmup launch, then the timed carry "
+                     "launch as the trace's last, undrained)")
 a = ap.parse_args()
 torch.cuda.set_device(0)
 torch.cuda.set_stream(torch.cuda.Stream(torch.device("cuda", 0)))
 sp = C4SelfPlay(a.games, a.sims, c=1.4, batch_size=a.batch, seed=0, device=0, record=True)
 burn = bench.burn_in(sp) if a.burn_in else 0
 print(f"burn-in {burn} steps", flush=True)
-r = bench.run_steps(sp, a.steps, warmup=0, launch=a.launch)
+r = bench.run_steps(sp, a.steps, warmup=2 if a.carry else 0, launch=a.launch, carry=a.carry, drain=False)
 print(f"steps {a.steps}: {r['expansions'] / r['dt'] / 1e9:.4f} G expansions/s, "
       f"launch ms {r['launch_ms']:.3f} ({r['launch_ms'] / a.steps:.3f} per move), "
       f"depth {r['depth_sum'] / max(r['expansions'], 1):.3f}", flush=True)

@@ -109,6 +109,16 @@ __device__ __forceinline__ uint32_t ff1(uint64_t m) {
 #ifndef ZC_RV
 #define ZC_RV 0  // experiment switches (tools/rv_libs.sh); 0 = the product kernel
 #endif
+#ifndef ZC_LAG_MODE
+#define ZC_LAG_MODE 3  // free runs' pace balancing (A/B builds): 0 off, 1 per move, 2/3 per flush (2/3 levels)
+#endif
+// wave priority from a uniform level 0..3 (s_setprio takes an immediate)
+__device__ __forceinline__ void set_prio(int lvl) {
+    if (lvl >= 3) __builtin_amdgcn_s_setprio(3);
+    else if (lvl == 2) __builtin_amdgcn_s_setprio(2);
+    else if (lvl == 1) __builtin_amdgcn_s_setprio(1);
+    else __builtin_amdgcn_s_setprio(0);
+}
 #ifndef ZC_RSTAMP
 #define ZC_RSTAMP 0  // diagnostic build: 1..6 = accumulate one rollout region's cycles into *sub
 #endif
@@ -1090,7 +1100,9 @@ __device__ __forceinline__ SearchLds search_lds(uint8_t *s_dyn, int bs) {
 template <bool STAMP, bool PHILOX, int WALK = 0>
 __device__ __forceinline__ void search_move(const SearchParams &p, const SearchLds &L, int gl, int g, const Tree &t,
                                             LRng &rng, uint32_t tag, Counters &cn, int &status, int &done_io,
-                                            int &nnodes_io, const int32_t *stop = nullptr, int32_t budget = 0) {
+                                            int &nnodes_io, const int32_t *stop = nullptr, int32_t budget = 0,
+                                            int *lagp = nullptr, const int32_t *progress = nullptr, int mv = 0) {
+    int lag = lagp ? *lagp : 0;
     const uint32_t lane = lane_id();
     const uint32_t *const s_order = L.s_order;
     Fresh *const fresh = L.fresh;
@@ -1158,9 +1170,11 @@ __device__ __forceinline__ void search_move(const SearchParams &p, const SearchL
 #ifndef ZC_ROLLOUT_PRIO
 #define ZC_ROLLOUT_PRIO 1  // A/B builds: the rollouts' wave priority
 #endif
-            __builtin_amdgcn_s_setprio(ZC_ROLLOUT_PRIO);
+            // `lag` (free runs): how far this game is behind the launch's average pace; its
+            // phases run that many levels up, so the arbiter evens the games' paces out
+            set_prio(lag + ZC_ROLLOUT_PRIO);
             c4_rollouts(leaves, nb, rng, s_order, cn, STAMP ? &stamp.ph[7] : nullptr);
-            __builtin_amdgcn_s_setprio(0);
+            set_prio(lag);
             if (WALK == 1) {
                 wave_mem_order();
                 for (int jj = (int)lane; jj < nb; jj += kBlock) p.walk_vals[wlog + jj] = (int8_t)leaves[jj].val;
@@ -1183,13 +1197,16 @@ __device__ __forceinline__ void search_move(const SearchParams &p, const SearchL
         const int par = __shfl((int)(fs.ppath & 0xFFFFu), (int)lane - 1);
         const int act = (int)(fs.ppath >> 16);
         int32_t na0 = 0, w0 = 0, spent_v = 0;
-        // carry launches: the budget's state, read beside the prefix counters (one round trip)
+        // carry launches: the budget's state, read beside the prefix counters (one round trip);
+        // free runs: the launch's finished moves (pace balancing)
         if (stop) spent_v = __hip_atomic_load(stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (ZC_LAG_MODE >= 2 && progress)
+            spent_v = __hip_atomic_load(progress, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (pre) {
             na0 = t.na(par)[act];
             w0 = t.w(par)[act];
         }
-        const int32_t spent = stop ? uni(spent_v) : 0;
+        const int32_t spent = stop || (ZC_LAG_MODE >= 2 && progress) ? uni(spent_v) : 0;
         if (fs.planned) {
             // The planned flush's fresh nodes are the draws 0..D-1 (leaf j <-> node f0 + j for
             // j < D; the leaves D..nb-1 sit on the terminal chain node).  A fresh node's subtree is
@@ -1330,9 +1347,19 @@ __device__ __forceinline__ void search_move(const SearchParams &p, const SearchL
         stamp.mark(6);
         done += nb;
         if (stop && done < p.sims && status == 0 && uni(spent) >= budget) break;  // suspend
+        if (ZC_LAG_MODE >= 2 && progress) {  // behind the average (in simulations): 1; by a move or more: 2
+            const int64_t own = ((int64_t)mv * p.sims + done) * p.n_games, avg = (int64_t)spent * p.sims;
+            const int64_t mvn = (int64_t)p.sims * p.n_games;  // one move behind
+            if (ZC_LAG_MODE == 4)  // behind by < 1/2 move: 1, < 1 move: 2, more: 3
+                lag = own >= avg ? 0 : own + mvn / 2 > avg ? 1 : own + mvn > avg ? 2 : 3;
+            else
+                lag = own < avg ? (ZC_LAG_MODE == 3 && own + mvn <= avg ? 2 : ZC_LAG_MODE == 3 ? 1 : 2) : 0;
+            set_prio(lag);
+        }
     }
     done_io = done;
     nnodes_io = nnodes;
+    if (lagp) *lagp = lag;
     if (STAMP && lane == 0)
         for (int k_ = 0; k_ < kPhases; ++k_) p.a.phase[kPhases * (size_t)g + k_] += (int64_t)stamp.ph[k_];
 }
@@ -1458,6 +1485,7 @@ __global__ __launch_bounds__(kSearchWaves * kBlock, 4) void c4_selfplay_kernel(S
     int64_t leaves = 0;
     uint64_t t_start = 0, t_last = 0;
     if (p.tstamps) t_start = t_last = __builtin_amdgcn_s_memrealtime();
+    int lag = 0;             // pace level of free runs (search_move)
     uint4 cy = a.carry[g];   // a carried move: {done, nodes, tag, -} (done 0: none)
     cy = make_uint4(uni(cy.x), uni(cy.y), uni(cy.z), 0u);
     bool resume = cy.x != 0;
@@ -1478,8 +1506,16 @@ __global__ __launch_bounds__(kSearchWaves * kBlock, 4) void c4_selfplay_kernel(S
         int done = resume ? (int)cy.x : 0, nnodes = resume ? (int)cy.y : 1;
         const uint32_t tag = resume ? cy.z : uni((uint32_t)(use0 + (uint64_t)(int64_t)rng.use()));
         const int done0 = done;
+        // free runs (every game exactly p.moves moves, the launch waits for the slowest): a game
+        // whose moves so far are below the launch's average raises its priority for this move
+        if (ZC_LAG_MODE == 1 && p.progress) {
+            const int32_t tot = __hip_atomic_load(p.progress, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            lag = (int64_t)mv * p.n_games < (int64_t)uni(tot) ? 2 : 0;
+            set_prio(lag);
+        }
         search_move<false, PHILOX>(p, L, gl, g, t, rng, tag, cn, status, done, nnodes, p.carry ? p.ticket : nullptr,
-                                   p.budget);
+                                   p.budget, &lag, ZC_LAG_MODE ? p.progress : nullptr, mv);
+        if (ZC_LAG_MODE && p.progress && lane == 0) atomicAdd(p.progress, 1);
         leaves += done - done0;
         if (done < p.sims) {  // suspended (carry launch, budget spent): the next launch resumes it
             if (lane == 0) a.carry[g] = make_uint4((uint32_t)done, (uint32_t)nnodes, tag, 0u);

@@ -104,6 +104,7 @@ size_t carve_arena(zc_engine *e, uint8_t *base) {
     carve(base, off, &a.rngpos, G * 2);
     carve(base, off, &a.logtab, M + 2);
     carve(base, off, &a.carry, G);
+    carve(base, off, &a.progress, 64);
     carve(base, off, &a.phase, G * zc::kPhases);
     carve(base, off, &a.roots, G);
     carve(base, off, &a.move, G);
@@ -459,6 +460,8 @@ int zc_c4_selfplay_async(zc_engine *eng, int32_t first, int32_t n, zc_c4_state *
     p.out_states = d_out_states;
     p.out_moves16 = d_out_moves;
     p.out_results = d_out_results;
+    ZC_HIP(hipMemsetAsync(eng->a.progress, 0, sizeof(int32_t), (hipStream_t)hip_stream));
+    p.progress = eng->a.progress;
     zc::launch_c4_selfplay(p, (hipStream_t)hip_stream);
     ZC_HIP(hipGetLastError());
     carry_covered(eng, first, n);   // carried moves resume first and this launch suspends none

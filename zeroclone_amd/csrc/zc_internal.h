@@ -50,6 +50,7 @@ struct Arena {
     uint64_t *rngpos = nullptr;   // [G][2]             {next word to use, words generated}
     double *logtab = nullptr;     // [M+2]              glibc log(n), n = 0..M+1
     uint4 *carry = nullptr;       // [G]                a carried self-play move {done, nodes, tag, 0}
+    int32_t *progress = nullptr;  // [64]               free self-play runs: moves finished so far
     int64_t *phase = nullptr;     // [G][kPhases]       diagnostic phase cycles (stamp build)
     // staging for the synchronous host entry points
     zc_c4_state *roots = nullptr;
@@ -103,6 +104,7 @@ struct SearchParams {
     int32_t *ticket;
     int32_t budget;
     int carry;   // 1: suspend in-flight moves once the budget is spent (zc_c4_selfplay_carry_async)
+    int32_t *progress;  // free runs: the launch's finished moves (pace balancing; null: off)
     // walk diagnostic (c4_walk_kernel): per game the rollout value of every simulation
     // [G][sims] and the rollout words of every flush [G][ceil(sims / bs)]
     int8_t *walk_vals;
