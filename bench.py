@@ -790,7 +790,9 @@ def run_rank(args, rank: int, world: int, local: int):
         if world == 1:
             out["extra"]["phases"] = phases(sp, args, bytes_launch, avg_kernel_s)
             other = "free" if args.launch == "pooled" else "pooled"
-            ro = run_steps(sp, args.steps, 0, launch=other)
+            # the other schedule's own steady state: its warmup first (a pooled window leaves
+            # more young, slow games in the pool than the lockstep schedule does)
+            ro = run_steps(sp, args.steps, args.warmup, launch=other)
             out["extra"][f"launch_{other}"] = {"value": round(ro["expansions"] / ro["dt"], 1), "unit": "expansions/s",
                                                "ms_per_step": round(ro["dt"] / args.steps * 1e3, 3),
                                                "moves": ro["moves"], "expansions": ro["expansions"]}
@@ -806,8 +808,10 @@ def run_rank(args, rank: int, world: int, local: int):
             out["extra"]["reference_schedule"] = {
                 "value": lock, "unit": "expansions/s",
                 "note": "scripts/train.py:151-170's lockstep schedule (every game exactly K moves per launch, the "
-                        "launch ends with its slowest game) on the same pool and kernel; the headline `value` is the "
-                        "pooled schedule (the games share K x G moves; each game's moves are its lockstep moves)"}
+                        "launch ends with its slowest game) on the same pool and kernel, after W warmup moves of its "
+                        "own; games behind the launch's average pace run at raised wave priority (pace balancing, "
+                        "DESIGN round 6); the headline `value` is the pooled schedule (the games share K x G moves; "
+                        "each game's moves are its lockstep moves)"}
         if world == 1 and args.net_steps > 0:
             out["extra"]["c2_philox"] = philox_mode(sp, args)
             out["extra"]["c2_value_net"] = net_mode(sp, G, S, B, args.c, args.net_steps, dev)

@@ -22,6 +22,8 @@ from __future__ import annotations
 import ctypes
 from dataclasses import dataclass
 
+import os
+
 import numpy as np
 import torch
 
@@ -536,7 +538,8 @@ class ChessSelfPlay:
             # a network with the convolutional head takes the planes in its input layout straight
             # from the select kernel (no conversion launch per flush)
             self.ps = ChessPuctSearch(self.eng, games, batch_size, seed=puct_seed, leaves=False,
-                                      planes_nhwc=bool(getattr(puct_net, "conv_head", False)))
+                                      planes_nhwc=bool(getattr(puct_net, "conv_head", False))
+                                      and os.environ.get("ZC_PUCT_NHWC", "1") != "0")   # 0: A/B runs only
             self.net_fn = PolicyNet(puct_net)
             if puct_streams > 1:   # the games in parts on their own streams (valued._split_flushes)
                 self.net_fn = [PolicyNet(puct_net.replica()) for _ in range(puct_streams)]
