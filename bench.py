@@ -769,8 +769,8 @@ def run_rank(args, rank: int, world: int, local: int):
                        "parallelism": (f"games sharded over {world} GPU(s), 1 process/GPU" if not args.share_device
                                        else f"rehearsal: {world} ranks sharing GPU 0 over {args.dist_backend}")},
             # The search kernel is a per-game serial chain: SQ counters show neither HBM nor
-            # an issue port saturated (profiles/: ~0.07 of HBM bandwidth, SALU ~0.36 / VALU
-            # ~0.27 issue) — latency and issue arbitration bound it.  achieved / peak / frac
+            # an issue port saturated (profiles/r06_c4_search_summary.json: ~0.03 of HBM
+            # bandwidth, SALU ~0.55 / VALU ~0.42 issue) — latency and issue arbitration bound it.  achieved / peak / frac
             # keep SURVEY §8(d)'s algorithmic HBM roofline; `issue` is the counter roofline.
             "roofline": {"bound": "issue", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 5),
