@@ -19,8 +19,8 @@ import oracle  # noqa: E402
 from zeroclone_amd import _native  # noqa: E402
 
 PHASES = ["walk", "policy+erase", "apply_move", "create_node", "values", "backup", "select_flush", "whole",
-          "legal_moves_check", "material", "node_writes", "lmc.emission", "lmc.copy", "lmc.legality", "lmc.bitview_check",
-          "-"]
+          "legal_moves_check", "material", "node_writes", "lmc.emission", "lmc.runs_masks", "lmc.legality", "lmc.bitview_check",
+          "lmc.runs_emit"]
 
 
 def main():
@@ -66,7 +66,7 @@ def main():
     med = np.median(per, axis=0)
     out = {"workload": "1024 games x 400 sims x bs 32, crude, half opening / half mixed roots (tools/ab_chess.py)",
            "cycles_per_simulation_median_over_games": {k: round(float(v), 1) for k, v in zip(PHASES, med)},
-           "share_of_whole": {k: round(float(v / med[7]), 4) for k, v in zip(PHASES, med) if k not in ("whole", "-")},
+           "share_of_whole": {k: round(float(v / med[7]), 4) for k, v in zip(PHASES, med) if k != "whole"},
            "expansions": int(st[:, 0].sum())}
     print(json.dumps(out), flush=True)
 

@@ -402,67 +402,61 @@ __device__ __forceinline__ uint64_t king_mask(const uint8_t *b, int side) {
 // when the position has more than 128 runs (never in reachable chess: <= 16 pieces).
 __device__ __forceinline__ bool bit_runs(const BitView &v, int s, uint32_t pc, bool mine, uint16_t *ps, uint32_t *rec,
                                          uint32_t &total) {
+    CDEV_T(cd12);
+    // Every lane computes every piece kind's runs and keeps its own kind's by selects: the
+    // kinds' branches diverge in every position, and their joins copied all eight masks.
     const int r = s >> 3, c = s & 7;
     const uint32_t up = upper(pc);
     const uint64_t empty = ~v.occ, ok = ~v.occ | v.cap;
     const uint64_t kb = 1ull << s;
-    uint64_t M[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    uint32_t desc = 0;  // bit k: run k is emitted from the highest index down
-    if (mine) {
-        if (up == 'P') {
-            const bool white = pc == 'P';
-            const int nr = r + (white ? -1 : 1);
-            if ((unsigned)nr < 8u) {
-                const int t1 = nr * 8 + c;
-                if ((empty >> t1) & 1ull) {
-                    M[0] = 1ull << t1;
-                    const int t2 = t1 + (white ? -8 : 8);
-                    if (r == (white ? 6 : 1) && ((empty >> t2) & 1ull)) M[1] = 1ull << t2;
-                }
-                if (c > 0) M[2] = v.cap & (1ull << (t1 - 1));
-                if (c < 7) M[3] = v.cap & (1ull << (t1 + 1));
-            }
-        } else if (up == 'N') {
-            M[0] = ok & (((kb << 17) & kNotA) | ((kb << 15) & kNotH) | ((kb << 10) & kNotAB) | ((kb << 6) & kNotGH) |
-                         ((kb >> 17) & kNotH) | ((kb >> 15) & kNotA) | ((kb >> 10) & kNotGH) | ((kb >> 6) & kNotAB));
-        } else if (up == 'K') {
-            const uint64_t T = ok & (((kb << 1) & kNotA) | ((kb >> 1) & kNotH) | (kb << 8) | (kb >> 8) |
-                                     ((kb << 9) & kNotA) | ((kb << 7) & kNotH) | ((kb >> 7) & kNotA) | ((kb >> 9) & kNotH));
-            constexpr int off[8] = {-9, -7, 7, 9, -8, 8, -1, 1};  // kAll8 order
+    const bool isP = mine && up == 'P', isN = mine && up == 'N', isK = mine && up == 'K';
+    const bool isS = mine && (up == 'B' || up == 'R' || up == 'Q');
+    const bool diagS = isS && up != 'R', orthS = isS && up != 'B';
+    const bool white = pc == 'P';
+    const uint64_t fwd = white ? kb >> 8 : kb << 8;  // the pawn's push square (none from its last rank)
+    const uint64_t p1 = fwd & empty;
+    // slider lines through s
+    const uint64_t low = kb - 1ull, high = ~low & ~kb;
+    const uint64_t file = kFileA << c, rank = 0xFFull << (8 * r);
+    const int dd = r - c, da = r + c - 7;
+    const uint64_t diag = dd >= 0 ? kDiag << (8 * dd) : kDiag >> (-8 * dd);
+    const uint64_t anti = da >= 0 ? kAnti << (8 * da) : kAnti >> (-8 * da);
+    auto up_ray = [&](uint64_t ray) {  // towards higher indices: through the nearest blocker
+        const uint64_t bl = ray & v.occ, first = bl & (0ull - bl);
+        return ok & (first ? ray & ((first << 1) - 1ull) : ray);
+    };
+    auto down_ray = [&](uint64_t ray) {  // towards lower indices
+        const uint64_t bl = ray & v.occ;
+        return ok & (bl ? ray & ~((1ull << (63 - __builtin_clzll(bl))) - 1ull) : ray);
+    };
+    uint64_t M[8];
 #pragma unroll
-            for (int i = 0; i < 8; ++i) {
-                const int to = s + off[i];
-                M[i] = (unsigned)to < 64u ? T & (1ull << (to & 63)) : 0ull;
-            }
-        } else if (up == 'B' || up == 'R' || up == 'Q') {
-            const uint64_t low = kb - 1ull, high = ~low & ~kb;
-            const uint64_t file = kFileA << c, rank = 0xFFull << (8 * r);
-            const int dd = r - c, da = r + c - 7;
-            const uint64_t diag = dd >= 0 ? kDiag << (8 * dd) : kDiag >> (-8 * dd);
-            const uint64_t anti = da >= 0 ? kAnti << (8 * da) : kAnti >> (-8 * da);
-            auto up_ray = [&](uint64_t ray) {  // towards higher indices: through the nearest blocker
-                const uint64_t bl = ray & v.occ, first = bl & (0ull - bl);
-                return ok & (first ? ray & ((first << 1) - 1ull) : ray);
-            };
-            auto down_ray = [&](uint64_t ray) {  // towards lower indices
-                const uint64_t bl = ray & v.occ;
-                return ok & (bl ? ray & ~((1ull << (63 - __builtin_clzll(bl))) - 1ull) : ray);
-            };
-            if (up != 'R') {  // kAll8[0..4): (-1,-1) (-1,1) (1,-1) (1,1)
-                M[0] = down_ray(diag & low);
-                M[1] = down_ray(anti & low);
-                M[2] = up_ray(anti & high);
-                M[3] = up_ray(diag & high);
-            }
-            if (up != 'B') {  // kAll8[4..8): (-1,0) (1,0) (0,-1) (0,1)
-                M[4] = down_ray(file & low);
-                M[5] = up_ray(file & high);
-                M[6] = down_ray(rank & low);
-                M[7] = up_ray(rank & high);
-            }
-            desc = 0x53u;  // runs 0, 1, 4, 6
-        }
+    for (int k = 0; k < 8; ++k) {  // one run at a time, each mask consumed where it is made
+        // run k of a slider: its ray in kAll8 order, away from s
+        const uint64_t line = k == 0 || k == 3 ? diag : k == 1 || k == 2 ? anti : k < 6 ? file : rank;
+        const bool dn = k == 0 || k == 1 || k == 4 || k == 6;
+        uint64_t m = (k < 4 ? diagS : orthS) ? (dn ? down_ray(line & low) : up_ray(line & high)) : 0ull;
+        // of a king: its neighbour in direction k (kAll8: -9, -7, 7, 9, -8, 8, -1, 1; no file wrap)
+        const uint64_t nbk = k == 0 ? (kb >> 9) & kNotH : k == 1 ? (kb >> 7) & kNotA : k == 2 ? (kb << 7) & kNotH
+                           : k == 3 ? (kb << 9) & kNotA : k == 4 ? kb >> 8 : k == 5 ? kb << 8
+                           : k == 6 ? (kb >> 1) & kNotH : (kb << 1) & kNotA;
+        m = isK ? ok & nbk : m;
+        // of a pawn: push, double push, captures towards the lower / higher file
+        if (k == 0) m = isP ? p1 : m;
+        if (k == 1)
+            m = isP ? ((p1 != 0ull && r == (white ? 6 : 1)) ? (white ? fwd >> 8 : fwd << 8) & empty : 0ull) : m;
+        if (k == 2) m = isP ? (fwd >> 1) & kNotH & v.cap : m;
+        if (k == 3) m = isP ? (fwd << 1) & kNotA & v.cap : m;
+        // of a knight: every target, one ascending run
+        if (k == 0)
+            m = isN ? ok & (((kb << 17) & kNotA) | ((kb << 15) & kNotH) | ((kb << 10) & kNotAB) | ((kb << 6) & kNotGH) |
+                            ((kb >> 17) & kNotH) | ((kb >> 15) & kNotA) | ((kb >> 10) & kNotGH) | ((kb >> 6) & kNotAB))
+                    : m;
+        M[k] = m;
+        __builtin_amdgcn_sched_barrier(0);
     }
+    const uint32_t desc = isS ? 0x53u : 0u;  // bit k: run k is emitted from the highest index down (0, 1, 4, 6)
+    CDEV_ADD(12, cd12);
     uint32_t nruns = 0, nmoves = 0;
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
@@ -487,6 +481,7 @@ __device__ __forceinline__ bool bit_runs(const BitView &v, int s, uint32_t pc, b
         }
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    CDEV_T(cd15);
     for (uint32_t base = 0; base < runs_total; base += 64) {
         const uint32_t j = base + lane();
         if (j < runs_total) {
@@ -511,6 +506,7 @@ __device__ __forceinline__ bool bit_runs(const BitView &v, int s, uint32_t pc, b
         }
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    CDEV_ADD(15, cd15);
     return true;
 }
 
@@ -540,8 +536,6 @@ __device__ __forceinline__ int legal_moves_view(const V &v, int t, uint32_t pc, 
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     }
     CDEV_ADD(11, cd11);
-    CDEV_T(cd12);
-    CDEV_ADD(12, cd12);
     CDEV_T(cd13);
     const uint32_t kch = t == 0 ? 'K' : 'k';
     int n = 0;
@@ -780,7 +774,7 @@ struct ChessScratch {
     uint8_t board[64];
     uint16_t legal[kMaxLegal];
     uint16_t pseudo[kMaxPseudo];
-    uint16_t region[64 * kRegion];
+    alignas(16) uint16_t region[64 * kRegion];  // also bit_runs' 16-byte run records
 };
 
 }  // namespace
