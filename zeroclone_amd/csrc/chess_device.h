@@ -93,6 +93,19 @@ constexpr uint64_t kNotA = ~kFileA, kNotH = ~(kFileA << 7);
 constexpr uint64_t kNotAB = ~(kFileA | (kFileA << 1)), kNotGH = ~((kFileA << 6) | (kFileA << 7));
 constexpr uint64_t kDiag = 0x8040201008040201ull;  // squares (i, i)
 constexpr uint64_t kAnti = 0x0102040810204080ull;  // squares (i, 7 - i)
+// A knight's / king's targets from square s as ONE signed shift of the pattern of a square
+// whose targets do not wrap (knight: square 18 = (2, 2); king: square 9 = (1, 1)), the files
+// a shift wraps into masked off (exhaustively equal to the eight masked shifts of kb).
+constexpr uint64_t kKnight18 = 0xA1100110Aull, kKing9 = 0x70507ull;
+__device__ __forceinline__ uint64_t shift_signed(uint64_t p, int d) { return d >= 0 ? p << d : p >> -d; }
+__device__ __forceinline__ uint64_t knight_targets(int s) {
+    const int c = s & 7;
+    return shift_signed(kKnight18, s - 18) & (c < 2 ? kNotGH : c > 5 ? kNotAB : ~0ull);
+}
+__device__ __forceinline__ uint64_t king_targets(int s) {
+    const int c = s & 7;
+    return shift_signed(kKing9, s - 9) & (c == 0 ? kNotH : c == 7 ? kNotA : ~0ull);
+}
 
 struct BitView {
     static constexpr bool kCheapProbe = true;  // generation from masks (bit_piece_moves)
@@ -125,12 +138,8 @@ struct BitView {
         const uint64_t kb = 1ull << k;
         const uint64_t pawns = t == 0 ? (((kb >> 9) & kNotH) | ((kb >> 7) & kNotA))
                                       : (((kb << 7) & kNotH) | ((kb << 9) & kNotA));
-        const uint64_t knights = ((kb << 17) & kNotA) | ((kb << 15) & kNotH) | ((kb << 10) & kNotAB) |
-                                 ((kb << 6) & kNotGH) | ((kb >> 17) & kNotH) | ((kb >> 15) & kNotA) |
-                                 ((kb >> 10) & kNotGH) | ((kb >> 6) & kNotAB);
-        const uint64_t king = ((kb << 1) & kNotA) | ((kb >> 1) & kNotH) | (kb << 8) | (kb >> 8) |
-                              ((kb << 9) & kNotA) | ((kb << 7) & kNotH) | ((kb >> 7) & kNotA) | ((kb >> 9) & kNotH);
-        if (((pawns & eP) | (knights & eN) | (king & eK)) & keep) return true;
+        const uint64_t knights = knight_targets(k), king = king_targets(k);
+        const bool leap = (((pawns & eP) | (knights & eN) | (king & eK)) & keep) != 0ull;
         // sliders: the nearest occupied square of each ray must not be an enemy slider of
         // the ray's kind (rook lines: rook or queen; diagonals: bishop or queen)
         const int r = k >> 3, c = k & 7;
@@ -148,9 +157,10 @@ struct BitView {
             const uint64_t bl = ray & o;
             return bl != 0ull && ((a >> (63 - __builtin_clzll(bl))) & 1ull);
         };
-        return lowest(file & high, ao) || lowest(rank & high, ao) || highest(file & low, ao) ||
-               highest(rank & low, ao) || lowest(diag & high, ad) || lowest(anti & high, ad) ||
-               highest(diag & low, ad) || highest(anti & low, ad);
+        // every test evaluated (no short-circuit branches: the lanes diverge on them)
+        return leap | lowest(file & high, ao) | lowest(rank & high, ao) | highest(file & low, ao) |
+               highest(rank & low, ao) | lowest(diag & high, ad) | lowest(anti & high, ad) |
+               highest(diag & low, ad) | highest(anti & low, ad);
     }
 };
 
@@ -449,9 +459,7 @@ __device__ __forceinline__ bool bit_runs(const BitView &v, int s, uint32_t pc, b
         if (k == 3) m = isP ? (fwd << 1) & kNotA & v.cap : m;
         // of a knight: every target, one ascending run
         if (k == 0)
-            m = isN ? ok & (((kb << 17) & kNotA) | ((kb << 15) & kNotH) | ((kb << 10) & kNotAB) | ((kb << 6) & kNotGH) |
-                            ((kb >> 17) & kNotH) | ((kb >> 15) & kNotA) | ((kb >> 10) & kNotGH) | ((kb >> 6) & kNotAB))
-                    : m;
+            m = isN ? ok & knight_targets(s) : m;
         M[k] = m;
         __builtin_amdgcn_sched_barrier(0);
     }
