@@ -498,18 +498,15 @@ __device__ __forceinline__ bool bit_runs(const BitView &v, int s, uint32_t pc, b
             uint16_t *dst = ps + q[2];
             const uint32_t meta = q[3];
             const int from = (int)(meta & 63u);
-            if (meta & 64u) {
-                while (T) {
-                    const int to = 63 - __builtin_clzll(T);
-                    T &= ~(1ull << to);
-                    *dst++ = (uint16_t)pack_move(from, to, 0u);
-                }
-            } else {
-                while (T) {
-                    const int to = __builtin_ctzll(T);
-                    T &= T - 1ull;
-                    *dst++ = (uint16_t)pack_move(from, to, 0u);
-                }
+            const bool down = (meta & 64u) != 0u;
+            // a run has at most 8 targets (a knight's); ascending and descending runs share
+            // one unrolled loop (their lanes would otherwise run two divergent loops in turn)
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                if (T == 0ull) break;
+                const int to = down ? 63 - __builtin_clzll(T) : __builtin_ctzll(T);
+                T &= ~(1ull << to);
+                dst[k] = (uint16_t)pack_move(from, to, 0u);
             }
         }
     }
