@@ -158,9 +158,9 @@ struct BitView {
             return bl != 0ull && ((a >> (63 - __builtin_clzll(bl))) & 1ull);
         };
         // every test evaluated (no short-circuit branches: the lanes diverge on them)
-        return leap | lowest(file & high, ao) | lowest(rank & high, ao) | highest(file & low, ao) |
-               highest(rank & low, ao) | lowest(diag & high, ad) | lowest(anti & high, ad) |
-               highest(diag & low, ad) | highest(anti & low, ad);
+        return ((int)leap | (int)lowest(file & high, ao) | (int)lowest(rank & high, ao) | (int)highest(file & low, ao) |
+                (int)highest(rank & low, ao) | (int)lowest(diag & high, ad) | (int)lowest(anti & high, ad) |
+                (int)highest(diag & low, ad) | (int)highest(anti & low, ad)) != 0;
     }
 };
 
