@@ -460,6 +460,8 @@ int zc_c4_selfplay_async(zc_engine *eng, int32_t first, int32_t n, zc_c4_state *
     p.out_states = d_out_states;
     p.out_moves16 = d_out_moves;
     p.out_results = d_out_results;
+    // the pace-balancing counter (priorities only: two free runs of one engine in flight on
+    // different streams would share it and balance less well, with the same outputs)
     ZC_HIP(hipMemsetAsync(eng->a.progress, 0, sizeof(int32_t), (hipStream_t)hip_stream));
     p.progress = eng->a.progress;
     zc::launch_c4_selfplay(p, (hipStream_t)hip_stream);

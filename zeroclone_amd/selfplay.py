@@ -304,6 +304,8 @@ class C4SelfPlay:
         """Every slot back to the opening; with a quota, slots beyond it idle and finished
         slots start new games only while fewer than `quota` have started."""
         if self.carry_pending:   # the games restart: their carried moves are dropped
+            # (after every stream's launches: the carry launch may have run on a caller's stream)
+            torch.cuda.synchronize(self.dev)
             self.eng.c4_carry_discard(0, self.G, torch.cuda.current_stream(self.dev).cuda_stream)
             self.carry_pending = False
         self.roots.zero_()
