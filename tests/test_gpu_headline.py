@@ -111,6 +111,39 @@ def test_free_launch_matches_oracle_at_headline_shape(pool):
     assert replay(sp.eng, snap, mts, sample, states, moves, res) == 3 * len(sample)
 
 
+def test_carry_launches_match_oracle_at_headline_shape(pool):
+    """The bench's carry launches (zc_c4_selfplay_carry_async) at the headline shape: two
+    launches whose in-flight moves carry over, then the drain; every sampled game's finished
+    moves, launch after launch, replay through the oracle from the snapshot, and each game's
+    stream ends where the oracle's does."""
+    sp = pool
+    sample = list(range(3, G, 16))
+    snap = sp.roots.cpu().numpy().copy()
+    mts = {g: oracle_mt(sp.eng, g) for g in sample}
+    parts = []
+    for k in (3, 2, None):
+        res = (sp.run_pooled(k * G, 2 * k, carry=True) if k else sp.drain()).cpu().numpy()
+        parts.append((res, sp._run_states.cpu().numpy(), sp._run_moves.cpu().numpy()))
+        assert int(sp.stats[:, 5].abs().sum()) == 0
+    played = [(r != SKIP).sum(0) for r, _, _ in parts]
+    assert int(sum(p.sum() for p in played)) == 5 * G   # every ticketed move finished once
+    assert int(played[0].sum()) < 3 * G                  # ... some of them in a later launch
+    # each game's finished moves in order: launch 1's prefix, then launch 2's, then the drain's
+    K = sum(r.shape[0] for r, _, _ in parts)
+    res_all = np.full((K, G), SKIP, np.int32)
+    st_all = np.zeros((K, G, 3), np.int64)
+    mv_all = np.zeros((K, G), np.int16)
+    for g in sample:
+        row = 0
+        for (r, st, mv), n in zip(parts, played):
+            c = int(n[g])
+            res_all[row:row + c, g], st_all[row:row + c, g], mv_all[row:row + c, g] = r[:c, g], st[:c, g], mv[:c, g]
+            row += c
+    checked = replay(sp.eng, snap, mts, sample, st_all, mv_all, res_all)
+    assert checked >= 5 * len(sample) * 0.8
+    assert not sp.carry_pending
+
+
 def test_pooled_launch_refuses_more_games_than_resident():
     """A pooled launch hands its budget only to resident waves: a grid larger than the chip
     holds at once is refused (the later games would never move)."""
