@@ -414,6 +414,8 @@ class C4SelfPlay:
         """Take over another pool's games in progress (positions and their recorded
         histories, game numbers; this pool's streams and pool stay its own) — e.g. a
         network-mode pool starting from a burned-in rollout pool's mixed game ages."""
+        if self.carry_pending:   # its carried searches belong to the roots being replaced
+            raise RuntimeError("moves carried over by run_pooled(carry=True) are in flight: drain() first")
         self.roots.copy_(other.roots)
         if self.traj is not None and other.traj is not None:
             t, o = self.traj, other.traj
