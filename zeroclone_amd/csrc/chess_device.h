@@ -410,9 +410,10 @@ __device__ __forceinline__ uint64_t king_mask(const uint8_t *b, int side) {
 // is as long as the longest run (<= 8) instead of a piece's whole move list.  Capture values
 // are added by the caller, as for bit_piece_moves.  Returns false, leaving nothing written,
 // when the position has more than 128 runs (never in reachable chess: <= 16 pieces).
-__device__ __forceinline__ bool bit_runs(const BitView &v, int s, uint32_t pc, bool mine, uint16_t *ps, uint32_t *rec,
-                                         uint32_t &total) {
-    CDEV_T(cd12);
+// The eight run masks of the piece on square s (bit_runs' first part; all zero for a square
+// that is not the mover's), and desc: bit k set when run k is emitted from the highest index down.
+__device__ __forceinline__ void run_masks(const BitView &v, int s, uint32_t pc, bool mine, uint64_t (&M)[8],
+                                          uint32_t &desc) {
     // Every lane computes every piece kind's runs and keeps its own kind's by selects: the
     // kinds' branches diverge in every position, and their joins copied all eight masks.
     const int r = s >> 3, c = s & 7;
@@ -439,7 +440,6 @@ __device__ __forceinline__ bool bit_runs(const BitView &v, int s, uint32_t pc, b
         const uint64_t bl = ray & v.occ;
         return ok & (bl ? ray & ~((1ull << (63 - __builtin_clzll(bl))) - 1ull) : ray);
     };
-    uint64_t M[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) {  // one run at a time, each mask consumed where it is made
         // run k of a slider: its ray in kAll8 order, away from s
@@ -463,7 +463,15 @@ __device__ __forceinline__ bool bit_runs(const BitView &v, int s, uint32_t pc, b
         M[k] = m;
         __builtin_amdgcn_sched_barrier(0);
     }
-    const uint32_t desc = isS ? 0x53u : 0u;  // bit k: run k is emitted from the highest index down (0, 1, 4, 6)
+    desc = isS ? 0x53u : 0u;  // runs 0, 1, 4, 6
+}
+
+__device__ __forceinline__ bool bit_runs(const BitView &v, int s, uint32_t pc, bool mine, uint16_t *ps, uint32_t *rec,
+                                         uint32_t &total) {
+    CDEV_T(cd12);
+    uint64_t M[8];
+    uint32_t desc;
+    run_masks(v, s, pc, mine, M, desc);
     CDEV_ADD(12, cd12);
     uint32_t nruns = 0, nmoves = 0;
 #pragma unroll
@@ -620,6 +628,52 @@ __device__ __forceinline__ int legal_moves_check(const uint8_t *b, uint32_t pc, 
 __device__ __forceinline__ int legal_moves_check(const uint8_t *b, int t, uint16_t *out, uint16_t *ps, uint16_t *reg,
                                                  bool &check) {
     return legal_moves_check(b, (uint32_t)b[lane()], t, out, ps, reg, check);
+}
+
+// Whether the position has a legal move, for a node that may never be expanded (the crude
+// search's lazy nodes): one pseudo-legal move per piece (its first run's first target) through
+// the same legality test as legal_moves_view.  When one of them is legal, returns 1 with
+// lazy = true and writes nothing (the list is generated if the node is ever expanded);
+// otherwise — every tested move illegal (typically in check), a position the bit view does not
+// cover, or insufficient material — the full legal_moves_check: the list in out, its length,
+// and the check flag of a position without moves.
+__device__ __forceinline__ int legal_moves_probe(const uint8_t *b, uint32_t pc, int t, uint16_t *out, uint16_t *ps,
+                                                 uint16_t *reg, bool &check, bool &lazy) {
+    lazy = false;
+    BitView bv;
+    const uint32_t up = upper(pc);
+    const uint64_t heavy = __ballot(up == 'P' || up == 'R' || up == 'Q');
+    const int minor = __popcll(__ballot(up == 'B' || up == 'N'));
+    if ((heavy || minor > 1) && make_bitview(pc, t, bv)) {
+        const int s = (int)lane();
+        const bool mine = !empty_sq(pc) && ((t == 0) == is_white(pc));
+        uint64_t M[8];
+        uint32_t desc;
+        run_masks(bv, s, pc, mine, M, desc);
+        uint64_t T = 0;
+        bool down = false;
+#pragma unroll
+        for (int k = 7; k >= 0; --k) {  // the first non-empty run
+            if (M[k] != 0ull) {
+                T = M[k];
+                down = ((desc >> k) & 1u) != 0u;
+            }
+        }
+        bool legal = false;
+        if (T != 0ull) {
+            const int to = down ? 63 - __builtin_clzll(T) : __builtin_ctzll(T);
+            const uint32_t kch = t == 0 ? 'K' : 'k';
+            const uint32_t mp = bv.piece_at(s);
+            const uint64_t km = (bv.kings & ~(1ull << s)) | (mp == kch ? (1ull << to) : 0ull);
+            legal = !bv.attacked(__builtin_ctzll(km), s, to, mp);  // km != 0: the bit view has a king
+        }
+        if (__ballot(legal) != 0ull) {
+            lazy = true;
+            check = false;
+            return 1;
+        }
+    }
+    return legal_moves_check(b, pc, t, out, ps, reg, check);
 }
 
 // Sum of piece values, white positive (crude_chess_score's material), by ballots.

@@ -117,8 +117,41 @@ struct Expansion {
     uint32_t base;   // X's first slot
 };
 
+#ifndef ZC_CHESS_LAZY
+#define ZC_CHESS_LAZY 1  // 1: crude-search nodes are created with a legal-move probe only (A/B: 0)
+#endif
+
+// The first expansion of a lazy node (created by create_child_gen<true>): its position into
+// L.st, the full get_legal_moves, and the node's move list committed as create_node_commit
+// would have at its creation (slots taken now, all moves untried, no children).  Returns the
+// list's length (nu == nmoves from here on) and its first slot in `base`.
+__device__ __forceinline__ int generate_lazy(const CTree &t, CLds &L, ChessNode *N, int &slots, int &status,
+                                             uint32_t &base) {
+    const uint32_t lane = lane_id();
+    if (lane < 18) ((uint32_t *)&L.st)[lane] = ((const uint32_t *)&N->st)[lane];
+    wave_sync_mem();
+    const NodeGen gen = create_node_gen(L);
+    const int b = slots;
+    const int n = create_node_take(t, gen, slots, status);
+    for (int j = (int)lane; j < n; j += 64) {
+        t.mv[b + j] = L.s.legal[j];
+        t.ut[b + j] = (uint8_t)j;
+        t.ch[b + j] = 0xFFFF;
+        t.na[b + j] = 0;
+        t.w[b + j] = 0.0;
+    }
+    if (lane == 0) {
+        N->base = (uint32_t)b;
+        N->nmoves = (uint16_t)n;
+        N->nu = (uint16_t)n;
+    }
+    wave_sync_mem();
+    base = (uint32_t)b;
+    return n;
+}
+
 __device__ __forceinline__ Expansion sim_front(const ChessParams &p, const CTree &t, ConstDouble *logtab, Rng &rng, int done,
-                               int &status, Resume &rs) {
+                               int &status, Resume &rs, CLds &L, int &slots) {
     const uint32_t lane = lane_id();
     int node = 0, depth = 0, nN = done;
     uint32_t pathv = 0;
@@ -134,7 +167,13 @@ __device__ __forceinline__ Expansion sim_front(const ChessParams &p, const CTree
     CSTAMP_T(cs1);
     ChessNode *N = &t.nodes[node];
     const bool hit = rs.cached;
-    const int nu = hit ? rs.nu : uni((int)N->nu);
+    int nu = hit ? rs.nu : uni((int)N->nu);
+    uint32_t lazy_base = 0;
+    bool lazy_gen = false;
+    if (ZC_CHESS_LAZY && !hit && nu > 0 && !status && uni((int)N->nmoves) == (int)kChessLazy) {
+        nu = generate_lazy(t, L, N, slots, status, lazy_base);
+        lazy_gen = true;
+    }
     rs.node = node;
     rs.depth = depth;
     rs.nN = nN;
@@ -150,7 +189,7 @@ __device__ __forceinline__ Expansion sim_front(const ChessParams &p, const CTree
         stw = lane < 18 ? ((const uint32_t *)&N->st)[lane] : 0u;
         vmem_ready(stw);
     }
-    const uint32_t base = hit ? rs.base : uni(N->base);
+    const uint32_t base = hit ? rs.base : lazy_gen ? lazy_base : uni(N->base);
     int local, midx;
     uint32_t m;
     if (nu <= 64) {
@@ -265,7 +304,7 @@ __device__ void helper_loop(Helper &h) {
         __syncthreads();  // a command is posted
         if (uni(h.cmd) != 1) return;  // plain LDS accesses: the barriers order them
         const uint32_t stw = lane < 18 ? h.stw[lane] : 0u;
-        const NodeGen gen = create_child_gen(h.L, stw, uni(h.m));
+        const NodeGen gen = create_child_gen<ZC_CHESS_LAZY != 0>(h.L, stw, uni(h.m));
         if (lane == 0) h.gen = gen;
         __syncthreads();  // the generated child is in h
     }
@@ -381,7 +420,7 @@ __device__ __forceinline__ int chess_select_flush(const ChessParams &p, const CT
     };
     auto leaf_path = [&](const Expansion &e) { return lane == (uint32_t)(e.depth + 1) ? e.base + (uint32_t)e.midx : e.pathv; };
     while (j < nb && !status) {
-        const Expansion a = sim_front(p, t, logtab, rng, done, status, rs);
+        const Expansion a = sim_front(p, t, logtab, rng, done, status, rs, L, slots);
         if (a.midx < 0 || status) {  // no expansion: the walk's end is the leaf
             record(a.node, a.depth, a.pathv);
             continue;
@@ -397,7 +436,7 @@ __device__ __forceinline__ int chess_select_flush(const ChessParams &p, const CT
         Expansion b{};
         const Rng rng_a = rng;  // the stream after a's draw: restored when a ends the flush
         if (pair) {
-            b = sim_front(p, t, logtab, rng, done, status, rs);
+            b = sim_front(p, t, logtab, rng, done, status, rs, L, slots);
             if (lane < 18) h->stw[lane] = b.stw;
             if (lane == 0) {
                 h->m = b.m;
@@ -408,7 +447,8 @@ __device__ __forceinline__ int chess_select_flush(const ChessParams &p, const CT
         const int ida = nnodes++;
         if (ida >= p.M) status = ZC_STATUS_INTERNAL;
         CSTAMP_T(cs3);
-        const NodeGen ga = create_child_gen(L, a.stw, a.m);  // play_move + Node(...) (mcts.cpp:74-76)
+        // play_move + Node(...) (mcts.cpp:74-76); its legal moves generated on its first expansion
+        const NodeGen ga = create_child_gen<ZC_CHESS_LAZY != 0>(L, a.stw, a.m);
         if (!status) commit_child(t, L, ga, a, ida, slots, status, cn);
         CSTAMP_ADD(3, cs3);
         record(ida, a.depth + 1, leaf_path(a));

@@ -91,11 +91,17 @@ struct NodeGen {
     int n;
     int check;
     int32_t mat;
+    int lazy;  // 1: the position has legal moves, not generated yet (legal_moves_probe); NodeGen{n, check, mat}: 0
 };
+
+// ChessNode::nmoves of a lazy node (nu = 1: the walk stops there, and its first expansion
+// generates the list: chess_search.hip generate_lazy)
+constexpr uint16_t kChessLazy = 0xFFFF;
 
 // The child of the position in `stw` (lanes 0..17: its zc_chess_state words) by move m, into
 // L.st, and its generation, with the child's squares kept in registers (one LDS round trip
 // fewer than staging the parent in L.st and applying the move there).
+template <bool PROBE = false>
 __device__ __forceinline__ NodeGen create_child_gen(CLds &L, uint32_t stw, uint32_t m) {
     const uint32_t lane = lane_id();
     uint32_t w16;
@@ -104,15 +110,17 @@ __device__ __forceinline__ NodeGen create_child_gen(CLds &L, uint32_t stw, uint3
     if (lane == 16) ((uint32_t *)&L.st)[16] = w16;
     if (lane == 17) ((uint32_t *)&L.st)[17] = stw;
     wave_sync_mem();
-    bool check;
+    bool check, lazy = false;
     CSTAMP_T(cs8);
-    const int n = chessdev::legal_moves_check(L.st.board, x, (int)(w16 & 0xFFu), L.s.legal, L.s.pseudo, L.s.region,
-                                              check);
+    const int n = PROBE ? chessdev::legal_moves_probe(L.st.board, x, (int)(w16 & 0xFFu), L.s.legal, L.s.pseudo,
+                                                      L.s.region, check, lazy)
+                        : chessdev::legal_moves_check(L.st.board, x, (int)(w16 & 0xFFu), L.s.legal, L.s.pseudo,
+                                                      L.s.region, check);
     CSTAMP_ADD(8, cs8);
     CSTAMP_T(cs9);
     const int32_t mat = chessdev::material(x);
     CSTAMP_ADD(9, cs9);
-    return NodeGen{n, check ? 1 : 0, mat};
+    return NodeGen{n, check ? 1 : 0, mat, lazy ? 1 : 0};
 }
 
 __device__ __forceinline__ NodeGen create_node_gen(CLds &L) {
@@ -134,6 +142,7 @@ __device__ __forceinline__ NodeGen create_node_gen(CLds &L) {
 // The slot range of a node of gen.n moves: its base (the next free slot) and the move count it
 // keeps (0 when the list overflowed or the slots ran out: ZC_STATUS_CAPACITY).
 __device__ __forceinline__ int create_node_take(const CTree &t, NodeGen gen, int &slots, int &status) {
+    if (gen.lazy) return 0;  // no list, no slots until its first expansion
     int n = gen.n;
     if (n < 0) {
         status = ZC_STATUS_CAPACITY;
@@ -165,8 +174,8 @@ __device__ __forceinline__ void create_node_commit(const CTree &t, const CLds &L
     if (lane < 18) ((uint32_t *)&N->st)[lane] = ((const uint32_t *)&L.st)[lane];
     if (lane == 0) {
         N->base = (uint32_t)base;
-        N->nmoves = (uint16_t)n;
-        N->nu = (uint16_t)n;
+        N->nmoves = gen.lazy ? kChessLazy : (uint16_t)n;
+        N->nu = gen.lazy ? (uint16_t)1 : (uint16_t)n;
         N->parent = (uint16_t)parent;
         N->pact = (uint16_t)pact;
         N->depth = (uint16_t)depth;
