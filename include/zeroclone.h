@@ -719,6 +719,8 @@ int zc_debug_rng_copy(zc_engine *eng, int32_t first_game, int32_t n_games, void 
  * move, prior, Na, Wa and child node (0xFFFF = none); out_counts = {nodes, slots used}.
  * The in-check flag is computed only for a node WITH NO legal move (checkmate vs stalemate,
  * the one case every caller reads): it is 0 for every node that has moves, in check or not.
+ * In a UCT tree (crude score, value network) a node never expanded is LAZY: #moves = 0xFFFF,
+ * #untried = 1, no slots — its legal moves exist but are generated at its first expansion.
  * Synchronises the device. */
 int zc_debug_chess_tree(zc_engine *eng, int32_t game, int32_t max_nodes, int32_t max_slots, void *out_nodes,
                         uint16_t *out_mv, float *out_prior, int32_t *out_na, double *out_w, uint16_t *out_child,
