@@ -43,6 +43,12 @@ extern "C" int zc_debug_conv_stamps(void *host, int n) {
 
 namespace zc {
 namespace {
+#ifndef ZC_TOWER_STAMP
+#define ZC_TOWER_STAMP 0  // diagnostic build: per-phase s_memtime cycles of the fused tower's waves
+#endif
+#if ZC_TOWER_STAMP
+__device__ unsigned long long g_tower_stamp[4];  // MFMA loop, epilogue, barrier wait, whole kernel
+#endif
 
 typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 typedef _Float16 h4 __attribute__((ext_vector_type(4)));
@@ -1131,6 +1137,10 @@ __global__ __launch_bounds__(256 * PG) __attribute__((amdgpu_waves_per_eu(WPE, W
         pyx[t] = (P < npix ? py << 8 : 64 << 8) | (rem - py * W);
     }
     __syncthreads();  // the input tile and the zero rows are in LDS
+#if ZC_TOWER_STAMP
+    uint64_t st_mfma = 0, st_epi = 0, st_bar = 0;
+    const uint64_t st_k0 = __builtin_amdgcn_s_memtime();
+#endif
     // layer l: src -> dst, then a barrier (dst complete before layer l+1 reads it; dst was
     // layer l-1's src, which every wave finished reading before the previous barrier)
     auto layer = [&](int l, auto kc_tag) {
@@ -1164,13 +1174,35 @@ __global__ __launch_bounds__(256 * PG) __attribute__((amdgpu_waves_per_eu(WPE, W
             float4 bv[2];
 #pragma unroll
             for (int m = 0; m < 2; ++m) bv[m] = *(const float4 *)(ball + (size_t)l * kCout + wave * 32 + 16 * m + 4 * q4);
+#if ZC_TOWER_STAMP
+            __builtin_amdgcn_sched_barrier(0);
+            const uint64_t ts0 = __builtin_amdgcn_s_memtime();
+            __builtin_amdgcn_sched_barrier(0);
+#endif
             tower_mfma16<H, W, NP, KC, 8, LD, tower_zero<NT>(), ZR>(lds, src, wa, wn, a, l16, py16, q4, acc);
+#if ZC_TOWER_STAMP
+            __builtin_amdgcn_sched_barrier(0);
+            const uint64_t ts1 = __builtin_amdgcn_s_memtime();
+            __builtin_amdgcn_sched_barrier(0);
+            st_mfma += ts1 - ts0;
+#endif
             if constexpr (EPI == 1)
                 tower_epilogue16_swap<NP>(lds + dst * LD, bv, l >= 2 && !(l & 1), npix, wave, l16, q4, acc);
             else if constexpr (EPI == 2)
                 tower_epilogue16<NP>(lds + dst * LD, bv, l >= 2 && !(l & 1), npix, wave, l16, q4, acc);
             else
                 tower_epilogue16b<NP>(lds + dst * LD, bv, l >= 2 && !(l & 1), npix, wave, l16, q4, acc);
+#if ZC_TOWER_STAMP
+            __builtin_amdgcn_sched_barrier(0);
+            const uint64_t ts2 = __builtin_amdgcn_s_memtime();
+            __builtin_amdgcn_sched_barrier(0);
+            st_epi += ts2 - ts1;
+            __syncthreads();
+            __builtin_amdgcn_sched_barrier(0);
+            st_bar += __builtin_amdgcn_s_memtime() - ts2;
+            __builtin_amdgcn_sched_barrier(0);
+            return;
+#endif
         } else {
             int pr[NT], py[NT];
 #pragma unroll
@@ -1194,6 +1226,14 @@ __global__ __launch_bounds__(256 * PG) __attribute__((amdgpu_waves_per_eu(WPE, W
     };
     layer(0, std::integral_constant<int, KC0>{});
     for (int l = 1; l < nconv; ++l) layer(l, std::integral_constant<int, 8>{});
+#if ZC_TOWER_STAMP
+    if (lane == 0) {
+        atomicAdd(&g_tower_stamp[0], (unsigned long long)st_mfma);
+        atomicAdd(&g_tower_stamp[1], (unsigned long long)st_epi);
+        atomicAdd(&g_tower_stamp[2], (unsigned long long)st_bar);
+        atomicAdd(&g_tower_stamp[3], (unsigned long long)(__builtin_amdgcn_s_memtime() - st_k0));
+    }
+#endif
     // the tower's output is the last layer's dst (buf0, nconv odd)
     if (values) {
         // the value head on it, one wave per board: value_head_kernel's arithmetic in its
@@ -1442,6 +1482,16 @@ void launch_conv(int n, const void *in, const void *wt, const float *bias, const
 }
 
 }  // namespace
+#if ZC_TOWER_STAMP
+extern "C" int zc_debug_tower_stamps(unsigned long long *host, int clear) {
+    if (hipMemcpyFromSymbol(host, HIP_SYMBOL(g_tower_stamp), sizeof(unsigned long long) * 4) != hipSuccess) return 1;
+    if (clear) {
+        static unsigned long long zeros[4];
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_tower_stamp), zeros, sizeof(zeros)) != hipSuccess) return 1;
+    }
+    return 0;
+}
+#endif
 
 bool launch_net_conv3x3(int n, int h, int w, int cin, const void *in, const void *wt, const float *bias,
                         const void *res, void *out, int relu, hipStream_t s) {
