@@ -29,14 +29,19 @@ def main():
             net.tower(x)
         torch.cuda.synchronize()
         assert f(buf.ctypes.data, 1) == 0
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
         for _ in range(5):
             net.tower(x)
+        e1.record()
         torch.cuda.synchronize()
         assert f(buf.ctypes.data, 1) == 0
         mf, ep, ba, tot = (float(v) for v in buf)
         print(json.dumps({"shape": f"{h}x{w}x{n}", "mfma_loop": round(mf / tot, 4), "epilogue": round(ep / tot, 4),
                           "barrier_wait": round(ba / tot, 4), "rest": round(1 - (mf + ep + ba) / tot, 4),
-                          "cycles_per_wave_launch": round(tot / 5 / (n * h * w / 128 * 4), 1)}), flush=True)
+                          "cycles_per_wave_launch": round(tot / 5 / (n * h * w / 128 * 4), 1),
+                          "mfma_loop_cycles_per_wave_launch": round(mf / 5 / (n * h * w / 128 * 4), 1),
+                          "ms": round(e0.elapsed_time(e1) / 5, 4), "lib": os.path.basename(_native.lib()._name)}), flush=True)
 
 
 if __name__ == "__main__":

@@ -441,6 +441,11 @@ template <int NT> constexpr size_t tower_lds_swz() { return (size_t)(64 * NT + 8
 // pixel l & 15 of each N tile and k-chunk q = l >> 4; the weight fragments come from the same
 // packed stream as tower_mfma's (lane l of M tile m reads the 8 halfs of fragment row
 // 16 m + (l & 15), k 8 q .. 8 q + 7: wa already holds the lane's offset), one tap ahead.
+#ifndef ZC_TOWER_DIAG
+#define ZC_TOWER_DIAG 0  // diagnostic builds (wrong outputs, timing only; tools/tower_diag_libs.sh): 1 = no weight
+                         // reloads, 2 = no B reloads, 4 = every layer reads layer 1's weights, 8 = every weight
+                         // load of a wave reads its first fragment (L1-resident)
+#endif
 template <int H, int W, int NN, int KC, int KCN, int LD, int ZERO, int ZR, int NA>
 __device__ __forceinline__ void tower_mfma16(const _Float16 *lds, int src, const _Float16 *wa, const _Float16 *wn,
                                              h8 (&a)[NA], int l16, const int (&pyx)[NN], int q,
@@ -467,7 +472,10 @@ __device__ __forceinline__ void tower_mfma16(const _Float16 *lds, int src, const
         if (tap + 1 < 9) rows(tap + 1, xbn);
 #pragma unroll
         for (int j = 0; j < J; ++j) {
-            if (j + 1 < J) {
+            if (ZC_TOWER_DIAG & 2) {
+#pragma unroll
+                for (int n = 0; n < NN; ++n) xn[n] = x[n];
+            } else if (j + 1 < J) {
 #pragma unroll
                 for (int n = 0; n < NN; ++n) xn[n] = *(const h8 *)(xb[n] + (j + 1) * 32);
             } else if (tap + 1 < 9) {
@@ -483,7 +491,9 @@ __device__ __forceinline__ void tower_mfma16(const _Float16 *lds, int src, const
             __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
             for (int m = 0; m < 2; ++m) {
-                if (tap + 1 < 9) a[2 * j + m] = *(const h8 *)(wa + (size_t)((tap + 1) * KC + 2 * j) * 2048 + m * 128);
+                if (ZC_TOWER_DIAG & 1) break;
+                if (ZC_TOWER_DIAG & 8) a[2 * j + m] = *(const h8 *)(wa + (size_t)(__builtin_amdgcn_readfirstlane(m * 0)));
+                else if (tap + 1 < 9) a[2 * j + m] = *(const h8 *)(wa + (size_t)((tap + 1) * KC + 2 * j) * 2048 + m * 128);
                 else if (JN == J && wn) a[2 * j + m] = *(const h8 *)(wn + (size_t)(2 * j) * 2048 + m * 128);
             }
 #pragma unroll
@@ -494,7 +504,7 @@ __device__ __forceinline__ void tower_mfma16(const _Float16 *lds, int src, const
             for (int n = 0; n < NN; ++n) xb[n] = xbn[n];
         }
     }
-    if (JN != J && wn) {
+    if (JN != J && wn && !(ZC_TOWER_DIAG & 1)) {
 #pragma unroll
         for (int j = 0; j < JN; ++j)
 #pragma unroll
@@ -1148,8 +1158,8 @@ __global__ __launch_bounds__(256 * PG) __attribute__((amdgpu_waves_per_eu(WPE, W
         // per-lane pixel coordinates re-derived inside the layer (opaque to the compiler), so
         // that the 36 tap addresses are not hoisted out of the layer loop into registers
         const int src = (l & 1) ? 0 : BUF1, dst = (l & 1) ? BUF1 : 0;
-        const _Float16 *const wa = l == 0 ? wl0 : wl0 + kW0 + (size_t)(l - 1) * kW;
-        const _Float16 *const wn = l + 1 < nconv ? wl0 + kW0 + (size_t)l * kW : nullptr;  // layer l+1's
+        const _Float16 *const wa = l == 0 ? wl0 : wl0 + kW0 + (size_t)((ZC_TOWER_DIAG & 4) ? 0 : l - 1) * kW;
+        const _Float16 *const wn = l + 1 < nconv ? wl0 + kW0 + (size_t)((ZC_TOWER_DIAG & 4) ? 0 : l) * kW : nullptr;  // layer l+1's
         if constexpr (MF == 16) {
             int py16[NP];  // (the pixel rows are l16 + 16 t: nothing to carry)
 #pragma unroll
