@@ -630,9 +630,38 @@ __device__ __forceinline__ int legal_moves_check(const uint8_t *b, int t, uint16
     return legal_moves_check(b, (uint32_t)b[lane()], t, out, ps, reg, check);
 }
 
+#ifndef ZC_CHESS_FREEPROBE
+#define ZC_CHESS_FREEPROBE 1  // legal_moves_probe tries has_free_move first (A/B: 0)
+#endif
+
+// A sufficient test for "the mover has a legal move" (legal_moves_probe's common case): the
+// mover's king (the first, as find_king) is not attacked, and some piece of the mover other than
+// a king, standing on none of the king's eight lines, has a pseudo-legal move.  Such a move
+// cannot unblock a line to the king (the piece is on none; its target only adds a blocker of
+// the mover's) and cannot add a leaper attack (it removes at most the piece it captures), so
+// BitView::attacked stays false after it and the move is legal.  The pseudo-legal moves are
+// the generator's (a pawn's push or capture; a knight's target; a slider's or queen's first
+// step along a line of its kind): a target that is empty or capturable.
+__device__ __forceinline__ bool has_free_move(const BitView &v, int s, uint32_t pc, bool mine) {
+    const int k = __builtin_ctzll(v.kings);  // the view has a king
+    if (v.attacked(k, -1, -1, 0)) return false;
+    const int r = s >> 3, c = s & 7, kr = k >> 3, kc = k & 7;
+    const bool aligned = r == kr || c == kc || r - c == kr - kc || r + c == kr + kc;
+    const uint32_t up = upper(pc);
+    const uint64_t ok = ~v.occ | v.cap, kb = 1ull << s;
+    const uint64_t near = king_targets(s) & ok;                              // one step, any line
+    const uint64_t orth = near & ((kFileA << c) | (0xFFull << (8 * r)));    // ... along a rank or file
+    const uint64_t fwd = pc == 'P' ? kb >> 8 : kb << 8;                     // a pawn's push square
+    const uint64_t pawn = (fwd & ~v.occ) | ((((fwd >> 1) & kNotH) | ((fwd << 1) & kNotA)) & v.cap);
+    const uint64_t T = up == 'P' ? pawn : up == 'N' ? knight_targets(s) & ok : up == 'B' ? near & ~orth
+                     : up == 'R' ? orth : up == 'Q' ? near : 0ull;
+    return __ballot(mine && !aligned && T != 0ull) != 0ull;
+}
+
 // Whether the position has a legal move, for a node that may never be expanded (the crude
-// search's lazy nodes): one pseudo-legal move per piece (its first run's first target) through
-// the same legality test as legal_moves_view.  When one of them is legal, returns 1 with
+// search's lazy nodes): has_free_move, else one pseudo-legal move per piece (its first run's
+// first target) through the same legality test as legal_moves_view.  When one of them is
+// legal, returns 1 with
 // lazy = true and writes nothing (the list is generated if the node is ever expanded);
 // otherwise — every tested move illegal (typically in check), a position the bit view does not
 // cover, or insufficient material — the full legal_moves_check: the list in out, its length,
@@ -647,6 +676,11 @@ __device__ __forceinline__ int legal_moves_probe(const uint8_t *b, uint32_t pc, 
     if ((heavy || minor > 1) && make_bitview(pc, t, bv)) {
         const int s = (int)lane();
         const bool mine = !empty_sq(pc) && ((t == 0) == is_white(pc));
+        if (ZC_CHESS_FREEPROBE && has_free_move(bv, s, pc, mine)) {
+            lazy = true;
+            check = false;
+            return 1;
+        }
         uint64_t M[8];
         uint32_t desc;
         run_masks(bv, s, pc, mine, M, desc);
