@@ -506,30 +506,128 @@ __device__ __forceinline__ void chess_backup_flush(const ChessParams &p, const C
     }
 }
 
+#ifndef ZC_CHESS_AGG_BACKUP
+#define ZC_CHESS_AGG_BACKUP 1  // crude_backup_flush aggregates each flush's edges (A/B: 0)
+#endif
+
+// crude_chess_score's value.batch (mcts.cpp:116-118) and backprop (mcts.cpp:80-100) of one
+// flush, the backup aggregated per edge.  The crude values are integers (material; +-1000 for
+// a mate), so an edge's Na += its leaves and Wa -= the sum of their signed values equals the
+// leaf-by-leaf updates exactly, whatever the order (every partial sum is an integer far below
+// 2^53).  The flush's (leaf, level) edges are gathered in an LDS hash table (slot -> count,
+// sum), eight leaves at a time (lane 8q + i: leaf j0 + q, level i + 1, + 8 per extra round),
+// and every distinct edge is then updated once, all in one pass: one memory round trip per
+// flush instead of a read-modify-write per leaf.  A flush of more than 64 leaves or with more
+// (leaf, level) pairs than half the table takes the leaf-by-leaf chess_backup_flush.
+constexpr int kBackupHash = 512;
+struct BackupTable {
+    uint32_t key[kBackupHash];  // slot + 1 (0: empty)
+    int32_t cnt[kBackupHash];
+    int32_t sum[kBackupHash];
+};
+
+__device__ __forceinline__ void backup_table_clear(BackupTable &T) {
+    for (int e = (int)lane_id(); e < kBackupHash; e += 64) {
+        T.key[e] = 0u;
+        T.cnt[e] = 0;
+        T.sum[e] = 0;
+    }
+    wave_sync_mem();
+}
+
+__device__ __forceinline__ void crude_values_backup(const ChessParams &p, const CTree &t, int g, const int32_t *ctl,
+                                                    double *s_vals, int nb, BackupTable *T) {
+    const uint32_t lane = lane_id();
+    const uint32_t *meta = p.ca.meta + (size_t)g * p.max_batch;
+    int dj = 0, vj = 0;  // lane j: leaf j's depth and crude value
+    CSTAMP_T(cs4);
+    for (int j = (int)lane; j < nb; j += 64) {
+        const uint32_t mj = meta[j];
+        const ChessNode *N = &t.nodes[mj & 0xFFFFu];
+        const int nm = N->nmoves, chk = N->check, turn = N->st.turn, mat = N->material;
+        vj = (nm == 0 && chk) ? 1000 : (turn * -2 + 1) * mat;
+        dj = (int)(mj >> 16);
+        s_vals[j] = (double)vj;
+    }
+    wave_sync_mem();
+    CSTAMP_ADD(4, cs4);
+    CSTAMP_T(cs5);
+    int pairs = dj;
+    for (int o = 32; o > 0; o >>= 1) pairs += __shfl_xor(pairs, o);
+    if (!ZC_CHESS_AGG_BACKUP || !T || nb > 64 || pairs > kBackupHash / 2) {
+        chess_backup_flush(p, t, g, ctl, s_vals, nb);
+        CSTAMP_ADD(5, cs5);
+        return;
+    }
+    const uint32_t *paths = p.ca.paths + (size_t)g * p.max_batch * kChessPath;
+    const int qd = (int)(lane >> 3), i = (int)(lane & 7);
+    for (int j0 = 0; j0 < nb; j0 += 8) {
+        const int j = j0 + qd;
+        const int d = __shfl(dj, j & 63), v = __shfl(vj, j & 63);
+        const int dq = j < nb ? d : 0;
+        int maxd = dq;
+        for (int o = 32; o > 0; o >>= 1) maxd = max(maxd, __shfl_xor(maxd, o));
+        for (int l0 = 1; l0 <= maxd; l0 += 8) {
+            const int l = l0 + i;
+            if (l <= dq) {
+                const uint32_t sl = paths[(size_t)j * kChessPath + l];
+                const int r = ((dq - l) & 1) ? -v : v;
+                uint32_t h = (sl * 2654435761u) >> 23;  // 9 bits
+                for (;;) {  // linear probing; the table is at most half full
+                    const uint32_t prev = atomicCAS(&T->key[h], 0u, sl + 1u);
+                    if (prev == 0u || prev == sl + 1u) break;
+                    h = (h + 1u) & (uint32_t)(kBackupHash - 1);
+                }
+                atomicAdd(&T->cnt[h], 1);
+                atomicAdd(&T->sum[h], r);
+            }
+        }
+    }
+    wave_sync_mem();
+    // every distinct edge once: the eight entries of each lane read, updated and cleared together
+    uint32_t key[kBackupHash / 64];
+    int32_t cnt[kBackupHash / 64], sum[kBackupHash / 64];
+#pragma unroll
+    for (int k = 0; k < kBackupHash / 64; ++k) {
+        const int e = k * 64 + (int)lane;
+        key[k] = T->key[e];
+        cnt[k] = T->cnt[e];
+        sum[k] = T->sum[e];
+    }
+    int32_t na[kBackupHash / 64];
+    double w[kBackupHash / 64];
+#pragma unroll
+    for (int k = 0; k < kBackupHash / 64; ++k) {
+        na[k] = key[k] ? t.na[key[k] - 1u] : 0;
+        w[k] = key[k] ? t.w[key[k] - 1u] : 0.0;
+    }
+#pragma unroll
+    for (int k = 0; k < kBackupHash / 64; ++k) {
+        if (key[k]) {
+            t.na[key[k] - 1u] = na[k] + cnt[k];
+            t.w[key[k] - 1u] = w[k] - (double)sum[k];
+            const int e = k * 64 + (int)lane;
+            T->key[e] = 0u;
+            T->cnt[e] = 0;
+            T->sum[e] = 0;
+        }
+    }
+    wave_sync_mem();
+    CSTAMP_ADD(5, cs5);
+}
+
 // ---------------------------------------------------------------- fused: crude_chess_score
 // The whole search of one game from p.roots[gl] (root_init .. the last backup).
 __device__ __forceinline__ void crude_search(const ChessParams &p, const CTree &t, CLds &L, double *s_vals, int gl, int g,
-                             int32_t *ctl, Helper *h = nullptr) {
+                             int32_t *ctl, Helper *h = nullptr, BackupTable *T = nullptr) {
     ConstDouble *logtab = (ConstDouble *)p.a.logtab;
     CSTAMP_T(cs7);
     root_init(p, t, L, gl, g, ctl);
-    const uint32_t *meta = p.ca.meta + (size_t)g * p.max_batch;
     for (int done = 0; done < p.sims && !uni(ctl[cStatus]);) {
         CSTAMP_T(cs6);
         const int nb = chess_select_flush(p, t, L, logtab, g, ctl, done, min(p.bs, p.sims - done), h);
         CSTAMP_ADD(6, cs6);
-        CSTAMP_T(cs4);
-        // value.batch: crude_chess_score of every pending leaf (mcts.cpp:116-118)
-        for (int j = (int)lane_id(); j < nb; j += 64) {
-            const ChessNode *N = &t.nodes[meta[j] & 0xFFFFu];
-            const int nm = N->nmoves, chk = N->check, turn = N->st.turn, mat = N->material;
-            s_vals[j] = (nm == 0 && chk) ? 1000.0 : (double)((turn * -2 + 1) * mat);
-        }
-        wave_sync_mem();
-        CSTAMP_ADD(4, cs4);
-        CSTAMP_T(cs5);
-        chess_backup_flush(p, t, g, ctl, s_vals, nb);
-        CSTAMP_ADD(5, cs5);
+        crude_values_backup(p, t, g, ctl, s_vals, nb, T);
         done += nb;
     }
     CSTAMP_ADD(7, cs7);
@@ -541,6 +639,7 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void c
     __shared__ CLds L;
     __shared__ double s_vals[256];
     __shared__ Helper H;
+    __shared__ BackupTable T;
     const int gl = blockIdx.x;
     if (gl >= p.n_games) return;
     const int g = p.first_game + gl;
@@ -554,7 +653,8 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void c
     __builtin_amdgcn_s_setprio(1);
     int32_t *ctl = p.ca.ctl + (size_t)g * kCtlWords;
     CSTAMP_INIT();
-    crude_search(p, t, L, s_vals, gl, g, ctl, &H);
+    if (ZC_CHESS_AGG_BACKUP) backup_table_clear(T);
+    crude_search(p, t, L, s_vals, gl, g, ctl, &H, &T);
     CSTAMP_FLUSH();
     finish(p, t, gl, g, ctl);
     helper_exit(&H);
@@ -660,6 +760,7 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void c
     __shared__ CLds L;
     __shared__ double s_vals[256];
     __shared__ Helper H;
+    __shared__ BackupTable T;
     const int gl = blockIdx.x;
     if (gl >= p.n_games) return;
     const int g = p.first_game + gl;
@@ -669,6 +770,7 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void c
         return;
     }
     __builtin_amdgcn_s_setprio(1);  // the leader first (chess_search_kernel)
+    if (ZC_CHESS_AGG_BACKUP) backup_table_clear(T);
     const uint32_t lane = lane_id();
     int32_t *ctl = p.ca.ctl + (size_t)g * kCtlWords;
     const uint64_t use_start = uni64(p.a.rngpos[2 * (size_t)g]);
@@ -680,7 +782,7 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void c
             if (lane == 0) tk = atomicAdd(q.ticket, 1);
             if (uni(tk) >= q.budget) break;
         }
-        crude_search(p, t, L, s_vals, gl, g, ctl, &H);
+        crude_search(p, t, L, s_vals, gl, g, ctl, &H, &T);
         status = uni(ctl[cStatus]);
         exp += uni(ctl[cExp]);
         depth += uni(ctl[cDepth]);
