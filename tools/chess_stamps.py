@@ -20,7 +20,9 @@ from zeroclone_amd import _native  # noqa: E402
 
 PHASES = ["walk", "policy+erase", "apply_move", "create_node", "values", "backup", "select_flush", "whole",
           "legal_moves_check", "material", "node_writes", "lmc.emission", "lmc.runs_masks", "lmc.legality", "lmc.bitview_check",
-          "lmc.runs_emit"]
+          "lmc.runs_emit", "pe.cached_path", "pe.node_fields+lazy_gen", "pe.untried_loads", "pe.pick+erase",
+          "pe.cached_count", "helper_wait", "pe.cached_pick", "pe.cached_erase"]
+NS = len(PHASES)
 
 
 def main():
@@ -51,7 +53,7 @@ def main():
     L = _native.lib()
     f = L.zc_debug_chess_stamps
     f.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
-    buf = np.zeros(4096 * 16, np.uint64)
+    buf = np.zeros(4096 * NS, np.uint64)
     run = lambda: eng.chess_search_async(0, G, roots.data_ptr(), S, 1.4, B, 1, 3.0, mv.data_ptr(),  # noqa: E731
                                          na.data_ptr(), st.data_ptr(), s)
     run()
@@ -62,7 +64,7 @@ def main():
         run()
     torch.cuda.synchronize()
     assert f(buf.ctypes.data, buf.size, 1) == 0
-    per = buf[: G * 16].reshape(G, 16).astype(np.float64) / reps / S   # cycles per simulation
+    per = buf[: G * NS].reshape(G, NS).astype(np.float64) / reps / S   # cycles per simulation
     med = np.median(per, axis=0)
     out = {"workload": "1024 games x 400 sims x bs 32, crude, half opening / half mixed roots (tools/ab_chess.py)",
            "cycles_per_simulation_median_over_games": {k: round(float(v), 1) for k, v in zip(PHASES, med)},

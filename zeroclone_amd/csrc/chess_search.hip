@@ -174,6 +174,9 @@ __device__ __forceinline__ Expansion sim_front(const ChessParams &p, const CTree
         nu = generate_lazy(t, L, N, slots, status, lazy_base);
         lazy_gen = true;
     }
+    if (hit) CSTAMP_COUNT(20);
+    if (!hit) CSTAMP_ADD(17, cs1);
+    CSTAMP_T(cs18);
     rs.node = node;
     rs.depth = depth;
     rs.nN = nN;
@@ -204,7 +207,10 @@ __device__ __forceinline__ Expansion sim_front(const ChessParams &p, const CTree
             utv = lane < (uint32_t)nu ? (int)t.ut[base + lane] : 0;
             mvv = lane < (uint32_t)nu ? (uint32_t)t.mv[base + utv] : 0u;
             vmem_ready(mvv);
+            CSTAMP_ADD(18, cs18);
         }
+        CSTAMP_T(cs19);
+        CSTAMP_T(cs22);
         if (p.policy == 1) {
             // Policy('immediate_value') (policy_functions.py:14-17): random.choice over the
             // untried moves whose capture value >= max - policy_freedom
@@ -228,6 +234,8 @@ __device__ __forceinline__ Expansion sim_front(const ChessParams &p, const CTree
         } else {
             local = (int)rng_below(rng, (uint32_t)nu);  // Policy('random'): random.choice(untried)
         }
+        if (hit) CSTAMP_ADD(22, cs22);
+        CSTAMP_T(cs23);
         midx = __builtin_amdgcn_readlane(utv, local);
         m = (uint32_t)__builtin_amdgcn_readlane((int)mvv, local);
         // untried.erase(begin + local): entry i takes entry i + 1
@@ -241,6 +249,8 @@ __device__ __forceinline__ Expansion sim_front(const ChessParams &p, const CTree
         rs.mvv = moved ? nmv : mvv;
         rs.base = base;
         rs.stw = stw;
+        if (!hit) CSTAMP_ADD(19, cs19);
+        if (hit) CSTAMP_ADD(23, cs23);
     } else {
         if (p.policy == 1) {
             int best = -1;
@@ -277,6 +287,7 @@ __device__ __forceinline__ Expansion sim_front(const ChessParams &p, const CTree
     }
     if (lane == 0) N->nu = (uint16_t)(nu - 1);
     CSTAMP_ADD(1, cs1);
+    if (hit) CSTAMP_ADD(16, cs1);
     return Expansion{node, depth, pathv, midx, m, stw, base};
 }
 
@@ -453,7 +464,9 @@ __device__ __forceinline__ int chess_select_flush(const ChessParams &p, const CT
         CSTAMP_ADD(3, cs3);
         record(ida, a.depth + 1, leaf_path(a));
         if (pair) {
+            CSTAMP_T(cs21);
             __syncthreads();  // b's child is generated
+            CSTAMP_ADD(21, cs21);
             if (status) {  // a ended the flush (a list past ZC_CHESS_MAX_MOVES): b's draw is not consumed
                 rng = rng_a;
                 break;
@@ -1243,10 +1256,10 @@ void launch_chess_leaf_moves(const ChessParams &p, hipStream_t s) {
 #if ZC_CHESS_STAMP
 // diagnostic build only (not in include/zeroclone.h): copy / clear the phase stamps
 extern "C" int zc_debug_chess_stamps(uint64_t *host, int n, int clear) {
-    if (n > 4096 * 16) n = 4096 * 16;
+    if (n > 4096 * zc::kCStamps) n = 4096 * zc::kCStamps;
     if (hipMemcpyFromSymbol(host, HIP_SYMBOL(zc::g_chess_stamp), (size_t)n * 8) != hipSuccess) return 1;
     if (clear) {
-        static uint64_t zeros[4096 * 16];
+        static uint64_t zeros[4096 * zc::kCStamps];
         if (hipMemcpyToSymbol(HIP_SYMBOL(zc::g_chess_stamp), zeros, sizeof(zeros)) != hipSuccess) return 1;
     }
     return 0;

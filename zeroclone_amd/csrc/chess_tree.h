@@ -8,15 +8,19 @@
 #define ZC_CHESS_STAMP 0  // diagnostic build: per-game s_memtime cycles per phase (tools/chess_stamps.py)
 #endif
 #if ZC_CHESS_STAMP
-// [game of the launch][16]: walk, policy + erase, apply_move, create_node, values, backup,
+// [game of the launch][kCStamps]: walk, policy + erase, apply_move, create_node, values, backup,
 // select flush (whole), whole search, legal_moves_check, material, node writes,
-// and inside legal_moves_check: emission, copy, legality, bit view + check.  A region adds
+// inside legal_moves_check: emission, copy, legality, bit view + check; then inside policy +
+// erase: the cached path, the node fields + lazy generation, the untried / move loads, the
+// pick + erase, and the count of cached expansions; the leader's wait for the helper, the
+// leaf records, the flush's stream open + close.  A region adds
 // its cycles to the workgroup's LDS copy with a no-return LDS atomic (no wait on the chain);
 // the kernel folds the LDS copy into the global table once at its end (CSTAMP_FLUSH).
 namespace zc {
 namespace {
-__device__ uint64_t g_chess_stamp[4096 * 16];
-__shared__ uint64_t s_chess_stamp[16];
+constexpr int kCStamps = 24;
+__device__ uint64_t g_chess_stamp[4096 * kCStamps];
+__shared__ uint64_t s_chess_stamp[kCStamps];
 }  // namespace
 }  // namespace zc
 #define CSTAMP_T(v) const uint64_t v = __builtin_amdgcn_s_memtime()
@@ -27,19 +31,26 @@ __shared__ uint64_t s_chess_stamp[16];
             __hip_atomic_fetch_add(&::zc::s_chess_stamp[(k)], now_ - (t0), __ATOMIC_RELAXED,       \
                                    __HIP_MEMORY_SCOPE_WORKGROUP);                                  \
     } while (0)
+#define CSTAMP_COUNT(k)                                                                            \
+    do {                                                                                           \
+        if (__lane_id() == 0)                                                                      \
+            __hip_atomic_fetch_add(&::zc::s_chess_stamp[(k)], (uint64_t)1, __ATOMIC_RELAXED,       \
+                                   __HIP_MEMORY_SCOPE_WORKGROUP);                                  \
+    } while (0)
 #define CSTAMP_INIT()                                                                              \
     do {                                                                                           \
-        if (__lane_id() < 16) ::zc::s_chess_stamp[__lane_id()] = 0;                                \
+        if (__lane_id() < ::zc::kCStamps) ::zc::s_chess_stamp[__lane_id()] = 0;                    \
     } while (0)
 #define CSTAMP_FLUSH()                                                                             \
     do {                                                                                           \
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");                                     \
-        if (__lane_id() < 16 && blockIdx.x < 4096)                                                 \
-            ::zc::g_chess_stamp[blockIdx.x * 16 + __lane_id()] += ::zc::s_chess_stamp[__lane_id()]; \
+        if (__lane_id() < ::zc::kCStamps && blockIdx.x < 4096)                                     \
+            ::zc::g_chess_stamp[blockIdx.x * ::zc::kCStamps + __lane_id()] += ::zc::s_chess_stamp[__lane_id()]; \
     } while (0)
 #else
 #define CSTAMP_T(v)
 #define CSTAMP_ADD(k, t0)
+#define CSTAMP_COUNT(k)
 #define CSTAMP_INIT()
 #define CSTAMP_FLUSH()
 #endif
