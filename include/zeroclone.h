@@ -726,6 +726,13 @@ int zc_debug_chess_tree(zc_engine *eng, int32_t game, int32_t max_nodes, int32_t
                         uint16_t *out_mv, float *out_prior, int32_t *out_na, double *out_w, uint16_t *out_child,
                         int32_t *out_counts);
 
+/* The crude search's lazy-node probe (legal_moves_probe: a sufficient free-move test, then one
+ * pseudo-legal move per piece through the legality test, then the full get_legal_moves) on n
+ * positions: d_out[i] = -2 when it proved a legal move without generating the list, else the
+ * generated list's length (-1 = overflow).  Device pointers, enqueued on hip_stream. */
+int zc_debug_chess_probe_async(zc_engine *eng, int32_t n, const zc_chess_state *d_states, int32_t *d_out,
+                               void *hip_stream);
+
 /* Diagnostic phase stamps: returns (into out8, may be NULL) the shader-cycle sums since the
  * previous call, over all games, of {RNG generation, first walk of each flush, resumed
  * walks, expansion + leaf bookkeeping, rollouts, backup, publish, 0}, resets them, and switches

@@ -341,3 +341,51 @@ def test_crowded_boards_match_oracle(eng):
             continue
         assert counts[i] == len(want), (i, b, stats[i])
         assert [decode(m) for m in moves[i, :counts[i]]] == want, (i, b, stats[i])
+
+
+PROBE_FENS = [
+    "rnb1kbnr/pppp1ppp/8/4p3/6Pq/5P2/PPPPP2P/RNBQKBNR w KQkq - 1 3",   # checkmated
+    "k7/8/1Q6/8/8/8/8/7K b - - 0 1",                                   # stalemate
+    "4k3/8/8/8/8/8/4r3/4K3 w - - 0 1",                                 # in check, king moves
+    "4k3/4r3/8/8/8/8/4B3/4K3 w - - 0 1",                               # the bishop pinned on the king's file
+    "7k/8/8/8/8/2b5/1P6/K7 w - - 0 1",                                 # pawn pinned on the king's diagonal
+    "4k3/8/8/8/8/8/8/r3K2r w - - 0 1",                                 # king boxed on its rank
+    "8/8/8/8/8/5k2/6q1/7K w - - 0 1",                                  # checkmated in the corner
+    "8/8/8/8/8/4k3/8/2r1K1r1 w - - 0 1",                               # checkmated on the back rank
+    "r3k2r/p1ppqpb1/bn2pnp1/3PN3/1p2P3/2N2Q1p/PPPBBPPP/R3K2R w KQkq - 0 1",
+]
+
+
+def test_lazy_node_probe_is_sound(eng):
+    """The crude search's lazy-node probe (chess_device.h legal_moves_probe: the free-move test,
+    then one pseudo-legal move per piece through the legality test, then the full generation),
+    via zc_debug_chess_probe_async, against the oracle's get_legal_moves on every position of 150
+    random playouts (checks, pins, captures, mates, stalemates) and crafted pins and mates: -2
+    (a legal move proven, no list) only where the list is non-empty, the exact length elsewhere."""
+    import random
+
+    import oracle
+    from zeroclone_amd._native import CHESS_STATE_DTYPE
+    rng = random.Random(11)
+    states = [oracle.chess_from_fen(f) for f in PROBE_FENS]
+    for _ in range(150):
+        s = oracle.chess_init()
+        for _ in range(160):
+            states.append(s)
+            ms = oracle.chess_moves(s)
+            if not ms:
+                break
+            s = oracle.chess_play(s, rng.choice(ms))
+    a = np.zeros(len(states), CHESS_STATE_DTYPE)
+    for i, s in enumerate(states):
+        a[i]["board"] = np.frombuffer(bytes(s.board), np.uint8)
+        a[i]["turn"], a[i]["fifty"], a[i]["castle"] = s.turn, s.fifty, s.castle
+    out = torch.zeros(len(states), dtype=torch.int32, device="cuda")
+    eng.debug_chess_probe_async(len(states), dev(a).data_ptr(), out.data_ptr())
+    torch.cuda.synchronize()
+    got = out.cpu().numpy()
+    want = np.array([len(oracle.chess_moves(s)) for s in states])
+    lazy = got == -2
+    assert np.all(want[lazy] > 0), np.flatnonzero(lazy & (want == 0))[:10]
+    np.testing.assert_array_equal(got[~lazy], want[~lazy])
+    assert lazy.mean() > 0.5 and (~lazy).sum() >= 20 and (want == 0).sum() >= 5

@@ -277,6 +277,8 @@ SIGNATURES = [
     ("zc_gen_end", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p]),
     ("zc_debug_uct", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p,
                                     ctypes.c_void_p, ctypes.c_double, ctypes.c_void_p]),
+    ("zc_debug_chess_probe_async", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p,
+                                                   ctypes.c_void_p]),
     ("zc_debug_chess_tree", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
                                            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
@@ -580,6 +582,11 @@ class NativeEngine:
     def chess_play_async(self, n: int, d_in: int, d_moves: int, d_out: int, stream: int = 0):
         check(lib().zc_chess_play_async(self._h, n, ctypes.c_void_p(d_in), ctypes.c_void_p(d_moves),
                                         ctypes.c_void_p(d_out), ctypes.c_void_p(stream or None)))
+
+    def debug_chess_probe_async(self, n: int, d_states: int, d_out: int, stream: int = 0):
+        """zc_debug_chess_probe_async: -2 (a legal move proven, no list) or the list length."""
+        check(lib().zc_debug_chess_probe_async(self._h, n, ctypes.c_void_p(d_states), ctypes.c_void_p(d_out),
+                                               ctypes.c_void_p(stream or None)))
 
     def chess_terminal_async(self, n: int, d_states: int, d_flags: int, stream: int = 0):
         check(lib().zc_chess_terminal_async(self._h, n, ctypes.c_void_p(d_states), ctypes.c_void_p(d_flags),

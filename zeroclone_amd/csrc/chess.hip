@@ -79,6 +79,20 @@ __global__ __launch_bounds__(64) void chess_terminal_kernel(int n, const zc_ches
     }
 }
 
+// legal_moves_probe (the crude search's lazy nodes, chess_device.h): out[i] = -2 when the
+// probe proved the position has a legal move without generating its list, else the length
+// of the list it generated (-1: overflow).  Diagnostic / parity-test entry point.
+__global__ __launch_bounds__(64) void chess_probe_kernel(int n, const zc_chess_state *states, int32_t *out) {
+    __shared__ ChessScratch S;
+    const int i = blockIdx.x;
+    if (i >= n) return;
+    load_board(S.board, states[i]);
+    const int t = __builtin_amdgcn_readfirstlane(states[i].turn);
+    bool check, lazy;
+    const int k = legal_moves_probe(S.board, S.board[lane()], t, S.legal, S.pseudo, S.region, check, lazy);
+    if (lane() == 0) out[i] = lazy ? -2 : k;
+}
+
 // has_repeated_prefix (:148-180) of both sides' move histories (chess_device.h::repetitions):
 // hist[i][side][k] = that side's k-th move in play order (k < len[i][side] <= cap); out[i] =
 // white's answer | black's << 1.  One wave per position, the history staged in LDS.
@@ -121,6 +135,9 @@ __global__ void chess_planes_kernel(int n, const zc_chess_state *states, void *p
 
 void launch_chess_legal(int n, const zc_chess_state *s, uint16_t *moves, int32_t *counts, hipStream_t st) {
     hipLaunchKernelGGL(chess_legal_kernel, dim3(n), dim3(64), 0, st, n, s, moves, counts);
+}
+void launch_chess_probe(int n, const zc_chess_state *s, int32_t *out, hipStream_t st) {
+    hipLaunchKernelGGL(chess_probe_kernel, dim3(n), dim3(64), 0, st, n, s, out);
 }
 void launch_chess_children(int n, const zc_chess_state *s, zc_chess_state *children, uint16_t *moves,
                            int32_t *counts, hipStream_t st) {

@@ -823,6 +823,14 @@ int zc_chess_legal_moves_async(zc_engine *eng, int32_t n, const zc_chess_state *
     return ZC_OK;
 }
 
+int zc_debug_chess_probe_async(zc_engine *eng, int32_t n, const zc_chess_state *d_states, int32_t *d_out,
+                               void *hip_stream) {
+    ZC_CHESS_ENTRY(d_states && d_out)
+    zc::launch_chess_probe(n, d_states, d_out, (hipStream_t)hip_stream);
+    ZC_HIP(hipGetLastError());
+    return ZC_OK;
+}
+
 int zc_chess_children_async(zc_engine *eng, int32_t n, const zc_chess_state *d_states, zc_chess_state *d_children,
                             uint16_t *d_moves, int32_t *d_counts, void *hip_stream) {
     ZC_CHESS_ENTRY(d_states && d_children && d_counts)

@@ -347,6 +347,7 @@ void launch_chess_puct_backup(const ChessParams &p, hipStream_t s);
 void launch_chess_puct_end(const ChessParams &p, hipStream_t s);
 
 void launch_chess_legal(int n, const zc_chess_state *s, uint16_t *moves, int32_t *counts, hipStream_t st);
+void launch_chess_probe(int n, const zc_chess_state *s, int32_t *out, hipStream_t st);
 void launch_chess_children(int n, const zc_chess_state *s, zc_chess_state *children, uint16_t *moves,
                            int32_t *counts, hipStream_t st);
 void launch_chess_play(int n, const zc_chess_state *in, const uint16_t *moves, zc_chess_state *out, hipStream_t st);
