@@ -274,3 +274,38 @@ def test_short_last_flush_runs_the_network_on_its_leaves_only(eng):
     for a, b in zip(*outs):
         assert (a == b).all()
     assert (outs[0][2][:, 5] == 0).all() and (outs[0][2][:, 0] == sims).all()
+
+
+@pytest.mark.parametrize("bs", [64, 128])
+def test_crude_search_large_flushes_match_oracle(bs):
+    """The fused crude search's backup (chess_search.hip crude_values_backup) aggregates a
+    flush's edges in an LDS hash table, and keeps the leaf-by-leaf backup for flushes of more
+    than 64 leaves or with more (leaf, level) pairs than half the table.  Flushes of 64 leaves
+    (the table, or leaf by leaf past half of it on the endgames' deep trees) and of 128 (leaf
+    by leaf), against the oracle's get_move: root visits, move and the words drawn."""
+    from zeroclone_amd._native import ZC_POLICY_IMMEDIATE_VALUE, NativeEngine
+    fens = FENS * 2 + ["8/8/3k4/8/8/3K4/3Q4/8 w - - 0 1", "6k1/5ppp/8/8/8/8/5PPP/3R2K1 w - - 0 1",
+                       "8/8/8/4k3/8/8/8/R3K3 w - - 0 1", "7k/8/8/8/8/8/8/K6Q w - - 0 1"]
+    n, sims = len(fens), 400
+    e = NativeEngine(max_games=n, max_sims=sims, max_batch=bs)
+    try:
+        seeds = [90 + i for i in range(n)]
+        e.seed(0, seeds)
+        roots = roots_of(fens)
+        mv = torch.zeros(n, dtype=torch.int16, device="cuda")
+        na = torch.zeros((n, MAXM), dtype=torch.int32, device="cuda")
+        st = torch.zeros((n, 8), dtype=torch.int64, device="cuda")
+        e.chess_search_async(0, n, roots.data_ptr(), sims, 1.4, bs, ZC_POLICY_IMMEDIATE_VALUE, 3.0, mv.data_ptr(),
+                             na.data_ptr(), st.data_ptr())
+        torch.cuda.synchronize()
+        mv, na, st = mv.cpu().numpy(), na.cpu().numpy(), st.cpu().numpy()
+        for i, fen in enumerate(fens):
+            mt = oracle.MT(seeds[i])
+            best, moves, rna = oracle.chess_get_move(oracle.chess_from_fen(fen), mt, sims, 1.4, bs, "immediate_value",
+                                                     3.0)
+            assert st[i, 5] == 0, (fen, st[i])
+            assert list(na[i, :len(moves)]) == rna, fen
+            assert decode(mv[i]) == list(moves[best]), fen
+            assert st[i, 4] == mt.drawn, fen
+    finally:
+        e.close()
