@@ -752,7 +752,9 @@ int zc_debug_net_switch(const char *name, int32_t value, int32_t *old);
 /* Launch-timeline stamps of the Connect4 self-play launches (the pooled launch's tail,
  * tools/launch_tail.py): with d_buf != NULL (device, 4 x uint64 per game of the engine),
  * every later Connect4 self-play launch (zc_c4_selfplay_async, its pooled form) writes per game {s_memrealtime at its wave's
- * start, at the start of its last move, at its end, moves played}; NULL switches them off. */
+ * start, at the start of its last move, at its end, moves played | placement << 32}
+ * (placement: HW_ID bits 15:0 — wave slot, SIMD, CU, SH, SE — and the XCC << 16); NULL
+ * switches them off. */
 int zc_debug_c4_launch_stamps(zc_engine *eng, uint64_t *d_buf);
 
 #ifdef __cplusplus

@@ -51,7 +51,8 @@ def main():
             buf.zero_()
             r = bench.run_steps(sp, k, warmup=a.warmup, launch="pooled", carry=False)
             ts = buf.cpu().numpy().astype(np.float64) / 1e5   # ms
-        start, last, end, moves = ts[:, 0], ts[:, 1], ts[:, 2], ts[:, 3] * 1e5
+        start, last, end = ts[:, 0], ts[:, 1], ts[:, 2]
+        moves = (buf[:, 3].cpu().numpy() & 0xFFFFFFFF).astype(np.float64)  # (high word: where the wave ran)
         t0, t1 = start.min(), end.max()
         budget_out = last.max()   # the last ticket was taken then (a wave's last move started)
         rec = {"steps": k, "carry": a.carry, "launch_ms": round(r["launch_ms"], 3), "per_step_ms": round(r["launch_ms"] / k, 4),

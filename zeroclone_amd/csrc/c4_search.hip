@@ -1552,7 +1552,11 @@ __global__ __launch_bounds__(kSearchWaves * kBlock, 4) void c4_selfplay_kernel(S
         ts[0] = t_start;
         ts[1] = t_last;
         ts[2] = __builtin_amdgcn_s_memrealtime();
-        ts[3] = (uint64_t)mv;
+        // moves played | where the wave ran << 32: HW_ID bits 15:0 (wave slot, SIMD, CU, SH,
+        // SE) and the XCC below them << 16
+        const uint32_t hw = (uint32_t)__builtin_amdgcn_s_getreg(4 | (15 << 11)) |
+                            ((uint32_t)__builtin_amdgcn_s_getreg(20 | (3 << 11)) << 16);
+        ts[3] = (uint64_t)mv | ((uint64_t)hw << 32);
     }
     // steps this game did not reach (budget spent, or a bad root): skipped by the recording
     for (int k = mv + (int)lane; k < p.moves; k += kBlock) {
